@@ -1,0 +1,411 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
+
+Run in the build container only (needs /root/reference, read-only):
+    python tests/golden/make_golden.py
+
+What it does:
+  * imports the reference (nexus-rl/dfd-starter @ /root/reference) with an in-script ``gym`` /
+    ``wandb`` stub -- neither is installed -- and with bytecode writing disabled so nothing is
+    written under /root/reference;
+  * runs the reference's own classes (SharedNoiseTable, DiscretePolicy, MujocoPolicy, Worker,
+    Agent, FiniteDifferences, DSGD, AdaptiveOmega, SequentialRunner, the trap env) on small
+    seeded inputs and stores inputs + outputs as .npz DATA;
+  * the only harness patches are the ones SURVEY.md section 8c lists (Worker.update,
+    learner.noise_std, RNGNoiseSource -> SharedNoiseTable) plus action sampling replaced by
+    injected noise (the torch multinomial / normal streams cannot be reproduced elsewhere).
+
+Nothing here ships to the GPU box: the box only sees the .npz files.
+"""
+import hashlib
+import io
+import os
+import sys
+import types
+import contextlib
+
+import numpy as np
+
+sys.dont_write_bytecode = True           # never write __pycache__ into /root/reference
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+
+# ------------------------------------------------------------------------------------------
+# gym / wandb stubs (the reference imports them at module level; neither is installed)
+# ------------------------------------------------------------------------------------------
+def _install_stubs():
+    gym = types.ModuleType("gym")
+    spaces = types.ModuleType("gym.spaces")
+
+    class Env(object):
+        pass
+
+    class Discrete(object):
+        def __init__(self, n):
+            self.n = n
+            self._rng = np.random.RandomState(0)
+
+        def seed(self, s):
+            self._rng = np.random.RandomState(s)
+
+        def sample(self):
+            return int(self._rng.randint(self.n))
+
+    class Box(object):
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            self.low, self.high, self.shape = low, high, tuple(shape)
+            self._rng = np.random.RandomState(0)
+
+        def seed(self, s):
+            self._rng = np.random.RandomState(s)
+
+        def sample(self):
+            return self._rng.uniform(-1, 1, size=self.shape).astype(np.float32)
+
+    registry = {}
+
+    def register(id, entry_point, **kw):
+        registry[id] = entry_point
+
+    def make(env_id, **kw):
+        return _ENV_FACTORY[env_id]()
+
+    spaces.Discrete, spaces.Box = Discrete, Box
+    gym.Env, gym.spaces, gym.register, gym.make = Env, spaces, register, make
+    sys.modules["gym"] = gym
+    sys.modules["gym.spaces"] = spaces
+    sys.modules["wandb"] = types.ModuleType("wandb")
+    return gym
+
+
+_ENV_FACTORY = {}
+gym = _install_stubs()
+sys.path.insert(0, REF)
+
+import torch  # noqa: E402
+from utils.noise_sources import SharedNoiseTable  # noqa: E402  (reference)
+from policies import DiscretePolicy, MujocoPolicy  # noqa: E402  (reference)
+from worker import Agent, Worker  # noqa: E402  (reference)
+from learner import FiniteDifferences, FDReturn, FDState  # noqa: E402  (reference)
+from dsgd import DSGD  # noqa: E402  (reference)
+from utils import AdaptiveOmega, math_helpers  # noqa: E402  (reference)
+from strategy import StrategyHandler  # noqa: E402  (reference)
+import run_sequential  # noqa: E402  (reference)
+
+from oracle.envs import SyntheticEnv  # noqa: E402  (build-defined env; ours)
+
+
+def _trap_env():
+    """Reference trap env constructed with opt_id=None so it never writes action logs."""
+    from custom_envs.simple_trap_env import Environment
+    cwd = os.getcwd()
+    os.chdir(REF)                      # map.txt is loaded by a relative path (read only)
+    try:
+        env = Environment(opt_id=None)
+    finally:
+        os.chdir(cwd)
+    return env
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print("wrote", os.path.relpath(path, REPO), sum(np.asarray(v).nbytes for v in arrays.values()), "bytes")
+
+
+def make_policy(kind, n_in, n_act, seed):
+    torch.manual_seed(seed)
+    if kind == "discrete":
+        return DiscretePolicy(n_in, n_act, seed=seed)
+    return MujocoPolicy(n_in, n_act, seed=seed)
+
+
+SHAPES = {"trap": ("discrete", 2, 9), "cartpole": ("discrete", 4, 2), "cheetah": ("mujoco", 17, 6)}
+
+
+# ------------------------------------------------------------------------------------------
+def g1_noise():
+    out = {}
+    for seed in (124, 7):
+        for P in (5197, 4874, 6092):
+            t = SharedNoiseTable(2 ** 22, P, random_seed=seed)
+            idx = np.array([int(t.sample()[0]) for _ in range(64)], dtype=np.int64)
+            key = "s%d_p%d" % (seed, P)
+            out[key + "_idx"] = idx
+            out[key + "_spot"] = t._table[[0, 1, 2, 1000, 2 ** 21, 2 ** 22 - 1]]
+            out[key + "_sha"] = np.array(sha(t._table))
+    t = SharedNoiseTable(25_000_000, 6092, random_seed=124)
+    out["big_idx"] = np.array([int(t.sample()[0]) for _ in range(256)], dtype=np.int64)
+    out["big_sha"] = np.array(sha(t._table))
+    out["big_spot"] = t._table[[0, 12_345_678, 24_999_999]]
+    save("g1_noise.npz", **out)
+
+
+def g2_perturb():
+    out = {}
+    for name, (kind, n_in, n_act) in SHAPES.items():
+        for seed in (124, 123):
+            pol = make_policy(kind, n_in, n_act, seed)
+            out["%s_s%d_theta" % (name, seed)] = pol.get_trainable_flat().copy()
+        pol = make_policy(kind, n_in, n_act, 124)
+        P = pol.num_params
+        table = SharedNoiseTable(2 ** 22, P, random_seed=124)
+        flat = pol.get_trainable_flat()
+        idx, new = [], []
+        for _ in range(4):
+            enc, noise = table.sample()
+            idx.append(int(enc))
+            new.append(flat + 0.02 * noise)          # worker/worker.py:28
+        out[name + "_idx"] = np.array(idx, dtype=np.int64)
+        out[name + "_perturbed"] = np.stack(new).astype(np.float32)
+    save("g2_perturb.npz", **out)
+
+
+def g3_forward():
+    out = {}
+    obs_rng = np.random.RandomState(5)
+    for name, (kind, n_in, n_act) in SHAPES.items():
+        pol = make_policy(kind, n_in, n_act, 124)
+        P = pol.num_params
+        table = SharedNoiseTable(2 ** 22, P, random_seed=124)
+        idx = int(table.sample()[0])
+        params = (table.decode(idx) * 0.1).astype(np.float32)
+        pol.set_trainable_flat(params)
+        x = obs_rng.randn(8, n_in).astype(np.float32)
+        out[name + "_idx"] = np.array(idx)
+        out[name + "_x"] = x
+        with torch.no_grad():
+            if kind == "discrete":
+                out[name + "_probs"] = pol.forward(x).numpy()
+                out[name + "_entropy"] = np.array(pol.get_entropy(x))
+                out[name + "_argmax"] = np.array([pol.get_action(x[i], deterministic=True) for i in range(8)])
+                # non-trivial BN running stats via the reference's own compute_vbn (policy.py:31-34)
+                buf = obs_rng.randn(32, n_in).astype(np.float32) * 2 + 0.5
+                pol.compute_vbn(buf)
+                bns = [m for m in pol.model if isinstance(m, torch.nn.BatchNorm1d)]
+                for i, m in enumerate(bns):
+                    out["%s_vbn_rm%d" % (name, i)] = m.running_mean.numpy().copy()
+                    out["%s_vbn_rv%d" % (name, i)] = m.running_var.numpy().copy()
+                out[name + "_vbn_buf"] = buf
+                out[name + "_vbn_probs"] = pol.forward(x).numpy()
+            else:
+                mean, std = pol.forward(x)
+                out[name + "_mean"] = mean.numpy()
+                out[name + "_std"] = std.numpy()
+                out[name + "_entropy"] = np.array(pol.get_entropy(x))
+                out[name + "_det_action"] = np.array([pol.get_action(x[i], deterministic=True) for i in range(8)])
+    save("g3_forward.npz", **out)
+
+
+def _fd_case(kind, n_in, n_act, N, omega_value, seed):
+    pol = make_policy(kind, n_in, n_act, 124)
+    P = pol.num_params
+    opt = DSGD(pol.parameters(), lr=0.01)
+    omega = AdaptiveOmega()
+    omega.omega = omega_value
+    table = SharedNoiseTable(2 ** 22, P, random_seed=124)
+    learner = FiniteDifferences(pol, opt, omega, table, noise_std=0.02, batch_size=N,
+                                max_delayed_return=10)
+    theta0 = pol.get_trainable_flat().copy()
+    rng = np.random.RandomState(seed)
+    rewards = rng.randn(N) * 3 + 1
+    batch, idx = [], []
+    for i in range(N):
+        r = FDReturn()
+        r.epoch = 0
+        r.encoded_noise = table.sample()[0]
+        r.reward = float(rewards[i])
+        batch.append(r)
+        idx.append(int(r.encoded_noise))
+    upd = learner.step(batch, 0.25, 0, 0)
+    g = learner.gradient_memory.copy()
+    theta1 = pol.get_trainable_flat().copy()
+    # second step: half the returns are one epoch stale -> lambda drift (finite_differences.py:88-89)
+    rewards2 = rng.randn(N)
+    batch2, idx2, ep2 = [], [], []
+    for i in range(N):
+        r = FDReturn()
+        r.epoch = 0 if i % 2 else 1
+        r.encoded_noise = table.sample()[0]
+        r.reward = float(rewards2[i])
+        batch2.append(r)
+        idx2.append(int(r.encoded_noise))
+        ep2.append(r.epoch)
+    upd2 = learner.step(batch2, -0.5, 0, 0)
+    return dict(theta0=theta0, idx=np.array(idx), rewards=rewards, update=np.array(upd), g=g, theta1=theta1,
+                idx2=np.array(idx2), ep2=np.array(ep2), rewards2=rewards2, update2=np.array(upd2),
+                g2=learner.gradient_memory.copy(), theta2=pol.get_trainable_flat().copy(),
+                omega=np.array(omega_value))
+
+
+def g4_fd_step():
+    out = {}
+    for name, N, om in (("cheetah", 16, 0.0), ("cheetah", 64, 0.5), ("trap", 16, 0.25)):
+        kind, n_in, n_act = SHAPES[name]
+        case = _fd_case(kind, n_in, n_act, N, om, seed=N)
+        for k, v in case.items():
+            out["%s_n%d_%s" % (name, N, k)] = v
+    save("g4_fd_step.npz", **out)
+
+
+def g5_trap():
+    env = _trap_env()
+    out = {"walkable": np.array([[n.walkable for n in row] for row in env.map.nodes], dtype=bool)}
+    rets, cols, rows = [], [], []
+    for a in range(9):
+        env.reset()
+        tot, done, steps = 0, False, 0
+        while not done:
+            _, r, done, _ = env.step(a)
+            tot += r
+            steps += 1
+        rets.append(tot)
+        cols.append(env.current_node.x // 7)
+        rows.append(env.current_node.y // 7)
+        assert steps == 201
+    out["const_return"] = np.array(rets)
+    out["const_col"] = np.array(cols)
+    out["const_row"] = np.array(rows)
+    out["start_obs"] = env.reset()
+    # deterministic DiscretePolicy episodes through the reference Agent (worker/agent.py:20-71)
+    for seed in (124, 1, 2):
+        pol = make_policy("discrete", 2, 9, seed)
+        agent = Agent(pol, env, random_seed=seed)
+        rew, ent, steps = agent.collect_return(eval_run=True)
+        out["det_s%d" % seed] = np.array([rew, ent, steps])
+        out["det_s%d_theta" % seed] = pol.get_trainable_flat().copy()
+    save("g5_trap.npz", **out)
+    np.savez_compressed(os.path.join(HERE, "trap_map.npz"), walkable=out["walkable"])
+
+
+class _InjectedDiscrete(object):
+    """Replaces DiscretePolicy.get_action: inverse CDF at a uniform from a fixed RandomState."""
+
+    def __init__(self, seed):
+        self.rng = np.random.RandomState(seed)
+
+    def __call__(self, policy, x, deterministic=False):
+        probs = policy.forward(x)
+        if deterministic:
+            return probs.argmax().item()
+        from oracle.policies import categorical_inverse_cdf   # ours: the rule being pinned
+        return categorical_inverse_cdf(probs[0].numpy(), np.float32(self.rng.uniform()))
+
+
+class _InjectedNormal(object):
+    def __init__(self, seed):
+        self.rng = np.random.RandomState(seed)
+
+    def __call__(self, policy, x, deterministic=False):
+        mean, std = policy.forward(x)
+        if deterministic:
+            return mean.flatten().tolist()
+        z = torch.as_tensor(self.rng.randn(mean.shape[-1]).astype(np.float32))
+        return (mean + std * z).flatten().tolist()
+
+
+def g6_runner_trap():
+    """Patched SequentialRunner on the trap env, 2 epochs x batch 16."""
+    _ENV_FACTORY["SimpleTrapEnv-v0"] = _trap_env
+    inj = _InjectedDiscrete(777)
+    orig_get_action = DiscretePolicy.get_action
+    DiscretePolicy.get_action = lambda self, x, deterministic=False: inj(self, x, deterministic)
+    orig_rng_src = run_sequential.RNGNoiseSource
+    run_sequential.RNGNoiseSource = lambda n, random_seed=123: SharedNoiseTable(2 ** 22, n, random_seed)
+    orig_update = Worker.update
+
+    def update(self, state):                                 # SURVEY 8c patch (1)
+        self.policy.set_trainable_flat(state.policy_params)
+        self.epoch = state.epoch
+        if state.obs_stats is not None:
+            self.fixed_obs_stats.deserialize(state.obs_stats)
+    Worker.update = update
+
+    idx_log = []
+    orig_sample = SharedNoiseTable.sample
+
+    def sample(self):
+        enc, noise = orig_sample(self)
+        idx_log.append(int(enc))
+        return enc, noise
+    SharedNoiseTable.sample = sample
+    step_log = []
+    orig_step = FiniteDifferences.step
+
+    def step(self, batch, pr, pn, pe):
+        step_log.append(dict(rewards=[r.reward for r in batch], idx=[int(r.encoded_noise) for r in batch],
+                             policy_reward=pr, omega=self.omega.omega))
+        return orig_step(self, batch, pr, pn, pe)
+    FiniteDifferences.step = step
+    try:
+        runner = run_sequential.SequentialRunner(env_id="SimpleTrapEnv-v0", batch_size=16, random_seed=124,
+                                                 zeta_size=4, max_strategy_history_size=4)
+        runner.learner.noise_std = 0.02                      # SURVEY 8c patch (2)
+        theta0 = runner.policy.get_trainable_flat().copy()
+        with contextlib.redirect_stdout(io.StringIO()) as buf:
+            runner.train(2)
+        report = buf.getvalue()
+        theta = runner.policy.get_trainable_flat().copy()
+        out = dict(theta0=theta0, theta_final=theta, sample_idx=np.array(idx_log),
+                   cum_steps=np.array(runner.agent.cumulative_timesteps),
+                   policy_reward=np.array(runner.policy_reward))
+        for e, s in enumerate(step_log):
+            out["e%d_rewards" % e] = np.array(s["rewards"])
+            out["e%d_idx" % e] = np.array(s["idx"])
+            out["e%d_policy_reward" % e] = np.array(s["policy_reward"])
+            out["e%d_omega" % e] = np.array(s["omega"])
+        mags = [float(l.split()[-1]) for l in report.splitlines() if l.startswith("Update Magnitude")]
+        out["update_magnitude_printed"] = np.array(mags)
+        save("g6_runner_trap.npz", **out)
+    finally:
+        DiscretePolicy.get_action = orig_get_action
+        run_sequential.RNGNoiseSource = orig_rng_src
+        Worker.update = orig_update
+        SharedNoiseTable.sample = orig_sample
+        FiniteDifferences.step = orig_step
+
+
+def g7_worker_synthetic():
+    """Reference Worker/Agent on the build's synthetic envs with injected noise (episode loop)."""
+    out = {}
+    for name, (kind, n_in, n_act), T in (("cheetah", SHAPES["cheetah"], 60), ("cartpole", SHAPES["cartpole"], 50)):
+        env = SyntheticEnv(n_in, n_act, kind == "discrete", T, env_seed=0)
+        pol = make_policy(kind, n_in, n_act, 124)
+        P = pol.num_params
+        cls = DiscretePolicy if kind == "discrete" else MujocoPolicy
+        inj = _InjectedDiscrete(31) if kind == "discrete" else _InjectedNormal(31)
+        orig = cls.get_action
+        cls.get_action = lambda self, x, deterministic=False: inj(self, x, deterministic)
+        try:
+            table = SharedNoiseTable(2 ** 22, P, random_seed=124)
+            agent = Agent(pol, env, random_seed=11)
+            handler = StrategyHandler(pol, math_helpers.categorical_tvd)
+            worker = Worker(pol, agent, table, handler, sigma=0.02, eval_prob=0.25, random_seed=3)
+            rets = worker.collect_returns(8)
+        finally:
+            cls.get_action = orig
+        out[name + "_theta"] = pol.get_trainable_flat().copy()
+        out[name + "_reward"] = np.array([r.reward for r in rets])
+        out[name + "_entropy"] = np.array([r.entropy for r in rets])
+        out[name + "_timesteps"] = np.array([r.timesteps for r in rets])
+        out[name + "_is_eval"] = np.array([r.is_eval for r in rets])
+        out[name + "_idx"] = np.array([int(r.encoded_noise) for r in rets])
+        out[name + "_T"] = np.array(T)
+    save("g7_worker_synthetic.npz", **out)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(1)
+    g1_noise()
+    g2_perturb()
+    g3_forward()
+    g4_fd_step()
+    g5_trap()
+    g6_runner_trap()
+    g7_worker_synthetic()
