@@ -1,0 +1,225 @@
+"""bench.py -- FD perturbation-evaluation hot path on MI355X (BASELINE.json metric).
+
+One "step" = one full FD step of BASELINE config 3 per GPU:
+  host index draw (SharedNoiseTable stream) -> one fdr_rollout launch over 4096 lanes
+  (2048 directions x {+eps, -eps}, HalfCheetah-shaped MujocoPolicy(17, 6), T = 1000 steps)
+  -> [all-gather rewards] -> fdr_fd_weights -> fdr_fd_grad -> [RCCL all-reduce of g] -> fdr_dsgd_step.
+Per-GPU work is fixed as N grows ("weak" scaling): the global batch is 4096 * N perturbations.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Prints ONE JSON line on rank 0.  The cpu_baseline leg (rank 0, N = 1) times the oracle's
+reference-shaped per-lane CPU loop (torch CPU forward per step, as worker/agent.py does) on a
+bounded sample, BEFORE the GPU is initialised.
+"""
+import argparse
+import json
+import multiprocessing
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "dfd-starter_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "env steps/sec (whole node) + sec/FD-grad-step, 4096 antithetic perturbations"
+FP32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 vector = FP32 matrix peak
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    # name: (policy kind, n_in, n_act, env shape name, episode_len)
+    "halfcheetah": ("mujoco", 17, 6, "halfcheetah", 1000),
+    "cartpole": ("discrete", 4, 2, "cartpole", 500),
+}
+
+
+def lane_step_flops(kind, n_in, n_act):
+    """Algorithmic FLOPs per (lane, env step): 2 x MACs of the policy MLP + the env dynamics."""
+    nout = n_act if kind == "discrete" else 2 * n_act
+    policy = n_in * 64 + 64 * 64 + 64 * nout
+    env = n_in * n_in + (0 if kind == "discrete" else n_in * n_act)
+    return 2 * (policy + env)
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU baseline (oracle restatement of the reference's per-lane loop), forked before any GPU use
+# ------------------------------------------------------------------------------------------------
+def _cpu_worker(args):
+    wid, seconds, cfg = args
+    import numpy as np
+    import torch
+    torch.set_num_threads(1)
+    from oracle import agent, envs, noise, policies
+    kind, n_in, n_act, _, T = CONFIGS[cfg]
+    torch.manual_seed(124)
+    pol = policies.TorchPolicy(kind, n_in, n_act, seed=124)
+    theta = pol.get_flat()
+    tab = noise.NoiseTable(1 << 22, theta.size, 124 + wid)
+    env = envs.SyntheticEnv(n_in, n_act, kind == "discrete", T)
+    rng = np.random.RandomState(wid)
+    steps, t0, obs = 0, time.perf_counter(), env.reset()
+    while time.perf_counter() - t0 < seconds:
+        idx = int(tab.sample_indices(1)[0])
+        sg = 1 if steps % 2 == 0 else -1
+        pol.set_flat(noise.perturb(theta, tab.table, [idx], [sg], 0.02)[0])
+        nf = (lambda t: np.float32(rng.uniform())) if kind == "discrete" else \
+             (lambda t: rng.randn(n_act).astype(np.float32))
+        _, _, n, obs = agent.collect_return(pol, env, obs, False, nf, lambda: rng.choice((-1e-12, 1e-12)))
+        steps += n
+    return steps, time.perf_counter() - t0
+
+
+def cpu_baseline(cfg, seconds, cores):
+    ctx = multiprocessing.get_context("fork")
+    with ctx.Pool(cores) as pool:
+        res = pool.map(_cpu_worker, [(i, seconds, cfg) for i in range(cores)])
+    steps = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return steps / wall, steps
+
+
+# ------------------------------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="halfcheetah", choices=list(CONFIGS))
+    ap.add_argument("--perturbations", type=int, default=4096, help="antithetic lanes per GPU")
+    ap.add_argument("--episode-len", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    kind, n_in, n_act, env_name, T = CONFIGS[args.config]
+    if args.episode_len:
+        T = args.episode_len
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cores = max(1, min(16, os.cpu_count() or 1))
+        v, steps = cpu_baseline(args.config, args.cpu_seconds, cores)
+        cpu = {"value": round(v, 1), "unit": "env steps/s", "cores": cores, "kind": "port",
+               "sample": "%d processes x %.0f s of whole episodes (T=%d, +/-eps perturbed %s policy, torch CPU "
+                         "forward per step, 1 thread each): %d env steps" % (cores, args.cpu_seconds, T, kind, steps)}
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dsgd import DSGD
+    from envs import SyntheticEnv
+    from learner import FiniteDifferences
+    from policies import DiscretePolicy, MujocoPolicy
+    from utils import AdaptiveOmega, SharedNoiseTable
+    from worker import Agent, Worker
+
+    torch.manual_seed(124)
+    Pol = DiscretePolicy if kind == "discrete" else MujocoPolicy
+    policy = Pol(n_in, n_act, seed=124, device=dev)
+    env = SyntheticEnv.named(env_name, device=dev, episode_len=T)
+    table = SharedNoiseTable(25_000_000, policy.num_params, random_seed=124)
+    table.device_table(dev)
+    agent = Agent(policy, env, random_seed=124 + rank)
+    worker = Worker(policy, agent, table, None, sigma=0.02, random_seed=124)
+    omega = AdaptiveOmega()
+    learner = FiniteDifferences(policy, DSGD(policy.parameters(), lr=0.01), omega, table, noise_std=0.02)
+
+    L = args.perturbations
+    n_dirs_global = (L // 2) * world
+    lane_range = (rank * L, (rank + 1) * L)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    roll_ms = []
+
+    def fd_step(timed):
+        if timed:
+            ev0.record()
+        batch = worker.evaluate(n_dirs_global, antithetic=True, lane_range=lane_range)
+        if timed:
+            ev1.record()
+        out = learner.step_async(batch, 0.0, 0.0, 0.0)
+        return out, batch
+
+    for _ in range(args.warmup):
+        out, _ = fd_step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out, batch = fd_step(True)
+        # the rollout brackets are read after the loop; keep one pair per step
+        roll_ms.append((ev0, ev1))
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    rollout_ms = float(np.mean([a.elapsed_time(b) for a, b in roll_ms]))
+    if world > 1:
+        t = torch.tensor([elapsed, rollout_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, rollout_ms = t.tolist()
+    upd, gnorm = out.tolist()
+    assert gnorm > 0 and np.isfinite(upd)
+
+    lane_steps = L * T * world * args.steps
+    value = lane_steps / elapsed
+    flops = lane_step_flops(kind, n_in, n_act) * L * T
+    achieved_tf = flops / (rollout_ms * 1e-3) / 1e12
+    traffic = None
+    pmc = os.path.join(REPO, "profiles", "pmc_rollout_%s.json" % args.config)
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "env steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "sec_per_fd_step": round(elapsed / args.steps, 6),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": "BASELINE config 3: HalfCheetah-shaped synthetic env (obs 17, act 6), "
+                               "MujocoPolicy(17,6) P=%d, %d antithetic perturbations per GPU (%d directions x +/-), "
+                               "T=%d fixed-length episodes, full FD step (rollout + weights + gradient + DSGD)"
+                               % (policy.num_params, L, L // 2, T) if args.config == "halfcheetah" else args.config,
+                   "perturbations_per_gpu": L, "global_perturbations": L * world, "episode_len": T,
+                   "n_params": policy.num_params, "parallelism": "dp%d" % world},
+        "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "kernel": "rollout_kernel<17,6,mujoco,synth>", "rollout_ms": round(rollout_ms, 4),
+                     "flop_per_lane_step": lane_step_flops(kind, n_in, n_act),
+                     "note": "fp32 VALU/matrix peak; theta' is VGPR-resident for the whole episode, so the "
+                             "kernel is compute-bound (DESIGN.md 'Roofline')"},
+        "cpu_baseline": cpu,
+        "update_norm": upd,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,230 @@
+// fdr_api.hip -- the extern "C" boundary (include/fdr.h): argument validation, error state,
+// descriptor translation, kernel dispatch.  No allocation, no host sync, no copies.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "fdr_internal.h"
+
+namespace fdr {
+
+static thread_local std::string g_err;
+
+int set_error(int code, const char* msg) {
+  g_err = msg ? msg : "";
+  return code;
+}
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return FDR_ERR_HIP;
+  }
+  return FDR_OK;
+}
+
+int launch_perturb(const float* theta, int64_t P, const float* table, int64_t table_size,
+                   const int64_t* idx, const int8_t* sign, int n, float sigma, float* out,
+                   hipStream_t stream);
+int launch_fd_weights(const double* r_all, int n_all, double pr, int lo, int n_local,
+                      const int8_t* sign, const double* n2, int lpd, float sigma, double* coef,
+                      hipStream_t stream);
+int64_t grad_workspace_bytes(int n_dirs, int64_t P);
+int launch_fd_grad(const float* table, int64_t table_size, const int64_t* idx, const double* coef,
+                   int n_dirs, int64_t P, double* g, void* ws, int64_t ws_bytes, hipStream_t stream);
+int64_t dsgd_workspace_bytes(int64_t P);
+int launch_dsgd(float* theta, const double* g, int64_t P, double lr, double lr_scale, double* out,
+                void* ws, int64_t ws_bytes, hipStream_t stream);
+
+static int policy_key(const fdr_policy_desc* p, PolicyKey* k) {
+  if (!p) return set_error(FDR_ERR_INVALID, "policy desc is NULL");
+  if (p->hidden != kHidden) return set_error(FDR_ERR_UNSUPPORTED, "hidden width must be 64");
+  if (p->kind != FDR_POLICY_DISCRETE && p->kind != FDR_POLICY_MUJOCO)
+    return set_error(FDR_ERR_INVALID, "unknown policy kind");
+  k->n_in = p->n_in;
+  k->n_act = p->n_act;
+  k->discrete = p->kind == FDR_POLICY_DISCRETE;
+  k->n_params = p->n_params;
+  return FDR_OK;
+}
+
+static int lanes_args(const fdr_lanes_desc* l, int n_lanes, int64_t P, LanesArgs* out) {
+  if (!l || !l->base) return set_error(FDR_ERR_INVALID, "lanes desc / base is NULL");
+  if (n_lanes < 0) return set_error(FDR_ERR_INVALID, "n_lanes < 0");
+  if (l->table) {
+    if (!l->idx) return set_error(FDR_ERR_INVALID, "table given without idx");
+    if (l->table_size < P) return set_error(FDR_ERR_INVALID, "table smaller than n_params");
+  }
+  out->base = l->base;
+  out->base_stride = l->base_stride;
+  out->table = l->table;
+  out->max_idx = l->table ? l->table_size - P : 0;
+  out->idx = l->idx;
+  out->sign = l->sign;
+  out->sigma = l->sigma;
+  out->deterministic = l->deterministic;
+  return FDR_OK;
+}
+
+}  // namespace fdr
+
+using namespace fdr;
+
+struct fdr_ctx {
+  int device;
+};
+
+extern "C" {
+
+const char* fdr_version(void) { return "fdr 0.1 gfx950"; }
+const char* fdr_last_error(void) { return g_err.c_str(); }
+
+int fdr_ctx_create(int device, fdr_ctx** out) {
+  if (!out) return set_error(FDR_ERR_INVALID, "out is NULL");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+    return set_error(FDR_ERR_HIP, "no such HIP device");
+  *out = new fdr_ctx{device};
+  return FDR_OK;
+}
+
+int fdr_ctx_destroy(fdr_ctx* ctx) {
+  delete ctx;
+  return FDR_OK;
+}
+
+int fdr_ctx_device(const fdr_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+int fdr_perturb(fdr_ctx* ctx, const float* theta, int64_t n_params, const float* table,
+                int64_t table_size, const int64_t* idx, const int8_t* sign, int32_t n_lanes,
+                float sigma, float* out, fdr_stream stream) {
+  (void)ctx;
+  if (!theta || !table || !idx || !out) return set_error(FDR_ERR_INVALID, "NULL pointer");
+  if (n_params <= 0 || table_size < n_params || n_lanes < 0)
+    return set_error(FDR_ERR_INVALID, "bad sizes");
+  if (n_lanes == 0) return FDR_OK;
+  return launch_perturb(theta, n_params, table, table_size, idx, sign, n_lanes, sigma, out,
+                        (hipStream_t)stream);
+}
+
+int fdr_policy_forward(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_lanes_desc* lanes,
+                       int32_t n_lanes, const float* x, float* out0, float* out1,
+                       fdr_stream stream) {
+  (void)ctx;
+  PolicyKey k;
+  int rc = policy_key(policy, &k);
+  if (rc) return rc;
+  LanesArgs la;
+  rc = lanes_args(lanes, n_lanes, k.n_params, &la);
+  if (rc) return rc;
+  if (!x || !out0 || (!k.discrete && !out1)) return set_error(FDR_ERR_INVALID, "NULL x/out");
+  if (n_lanes == 0) return FDR_OK;
+  return launch_policy_forward(k, la, n_lanes, policy->bn_mean, policy->bn_var, x, out0, out1,
+                               (hipStream_t)stream);
+}
+
+int fdr_rollout(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc* env,
+                const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
+                const float* obs_mean, const float* obs_std, double* ret, double* ent,
+                int32_t* steps, double* norm2, fdr_stream stream) {
+  (void)ctx;
+  PolicyKey k;
+  int rc = policy_key(policy, &k);
+  if (rc) return rc;
+  RolloutArgs a;
+  std::memset(&a, 0, sizeof(a));
+  rc = lanes_args(lanes, n_lanes, k.n_params, &a.lanes);
+  if (rc) return rc;
+  if (!env) return set_error(FDR_ERR_INVALID, "env desc is NULL");
+  if (!ret || !ent || !steps) return set_error(FDR_ERR_INVALID, "NULL output");
+  if ((obs_mean == nullptr) != (obs_std == nullptr))
+    return set_error(FDR_ERR_INVALID, "obs_mean and obs_std must both be given or both NULL");
+  if (env->episode_len <= 0 || env->episode_len >= (1 << 28))
+    return set_error(FDR_ERR_INVALID, "episode_len out of range");
+  if (env->obs_dim != k.n_in || env->act_dim != k.n_act)
+    return set_error(FDR_ERR_INVALID, "env obs/act dims do not match the policy");
+  if (env->kind == FDR_ENV_SYNTH) {
+    if (!env->M || !env->K || !env->s0) return set_error(FDR_ERR_INVALID, "synthetic env needs M, K, s0");
+  } else if (env->kind == FDR_ENV_TRAP) {
+    if (!env->walkable || env->map_w <= 0 || env->map_h <= 0)
+      return set_error(FDR_ERR_INVALID, "trap env needs the walkable map");
+    if (!k.discrete || k.n_in != 2 || k.n_act != 9)
+      return set_error(FDR_ERR_INVALID, "trap env needs a DiscretePolicy(2, 9)");
+  } else {
+    return set_error(FDR_ERR_INVALID, "unknown env kind");
+  }
+  if (n_lanes == 0) return FDR_OK;
+  a.n_lanes = n_lanes;
+  a.T = env->episode_len;
+  a.key = mix64(seed);
+  a.jiggle = jiggle;
+  a.bn_mean = policy->bn_mean;
+  a.bn_var = policy->bn_var;
+  a.obs_mean = obs_mean;
+  a.obs_std = obs_std;
+  a.M = env->M;
+  a.K = env->K;
+  a.s0 = env->s0;
+  a.walkable = env->walkable;
+  a.map_w = env->map_w;
+  a.map_h = env->map_h;
+  // environment.py:21 -> tile_map.get_node(width*r//2, height*r//2) with r = 7
+  a.trap_start_col = (env->map_w * 7 / 2) / 7;
+  a.trap_start_row = (env->map_h * 7 / 2) / 7;
+  a.ret = ret;
+  a.ent = ent;
+  a.steps = steps;
+  a.norm2 = norm2;
+  return launch_rollout(k, env->kind, a, (hipStream_t)stream);
+}
+
+int fdr_fd_weights(fdr_ctx* ctx, const double* rewards_all, int32_t n_all, double policy_reward,
+                   int32_t lane_lo, int32_t n_local, const int8_t* sign_local,
+                   const double* norm2_local, int32_t lanes_per_dir, float sigma, double* coef,
+                   fdr_stream stream) {
+  (void)ctx;
+  if (!rewards_all || !sign_local || !norm2_local || !coef)
+    return set_error(FDR_ERR_INVALID, "NULL pointer");
+  if (n_all <= 0 || lane_lo < 0 || n_local < 0 || lane_lo + n_local > n_all)
+    return set_error(FDR_ERR_INVALID, "bad lane range");
+  if (lanes_per_dir < 1 || n_local % lanes_per_dir != 0)
+    return set_error(FDR_ERR_INVALID, "n_local must be a multiple of lanes_per_dir");
+  return launch_fd_weights(rewards_all, n_all, policy_reward, lane_lo, n_local, sign_local,
+                           norm2_local, lanes_per_dir, sigma, coef, (hipStream_t)stream);
+}
+
+int64_t fdr_fd_grad_workspace_bytes(int32_t n_dirs, int64_t n_params) {
+  return grad_workspace_bytes(n_dirs, n_params);
+}
+
+int fdr_fd_grad(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx,
+                const double* coef, int32_t n_dirs, int64_t n_params, double* g, void* workspace,
+                int64_t workspace_bytes, fdr_stream stream) {
+  (void)ctx;
+  if (!table || !g || n_params <= 0 || table_size < n_params || n_dirs < 0)
+    return set_error(FDR_ERR_INVALID, "bad arguments");
+  if (n_dirs == 0) {
+    const hipError_t e = hipMemsetAsync(g, 0, n_params * sizeof(double), (hipStream_t)stream);
+    return e == hipSuccess ? FDR_OK : set_error(FDR_ERR_HIP, hipGetErrorString(e));
+  }
+  if (!idx || !coef) return set_error(FDR_ERR_INVALID, "NULL idx/coef");
+  return launch_fd_grad(table, table_size, idx, coef, n_dirs, n_params, g, workspace,
+                        workspace_bytes, (hipStream_t)stream);
+}
+
+int64_t fdr_dsgd_workspace_bytes(int64_t n_params) { return dsgd_workspace_bytes(n_params); }
+
+int fdr_dsgd_step(fdr_ctx* ctx, float* theta, const double* g, int64_t n_params, double lr,
+                  double lr_scale, double* out, void* workspace, int64_t workspace_bytes,
+                  fdr_stream stream) {
+  (void)ctx;
+  if (!theta || !g || !out || n_params <= 0) return set_error(FDR_ERR_INVALID, "bad arguments");
+  return launch_dsgd(theta, g, n_params, lr, lr_scale, out, workspace, workspace_bytes,
+                     (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,92 @@
+// Shared device helpers for the FD engine kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fdr.h"
+
+namespace fdr {
+
+constexpr int kWave = 64;
+constexpr int kHidden = 64;  // policies/discrete.py:35-36, policies/mujoco.py:33-34
+
+// ---------------------------------------------------------------------------------------------
+// Counter random stream (oracle/rng.py restates it for the checker; DESIGN.md "Random streams")
+// ---------------------------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t hash_ctr(uint64_t key, uint64_t lane, uint64_t t, uint64_t k) {
+  const uint64_t c = (lane << 32) | (t << 4) | k;
+  return mix64(key + c * 0x9E3779B97F4A7C15ull);
+}
+constexpr uint64_t kJiggleT = (1ull << 28) - 1;
+
+__device__ __forceinline__ float uniform24(uint64_t h) {
+  return (float)(uint32_t)(h >> 40) * 0x1p-24f;
+}
+// Box-Muller on the hardware transcendental units: v_log_f32 is log2, v_cos_f32 takes revolutions,
+// so cos(2*pi*u2) needs no range reduction.  Agrees with oracle/rng.py to a few ulp.
+__device__ __forceinline__ float normal_bm(uint64_t h) {
+  const float u1 = (float)((uint32_t)(h >> 40) + 1u) * 0x1p-24f;
+  const float u2 = (float)((uint32_t)(h >> 16) & 0xFFFFFFu) * 0x1p-24f;
+  const float r = __builtin_sqrtf(-1.38629436111989061f * __builtin_amdgcn_logf(u1));  // -2 ln u1
+  return r * __builtin_amdgcn_cosf(u2);
+}
+
+// tanh(x) = 1 - 2 / (1 + e^{2x}) on v_exp_f32 / v_rcp_f32 (abs error ~3e-7; saturates to +-1)
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * 2.88539008177792681f);  // 2 * log2(e)
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Wave-scope LDS ordering: LDS ops of one wave complete in order, so a wave that only talks to
+// itself through LDS needs a compiler fence, not an s_barrier (no cross-wave hand-off here).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
+  return v;
+}
+
+// theta'[p] = fl32(base[p] +/- fl32(sigma * eps[p]))  -- no contraction (bit-exact with numpy).
+struct ParamSrc {
+  const float* base;
+  const float* eps;  // table + idx, or nullptr
+  float sigma;
+  int sgn;           // +1 / -1 / 0
+  double n2;         // running sum of fl32(sigma*eps)^2 over the elements this thread loaded
+
+  __device__ __forceinline__ float get(int64_t p) {
+#pragma clang fp contract(off)
+    float t = base[p];
+    if (sgn != 0) {
+      const float st = sigma * eps[p];
+      n2 += (double)st * (double)st;
+      t = sgn > 0 ? t + st : t - st;
+    }
+    return t;
+  }
+  // same value, but not counted in n2 (an element several threads replicate)
+  __device__ __forceinline__ float get_nocount(int64_t p) const {
+#pragma clang fp contract(off)
+    float t = base[p];
+    if (sgn != 0) {
+      const float st = sigma * eps[p];
+      t = sgn > 0 ? t + st : t - st;
+    }
+    return t;
+  }
+};
+
+}  // namespace fdr

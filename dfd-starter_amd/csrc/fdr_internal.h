@@ -1,0 +1,82 @@
+// Internal (non-ABI) declarations shared by the fdr translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fdr_common.h"
+
+namespace fdr {
+
+int set_error(int code, const char* msg);
+int check_launch(const char* what);
+
+struct PolicyKey {
+  int n_in, n_act;
+  bool discrete;
+  int64_t n_params;
+};
+
+// Device-side view of fdr_lanes_desc (passed by value as a kernel argument).
+struct LanesArgs {
+  const float* base;
+  int64_t base_stride;
+  const float* table;
+  int64_t max_idx;  // table_size - n_params: largest legal offset
+  const int64_t* idx;
+  const int8_t* sign;
+  float sigma;
+  const int8_t* deterministic;
+
+  // A lane whose table offset is out of range is never dereferenced: it runs unperturbed and
+  // reports norm2 = NaN, which poisons the FD step visibly instead of faulting the GPU.
+  __device__ __forceinline__ ParamSrc src(int lane) const {
+    ParamSrc s;
+    s.base = base + (int64_t)lane * base_stride;
+    s.sigma = sigma;
+    s.n2 = 0.0;
+    s.sgn = 0;
+    s.eps = nullptr;
+    if (table != nullptr) {
+      const int64_t off = idx[lane];
+      const int sg = sign ? (int)sign[lane] : 1;
+      if (off < 0 || off > max_idx) {
+        s.n2 = __builtin_nan("");
+      } else if (sg != 0) {
+        s.sgn = sg > 0 ? 1 : -1;
+        s.eps = table + off;
+      }
+    }
+    return s;
+  }
+};
+
+struct RolloutArgs {
+  LanesArgs lanes;
+  int n_lanes;
+  int T;
+  uint64_t key;
+  int jiggle;
+  const float* bn_mean;
+  const float* bn_var;
+  const float* obs_mean;
+  const float* obs_std;
+  // synthetic env
+  const float* M;
+  const float* K;
+  const float* s0;
+  // trap env
+  const uint8_t* walkable;
+  int map_w, map_h, trap_start_col, trap_start_row;
+  // outputs
+  double* ret;
+  double* ent;
+  int32_t* steps;
+  double* norm2;
+};
+
+int launch_policy_forward(const PolicyKey& k, const LanesArgs& lanes, int n_lanes,
+                          const float* bn_mean, const float* bn_var, const float* x, float* out0,
+                          float* out1, hipStream_t stream);
+int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream);
+
+}  // namespace fdr

@@ -1,0 +1,289 @@
+// fdr_learner.hip -- perturbation batch, FD weighting, noise-weighted gradient reduce, DSGD.
+//
+// All of these are HBM-bound integer/byte-indexed streams (DESIGN.md "Learner kernels"):
+//   perturb       reads P floats of theta (L2-resident) + n*P table floats, writes n*P
+//   fd_weights    one workgroup, N rewards (a few KB)
+//   fd_grad       reads n_dirs * P table floats once (dword loads: table offsets are arbitrary,
+//                 so rows are only 4-B aligned), f64 column partial sums per row-chunk, then a
+//                 fixed-order chunk reduce -> deterministic result independent of launch shape
+//   dsgd          two passes over P (norm partials, then update + update-norm partials)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "fdr_common.h"
+#include "fdr_internal.h"
+
+namespace fdr {
+
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void perturb_kernel(const float* __restrict__ theta, int64_t P,
+                                                       const float* __restrict__ table, int64_t max_idx,
+                                                       const int64_t* __restrict__ idx,
+                                                       const int8_t* __restrict__ sign, float sigma,
+                                                       float* __restrict__ out) {
+#pragma clang fp contract(off)
+  const int l = blockIdx.y;
+  const int s = sign ? sign[l] : 1;
+  const int64_t off = idx[l];
+  const bool bad = off < 0 || off > max_idx;  // never dereference an out-of-range offset
+  const float* eps = table + (bad ? 0 : off);
+  float* o = out + (int64_t)l * P;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const float t = theta[p];
+    if (bad) {
+      o[p] = __builtin_nanf("");
+      continue;
+    }
+    const float st = sigma * eps[p];
+    o[p] = s > 0 ? t + st : (s < 0 ? t - st : t);
+  }
+}
+
+int launch_perturb(const float* theta, int64_t P, const float* table, int64_t table_size,
+                   const int64_t* idx, const int8_t* sign, int n, float sigma, float* out,
+                   hipStream_t stream) {
+  const int bx = (int)std::min<int64_t>((P + 255) / 256, 64);
+  hipLaunchKernelGGL(perturb_kernel, dim3(bx, n), dim3(256), 0, stream, theta, P, table,
+                     table_size - P, idx, sign, sigma, out);
+  return check_launch("perturb_kernel");
+}
+
+// ------------------------------------------------------------------------------------------
+// FD weighting: one 1024-thread workgroup.  Deterministic tree sums in f64.
+// ------------------------------------------------------------------------------------------
+__device__ double block_sum_1024(double v, double* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
+  __syncthreads();
+  if (j == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+  return s;
+}
+
+__global__ __launch_bounds__(1024) void fd_weights_kernel(const double* __restrict__ r_all, int n_all,
+                                                           double pr, int lo, int n_local,
+                                                           const int8_t* __restrict__ sign,
+                                                           const double* __restrict__ n2, int lpd,
+                                                           float sigma, double* __restrict__ coef) {
+  __shared__ double red[16];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n_all; i += blockDim.x) s += r_all[i] - pr;
+  const double mean = block_sum_1024(s, red) / (double)n_all;
+  double q = 0.0;
+  for (int i = threadIdx.x; i < n_all; i += blockDim.x) {
+    const double d = (r_all[i] - pr) - mean;
+    q += d * d;
+  }
+  const double var = block_sum_1024(q, red) / (double)n_all;
+  const double sd = sqrt(var);
+  const int n_dirs = n_local / lpd;
+  for (int d = threadIdx.x; d < n_dirs; d += blockDim.x) {
+    double c = 0.0;
+    for (int k = 0; k < lpd; ++k) {
+      const int i = d * lpd + k;
+      const int sg = sign[i];
+      if (sg == 0) continue;
+      const double x = r_all[lo + i] - pr;
+      const double z = sd == 0.0 ? x : (x - mean) / sd;  // utils/math_helpers.py:127-134
+      c += z * (double)sg * (double)sigma / n2[i];
+    }
+    coef[d] = c;
+  }
+}
+
+int launch_fd_weights(const double* r_all, int n_all, double pr, int lo, int n_local,
+                      const int8_t* sign, const double* n2, int lpd, float sigma, double* coef,
+                      hipStream_t stream) {
+  hipLaunchKernelGGL(fd_weights_kernel, dim3(1), dim3(1024), 0, stream, r_all, n_all, pr, lo,
+                     n_local, sign, n2, lpd, sigma, coef);
+  return check_launch("fd_weights_kernel");
+}
+
+// ------------------------------------------------------------------------------------------
+// Noise-weighted gradient: g[p] = sum_d coef[d] * table[idx[d] + p]
+// ------------------------------------------------------------------------------------------
+constexpr int kGradThreads = 256;
+constexpr int kGradCols = 4 * kGradThreads;  // 4 strided columns per thread (coalesced)
+
+struct GradPlan {
+  int col_blocks, rows_per_chunk, n_chunks;
+};
+static GradPlan grad_plan(int n_dirs, int64_t P) {
+  GradPlan g;
+  g.col_blocks = (int)((P + kGradCols - 1) / kGradCols);
+  // aim for ~1024 workgroups (4 per CU), at least 8 rows per chunk
+  int target_chunks = std::max(1, 1024 / std::max(1, g.col_blocks));
+  g.rows_per_chunk = std::max(8, (n_dirs + target_chunks - 1) / target_chunks);
+  g.n_chunks = (n_dirs + g.rows_per_chunk - 1) / g.rows_per_chunk;
+  return g;
+}
+
+int64_t grad_workspace_bytes(int n_dirs, int64_t P) {
+  if (n_dirs <= 0 || P <= 0) return 0;
+  const GradPlan g = grad_plan(n_dirs, P);
+  return (int64_t)g.n_chunks * P * (int64_t)sizeof(double);
+}
+
+__global__ __launch_bounds__(kGradThreads) void fd_grad_partial_kernel(
+    const float* __restrict__ table, int64_t max_idx, const int64_t* __restrict__ idx,
+    const double* __restrict__ coef, int n_dirs, int64_t P, int rows_per_chunk,
+    double* __restrict__ partial) {
+  const int64_t c0 = (int64_t)blockIdx.x * kGradCols + threadIdx.x;
+  const int chunk = blockIdx.y;
+  const int d0 = chunk * rows_per_chunk;
+  const int d1 = min(n_dirs, d0 + rows_per_chunk);
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  bool ok[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) ok[q] = c0 + q * kGradThreads < P;
+  int d = d0;
+  // an out-of-range offset reads row 0 with a NaN weight: the gradient is poisoned, never a fault
+  auto row = [&](int dd, double& c) {
+    const int64_t off = idx[dd];
+    const bool bad = off < 0 || off > max_idx;
+    c = bad ? __builtin_nan("") : coef[dd];
+    return table + (bad ? 0 : off);
+  };
+  for (; d + 2 <= d1; d += 2) {  // two rows in flight per iteration
+    double ca, cb;
+    const float* ra = row(d, ca);
+    const float* rb = row(d + 1, cb);
+    float va[4], vb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      va[q] = ok[q] ? ra[c0 + q * kGradThreads] : 0.f;
+      vb[q] = ok[q] ? rb[c0 + q * kGradThreads] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc[q] = fma(ca, (double)va[q], acc[q]);
+      acc[q] = fma(cb, (double)vb[q], acc[q]);
+    }
+  }
+  for (; d < d1; ++d) {
+    double ca;
+    const float* ra = row(d, ca);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (ok[q]) acc[q] = fma(ca, (double)ra[c0 + q * kGradThreads], acc[q]);
+  }
+  double* out = partial + (int64_t)chunk * P;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (ok[q]) out[c0 + q * kGradThreads] = acc[q];
+}
+
+__global__ __launch_bounds__(256) void fd_grad_reduce_kernel(const double* __restrict__ partial,
+                                                              int n_chunks, int64_t P,
+                                                              double* __restrict__ g) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int c = 0; c < n_chunks; ++c) s += partial[(int64_t)c * P + p];
+    g[p] = s;
+  }
+}
+
+int launch_fd_grad(const float* table, int64_t table_size, const int64_t* idx, const double* coef,
+                   int n_dirs, int64_t P, double* g, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  const GradPlan pl = grad_plan(n_dirs, P);
+  if (ws_bytes < grad_workspace_bytes(n_dirs, P) || ws == nullptr)
+    return set_error(FDR_ERR_WORKSPACE, "fd_grad workspace too small");
+  double* partial = static_cast<double*>(ws);
+  hipLaunchKernelGGL(fd_grad_partial_kernel, dim3(pl.col_blocks, pl.n_chunks), dim3(kGradThreads), 0,
+                     stream, table, table_size - P, idx, coef, n_dirs, P, pl.rows_per_chunk, partial);
+  int rc = check_launch("fd_grad_partial_kernel");
+  if (rc) return rc;
+  const int rb = (int)std::min<int64_t>((P + 255) / 256, 2048);
+  hipLaunchKernelGGL(fd_grad_reduce_kernel, dim3(rb), dim3(256), 0, stream, partial, pl.n_chunks, P, g);
+  return check_launch("fd_grad_reduce_kernel");
+}
+
+// ------------------------------------------------------------------------------------------
+// DSGD (dsgd/dynamic_sgd.py:19-39)
+// ------------------------------------------------------------------------------------------
+constexpr int kDsgdBlocks = 256;
+int64_t dsgd_workspace_bytes(int64_t) { return (int64_t)(2 * kDsgdBlocks + 8) * sizeof(double); }
+
+__device__ double block_sum_256(double v, double* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
+  if (j == 0) red[w] = v;
+  __syncthreads();
+  const double s = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return s;
+}
+
+__global__ __launch_bounds__(256) void dsgd_norm_kernel(const double* __restrict__ g, int64_t P,
+                                                         double* __restrict__ part) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const float gr = (float)(-g[p]);  // set_grad_from_flat casts to f32 (policy.py:68)
+    s += (double)gr * (double)gr;
+  }
+  s = block_sum_256(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void dsgd_apply_kernel(float* __restrict__ theta,
+                                                          const double* __restrict__ g, int64_t P,
+                                                          double lr, double lr_scale,
+                                                          double* __restrict__ part) {
+#pragma clang fp contract(off)
+  __shared__ double red[4];
+  // every block re-reduces the norm partials in the same fixed order -> identical coef
+  double ss = 0.0;
+  for (int i = 0; i < (int)gridDim.x; ++i) ss += part[i];
+  const float norm = (float)sqrt(ss);  // flat_grad.norm().item() (dynamic_sgd.py:27)
+  double s = 0.0;
+  if (norm > 0.f) {
+    const double coef = lr * sqrt((double)P) * lr_scale / (double)norm;  // dynamic_sgd.py:30,51
+    const float c32 = (float)coef;
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P;
+         p += (int64_t)gridDim.x * blockDim.x) {
+      const float gr = (float)(-g[p]);
+      const float old = theta[p];
+      const float nw = old - c32 * gr;  // p.sub_(coef * grad_slice) (dynamic_sgd.py:36)
+      theta[p] = nw;
+      const float dd = old - nw;
+      s += (double)dd * (double)dd;
+    }
+  }
+  s = block_sum_256(s, red);
+  if (threadIdx.x == 0) part[gridDim.x + blockIdx.x] = s;
+  if (blockIdx.x == 0 && threadIdx.x == 0) part[2 * gridDim.x] = (double)norm;
+}
+
+__global__ void dsgd_final_kernel(const double* __restrict__ part, int nb, double* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int i = 0; i < nb; ++i) s += part[nb + i];
+    out[0] = sqrt(s);
+    out[1] = part[2 * nb];
+  }
+}
+
+int launch_dsgd(float* theta, const double* g, int64_t P, double lr, double lr_scale, double* out,
+                void* ws, int64_t ws_bytes, hipStream_t stream) {
+  if (ws == nullptr || ws_bytes < dsgd_workspace_bytes(P))
+    return set_error(FDR_ERR_WORKSPACE, "dsgd workspace too small");
+  double* part = static_cast<double*>(ws);
+  const int nb = (int)std::min<int64_t>(kDsgdBlocks, (P + 255) / 256);
+  hipLaunchKernelGGL(dsgd_norm_kernel, dim3(nb), dim3(256), 0, stream, g, P, part);
+  int rc = check_launch("dsgd_norm_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(dsgd_apply_kernel, dim3(nb), dim3(256), 0, stream, theta, g, P, lr, lr_scale, part);
+  rc = check_launch("dsgd_apply_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(dsgd_final_kernel, dim3(1), dim3(64), 0, stream, part, nb, out);
+  return check_launch("dsgd_final_kernel");
+}
+
+}  // namespace fdr

@@ -1,0 +1,85 @@
+"""ctypes binding of libfdr.so (include/fdr.h) -- the only path to the HIP kernels.
+
+There is deliberately no fallback: if libfdr.so is missing or cannot be loaded, importing this
+module raises, and every product call that needs the GPU fails loudly.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FDR_LIB", os.path.join(_HERE, "libfdr.so"))
+
+FDR_OK, FDR_ERR_INVALID, FDR_ERR_UNSUPPORTED, FDR_ERR_HIP, FDR_ERR_WORKSPACE = 0, 1, 2, 3, 4
+FDR_POLICY_DISCRETE, FDR_POLICY_MUJOCO = 0, 1
+FDR_ENV_SYNTH, FDR_ENV_TRAP = 0, 1
+
+EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy", "fdr_ctx_device",
+           "fdr_perturb", "fdr_policy_forward", "fdr_rollout", "fdr_fd_weights",
+           "fdr_fd_grad_workspace_bytes", "fdr_fd_grad", "fdr_dsgd_workspace_bytes", "fdr_dsgd_step")
+
+
+class FDRError(RuntimeError):
+    pass
+
+
+class PolicyDesc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("n_in", ctypes.c_int32), ("n_act", ctypes.c_int32),
+                ("hidden", ctypes.c_int32), ("n_params", ctypes.c_int64),
+                ("bn_mean", ctypes.c_void_p), ("bn_var", ctypes.c_void_p)]
+
+
+class EnvDesc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32),
+                ("episode_len", ctypes.c_int32), ("M", ctypes.c_void_p), ("K", ctypes.c_void_p),
+                ("s0", ctypes.c_void_p), ("walkable", ctypes.c_void_p), ("map_w", ctypes.c_int32),
+                ("map_h", ctypes.c_int32)]
+
+
+class LanesDesc(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p), ("base_stride", ctypes.c_int64), ("table", ctypes.c_void_p),
+                ("table_size", ctypes.c_int64), ("idx", ctypes.c_void_p), ("sign", ctypes.c_void_p),
+                ("sigma", ctypes.c_float), ("deterministic", ctypes.c_void_p)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libfdr.so not found at %s -- build it with `python -c 'import __graft_entry__ as g; "
+                          "g.build()'` (or `make -C dfd-starter_amd/csrc`)" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    P, I32, I64, F32, F64, U64 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float,
+                                  ctypes.c_double, ctypes.c_uint64)
+    sig = {
+        "fdr_version": (ctypes.c_char_p, []),
+        "fdr_last_error": (ctypes.c_char_p, []),
+        "fdr_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+        "fdr_ctx_destroy": (ctypes.c_int, [P]),
+        "fdr_ctx_device": (ctypes.c_int, [P]),
+        "fdr_perturb": (ctypes.c_int, [P, P, I64, P, I64, P, P, I32, F32, P, P]),
+        "fdr_policy_forward": (ctypes.c_int, [P, ctypes.POINTER(PolicyDesc), ctypes.POINTER(LanesDesc), I32, P,
+                                              P, P, P]),
+        "fdr_rollout": (ctypes.c_int, [P, ctypes.POINTER(PolicyDesc), ctypes.POINTER(EnvDesc),
+                                       ctypes.POINTER(LanesDesc), I32, U64, I32, P, P, P, P, P, P, P]),
+        "fdr_fd_weights": (ctypes.c_int, [P, P, I32, F64, I32, I32, P, P, I32, F32, P, P]),
+        "fdr_fd_grad_workspace_bytes": (I64, [I32, I64]),
+        "fdr_fd_grad": (ctypes.c_int, [P, P, I64, P, P, I32, I64, P, P, I64, P]),
+        "fdr_dsgd_workspace_bytes": (I64, [I64]),
+        "fdr_dsgd_step": (ctypes.c_int, [P, P, P, I64, F64, F64, P, P, I64, P]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc, what=""):
+    if rc != FDR_OK:
+        msg = lib.fdr_last_error().decode(errors="replace")
+        raise FDRError("%s failed (code %d): %s" % (what, rc, msg))
+
+
+def version():
+    return lib.fdr_version().decode()

@@ -1,0 +1,159 @@
+"""Device-level operations of the FD engine: thin torch-tensor wrappers over the C ABI.
+
+PyTorch-ROCm is plumbing here (device memory, streams, torch.distributed); every computation
+runs in libfdr.so.  All calls are asynchronous on the current HIP stream.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class PolicySpec(object):
+    """Shape of a policy family (policies/discrete.py:34-48, policies/mujoco.py:32-41)."""
+
+    def __init__(self, kind, n_in, n_act, n_params):
+        assert kind in ("discrete", "mujoco")
+        self.kind, self.n_in, self.n_act, self.n_params = kind, int(n_in), int(n_act), int(n_params)
+
+    def desc(self, bn_mean=None, bn_var=None):
+        return _lib.PolicyDesc(_lib.FDR_POLICY_DISCRETE if self.kind == "discrete" else _lib.FDR_POLICY_MUJOCO,
+                               self.n_in, self.n_act, 64, self.n_params,
+                               None if bn_mean is None else bn_mean.data_ptr(),
+                               None if bn_var is None else bn_var.data_ptr())
+
+
+def _check_dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("fdr: tensors must live on the GPU (got %s)" % t.device)
+
+
+def lanes_desc(base, base_stride, table=None, idx=None, sign=None, sigma=0.0, deterministic=None):
+    _check_dev(base, table, idx, sign, deterministic)
+    if base.dtype != torch.float32 or not base.is_contiguous():
+        raise ValueError("base must be contiguous float32")
+    if idx is not None and idx.dtype != torch.int64:
+        raise ValueError("idx must be int64")
+    if sign is not None and sign.dtype != torch.int8:
+        raise ValueError("sign must be int8")
+    if deterministic is not None and deterministic.dtype != torch.int8:
+        raise ValueError("deterministic must be int8")
+    d = _lib.LanesDesc(base.data_ptr(), int(base_stride),
+                       None if table is None else table.data_ptr(),
+                       0 if table is None else table.numel(),
+                       None if idx is None else idx.data_ptr(),
+                       None if sign is None else sign.data_ptr(),
+                       float(sigma),
+                       None if deterministic is None else deterministic.data_ptr())
+    # the descriptor holds raw device pointers: keep the tensors alive as long as it lives, or the
+    # caching allocator may hand their blocks to the next allocation before the kernel runs
+    d._refs = (base, table, idx, sign, deterministic)
+    return d
+
+
+def perturb(theta, table, idx, sign, sigma):
+    """theta' = theta + sign * fl32(sigma * table[idx:idx+P]) -> [n, P] (worker/worker.py:28)."""
+    _check_dev(theta, table, idx, sign)
+    n, P = idx.numel(), theta.numel()
+    out = torch.empty((n, P), dtype=torch.float32, device=theta.device)
+    check(lib.fdr_perturb(None, _p(theta), P, _p(table), table.numel(), _p(idx), _p(sign), n,
+                          float(sigma), _p(out), _stream(theta.device)), "fdr_perturb")
+    return out
+
+
+def policy_forward(spec, lanes, n_lanes, x, bn_mean=None, bn_var=None):
+    """One observation per lane.  discrete -> probs [n, A]; mujoco -> (mean, std) [n, A]."""
+    _check_dev(x, bn_mean, bn_var)
+    x = x.to(torch.float32).contiguous()
+    dev = x.device
+    out0 = torch.empty((n_lanes, spec.n_act), dtype=torch.float32, device=dev)
+    out1 = None if spec.kind == "discrete" else torch.empty_like(out0)
+    pd = spec.desc(bn_mean, bn_var)
+    check(lib.fdr_policy_forward(None, ctypes.byref(pd), ctypes.byref(lanes), n_lanes, _p(x), _p(out0),
+                                 _p(out1), _stream(dev)), "fdr_policy_forward")
+    return out0 if out1 is None else (out0, out1)
+
+
+class RolloutResult(object):
+    """SoA result of one batched rollout (the FDReturn fields, learner/fd_return.py:5-16)."""
+
+    def __init__(self, ret, ent, steps, norm2):
+        self.reward, self.entropy, self.timesteps, self.norm2 = ret, ent, steps, norm2
+
+
+def rollout(spec, env, lanes, n_lanes, seed, jiggle=True, obs_mean=None, obs_std=None,
+            bn_mean=None, bn_var=None, out=None, device=None):
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    _check_dev(obs_mean, obs_std, bn_mean, bn_var)
+    if out is None:
+        out = RolloutResult(torch.empty(n_lanes, dtype=torch.float64, device=dev),
+                            torch.empty(n_lanes, dtype=torch.float64, device=dev),
+                            torch.empty(n_lanes, dtype=torch.int32, device=dev),
+                            torch.empty(n_lanes, dtype=torch.float64, device=dev))
+    pd = spec.desc(bn_mean, bn_var)
+    ed = env.desc()
+    check(lib.fdr_rollout(None, ctypes.byref(pd), ctypes.byref(ed), ctypes.byref(lanes), n_lanes,
+                          ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(obs_mean),
+                          _p(obs_std), _p(out.reward), _p(out.entropy), _p(out.timesteps), _p(out.norm2),
+                          _stream(dev)), "fdr_rollout")
+    return out
+
+
+def fd_weights(rewards_all, policy_reward, lane_lo, sign_local, norm2_local, lanes_per_dir, sigma, coef=None):
+    _check_dev(rewards_all, sign_local, norm2_local)
+    n_local = sign_local.numel()
+    n_dirs = n_local // lanes_per_dir
+    if coef is None:
+        coef = torch.empty(n_dirs, dtype=torch.float64, device=rewards_all.device)
+    check(lib.fdr_fd_weights(None, _p(rewards_all), rewards_all.numel(), float(policy_reward), int(lane_lo),
+                             n_local, _p(sign_local), _p(norm2_local), int(lanes_per_dir), float(sigma),
+                             _p(coef), _stream(rewards_all.device)), "fdr_fd_weights")
+    return coef
+
+
+_WS = {}
+
+
+def _workspace(key, nbytes, device):
+    buf = _WS.get((key, device))
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+        _WS[(key, device)] = buf
+    return buf
+
+
+def fd_grad(table, idx_dirs, coef, n_params, g=None):
+    _check_dev(table, idx_dirs, coef)
+    dev = table.device
+    n_dirs = idx_dirs.numel()
+    if g is None:
+        g = torch.empty(n_params, dtype=torch.float64, device=dev)
+    nb = lib.fdr_fd_grad_workspace_bytes(n_dirs, n_params)
+    ws = _workspace("grad", nb, dev)
+    check(lib.fdr_fd_grad(None, _p(table), table.numel(), _p(idx_dirs), _p(coef), n_dirs, n_params, _p(g),
+                          _p(ws), ws.numel(), _stream(dev)), "fdr_fd_grad")
+    return g
+
+
+def dsgd_step(theta, g, lr, lr_scale, out=None):
+    """In-place theta update; returns device f64[2] = (||d theta||, ||grad||)."""
+    _check_dev(theta, g)
+    dev = theta.device
+    if out is None:
+        out = torch.empty(2, dtype=torch.float64, device=dev)
+    nb = lib.fdr_dsgd_workspace_bytes(theta.numel())
+    ws = _workspace("dsgd", nb, dev)
+    check(lib.fdr_dsgd_step(None, _p(theta), _p(g), theta.numel(), float(lr), float(lr_scale), _p(out), _p(ws),
+                            ws.numel(), _stream(dev)), "fdr_dsgd_step")
+    return out

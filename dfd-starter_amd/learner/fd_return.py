@@ -1,0 +1,80 @@
+"""FDReturn record (learner/fd_return.py:5-56) and FDBatch, its struct-of-arrays device form.
+
+The hot path never builds per-return Python objects: ``Worker.evaluate`` returns an FDBatch whose
+fields are device tensors written by the rollout kernel, and ``FiniteDifferences.step`` consumes
+it directly.  ``FDBatch.to_returns()`` / ``FDBatch.from_returns()`` adapt to the reference's
+list-of-FDReturn API.
+"""
+import numpy as np
+import torch
+
+
+class FDReturn(object):
+    def __init__(self):
+        self.epoch = -1
+        self.encoded_noise = "-1"
+        self.perturbation = None
+        self.reward = 0
+        self.novelty = 0
+        self.entropy = 0
+        self.timesteps = 0
+        self.is_eval = False
+        self.eval_states = []
+        self.obs_stats_update = []
+        self.sign = 1          # build extension: -1 for the antithetic partner
+        self.norm2 = None      # build extension: ||lambda||^2 from the rollout kernel
+
+    def serialize(self):
+        return (self.reward, self.novelty, self.entropy, self.timesteps, self.encoded_noise, self.perturbation,
+                self.epoch, self.is_eval, self.eval_states, self.obs_stats_update)
+
+    def deserialize(self, other):
+        (self.reward, self.novelty, self.entropy, self.timesteps, self.encoded_noise, self.perturbation,
+         self.epoch, self.is_eval, self.eval_states, self.obs_stats_update) = other
+
+
+class FDBatch(object):
+    """One batched evaluation.  Lanes of one direction are contiguous (lanes_per_dir = 2 when
+    antithetic: +eps then -eps).  All tensors live on ``device``; ``idx_host`` mirrors idx."""
+
+    def __init__(self, reward, entropy, timesteps, norm2, idx, sign, idx_host, sign_host, epoch,
+                 lanes_per_dir=1, is_eval=None, novelty=None):
+        self.reward, self.entropy, self.timesteps, self.norm2 = reward, entropy, timesteps, norm2
+        self.idx, self.sign = idx, sign
+        self.idx_host, self.sign_host = np.asarray(idx_host), np.asarray(sign_host)
+        self.epoch = epoch
+        self.lanes_per_dir = lanes_per_dir
+        self.is_eval = np.zeros(len(self.sign_host), bool) if is_eval is None else np.asarray(is_eval)
+        self.novelty = novelty
+
+    def __len__(self):
+        return len(self.sign_host)
+
+    @property
+    def n_dirs(self):
+        return len(self) // self.lanes_per_dir
+
+    def dir_idx(self):
+        """Device int64 [n_dirs]: table offset of each direction."""
+        if self.lanes_per_dir == 1:
+            return self.idx
+        return self.idx[::self.lanes_per_dir].contiguous()
+
+    def to_returns(self):
+        rew = self.reward.double().cpu().numpy()
+        ent = self.entropy.double().cpu().numpy()
+        ts = self.timesteps.cpu().numpy()
+        n2 = self.norm2.cpu().numpy() if self.norm2 is not None else [None] * len(rew)
+        nov = np.zeros(len(rew)) if self.novelty is None else np.asarray(self.novelty)
+        out = []
+        for i in range(len(rew)):
+            r = FDReturn()
+            r.epoch = self.epoch
+            r.is_eval = bool(self.is_eval[i])
+            r.encoded_noise = "0" if r.is_eval else "{}".format(int(self.idx_host[i]))
+            r.sign = int(self.sign_host[i])
+            r.reward, r.entropy, r.timesteps = float(rew[i]), float(ent[i]), int(ts[i])
+            r.novelty = float(nov[i])
+            r.norm2 = None if n2[i] is None else float(n2[i])
+            out.append(r)
+        return out

@@ -1,0 +1,182 @@
+"""FiniteDifferences -- the reference learner's API (learner/finite_differences.py:6-114) on the GPU.
+
+``step(batch, policy_reward, policy_novelty, policy_entropy)`` accepts either the reference's
+list of FDReturn or an FDBatch (device SoA from Worker.evaluate) and runs, all on the device:
+
+    fdr_fd_weights   z = standardize(r - r_pol) over the batch; coef_d = sum_i z_i s_i sigma / ||lambda_i||^2
+    fdr_fd_grad      g = sum_d coef_d * table[idx_d : idx_d + P]            (f64, fixed order)
+    [all_reduce(g)]  one RCCL all-reduce when the batch is sharded over ranks (DESIGN.md "Multi-GPU")
+    fdr_dsgd_step    theta <- theta - lr*sqrt(P)*lr_scale * fl32(-g) / ||fl32(-g)||
+
+Returns carry a current epoch in the synchronous engine; returns from an older epoch (the
+reference's async server mode) add the parameter drift theta_epoch - theta_now to lambda
+(finite_differences.py:66-92) -- that rare path runs as plain torch device ops (not a hot path).
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from dsgd import DSGD
+from fdr import engine
+from utils import math_helpers
+
+from .fd_return import FDBatch
+
+
+class FiniteDifferences(object):
+    def __init__(self, policy, gradient_optimizer, omega, noise_source, noise_std=0.1, batch_size=100,
+                 ent_coef=0.0, max_delayed_return=10, process_group=None):
+        self.max_delayed_return = max_delayed_return
+        self.ent_coef = ent_coef
+        self.noise_std = noise_std
+        self.policy = policy
+        self.gradient_optimizer = gradient_optimizer
+        self.noise_source = noise_source
+        self.omega = omega
+        self.batch_size = batch_size
+        self.process_group = process_group
+        self.epoch = 0
+        self.discarded_returns = 0
+        self.policy_history = [(policy.flat.detach().clone(), 0)]
+        self.dist_map = {0: None}
+        self.using_dsgd = isinstance(gradient_optimizer, DSGD)
+        P = policy.num_params
+        self.gradient_memory = torch.zeros(P, dtype=torch.float64, device=policy.flat.device)
+        self._out = torch.zeros(2, dtype=torch.float64, device=policy.flat.device)
+
+    # ------------------------------------------------------------------------------------------
+    def _distributed(self):
+        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.process_group) > 1
+
+    def step(self, batch, policy_reward, policy_novelty, policy_entropy):
+        """Reference signature; returns the update magnitude ||d theta|| as a float."""
+        out = self.step_async(batch, policy_reward, policy_novelty, policy_entropy)
+        if out is None:
+            return 0
+        upd, gnorm = out.tolist()
+        assert gnorm > 0, "DSGD ENCOUNTERED GRADIENT WITH NORM OF ZERO"   # dynamic_sgd.py:28
+        return upd
+
+    def step_async(self, batch, policy_reward, policy_novelty, policy_entropy):
+        """Same as step() but leaves (||d theta||, ||grad||) on the device: no host sync."""
+        if policy_reward is None:
+            policy_reward = 0
+        if isinstance(batch, FDBatch):
+            return self._step_batch(batch, float(policy_reward))
+        return self._step_returns(list(batch), float(policy_reward))
+
+    # ------------------------------------------------------------------------------------------
+    def _step_batch(self, b, policy_reward, extra_grad=None):
+        table = self.noise_source.device_table(self.policy.flat.device)
+        train = torch.as_tensor(b.sign_host != 0)
+        if not bool(train.all()):
+            raise ValueError("FDBatch for the learner must not contain eval lanes (sign 0)")
+        P = self.policy.num_params
+        if self._distributed():
+            rewards_all, lane_lo = self._gather_rewards(b.reward)
+        else:
+            rewards_all, lane_lo = b.reward, 0
+        coef = engine.fd_weights(rewards_all, policy_reward, lane_lo, b.sign, b.norm2, b.lanes_per_dir,
+                                 self.noise_std)
+        g = engine.fd_grad(table, b.dir_idx(), coef, P, self.gradient_memory)
+        if extra_grad is not None:
+            g.add_(extra_grad)
+        if self._distributed():
+            dist.all_reduce(g, group=self.process_group)
+        return self._apply(g)
+
+    def _gather_rewards(self, local):
+        ws = dist.get_world_size(self.process_group)
+        rank = dist.get_rank(self.process_group)
+        n = torch.tensor([local.numel()], device=local.device)
+        sizes = [torch.zeros_like(n) for _ in range(ws)]
+        dist.all_gather(sizes, n, group=self.process_group)
+        sizes = [int(s.item()) for s in sizes]
+        bufs = [torch.empty(s, dtype=local.dtype, device=local.device) for s in sizes]
+        dist.all_gather(bufs, local.contiguous(), group=self.process_group)
+        return torch.cat(bufs), sum(sizes[:rank])
+
+    def _apply(self, g):
+        lr_scale = 1.0
+        if self.using_dsgd:
+            self.gradient_optimizer.adjust_lr(self.omega)
+            lr_scale = self.gradient_optimizer.lr_scale
+            lr = self.gradient_optimizer.lr
+        else:
+            lr = self.gradient_optimizer.param_groups[0]["lr"]
+        engine.dsgd_step(self.policy.flat, g, lr, lr_scale, self._out)
+        self.epoch += 1
+        self._build_distance_map()
+        self._update_policy_history()
+        return self._out
+
+    def _build_distance_map(self):
+        # finite_differences.py:66-73 (device copies of the recent parameter vectors)
+        flat = self.policy.flat.detach()
+        self.dist_map = {self.epoch: None}
+        for params, ep in self.policy_history:
+            self.dist_map[ep] = params - flat
+
+    def _update_policy_history(self):
+        self.policy_history.append((self.policy.flat.detach().clone(), self.epoch))
+        while len(self.policy_history) > self.max_delayed_return:
+            self.policy_history.pop(0)
+
+    # ------------------------------------------------------------------------------------------
+    def _step_returns(self, rets, policy_reward):
+        """list[FDReturn] path (finite_differences.py:24-64, 80-114)."""
+        keep = []
+        for r in rets:
+            if r.epoch not in self.dist_map:
+                print("FINITE DIFFERENCE LEARNER RECEIVED RETURN THAT WAS TOO OLD")
+                print("RECEIVED EPOCH:", r.epoch, "ACCEPTABLE EPOCHS:", list(self.dist_map.keys()))
+                self.discarded_returns += 1
+                continue
+            keep.append(r)
+        if not keep:
+            return None
+        dev = self.policy.flat.device
+        table = self.noise_source.device_table(dev)
+        P = self.policy.num_params
+        sigma32 = np.float32(self.noise_std)
+        current = [r for r in keep if self.dist_map[r.epoch] is None]
+        stale = [r for r in keep if self.dist_map[r.epoch] is not None]
+        # z-score over ALL kept returns (finite_differences.py:40-43)
+        order = current + stale
+        rewards = torch.as_tensor([r.reward for r in order], dtype=torch.float64, device=dev)
+        extra = None
+        if stale:
+            z = torch.as_tensor(math_helpers.standardize_arr(np.subtract([r.reward for r in order], policy_reward)),
+                                dtype=torch.float64, device=dev)
+            extra = torch.zeros(P, dtype=torch.float64, device=dev)
+            for k, r in enumerate(stale):
+                i = int(r.encoded_noise)
+                lam = table[i:i + P] * torch.tensor(sigma32, device=dev) * float(getattr(r, "sign", 1) or 1)
+                lam = lam + self.dist_map[r.epoch]
+                nrm = torch.linalg.vector_norm(lam)
+                extra += z[len(current) + k] * (lam / (nrm * nrm)).double()
+        if not current:
+            g = extra
+            if self._distributed():
+                dist.all_reduce(g, group=self.process_group)
+            return self._apply(g)
+        idx = np.array([int(r.encoded_noise) for r in current], dtype=np.int64)
+        sign = np.array([int(getattr(r, "sign", 1) or 1) for r in current], dtype=np.int8)
+        idx_d = torch.as_tensor(idx, device=dev)
+        sign_d = torch.as_tensor(sign, device=dev)
+        if all(getattr(r, "norm2", None) is not None for r in current):
+            n2 = torch.as_tensor([r.norm2 for r in current], dtype=torch.float64, device=dev)
+        else:
+            rows = torch.stack([table[i:i + P] for i in idx])
+            lam = (rows * torch.tensor(sigma32, device=dev)).double()
+            n2 = (lam * lam).sum(dim=1)
+        b = FDBatch(rewards[:len(current)], None, None, n2, idx_d, sign_d, idx, sign, self.epoch)
+        if stale:
+            # weights over the full set: pass every reward, local lanes = the current ones
+            coef = engine.fd_weights(rewards, policy_reward, 0, b.sign, b.norm2, 1, self.noise_std)
+            g = engine.fd_grad(table, b.idx, coef, P, self.gradient_memory)
+            g.add_(extra)
+            if self._distributed():
+                dist.all_reduce(g, group=self.process_group)
+            return self._apply(g)
+        return self._step_batch(b, policy_reward)

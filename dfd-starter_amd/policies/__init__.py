@@ -1,0 +1,3 @@
+from .policy import Policy  # noqa: F401
+from .discrete import DiscretePolicy  # noqa: F401
+from .mujoco import MujocoPolicy  # noqa: F401

@@ -1,0 +1,159 @@
+"""SequentialRunner -- run_sequential.py:17-213 on one MI355X.
+
+Same constructor keywords and train(n_epochs) loop as the reference, with its three crash /
+silent-NaN bugs fixed (Worker.update takes the parameter vector, noise_std is
+passed by keyword, SharedNoiseTable instead of the numpy-2-broken RNGNoiseSource) and with the
+per-episode host loop replaced by ONE batched rollout launch per epoch:
+
+  1. eval coin flips (Worker.rng) until ``batch_size`` training returns are scheduled, exactly as
+     run_sequential.py:134-147 consumes them; noise indices in the reference's order;
+  2. one fdr_rollout over all those lanes (eval lanes: theta, deterministic actions);
+  3. eval EMA / omega update on the host (run_sequential.py:137-151);
+  4. FiniteDifferences.step on the device (fd weights -> gradient reduce -> DSGD);
+  5. optional BN refresh (compute_vbn), report.
+
+``antithetic=True`` evaluates +eps/-eps pairs (build extension; batch_size then counts directions).
+Environments are GPU-resident (envs/): the trap env exactly, MuJoCo / CartPole ids map to the
+build's synthetic fixed-length envs of the same shapes (no simulator exists on this platform).
+"""
+import time
+
+import numpy as np
+import torch
+
+from dsgd import DSGD
+from envs import SyntheticEnv, TrapEnv
+from learner import FDBatch, FDState, FiniteDifferences
+from policies import DiscretePolicy, MujocoPolicy
+from strategy import StrategyHandler
+from utils import AdaptiveOmega, SharedNoiseTable, math_helpers
+from worker import Agent, Worker
+
+
+def make_env(env_id, device=None, episode_len=None, env_seed=0):
+    if env_id.startswith("SimpleTrapEnv"):
+        return TrapEnv(device=device)
+    name = "cartpole" if env_id.startswith("CartPole") else "halfcheetah"
+    kw = {} if episode_len is None else {"episode_len": episode_len}
+    return SyntheticEnv.named(name, device=device, env_seed=env_seed, **kw)
+
+
+class SequentialRunner(object):
+    def __init__(self, opt_fn=DSGD, env_id="Walker2d-v2", normalize_obs=False, learning_rate=0.01,
+                 noise_std=0.02, batch_size=40, ent_coef=0.0, random_seed=123, max_delayed_return=10,
+                 vbn_buffer_size=0, zeta_size=200, max_strategy_history_size=200, eval_prob=0.05,
+                 omega_default_value=0, omega_improvement_threshold=1.035, omega_reward_history_size=20,
+                 omega_min_value=0, omega_max_value=1, omega_steps_to_min=25, omega_steps_to_max=75,
+                 log_to_wandb=False, wandb_project="fd-starter", wandb_group=None, wandb_run_name=None,
+                 noise_table_size=25_000_000, antithetic=False, episode_len=None, device=None, verbose=True):
+        if log_to_wandb:
+            raise NotImplementedError("wandb logging is not part of the MI355X engine (no network)")
+        self.verbose = verbose
+        self.rng = np.random.RandomState(random_seed)
+        self.omega = AdaptiveOmega(default_value=omega_default_value, improvement_threshold=omega_improvement_threshold,
+                                   reward_history_size=omega_reward_history_size, min_value=omega_min_value,
+                                   max_value=omega_max_value, steps_to_min=omega_steps_to_min,
+                                   steps_to_max=omega_steps_to_max)
+        self.batch_size = batch_size
+        self.zeta_size = zeta_size
+        self.antithetic = antithetic
+        torch.manual_seed(random_seed)
+        np.random.seed(random_seed)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.env = make_env(env_id, self.device, episode_len)
+        if self.env.discrete:
+            self.policy = DiscretePolicy(self.env.obs_dim, self.env.act_dim, seed=random_seed, device=self.device)
+            dist_fn = math_helpers.categorical_tvd
+        else:
+            self.policy = MujocoPolicy(self.env.obs_dim, self.env.act_dim, seed=random_seed, device=self.device)
+            dist_fn = math_helpers.gaussian_wasserstein_dist_from_strategies   # SURVEY finding 6 fixed
+        opt = opt_fn(self.policy.parameters(), lr=learning_rate)
+        self.noise_source = SharedNoiseTable(noise_table_size, self.policy.num_params, random_seed=random_seed)
+        self.strategy_handler = StrategyHandler(self.policy, dist_fn, max_history_size=max_strategy_history_size)
+        self.agent = Agent(self.policy, self.env, random_seed, normalize_obs=normalize_obs)
+        self.worker = Worker(self.policy, self.agent, self.noise_source, self.strategy_handler, sigma=noise_std,
+                             random_seed=random_seed, eval_prob=eval_prob)
+        self.learner = FiniteDifferences(self.policy, opt, self.omega, self.noise_source, noise_std=noise_std,
+                                         batch_size=batch_size, ent_coef=ent_coef,
+                                         max_delayed_return=max_delayed_return)
+        self.policy_reward = 0
+        self.policy_entropy = 0
+        self.policy_novelty = 0
+        self.vbn_buffer = None
+        if vbn_buffer_size > 0:
+            # run_sequential.py:198-213 samples the buffer from env steps; the GPU envs expose no host
+            # stepping, so the buffer is drawn around the reset state (documented deviation)
+            s0 = getattr(self.env, "s0_host", np.zeros(self.env.obs_dim, np.float32))
+            self.vbn_buffer = (s0 + 0.1 * self.rng.randn(vbn_buffer_size, self.env.obs_dim)).astype(np.float32)
+        self.current_state = FDState()
+        self.current_state.policy_params = self.policy.get_trainable_flat()
+        self.current_state.epoch = 0
+        self.history = []
+
+    def _schedule(self):
+        """Eval coins in the reference's order until batch_size training returns (run_sequential.py:134)."""
+        evals = []
+        n_train = 0
+        while n_train < self.batch_size:
+            e = self.worker.rng.uniform(0, 1) < self.worker.eval_prob
+            evals.append(e)
+            n_train += 0 if e else 1
+        return np.array(evals)
+
+    @torch.no_grad()
+    def train(self, n_epochs):
+        self.strategy_handler.add_policy(self.policy)
+        self.worker.update(self.current_state)
+        for _ in range(n_epochs):
+            t1 = time.perf_counter()
+            is_eval = self._schedule()
+            n_dirs = int((~is_eval).sum())
+            idx_dirs = self.noise_source.sample_batch(n_dirs)
+            lpd = 2 if self.antithetic else 1
+            # lane layout: training lanes first (lanes of a direction contiguous), eval lanes last
+            lidx = np.concatenate([np.repeat(idx_dirs, lpd), np.zeros(int(is_eval.sum()), np.int64)])
+            sign = np.concatenate([np.tile(np.array([1, -1], np.int8), n_dirs) if self.antithetic
+                                   else np.ones(n_dirs, np.int8), np.zeros(int(is_eval.sum()), np.int8)])
+            det = (sign == 0).astype(np.int8)
+            res, idx_d, sign_d = self.worker.launch(lidx, sign, det, jiggle=False)
+            rew = res.reward.cpu().numpy() + np.array([self.agent.rng.choice((-1e-12, 1e-12)) for _ in lidx])
+            ent = res.entropy.cpu().numpy()
+            steps = int(res.timesteps.sum().item())
+            self.agent.cumulative_timesteps += steps
+            n_train = n_dirs * lpd
+            for r, e in zip(rew[n_train:], ent[n_train:]):
+                self.policy_reward = self.policy_reward * 0.9 + r * 0.1
+                self.policy_entropy = self.policy_entropy * 0.9 + e * 0.1
+            if is_eval.any():
+                self.omega.step(float(np.mean(rew[:n_train])))
+            dev = self.policy.flat.device
+            batch = FDBatch(torch.as_tensor(rew[:n_train], device=dev), res.entropy[:n_train],
+                            res.timesteps[:n_train], res.norm2[:n_train], idx_d[:n_train], sign_d[:n_train],
+                            lidx[:n_train], sign[:n_train], self.learner.epoch, lanes_per_dir=lpd)
+            update_magnitude = self.learner.step(batch, self.policy_reward, self.policy_novelty, self.policy_entropy)
+            if self.vbn_buffer is not None:
+                self.policy.compute_vbn(self.vbn_buffer)
+            if update_magnitude > 0:
+                self.current_state.policy_params = self.policy.get_trainable_flat()
+                self.current_state.epoch = self.learner.epoch
+                self.worker.update(self.current_state)
+                report = {"Epoch": self.learner.epoch,
+                          "Epoch Time": time.perf_counter() - t1,
+                          "Cumulative Timesteps": self.agent.cumulative_timesteps,
+                          "Policy Reward": self.policy_reward,
+                          "Policy Entropy": self.policy_entropy,
+                          "Policy Novelty": self.policy_novelty,
+                          "Noisy Reward": float(np.mean(rew[:n_train])),
+                          "Noisy Novelty": 0.0,
+                          "Update Magnitude": update_magnitude,
+                          "Omega": self.omega.omega}
+                self.history.append(dict(report, idx=idx_dirs, rewards=rew[:n_train]))
+                self._report_epoch(report)
+
+    def _report_epoch(self, report):
+        if not self.verbose:
+            return
+        print("\n***********Begin Epoch Report***********")
+        for k, v in report.items():
+            print("{} {:7.4f}".format(k, v) if isinstance(v, (float, np.floating)) else "{} {}".format(k, v))
+        print("***********End Epoch Report***********")

@@ -1,0 +1,84 @@
+"""Noise sources -- the API of utils/noise_sources.py:4-51, with a GPU-resident shared table.
+
+``SharedNoiseTable`` is the hot-path source:
+  * table = RandomState(seed).randn(size).astype(float32)       (noise_sources.py:39-40)
+  * indices drawn from the SAME RandomState, continuing after the table draw
+    (noise_sources.py:45): sample() draws one, ``sample_batch(n)`` draws n at once -- numpy's
+    vectorised randint yields the identical MT19937 stream (pinned in tests/test_oracle_golden.py);
+  * the table is uploaded once per device and stays resident in HBM (100 MB at 25M entries);
+    the HIP kernels gather table[idx : idx + P] directly, theta' is never materialised.
+"""
+import numpy as np
+import torch
+
+
+class SharedNoiseTable(object):
+    def __init__(self, size, n_params, random_seed=123):
+        assert size > n_params, "!ATTEMPTED TO MAKE NOISE TABLE WITH SIZE {} FOR {} PARAMETERS!".format(size, n_params)
+        self._rng = np.random.RandomState(random_seed)
+        self._table = self._rng.randn(size).astype(np.float32)
+        self._n_params = n_params
+        self._max_sample_idx = size - n_params
+        self._device_tables = {}
+
+    @property
+    def size(self):
+        return self._table.size
+
+    def sample(self):
+        idx = int(self._rng.randint(0, self._max_sample_idx))
+        return "{}".format(idx), self._table[idx:idx + self._n_params]
+
+    def sample_batch(self, n):
+        """n indices in the order n sample() calls would draw them (int64 numpy array)."""
+        return self._rng.randint(0, self._max_sample_idx, size=int(n)).astype(np.int64)
+
+    def decode(self, noise_idx):
+        noise_idx = int(noise_idx)
+        return self._table[noise_idx:noise_idx + self._n_params]
+
+    def device_table(self, device=None):
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        t = self._device_tables.get(dev)
+        if t is None:
+            t = torch.from_numpy(self._table).to(dev)
+            self._device_tables[dev] = t
+        return t
+
+
+class RNGNoiseSource(object):
+    """noise_sources.py:4-20 (PCG64 state string).  Uses bit_generator.state: Generator.__getstate__
+    returns None on numpy >= 2, which breaks the reference (SURVEY.md finding 3).  Host-only: the
+    GPU path needs a table (SharedNoiseTable)."""
+
+    def __init__(self, n_params, random_seed=123):
+        self.rng = np.random.default_rng(np.random.SeedSequence(random_seed))
+        self.n_params = n_params
+
+    def sample(self):
+        st = self.rng.bit_generator.state["state"]
+        enc = "{},{}".format(st["state"], st["inc"])
+        return enc, self.rng.standard_normal(size=self.n_params)
+
+    def decode(self, state):
+        s, inc = (int(v) for v in state.split(","))
+        bg = np.random.PCG64()
+        st = bg.state
+        st["state"]["state"], st["state"]["inc"] = s, inc
+        bg.state = st
+        return np.random.Generator(bg).standard_normal(size=self.n_params)
+
+
+class SimpleNoiseSource(object):
+    """noise_sources.py:23-33: ships the raw noise vector.  Host-only."""
+
+    def __init__(self, n_params, random_seed=123):
+        self.rng = np.random.RandomState(random_seed)
+        self.n_params = n_params
+
+    def sample(self):
+        noise = self.rng.randn(self.n_params)
+        return noise, noise
+
+    def decode(self, noise):
+        return noise

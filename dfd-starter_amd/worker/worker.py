@@ -1,0 +1,121 @@
+"""Worker -- worker/worker.py:7-57, batched: one rollout launch evaluates many perturbations.
+
+``evaluate(n_dirs, antithetic)`` is the hot path (north star ``worker.worker.evaluate``): it draws
+the noise-table indices on the host in the reference's order (utils/noise_sources.py:44-47), ships
+them to the device and runs every (perturbation x env) lane for a whole episode in ONE
+fdr_rollout launch.  theta' = theta + sign * fl32(sigma * eps) is formed inside the kernel
+(bit-exact with worker.py:28) and never materialised.  The result is an FDBatch (device SoA).
+
+``collect_returns(n)`` keeps the reference's list-of-FDReturn API: the eval coin flips
+(worker.py:23) and index draws happen in the reference's order, then all n episodes run in one
+launch (eval lanes: unperturbed theta, deterministic actions, worker.py:33-35).
+"""
+import numpy as np
+import torch
+
+from fdr import engine
+from learner.fd_return import FDBatch
+from utils.math_helpers import WelfordRunningStat
+
+
+class Worker(object):
+    def __init__(self, policy, agent, noise_source, strategy_handler, sigma=0.02, eval_prob=0.1, random_seed=123):
+        self.policy = policy
+        self.agent = agent
+        self.noise_source = noise_source
+        self.strategy_handler = strategy_handler
+        self.sigma = sigma
+        self.epoch = -1
+        self.rng = np.random.RandomState(random_seed)
+        self.eval_prob = eval_prob
+        self.fixed_obs_stats = WelfordRunningStat(policy.input_shape)
+        self._pinned = {}
+
+    # ---- hot path ---------------------------------------------------------------------------
+    def _to_device(self, arr, dtype):
+        """Async H2D through a small ring of pinned buffers; an event guards each buffer's reuse."""
+        dev = self.policy.flat.device
+        key = (dtype, len(arr))
+        ring = self._pinned.setdefault(key, {"bufs": [], "events": [], "next": 0})
+        if len(ring["bufs"]) < 4:
+            ring["bufs"].append(torch.empty(len(arr), dtype=dtype).pin_memory())
+            ring["events"].append(None)
+            slot = len(ring["bufs"]) - 1
+        else:
+            slot = ring["next"]
+            ring["next"] = (slot + 1) % 4
+            if ring["events"][slot] is not None:
+                ring["events"][slot].synchronize()
+        buf = ring["bufs"][slot]
+        buf.numpy()[:] = arr
+        out = buf.to(dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        ring["events"][slot] = ev
+        return out
+
+    def launch(self, idx, sign, det, seed=None, out=None, jiggle=True):
+        """Run one rollout over explicit lanes (host arrays) -> FDBatch (asynchronous)."""
+        p = self.policy
+        n = len(idx)
+        idx_d = self._to_device(np.asarray(idx, np.int64), torch.int64)
+        sign_d = self._to_device(np.asarray(sign, np.int8), torch.int8)
+        det_d = self._to_device(np.asarray(det, np.int8), torch.int8)
+        table = self.noise_source.device_table(p.flat.device)
+        lanes = engine.lanes_desc(p.flat, 0, table, idx_d, sign_d, self.sigma, det_d)
+        om, osd = self.agent.obs_norm_tensors(self.fixed_obs_stats.mean, self.fixed_obs_stats.std)
+        bm, bv = p.bn_stats()
+        if seed is None:
+            seed = self.agent.next_seed(n)
+        res = engine.rollout(p.spec, self.agent.env, lanes, n, seed, jiggle=jiggle, obs_mean=om, obs_std=osd,
+                             bn_mean=bm, bn_var=bv, out=out, device=p.flat.device)
+        return res, idx_d, sign_d
+
+    def evaluate(self, n_dirs, antithetic=True, seed=None, lane_range=None, out=None):
+        """n_dirs perturbation directions (x2 lanes if antithetic) -> FDBatch on the device.
+
+        lane_range=(lo, hi) evaluates only that slice of the lanes (multi-GPU sharding: every rank
+        draws the full index list, in order, and keeps its contiguous share)."""
+        idx = self.noise_source.sample_batch(n_dirs)
+        lpd = 2 if antithetic else 1
+        lidx = np.repeat(idx, lpd)
+        sign = np.tile(np.array([1, -1], np.int8), n_dirs) if antithetic else np.ones(n_dirs, np.int8)
+        if lane_range is not None:
+            lo, hi = lane_range
+            lidx, sign = lidx[lo:hi], sign[lo:hi]
+        det = np.zeros(len(lidx), np.int8)
+        res, idx_d, sign_d = self.launch(lidx, sign, det, seed=seed, out=out)
+        self.agent.cumulative_timesteps += int(len(lidx)) * self.agent.env.episode_len
+        return FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, lidx, sign, self.epoch,
+                       lanes_per_dir=lpd)
+
+    # ---- reference API ----------------------------------------------------------------------
+    @torch.no_grad()
+    def collect_returns(self, n=1):
+        is_eval = np.array([self.rng.uniform(0, 1) < self.eval_prob for _ in range(n)])
+        idx = np.zeros(n, np.int64)
+        k = int((~is_eval).sum())
+        if k:
+            idx[~is_eval] = self.noise_source.sample_batch(k)
+        sign = np.where(is_eval, 0, 1).astype(np.int8)
+        res, idx_d, sign_d = self.launch(idx, sign, is_eval.astype(np.int8), jiggle=False)
+        b = FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, idx, sign, self.epoch,
+                    is_eval=is_eval)
+        rets = b.to_returns()
+        for r in rets:
+            r.reward += self.agent.rng.choice((-1e-12, 1e-12))     # agent.py:69
+            self.agent.cumulative_timesteps += r.timesteps
+            r.novelty = self.strategy_handler.compute_novelty(self.policy) if self.strategy_handler else 0
+            r.obs_stats_update = self.agent.obs_stats.serialize()
+        return rets
+
+    def update(self, state):
+        # worker.py:40-43, with SURVEY finding 1 fixed: policy_params is the trainable flat vector
+        params = np.asarray(state.policy_params)
+        if params.size == self.policy.num_params:
+            self.policy.set_trainable_flat(params)
+        else:
+            self.policy.deserialize(list(params))
+        self.epoch = state.epoch
+        if state.obs_stats is not None:
+            self.fixed_obs_stats.deserialize(state.obs_stats)

@@ -1,0 +1,153 @@
+/*
+ * fdr.h -- C ABI of the MI355X finite-difference rollout + gradient engine (libfdr.so).
+ *
+ * This is the drop-in boundary for the reference's perturbation-evaluation hot path
+ * (nexus-rl/dfd-starter).  The reference has no FFI layer: its boundary is a set of Python
+ * duck-typed interfaces.  Each entry point below names the reference
+ * interface it replaces; the Python host layer (dfd-starter_amd/fdr/_lib.py, ctypes) binds
+ * exactly these symbols -- INTEGRATION.md shows the binding a maintainer would add.
+ *
+ * Conventions
+ *   - Every pointer argument is a DEVICE pointer owned by the caller (PyTorch-ROCm tensors),
+ *     unless documented as host.  Nothing here allocates or frees memory.
+ *   - Every compute call is asynchronous on the caller's stream (`fdr_stream` = hipStream_t;
+ *     NULL = the legacy default stream) and performs no host synchronisation, no allocation and
+ *     no host<->device copy, so the calls can be captured into a hipGraph.
+ *   - Return value: FDR_OK or an error code; fdr_last_error() gives a thread-local message.
+ *     No C++ exception crosses this boundary.
+ *   - Numerics: see DESIGN.md.  theta' (fdr_perturb, and the in-kernel perturbation of
+ *     fdr_rollout / fdr_policy_forward) is bit-exact with the reference's numpy f32 arithmetic.
+ */
+#ifndef FDR_H_
+#define FDR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FDR_OK 0
+#define FDR_ERR_INVALID 1     /* bad argument (null pointer, size, shape mismatch) */
+#define FDR_ERR_UNSUPPORTED 2 /* policy/env shape with no compiled kernel instance */
+#define FDR_ERR_HIP 3         /* HIP runtime error (launch failure, no device) */
+#define FDR_ERR_WORKSPACE 4   /* caller's workspace too small */
+
+typedef void* fdr_stream; /* hipStream_t */
+
+/* Policy families (policies/discrete.py:34-48, policies/mujoco.py:32-41). */
+#define FDR_POLICY_DISCRETE 0 /* BN-Linear-ReLU-BN-Linear-ReLU-BN-Linear-Softmax, hidden 64 */
+#define FDR_POLICY_MUJOCO 1   /* Linear-Tanh-Linear-Tanh-Linear-tanh head, hidden 64 */
+
+/* Environments run inside the rollout kernel. */
+#define FDR_ENV_SYNTH 0 /* contractive linear-tanh system (DESIGN.md "Synthetic envs") */
+#define FDR_ENV_TRAP 1  /* custom_envs/simple_trap_env (integer-exact) */
+
+typedef struct fdr_policy_desc {
+  int32_t kind;     /* FDR_POLICY_* */
+  int32_t n_in;     /* observation size (policy.input_shape) */
+  int32_t n_act;    /* discrete: number of actions; mujoco: action dims (head = 2*n_act) */
+  int32_t hidden;   /* must be 64 (hard-coded by the reference) */
+  int64_t n_params; /* P = len(get_trainable_flat()) */
+  /* discrete only: eval-mode BatchNorm running stats of the 3 BN layers, concatenated
+     [n_in | 64 | 64] (policies/discrete.py:38,42,46); NULL = (mean 0, var 1). */
+  const float* bn_mean;
+  const float* bn_var;
+} fdr_policy_desc;
+
+typedef struct fdr_env_desc {
+  int32_t kind;        /* FDR_ENV_* */
+  int32_t obs_dim;     /* must equal policy n_in */
+  int32_t act_dim;     /* must equal policy n_act */
+  int32_t episode_len; /* fixed episode length T (FDR_ENV_TRAP: 201, environment.py:19,43) */
+  const float* M;      /* SYNTH: [obs_dim, obs_dim] row-major */
+  const float* K;      /* SYNTH: [obs_dim, act_dim] row-major */
+  const float* s0;     /* SYNTH: [obs_dim] reset state */
+  const uint8_t* walkable; /* TRAP: [map_h, map_w] 1 = walkable (tile_map.py:40) */
+  int32_t map_w, map_h;
+} fdr_env_desc;
+
+/* Where each lane's parameter vector comes from:
+ *   theta'_l[p] = base[l * base_stride + p] (+ sign_l * fl32(sigma * table[idx_l + p]))
+ * base_stride = 0 -> every lane shares theta (the FD case); table = NULL -> no perturbation.
+ * Replaces worker/worker.py:26-30 (flat + sigma * noise) without materialising theta'. */
+typedef struct fdr_lanes_desc {
+  const float* base;
+  int64_t base_stride;
+  const float* table;   /* shared noise table (utils/noise_sources.py:40), may be NULL */
+  int64_t table_size;
+  const int64_t* idx;   /* [n_lanes] table offsets, 0 <= idx <= table_size - P */
+  const int8_t* sign;   /* [n_lanes] +1 / -1 (antithetic) / 0 (unperturbed, eval lane) */
+  float sigma;          /* noise_std */
+  const int8_t* deterministic; /* [n_lanes] 1 = argmax/mean action; NULL -> all stochastic */
+} fdr_lanes_desc;
+
+/* ---- context / errors ---------------------------------------------------------------- */
+const char* fdr_version(void);
+const char* fdr_last_error(void);
+typedef struct fdr_ctx fdr_ctx;
+int fdr_ctx_create(int device, fdr_ctx** out);
+int fdr_ctx_destroy(fdr_ctx* ctx);
+int fdr_ctx_device(const fdr_ctx* ctx);
+
+/* ---- perturbation batch (worker/worker.py:26-30) ------------------------------------
+ * out[l, p] = fl32(theta[p] + sign_l * fl32(fl32(sigma) * table[idx_l + p]))  (no FMA)   */
+int fdr_perturb(fdr_ctx* ctx, const float* theta, int64_t n_params, const float* table,
+                int64_t table_size, const int64_t* idx, const int8_t* sign, int32_t n_lanes,
+                float sigma, float* out, fdr_stream stream);
+
+/* ---- batched policy forward (policies/policy.py:26-29 + discrete.py / mujoco.py) -----
+ * One observation per lane: x [n_lanes, n_in].  discrete: out0 = probs [n_lanes, n_act];
+ * mujoco: out0 = mean, out1 = std [n_lanes, n_act].  Replaces Policy.forward / get_strategy. */
+int fdr_policy_forward(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_lanes_desc* lanes,
+                       int32_t n_lanes, const float* x, float* out0, float* out1,
+                       fdr_stream stream);
+
+/* ---- batched episodes (worker/agent.py:20-71 + worker/worker.py:20-57) ----------------
+ * Each lane runs one full episode of env `env` from reset with theta'_l, in ONE launch.
+ *   ret   [n_lanes] f64  sum of rewards (+ counter-stream jiggle if `jiggle`, agent.py:69)
+ *   ent   [n_lanes] f64  mean per-step policy entropy (discrete.py:26-29 / mujoco.py:24-26)
+ *   steps [n_lanes] i32  env.step calls (agent.py:47)
+ *   norm2 [n_lanes] f64  ||sign * fl32(sigma * eps_l)||^2, consumed by fdr_fd_weights
+ *                        (learner/finite_differences.py:107); NULL allowed
+ * obs_mean / obs_std: fixed observation statistics (agent.py:37-41), NULL = no normalisation.
+ * seed: key of the counter random stream for stochastic actions. */
+int fdr_rollout(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc* env,
+                const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
+                const float* obs_mean, const float* obs_std, double* ret, double* ent,
+                int32_t* steps, double* norm2, fdr_stream stream);
+
+/* ---- FD weighting (learner/finite_differences.py:40-49, utils/math_helpers.py:127-134) --
+ * z = standardize(rewards_all - policy_reward) over ALL n_all lanes (f64, population std,
+ * unchanged if std == 0); for the local lanes [lane_lo, lane_lo + n_local):
+ *   coef[d] = sum over the lanes_per_dir lanes of direction d of  z_i * sign_i * sigma / norm2_i
+ * so that g = sum_d coef[d] * table[idx_d : idx_d + P]  ==  sum_i z_i * lambda_i / ||lambda_i||^2.
+ * Lanes with sign 0 contribute nothing (they must not be in rewards_all). */
+int fdr_fd_weights(fdr_ctx* ctx, const double* rewards_all, int32_t n_all, double policy_reward,
+                   int32_t lane_lo, int32_t n_local, const int8_t* sign_local,
+                   const double* norm2_local, int32_t lanes_per_dir, float sigma, double* coef,
+                   fdr_stream stream);
+
+/* ---- noise-weighted gradient reduce (learner/finite_differences.py:49) -----------------
+ * g[p] = sum_d coef[d] * table[idx[d] + p]   (f64, deterministic order)
+ * workspace: device scratch of fdr_fd_grad_workspace_bytes(n_dirs, P) bytes. */
+int64_t fdr_fd_grad_workspace_bytes(int32_t n_dirs, int64_t n_params);
+int fdr_fd_grad(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx,
+                const double* coef, int32_t n_dirs, int64_t n_params, double* g, void* workspace,
+                int64_t workspace_bytes, fdr_stream stream);
+
+/* ---- DSGD update (dsgd/dynamic_sgd.py:19-51, policies/policy.py:63-70) -----------------
+ * grad = fl32(-g); norm = ||grad||; coef = lr * sqrt(P) * lr_scale / norm;
+ * theta <- fl32(theta - fl32(fl32(coef) * grad)).
+ * out[0] = ||theta_old - theta_new|| (learner/finite_differences.py:59), out[1] = ||grad||
+ * (0 -> the reference's `assert norm > 0` failed; theta is left unchanged).  out: device f64[2].
+ * workspace: fdr_dsgd_workspace_bytes(P) bytes. */
+int64_t fdr_dsgd_workspace_bytes(int64_t n_params);
+int fdr_dsgd_step(fdr_ctx* ctx, float* theta, const double* g, int64_t n_params, double lr,
+                  double lr_scale, double* out, void* workspace, int64_t workspace_bytes,
+                  fdr_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FDR_H_ */

@@ -282,6 +282,9 @@ def g5_trap():
         out["det_s%d_theta" % seed] = pol.get_trainable_flat().copy()
     save("g5_trap.npz", **out)
     np.savez_compressed(os.path.join(HERE, "trap_map.npz"), walkable=out["walkable"])
+    # the same bitmap ships with the product's GPU trap env (data, not code)
+    np.savez_compressed(os.path.join(REPO, "dfd-starter_amd", "custom_envs", "simple_trap_env", "trap_map.npz"),
+                        walkable=out["walkable"])
 
 
 class _InjectedDiscrete(object):

@@ -1,0 +1,59 @@
+"""CPU checks of the C-ABI boundary: libfdr.so loads and exports every symbol include/fdr.h declares."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "fdr.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fdr_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for required in ("fdr_perturb", "fdr_policy_forward", "fdr_rollout", "fdr_fd_weights", "fdr_fd_grad",
+                     "fdr_dsgd_step", "fdr_ctx_create", "fdr_last_error"):
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    from fdr import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    assert set(_lib.EXPORTS) == set(declared_functions())
+
+
+def test_version_and_workspace_queries():
+    from fdr import _lib
+    assert "gfx950" in _lib.version()
+    assert _lib.lib.fdr_fd_grad_workspace_bytes(2048, 6092) >= 6092 * 8
+    assert _lib.lib.fdr_dsgd_workspace_bytes(6092) > 0
+
+
+def test_argument_validation_without_gpu():
+    """Invalid calls are rejected before any device work (no GPU needed)."""
+    from fdr import _lib
+    rc = _lib.lib.fdr_perturb(None, None, 10, None, 100, None, None, 1, 0.1, None, None)
+    assert rc == _lib.FDR_ERR_INVALID
+    assert b"NULL" in _lib.lib.fdr_last_error()
+    pd = _lib.PolicyDesc(_lib.FDR_POLICY_MUJOCO, 17, 6, 32, 6092, None, None)   # hidden != 64
+    ld = _lib.LanesDesc(1, 0, None, 0, None, None, 0.0, None)
+    rc = _lib.lib.fdr_policy_forward(None, ctypes.byref(pd), ctypes.byref(ld), 1, 1, 1, 1, None)
+    assert rc == _lib.FDR_ERR_UNSUPPORTED
+
+
+def test_ctx_create_reports_missing_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from fdr import _lib
+    c = ctypes.c_void_p()
+    assert _lib.lib.fdr_ctx_create(0, ctypes.byref(c)) == _lib.FDR_ERR_HIP

@@ -1,0 +1,305 @@
+"""GPU parity of the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Tolerances (DESIGN.md "Parity"):
+  theta' / noise indices / trap-env returns   bit-exact
+  per-step forward                            <= 1e-5 abs (fp32)
+  episode returns (contractive synthetic env) <= 1e-4 relative (+1e-4 abs)
+  gradient                                    rel-L2 <= 1e-5;  theta after DSGD <= 1e-6 abs
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import agent as oagent
+from oracle import envs as oenvs
+from oracle import learner as olearn
+from oracle import noise as onoise
+from oracle import policies as opol
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = {"trap": ("discrete", 2, 9), "cartpole": ("discrete", 4, 2), "cheetah": ("mujoco", 17, 6)}
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from fdr import engine
+    return engine
+
+
+def dev(a, dtype=None):
+    t = torch.as_tensor(np.asarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(DEV).contiguous()
+
+
+_TABLES = {}
+
+
+def table(P, seed=124, size=2 ** 22):
+    k = (P, seed, size)
+    if k not in _TABLES:
+        t = onoise.NoiseTable(size, P, seed)
+        _TABLES[k] = (t, dev(t.table))
+    return _TABLES[k]
+
+
+@pytest.mark.parametrize("name", list(SHAPES))
+def test_perturb_bit_exact_vs_reference(golden, eng, name):
+    g = golden("g2_perturb.npz")
+    theta = g["%s_s124_theta" % name]
+    t, tab = table(theta.size)
+    idx = g[name + "_idx"]
+    sign = np.array([1, 1, 1, 1], np.int8)
+    out = eng.perturb(dev(theta), tab, dev(idx, torch.int64), dev(sign), 0.02).cpu().numpy()
+    assert np.array_equal(out, g[name + "_perturbed"])
+    # antithetic / eval lanes against the oracle's numpy arithmetic
+    sign = np.array([-1, 1, 0, -1], np.int8)
+    out = eng.perturb(dev(theta), tab, dev(idx, torch.int64), dev(sign), 0.02).cpu().numpy()
+    assert np.array_equal(out, onoise.perturb(theta, t.table, idx, sign, 0.02))
+
+
+@pytest.mark.parametrize("name", list(SHAPES))
+def test_policy_forward_vs_reference(golden, eng, name):
+    g = golden("g3_forward.npz")
+    kind, n_in, n_act = SHAPES[name]
+    P = opol.num_params(kind, n_in, n_act)
+    t, tab = table(P)
+    params = (t.decode(int(g[name + "_idx"])) * 0.1).astype(np.float32)
+    x = g[name + "_x"]
+    spec = eng.PolicySpec(kind, n_in, n_act, P)
+    lanes = eng.lanes_desc(dev(params), 0)
+    base = dev(params)
+    lanes = eng.lanes_desc(base, 0)
+    out = eng.policy_forward(spec, lanes, len(x), dev(x))
+    if kind == "discrete":
+        np.testing.assert_allclose(out.cpu().numpy(), g[name + "_probs"], atol=1e-5)
+        stats = [(g["%s_vbn_rm%d" % (name, i)], g["%s_vbn_rv%d" % (name, i)]) for i in range(3)]
+        bm = dev(np.concatenate([s[0] for s in stats]))
+        bv = dev(np.concatenate([s[1] for s in stats]))
+        out = eng.policy_forward(spec, lanes, len(x), dev(x), bm, bv)
+        np.testing.assert_allclose(out.cpu().numpy(), g[name + "_vbn_probs"], atol=1e-5)
+    else:
+        m, s = out
+        np.testing.assert_allclose(m.cpu().numpy(), g[name + "_mean"], atol=1e-5)
+        np.testing.assert_allclose(s.cpu().numpy(), g[name + "_std"], atol=1e-5)
+
+
+@pytest.mark.parametrize("name", list(SHAPES))
+def test_policy_forward_perturbed_lanes(eng, name):
+    kind, n_in, n_act = SHAPES[name]
+    torch.manual_seed(124)
+    pol = opol.TorchPolicy(kind, n_in, n_act, seed=124)
+    theta = pol.get_flat()
+    P = theta.size
+    t, tab = table(P)
+    L = 96
+    idx = t.sample_indices(L)
+    sign = np.tile(np.array([1, -1, 0], np.int8), L // 3)
+    x = np.random.RandomState(3).randn(L, n_in).astype(np.float32)
+    spec = eng.PolicySpec(kind, n_in, n_act, P)
+    lanes = eng.lanes_desc(dev(theta), 0, tab, dev(idx, torch.int64), dev(sign), 0.02)
+    out = eng.policy_forward(spec, lanes, L, dev(x))
+    thetas = onoise.perturb(theta, t.table, idx, sign, 0.02)
+    ref = opol.lanes_forward(kind, n_in, n_act, thetas, x)
+    if kind == "discrete":
+        np.testing.assert_allclose(out.cpu().numpy(), ref, atol=1e-5)
+    else:
+        np.testing.assert_allclose(out[0].cpu().numpy(), ref[0], atol=1e-5)
+        np.testing.assert_allclose(out[1].cpu().numpy(), ref[1], atol=1e-5)
+
+
+def _rollout_case(eng, name, L, T, det, seed=7, antithetic=True):
+    kind, n_in, n_act = SHAPES[name]
+    torch.manual_seed(124)
+    pol = opol.TorchPolicy(kind, n_in, n_act, seed=124)
+    theta = pol.get_flat()
+    P = theta.size
+    t, tab = table(P)
+    if antithetic:
+        idx = np.repeat(t.sample_indices(L // 2), 2)
+        sign = np.tile(np.array([1, -1], np.int8), L // 2)
+    else:
+        idx = t.sample_indices(L)
+        sign = np.ones(L, np.int8)
+    sign[-2:] = 0                              # two eval lanes
+    dflag = np.full(L, 1 if det else 0, np.int8)
+    dflag[-2:] = 1
+    from envs import SyntheticEnv
+    env = SyntheticEnv(n_in, n_act, kind == "discrete", T, env_seed=0)
+    spec = eng.PolicySpec(kind, n_in, n_act, P)
+    lanes = eng.lanes_desc(dev(theta), 0, tab, dev(idx, torch.int64), dev(sign), 0.02, dev(dflag))
+    res = eng.rollout(spec, env, lanes, L, seed)
+    oenv = oenvs.BatchedSyntheticEnv(n_in, n_act, kind == "discrete", T, L, env_seed=0)
+    ref = oagent.evaluate_lanes(kind, n_in, n_act, theta, t.table, idx, sign, 0.02, oenv, seed,
+                                deterministic=dflag.astype(bool))
+    return res, ref
+
+
+@pytest.mark.parametrize("name,det", [("cheetah", False), ("cheetah", True), ("cartpole", False),
+                                      ("cartpole", True)])
+def test_rollout_vs_oracle(eng, name, det):
+    res, (r_ret, r_ent, r_steps, r_n2) = _rollout_case(eng, name, 64, 200, det)
+    ret = res.reward.cpu().numpy()
+    np.testing.assert_allclose(ret, r_ret, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(res.entropy.cpu().numpy(), r_ent, rtol=1e-5, atol=1e-5)
+    assert np.array_equal(res.timesteps.cpu().numpy(), r_steps)
+    np.testing.assert_allclose(res.norm2.cpu().numpy(), r_n2, rtol=1e-9, atol=0)
+
+
+def test_rollout_reproducible_and_antithetic_norms(eng):
+    torch.manual_seed(124)
+    pol = opol.TorchPolicy("mujoco", 17, 6, seed=124)
+    theta = pol.get_flat()
+    t, tab = table(theta.size)
+    L = 32
+    idx = np.repeat(t.sample_indices(L // 2), 2)
+    sign = np.tile(np.array([1, -1], np.int8), L // 2)
+    sign[-2:] = 0
+    from envs import SyntheticEnv
+    env = SyntheticEnv(17, 6, False, 50)
+    spec = eng.PolicySpec("mujoco", 17, 6, theta.size)
+    lanes = eng.lanes_desc(dev(theta), 0, tab, dev(idx, torch.int64), dev(sign), 0.02)
+    res1 = eng.rollout(spec, env, lanes, L, 7)
+    res2 = eng.rollout(spec, env, lanes, L, 7)
+    assert torch.equal(res1.reward, res2.reward) and torch.equal(res1.entropy, res2.entropy)
+    n2 = res1.norm2.cpu().numpy()
+    assert np.array_equal(n2[0:-2:2], n2[1:-2:2])     # +eps / -eps lanes share ||lambda||
+    assert np.all(n2[-2:] == 0)                       # eval lanes are unperturbed
+
+
+def test_trap_env_deterministic_vs_reference(golden, eng):
+    g = golden("g5_trap.npz")
+    from envs import TrapEnv
+    env = TrapEnv()
+    for seed in (124, 1, 2):
+        theta = g["det_s%d_theta" % seed]
+        spec = eng.PolicySpec("discrete", 2, 9, theta.size)
+        lanes = eng.lanes_desc(dev(theta), 0, deterministic=dev(np.ones(1, np.int8)))
+        res = eng.rollout(spec, env, lanes, 1, 0, jiggle=False)
+        ref = g["det_s%d" % seed]
+        assert res.reward.item() == round(ref[0])              # integer-exact (jiggle off)
+        assert res.timesteps.item() == ref[2]
+        assert abs(res.entropy.item() - ref[1]) < 1e-5
+
+
+def test_trap_env_sampled_vs_oracle(eng):
+    torch.manual_seed(124)
+    pol = opol.TorchPolicy("discrete", 2, 9, seed=124)
+    theta = pol.get_flat()
+    t, tab = table(theta.size)
+    L = 8
+    idx = t.sample_indices(L)
+    sign = np.ones(L, np.int8)
+    from envs import TrapEnv
+    from oracle import rng as crng
+    spec = eng.PolicySpec("discrete", 2, 9, theta.size)
+    lanes = eng.lanes_desc(dev(theta), 0, tab, dev(idx, torch.int64), dev(sign), 0.5)
+    res = eng.rollout(spec, TrapEnv(), lanes, L, 99, jiggle=False)
+    thetas = onoise.perturb(theta, t.table, idx, sign, 0.5)
+    for l in range(L):
+        pol.set_flat(thetas[l])
+        env = oenvs.TrapEnv()
+        r, e, steps, _ = oagent.collect_return(
+            pol, env, env.reset(), False, lambda s, l=l: np.float32(crng.uniform(99, l, s, 0)), lambda: 0.0)
+        assert res.reward[l].item() == r
+        assert res.timesteps[l].item() == steps == 201
+        assert abs(res.entropy[l].item() - e) < 1e-5
+
+
+@pytest.mark.parametrize("case", ["cheetah_n16", "cheetah_n64", "trap_n16"])
+def test_fd_step_vs_reference(golden, eng, case):
+    """weights -> gradient reduce -> DSGD on the device vs the reference's FiniteDifferences.step."""
+    g = golden("g4_fd_step.npz")
+    theta0 = g[case + "_theta0"]
+    P = theta0.size
+    t, tab = table(P)
+    idx = g[case + "_idx"]
+    N = idx.size
+    sign = np.ones(N, np.int8)
+    s32 = np.float32(0.02)
+    n2 = np.array([float(np.dot((t.decode(i) * s32).astype(np.float64), (t.decode(i) * s32).astype(np.float64)))
+                   for i in idx])
+    rewards = dev(g[case + "_rewards"])
+    coef = eng.fd_weights(rewards, 0.25, 0, dev(sign), dev(n2), 1, 0.02)
+    grad = eng.fd_grad(tab, dev(idx, torch.int64), coef, P)
+    gref = g[case + "_g"]
+    assert np.linalg.norm(grad.cpu().numpy() - gref) / np.linalg.norm(gref) < 1e-5
+    theta = dev(theta0)
+    om = float(g[case + "_omega"])
+    lr_scale = olearn.affine_transform(om, 0, 1, 0.23, 1.0)
+    out = eng.dsgd_step(theta, grad, 0.01, lr_scale).cpu().numpy()
+    np.testing.assert_allclose(theta.cpu().numpy(), g[case + "_theta1"], rtol=0, atol=1e-6)
+    assert abs(out[0] - float(g[case + "_update"])) < 1e-5
+
+
+def test_fd_grad_matches_oracle_antithetic(eng):
+    P = 6092
+    t, tab = table(P)
+    D = 300
+    idx = t.sample_indices(D)
+    rng = np.random.RandomState(4)
+    r = rng.randn(2 * D)
+    lidx = np.repeat(idx, 2)
+    sign = np.tile(np.array([1, -1], np.int8), D)
+    s32 = np.float32(0.02)
+    n2 = np.array([float(np.dot((t.decode(i) * s32).astype(np.float64), (t.decode(i) * s32).astype(np.float64)))
+                   for i in lidx])
+    coef = eng.fd_weights(dev(r), -0.3, 0, dev(sign), dev(n2), 2, 0.02)
+    grad = eng.fd_grad(tab, dev(idx, torch.int64), coef, P).cpu().numpy()
+    gref, _ = olearn.fd_gradient(t.table, P, lidx, sign, r, -0.3, 0.02)
+    assert np.linalg.norm(grad - gref) / np.linalg.norm(gref) < 1e-5
+
+
+def test_dsgd_zero_gradient_reports_norm_zero(eng):
+    theta = dev(np.ones(100, np.float32))
+    out = eng.dsgd_step(theta, torch.zeros(100, dtype=torch.float64, device=DEV), 0.01, 1.0).cpu().numpy()
+    assert out[1] == 0.0 and out[0] == 0.0
+    assert torch.all(theta == 1)
+
+
+def test_full_size_properties(eng):
+    """BASELINE config 3 size (4096 lanes x T=1000): size-independent properties + sampled parity."""
+    name = "cheetah"
+    kind, n_in, n_act = SHAPES[name]
+    torch.manual_seed(124)
+    pol = opol.TorchPolicy(kind, n_in, n_act, seed=124)
+    theta = pol.get_flat()
+    P = theta.size
+    t, tab = table(P, size=25_000_000)
+    L, T = 4096, 1000
+    idx = np.repeat(t.sample_indices(L // 2), 2)
+    sign = np.tile(np.array([1, -1], np.int8), L // 2)
+    from envs import SyntheticEnv
+    env = SyntheticEnv(n_in, n_act, False, T)
+    spec = eng.PolicySpec(kind, n_in, n_act, P)
+    lanes = eng.lanes_desc(dev(theta), 0, tab, dev(idx, torch.int64), dev(sign), 0.02)
+    res = eng.rollout(spec, env, lanes, L, 5)
+    res2 = eng.rollout(spec, env, lanes, L, 5)
+    ret = res.reward.cpu().numpy()
+    assert np.isfinite(ret).all() and torch.equal(res.reward, res2.reward)
+    assert (res.timesteps.cpu().numpy() == T).all()
+    n2 = res.norm2.cpu().numpy()
+    assert np.array_equal(n2[0::2], n2[1::2])
+    # sampled lanes against the oracle at full episode length
+    pick = np.array([0, 1, 777, 2048, 4095])
+    oenv = oenvs.BatchedSyntheticEnv(n_in, n_act, False, T, len(pick), env_seed=0)
+    # the counter stream is keyed by the lane id, so evaluate the picked lanes with their ids
+    ref = _oracle_lanes_with_ids(kind, n_in, n_act, theta, t.table, idx[pick], sign[pick], oenv, 5, pick)
+    np.testing.assert_allclose(ret[pick], ref, rtol=1e-4, atol=1e-4)
+
+
+def _oracle_lanes_with_ids(kind, n_in, n_act, theta, tab, idx, sign, env, seed, ids):
+    from oracle import rng as crng
+    thetas = onoise.perturb(theta, tab, idx, sign, 0.02)
+    obs = env.reset()
+    ret = np.zeros(len(ids))
+    lanes = np.asarray(ids, dtype=np.uint64)
+    for s in range(env.episode_len):
+        mean, std = opol.lanes_forward(kind, n_in, n_act, thetas, obs)
+        z = crng.normal(seed, lanes[:, None], s, np.arange(n_act, dtype=np.uint64)[None, :])
+        obs, r = env.step((mean + std * z).astype(np.float32))
+        ret += r
+    return ret + crng.jiggle(seed, lanes)
