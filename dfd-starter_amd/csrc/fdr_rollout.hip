@@ -150,14 +150,14 @@ struct MlpLane {
   // Both hidden layers and the head: returns the head pre-activation for output o = j & 15
   // (identical in the 4 rows).  X = row all-gather of the policy input.
   __device__ __forceinline__ float forward(const float (&X)[NQI], int j) const {
-    float z = b1;
+    float z;
     if constexpr (kW1Lds) {
       float wt[NIN];
 #pragma unroll
       for (int k = 0; k < NIN; ++k) wt[k] = w1s[k * kWave + j];
-      fmac_vec<NIN>(z, X, wt);
+      z = dot_gathered<NIN>(X, wt, b1);
     } else {
-      fmac_vec<NIN>(z, X, w1);
+      z = dot_gathered<NIN>(X, w1, b1);
     }
     float h;
     if constexpr (DISC) {
@@ -167,15 +167,13 @@ struct MlpLane {
     }
     float Hq[4];
     row_allgather<4>(h, Hq);
-    z = b2;
-    fmac_vec<kHidden>(z, Hq, w2);
+    z = dot_gathered<kHidden>(Hq, w2, b2);
     if constexpr (DISC) {
       h = fmaf(fmaxf(z, 0.f), a2, c2);
     } else {
       h = tanh_fast(z);
     }
-    float y = 0.f;
-    fmac_bcast16(y, h, w3);  // row r: inputs 16 r .. 16 r + 15 are the row's own lanes
+    const float y = dot_row16(h, w3, 0.f);  // row r: inputs 16 r .. 16 r + 15 are its own lanes
     return row_allreduce_sum(y) + b3;
   }
 
@@ -273,10 +271,23 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
   const int T = a.T;
   const uint64_t key = a.key;
   const uint64_t ulane = (uint64_t)lane;
-  double racc = 0.0, eacc = 0.0;
+  double racc = 0.0;
+  float eacc = 0.f;  // per-lane entropy sum (f32: T terms of O(1), rel. error ~1e-7 * sqrt(T))
   const int o = j & 15;
+  // Random draws are made in batches: one counter hash per lane covers up to 64 future draws
+  // (discrete: lane i holds the uniform of step t0 + i; continuous: lane i holds the normal of
+  // step t0 + i / NA, dim i % NA).  Same (lane, t, k) counters as drawing them one at a time.
+  constexpr int kDrawsPerStep = DISC ? 1 : NA;
+  constexpr int kStepsPerBatch = 64 / kDrawsPerStep;
+  float rbuf = 0.f;
 
   for (int t = 0; t < T; ++t) {
+    const int tb = t % kStepsPerBatch;
+    if (!det && tb == 0) {
+      const int ds = j / kDrawsPerStep, dk = j % kDrawsPerStep;
+      const uint64_t h = hash_ctr(key, ulane, (uint64_t)(t + ds), (uint64_t)dk);
+      rbuf = DISC ? uniform24(h) : normal_bm(h);
+    }
     float X[NQI];
     row_allgather<NQI>(policy_input(s), X);
     const float y = pl.forward(X, j);
@@ -290,49 +301,51 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
       float tot = 0.f;  // sequential f32 cumsum, the oracle's order
 #pragma unroll
       for (int i = 0; i < NA; ++i) tot += pv[i];
+      // Branch-free selection (selects, no data-dependent control flow):
+      //   argmax = first maximal index; inverse CDF = first i with cumsum_i > target, i.e. the
+      //   number of (monotone) partial sums <= target, capped at NA - 1.
       if (det) {
         float best = pv[0];
 #pragma unroll
-        for (int i = 1; i < NA; ++i)
-          if (pv[i] > best) {
-            best = pv[i];
-            act_d = i;
-          }
+        for (int i = 1; i < NA; ++i) {
+          act_d = pv[i] > best ? i : act_d;
+          best = fmaxf(best, pv[i]);
+        }
       } else {
-        const float target = uniform24(hash_ctr(key, ulane, (uint64_t)t, 0)) * tot;
+        const float target = readlane_f(rbuf, tb) * tot;
         float c = 0.f;
-        act_d = NA - 1;
-        bool found = false;
 #pragma unroll
-        for (int i = 0; i < NA; ++i) {
+        for (int i = 0; i < NA - 1; ++i) {
           c += pv[i];
-          if (!found && c > target) {
-            act_d = i;
-            found = true;
-          }
+          act_d += c <= target ? 1 : 0;
         }
       }
       // Categorical(probs) entropy: probs normalised, log clamped (torch semantics)
       const float pn = p / tot;
       const float lg = pn > 0.f ? logf(pn) : -FLT_MAX;
-      eacc -= (j < NA) ? (double)(pn * lg) : 0.0;
+      eacc -= (j < NA) ? pn * lg : 0.f;
     } else {
       const float th = tanh_fast(y);
       const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
-      eacc += (j < NA) ? (double)logf(sd) : 0.0;
-      act_c = det ? th : gauss_action(th, sd, normal_bm(hash_ctr(key, ulane, (uint64_t)t, (uint64_t)o)));
+      eacc += (j < NA) ? __logf(sd) : 0.f;
+      const float z = __shfl(rbuf, tb * NA + (o < NA ? o : 0), kWave);  // normal (t, o)
+      act_c = det ? th : gauss_action(th, sd, z);
     }
 
     // ---- env step ----
     if constexpr (ENV == FDR_ENV_SYNTH) {
       float S[NQI];
-      row_allgather<NQI>(s, S);
+      if (!DISC && !norm_obs) {
+#pragma unroll
+        for (int q = 0; q < NQI; ++q) S[q] = X[q];  // policy input == env state: reuse the gather
+      } else {
+        row_allgather<NQI>(s, S);
+      }
       const float* mrow = envM + ji * MS;
       float mr[NIN];
 #pragma unroll
       for (int k = 0; k < NIN; ++k) mr[k] = mrow[k];
-      float pre = 0.f;
-      fmac_vec<NIN>(pre, S, mr);
+      float pre = dot_gathered<NIN>(S, mr, 0.f);
       if constexpr (DISC) {
         pre += envK[ji * KS + act_d];
       } else {
@@ -340,7 +353,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
         float kr[NA];
 #pragma unroll
         for (int m = 0; m < NA; ++m) kr[m] = krow[m];
-        fmac_bcast_tail<0, NA>(pre, act_c, kr);  // a[m] sits in lane m of every row
+        dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in lane m of every row
       }
       s = tanh_fast(pre);
       racc += (double)s;  // lane 0 holds the reward s'[0]; other lanes' sums are discarded
@@ -358,7 +371,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
   }
 
   // ---- epilogue ----
-  const double esum = wave_sum((j < NA) ? eacc : 0.0);
+  const double esum = wave_sum((j < NA) ? (double)eacc : 0.0);
   if (j == 0) {
     double r = racc;
     if (a.jiggle) r += (hash_ctr(key, ulane, kJiggleT, 15) & 1ull) ? 1e-12 : -1e-12;
