@@ -139,7 +139,8 @@ def main():
 
     L = args.perturbations
     n_dirs_global = (L // 2) * world
-    lane_range = (rank * L, (rank + 1) * L)
+    from fdr import dist as fdist
+    lane_range = fdist.lane_range(n_dirs_global, 2, world, rank)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     roll_ms = []
 

@@ -67,6 +67,7 @@ static int lanes_args(const fdr_lanes_desc* l, int n_lanes, int64_t P, LanesArgs
   out->sign = l->sign;
   out->sigma = l->sigma;
   out->deterministic = l->deterministic;
+  out->lane_offset = l->lane_offset;
   return FDR_OK;
 }
 

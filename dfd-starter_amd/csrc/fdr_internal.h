@@ -26,6 +26,7 @@ struct LanesArgs {
   const int8_t* sign;
   float sigma;
   const int8_t* deterministic;
+  int64_t lane_offset;
 
   // A lane whose table offset is out of range is never dereferenced: it runs unperturbed and
   // reports norm2 = NaN, which poisons the FD step visibly instead of faulting the GPU.

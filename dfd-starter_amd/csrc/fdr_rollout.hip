@@ -270,7 +270,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
   }
   const int T = a.T;
   const uint64_t key = a.key;
-  const uint64_t ulane = (uint64_t)lane;
+  const uint64_t ulane = (uint64_t)(a.lanes.lane_offset + lane);  // global lane id
   double racc = 0.0;
   float eacc = 0.f;  // per-lane entropy sum (f32: T terms of O(1), rel. error ~1e-7 * sqrt(T))
   const int o = j & 15;

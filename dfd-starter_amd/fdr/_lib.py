@@ -38,7 +38,7 @@ class EnvDesc(ctypes.Structure):
 class LanesDesc(ctypes.Structure):
     _fields_ = [("base", ctypes.c_void_p), ("base_stride", ctypes.c_int64), ("table", ctypes.c_void_p),
                 ("table_size", ctypes.c_int64), ("idx", ctypes.c_void_p), ("sign", ctypes.c_void_p),
-                ("sigma", ctypes.c_float), ("deterministic", ctypes.c_void_p)]
+                ("sigma", ctypes.c_float), ("deterministic", ctypes.c_void_p), ("lane_offset", ctypes.c_int64)]
 
 
 def _load():

@@ -1,0 +1,55 @@
+"""Multi-GPU sharding of the FD step (DESIGN.md "Multi-GPU").
+
+One process per GPU; the perturbation set is split into contiguous lane slices, one per rank:
+  * every rank draws the FULL index list from its own copy of the shared noise table stream, in
+    the reference's order (utils/noise_sources.py:44-47), and keeps its slice -- no index exchange;
+  * antithetic pairs are never split across ranks (slices are whole directions);
+  * the only data-path exchange per FD step is (1) an all-gather of the per-lane returns (a few KB,
+    needed because the z-score is global: learner/finite_differences.py:43) and (2) ONE all-reduce
+    of the f64 gradient vector (P * 8 bytes); DSGD then runs replicated and bit-identically on
+    every rank.
+Backend "nccl" is RCCL on ROCm (xGMI); the same helpers run on gloo for CPU tests.
+"""
+import torch
+import torch.distributed as dist
+
+
+def active(group=None):
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
+
+def world_rank(group=None):
+    if not active(group):
+        return 1, 0
+    return dist.get_world_size(group), dist.get_rank(group)
+
+
+def lane_range(n_dirs, lanes_per_dir, world, rank):
+    """Contiguous [lo, hi) lane slice of `rank`; whole directions only, remainder to the low ranks."""
+    base, extra = divmod(n_dirs, world)
+    d_lo = rank * base + min(rank, extra)
+    d_hi = d_lo + base + (1 if rank < extra else 0)
+    return d_lo * lanes_per_dir, d_hi * lanes_per_dir
+
+
+def gather_rewards(local, group=None):
+    """All-gather variable-length per-lane rewards -> (all rewards in rank order, this rank's offset)."""
+    ws, rank = world_rank(group)
+    if ws == 1:
+        return local, 0
+    n = torch.tensor([local.numel()], dtype=torch.int64, device=local.device)
+    sizes = [torch.zeros_like(n) for _ in range(ws)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes)
+    buf = torch.zeros(m, dtype=local.dtype, device=local.device)
+    buf[:local.numel()] = local
+    outs = [torch.empty_like(buf) for _ in range(ws)]
+    dist.all_gather(outs, buf, group=group)
+    return torch.cat([o[:s] for o, s in zip(outs, sizes)]), sum(sizes[:rank])
+
+
+def allreduce_grad(g, group=None):
+    if active(group):
+        dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
+    return g

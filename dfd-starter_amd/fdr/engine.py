@@ -39,7 +39,7 @@ def _check_dev(*ts):
             raise ValueError("fdr: tensors must live on the GPU (got %s)" % t.device)
 
 
-def lanes_desc(base, base_stride, table=None, idx=None, sign=None, sigma=0.0, deterministic=None):
+def lanes_desc(base, base_stride, table=None, idx=None, sign=None, sigma=0.0, deterministic=None, lane_offset=0):
     _check_dev(base, table, idx, sign, deterministic)
     if base.dtype != torch.float32 or not base.is_contiguous():
         raise ValueError("base must be contiguous float32")
@@ -55,7 +55,8 @@ def lanes_desc(base, base_stride, table=None, idx=None, sign=None, sigma=0.0, de
                        None if idx is None else idx.data_ptr(),
                        None if sign is None else sign.data_ptr(),
                        float(sigma),
-                       None if deterministic is None else deterministic.data_ptr())
+                       None if deterministic is None else deterministic.data_ptr(),
+                       int(lane_offset))
     # the descriptor holds raw device pointers: keep the tensors alive as long as it lives, or the
     # caching allocator may hand their blocks to the next allocation before the kernel runs
     d._refs = (base, table, idx, sign, deterministic)

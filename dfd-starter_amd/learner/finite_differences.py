@@ -14,9 +14,9 @@ reference's async server mode) add the parameter drift theta_epoch - theta_now t
 """
 import numpy as np
 import torch
-import torch.distributed as dist
 
 from dsgd import DSGD
+from fdr import dist as fdist
 from fdr import engine
 from utils import math_helpers
 
@@ -46,7 +46,7 @@ class FiniteDifferences(object):
 
     # ------------------------------------------------------------------------------------------
     def _distributed(self):
-        return dist.is_available() and dist.is_initialized() and dist.get_world_size(self.process_group) > 1
+        return fdist.active(self.process_group)
 
     def step(self, batch, policy_reward, policy_novelty, policy_entropy):
         """Reference signature; returns the update magnitude ||d theta|| as a float."""
@@ -72,29 +72,14 @@ class FiniteDifferences(object):
         if not bool(train.all()):
             raise ValueError("FDBatch for the learner must not contain eval lanes (sign 0)")
         P = self.policy.num_params
-        if self._distributed():
-            rewards_all, lane_lo = self._gather_rewards(b.reward)
-        else:
-            rewards_all, lane_lo = b.reward, 0
+        rewards_all, lane_lo = fdist.gather_rewards(b.reward, self.process_group)
         coef = engine.fd_weights(rewards_all, policy_reward, lane_lo, b.sign, b.norm2, b.lanes_per_dir,
                                  self.noise_std)
         g = engine.fd_grad(table, b.dir_idx(), coef, P, self.gradient_memory)
         if extra_grad is not None:
             g.add_(extra_grad)
-        if self._distributed():
-            dist.all_reduce(g, group=self.process_group)
+        fdist.allreduce_grad(g, self.process_group)
         return self._apply(g)
-
-    def _gather_rewards(self, local):
-        ws = dist.get_world_size(self.process_group)
-        rank = dist.get_rank(self.process_group)
-        n = torch.tensor([local.numel()], device=local.device)
-        sizes = [torch.zeros_like(n) for _ in range(ws)]
-        dist.all_gather(sizes, n, group=self.process_group)
-        sizes = [int(s.item()) for s in sizes]
-        bufs = [torch.empty(s, dtype=local.dtype, device=local.device) for s in sizes]
-        dist.all_gather(bufs, local.contiguous(), group=self.process_group)
-        return torch.cat(bufs), sum(sizes[:rank])
 
     def _apply(self, g):
         lr_scale = 1.0
@@ -105,6 +90,7 @@ class FiniteDifferences(object):
         else:
             lr = self.gradient_optimizer.param_groups[0]["lr"]
         engine.dsgd_step(self.policy.flat, g, lr, lr_scale, self._out)
+        self.gradient_optimizer.steps = getattr(self.gradient_optimizer, "steps", 0) + 1
         self.epoch += 1
         self._build_distance_map()
         self._update_policy_history()
@@ -145,6 +131,9 @@ class FiniteDifferences(object):
         order = current + stale
         rewards = torch.as_tensor([r.reward for r in order], dtype=torch.float64, device=dev)
         extra = None
+        if stale and self._distributed():
+            raise NotImplementedError("stale (delayed) returns are a single-process path; the sharded "
+                                      "engine is synchronous and never produces them")
         if stale:
             z = torch.as_tensor(math_helpers.standardize_arr(np.subtract([r.reward for r in order], policy_reward)),
                                 dtype=torch.float64, device=dev)
@@ -157,8 +146,7 @@ class FiniteDifferences(object):
                 extra += z[len(current) + k] * (lam / (nrm * nrm)).double()
         if not current:
             g = extra
-            if self._distributed():
-                dist.all_reduce(g, group=self.process_group)
+            fdist.allreduce_grad(g, self.process_group)
             return self._apply(g)
         idx = np.array([int(r.encoded_noise) for r in current], dtype=np.int64)
         sign = np.array([int(getattr(r, "sign", 1) or 1) for r in current], dtype=np.int8)
@@ -176,7 +164,6 @@ class FiniteDifferences(object):
             coef = engine.fd_weights(rewards, policy_reward, 0, b.sign, b.norm2, 1, self.noise_std)
             g = engine.fd_grad(table, b.idx, coef, P, self.gradient_memory)
             g.add_(extra)
-            if self._distributed():
-                dist.all_reduce(g, group=self.process_group)
+            fdist.allreduce_grad(g, self.process_group)
             return self._apply(g)
         return self._step_batch(b, policy_reward)

@@ -54,7 +54,7 @@ class Worker(object):
         ring["events"][slot] = ev
         return out
 
-    def launch(self, idx, sign, det, seed=None, out=None, jiggle=True):
+    def launch(self, idx, sign, det, seed=None, out=None, jiggle=True, lane_offset=0):
         """Run one rollout over explicit lanes (host arrays) -> FDBatch (asynchronous)."""
         p = self.policy
         n = len(idx)
@@ -62,7 +62,7 @@ class Worker(object):
         sign_d = self._to_device(np.asarray(sign, np.int8), torch.int8)
         det_d = self._to_device(np.asarray(det, np.int8), torch.int8)
         table = self.noise_source.device_table(p.flat.device)
-        lanes = engine.lanes_desc(p.flat, 0, table, idx_d, sign_d, self.sigma, det_d)
+        lanes = engine.lanes_desc(p.flat, 0, table, idx_d, sign_d, self.sigma, det_d, lane_offset)
         om, osd = self.agent.obs_norm_tensors(self.fixed_obs_stats.mean, self.fixed_obs_stats.std)
         bm, bv = p.bn_stats()
         if seed is None:
@@ -80,11 +80,17 @@ class Worker(object):
         lpd = 2 if antithetic else 1
         lidx = np.repeat(idx, lpd)
         sign = np.tile(np.array([1, -1], np.int8), n_dirs) if antithetic else np.ones(n_dirs, np.int8)
+        if lane_range == "auto":
+            from fdr import dist as fdist
+            lane_range = fdist.lane_range(n_dirs, lpd, *fdist.world_rank())
         if lane_range is not None:
             lo, hi = lane_range
+            if lo % lpd or hi % lpd:
+                raise ValueError("lane_range must not split antithetic pairs")
             lidx, sign = lidx[lo:hi], sign[lo:hi]
         det = np.zeros(len(lidx), np.int8)
-        res, idx_d, sign_d = self.launch(lidx, sign, det, seed=seed, out=out)
+        lo = 0 if lane_range is None else lane_range[0]
+        res, idx_d, sign_d = self.launch(lidx, sign, det, seed=seed, out=out, lane_offset=lo)
         self.agent.cumulative_timesteps += int(len(lidx)) * self.agent.env.episode_len
         return FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, lidx, sign, self.epoch,
                        lanes_per_dir=lpd)

@@ -80,6 +80,8 @@ typedef struct fdr_lanes_desc {
   const int8_t* sign;   /* [n_lanes] +1 / -1 (antithetic) / 0 (unperturbed, eval lane) */
   float sigma;          /* noise_std */
   const int8_t* deterministic; /* [n_lanes] 1 = argmax/mean action; NULL -> all stochastic */
+  int64_t lane_offset;  /* global id of lane 0: keys the action random stream, so a lane draws the
+                           same numbers whichever GPU shard evaluates it */
 } fdr_lanes_desc;
 
 /* ---- context / errors ---------------------------------------------------------------- */

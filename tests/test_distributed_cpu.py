@@ -1,0 +1,83 @@
+"""N>1 path on CPU: world_size-2 gloo ranks run the engine's exchange protocol (fdr.dist) with the
+oracle's arithmetic and must reproduce the single-process FD gradient."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from conftest import PKG, REPO
+
+
+def test_lane_range_partitions_whole_directions():
+    from fdr import dist as fdist
+    for n_dirs in (1, 7, 64, 2048, 2049):
+        for world in (1, 2, 3, 8):
+            for lpd in (1, 2):
+                covered = []
+                for r in range(world):
+                    lo, hi = fdist.lane_range(n_dirs, lpd, world, r)
+                    assert lo % lpd == 0 and hi % lpd == 0
+                    covered.extend(range(lo, hi))
+                assert covered == list(range(n_dirs * lpd))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, out_dir):
+    sys.path[:0] = [REPO, PKG]
+    import torch.distributed as dist
+    from fdr import dist as fdist
+    from oracle import learner as olearn
+    from oracle import noise as onoise
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    P, D, sigma = 1000, 37, 0.02
+    t = onoise.NoiseTable(1 << 16, P, 5)
+    idx = t.sample_indices(D)                        # every rank draws the full stream
+    lidx = np.repeat(idx, 2)
+    sign = np.tile(np.array([1, -1], np.int8), D)
+    rewards = np.random.RandomState(3).randn(2 * D)  # "rollout" results, globally consistent
+    lo, hi = fdist.lane_range(D, 2, world, rank)
+    local = torch.as_tensor(rewards[lo:hi])
+    r_all, lane_lo = fdist.gather_rewards(local)
+    assert lane_lo == lo and np.array_equal(r_all.numpy(), rewards)
+    # coefficient of every local lane with the GLOBAL z-score, then the local partial gradient
+    x = r_all.numpy() - 0.1
+    m, s = x.mean(), x.std()
+    z = (x - m) / s
+    V, _ = olearn.perturbation_vectors(t.table, P, lidx[lo:hi], sign[lo:hi], sigma)
+    g = torch.as_tensor(np.dot(z[lo:hi], V))
+    fdist.allreduce_grad(g)
+    np.save(os.path.join(out_dir, "g%d.npy" % rank), g.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_two_rank_gradient_matches_single_process(tmp_path, world):
+    port = _free_port()
+    mp.spawn(_rank_main, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    from oracle import learner as olearn
+    from oracle import noise as onoise
+    P, D = 1000, 37
+    t = onoise.NoiseTable(1 << 16, P, 5)
+    idx = t.sample_indices(D)
+    lidx = np.repeat(idx, 2)
+    sign = np.tile(np.array([1, -1], np.int8), D)
+    rewards = np.random.RandomState(3).randn(2 * D)
+    g_ref, _ = olearn.fd_gradient(t.table, P, lidx, sign, rewards, 0.1, 0.02)
+    for r in range(world):
+        g = np.load(os.path.join(str(tmp_path), "g%d.npy" % r))
+        assert np.linalg.norm(g - g_ref) / np.linalg.norm(g_ref) < 1e-12
+    # every rank holds the identical reduced gradient -> replicated DSGD stays in lock-step
+    assert np.array_equal(np.load(os.path.join(str(tmp_path), "g0.npy")),
+                          np.load(os.path.join(str(tmp_path), "g1.npy")))

@@ -1,0 +1,24 @@
+#!/bin/bash
+# rocprofv3 runs for the bench workload (GPU box).  Kernel trace + stats, then separate PMC passes.
+# Usage: bash tools/profile.sh <tag> [bench args...]
+set -u
+TAG=${1:-r01}; shift || true
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+FAULT='HSA_STATUS_ERROR|illegal memory access|Memory access fault|hipErrorIllegalAddress'
+run() {  # run <name> <rocprof args...> -- handled by caller
+  local name=$1; shift
+  timeout -k 10 600 rocprofv3 "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -3 "$OUT/$name.log"
+  if grep -qE "$FAULT" "$OUT/$name.log"; then echo "GPU FAULT -- stopping"; exit 3; fi
+  [ "$rc" -eq 0 ] || exit "$rc"
+}
+BENCH="bench.py --steps 20 --warmup 3 --no-cpu-baseline $*"
+run trace --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 $BENCH
+run pmc_fetch --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 $BENCH
+run pmc_write --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 $BENCH
+run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
+    --output-format csv -d "$OUT/pmc_sq" -o run -- python3 $BENCH
+ls -R "$OUT" | head -50

@@ -1,0 +1,71 @@
+"""Summarise a tools/profile.sh output directory into profiles/<tag>_summary.md + the PMC json
+bench.py reads (profiles/pmc_rollout_<config>.json).
+
+    python tools/summarize_prof.py gpurun_out/prof_r01 r01 [config]
+
+HBM bytes per launch = FETCH_SIZE*1024*2 + WRITE_SIZE*1024: MI355X_MICROARCH.md section HBM --
+on gfx950 FETCH_SIZE reports half of a wide coalesced read; that x2 correction is applied to the
+read side, and the raw counters are kept beside it (other access widths are uncalibrated).
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def per_kernel(path, counter=None):
+    out = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if counter is None or r.get("Counter_Name") == counter:
+            out[r["Kernel_Name"]].append(r)
+    return out
+
+
+def main(d, tag, config="halfcheetah"):
+    stats = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
+    fetch = per_kernel(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = per_kernel(os.path.join(d, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    sq = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(os.path.join(d, "pmc_sq", "run_counter_collection.csv"))):
+        sq[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    lines = ["# rocprofv3 summary -- %s (bench.py --steps 20 --warmup 3, 1x MI355X)" % tag, "",
+             "Kernel stats (`rocprofv3 --kernel-trace --stats`):", "",
+             "| kernel | calls | total ms | avg us | pct |", "|---|---|---|---|---|"]
+    for s in stats:
+        lines.append("| %s | %s | %.3f | %.2f | %.1f |" % (s["Name"][:70], s["Calls"], float(s["TotalDurationNs"]) / 1e6,
+                                                          float(s["AverageNs"]) / 1e3, float(s["Percentage"])))
+    lines += ["", "PMC (separate passes, averaged over dispatches):", "",
+              "| kernel | FETCH_SIZE KB | WRITE_SIZE KB | HBM bytes/launch (fetch x2 + write) | SQ_INSTS_VALU | "
+              "SQ_INSTS_LDS | SQ_WAVES | GRBM_GUI_ACTIVE |", "|---|---|---|---|---|---|---|---|"]
+    rollout = None
+    for k in fetch:
+        f = sum(float(r["Counter_Value"]) for r in fetch[k]) / len(fetch[k])
+        w = sum(float(r["Counter_Value"]) for r in write.get(k, [])) / max(1, len(write.get(k, [])))
+        hbm = f * 1024 * 2 + w * 1024
+        q = {c: sum(v) / len(v) for c, v in sq.get(k, {}).items()}
+        lines.append("| %s | %.1f | %.1f | %.0f | %.0f | %.0f | %.0f | %.0f |" % (
+            k[:70], f, w, hbm, q.get("SQ_INSTS_VALU", 0), q.get("SQ_INSTS_LDS", 0), q.get("SQ_WAVES", 0),
+            q.get("GRBM_GUI_ACTIVE", 0)))
+        if "rollout_kernel" in k:
+            rollout = dict(kernel=k, fetch_size_kb=f, write_size_kb=w, hbm_bytes_per_launch=hbm, sq=q)
+    if rollout:
+        st = [s for s in stats if "rollout_kernel" in s["Name"]][0]
+        avg_ns = float(st["AverageNs"])
+        q = rollout["sq"]
+        clk = q.get("GRBM_GUI_ACTIVE", 0) / 8 / (avg_ns * 1e-9) / 1e9 if avg_ns else 0
+        rollout["avg_duration_us"] = avg_ns / 1e3
+        rollout["effective_clock_ghz"] = clk
+        lines += ["", "Rollout kernel: avg %.1f us, effective clock %.2f GHz (GRBM_GUI_ACTIVE/8/duration), "
+                      "VALU instructions per wave-step %.1f, LDS per wave-step %.1f." % (
+                          avg_ns / 1e3, clk, q.get("SQ_INSTS_VALU", 0) / max(1, q.get("SQ_WAVES", 1)) / 1000,
+                          q.get("SQ_INSTS_LDS", 0) / max(1, q.get("SQ_WAVES", 1)) / 1000)]
+        with open(os.path.join("profiles", "pmc_rollout_%s.json" % config), "w") as fh:
+            json.dump(dict(rollout, source=d, tag=tag), fh, indent=1)
+    with open(os.path.join("profiles", "%s_summary.md" % tag), "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
