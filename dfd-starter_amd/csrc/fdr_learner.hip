@@ -106,18 +106,18 @@ int launch_fd_weights(const double* r_all, int n_all, double pr, int lo, int n_l
 // ------------------------------------------------------------------------------------------
 // Noise-weighted gradient: g[p] = sum_d coef[d] * table[idx[d] + p]
 // ------------------------------------------------------------------------------------------
-constexpr int kGradThreads = 256;
-constexpr int kGradCols = 4 * kGradThreads;  // 4 strided columns per thread (coalesced)
+constexpr int kGradThreads = 256;  // one column per thread: a wave reads 256 contiguous bytes per row
+constexpr int kGradMinRows = 64;   // rows per chunk: bounds the partial slabs to n_dirs/64 * P * 8 B
 
 struct GradPlan {
   int col_blocks, rows_per_chunk, n_chunks;
 };
 static GradPlan grad_plan(int n_dirs, int64_t P) {
   GradPlan g;
-  g.col_blocks = (int)((P + kGradCols - 1) / kGradCols);
-  // aim for ~1024 workgroups (4 per CU), at least 8 rows per chunk
-  int target_chunks = std::max(1, 1024 / std::max(1, g.col_blocks));
-  g.rows_per_chunk = std::max(8, (n_dirs + target_chunks - 1) / target_chunks);
+  g.col_blocks = (int)((P + kGradThreads - 1) / kGradThreads);
+  // aim for ~1024 workgroups (4 per CU) without letting the slab count explode
+  const int target_chunks = std::max(1, 1024 / std::max(1, g.col_blocks));
+  g.rows_per_chunk = std::max(kGradMinRows, (n_dirs + target_chunks - 1) / target_chunks);
   g.n_chunks = (n_dirs + g.rows_per_chunk - 1) / g.rows_per_chunk;
   return g;
 }
@@ -132,49 +132,36 @@ __global__ __launch_bounds__(kGradThreads) void fd_grad_partial_kernel(
     const float* __restrict__ table, int64_t max_idx, const int64_t* __restrict__ idx,
     const double* __restrict__ coef, int n_dirs, int64_t P, int rows_per_chunk,
     double* __restrict__ partial) {
-  const int64_t c0 = (int64_t)blockIdx.x * kGradCols + threadIdx.x;
+  const int64_t c = (int64_t)blockIdx.x * kGradThreads + threadIdx.x;
   const int chunk = blockIdx.y;
   const int d0 = chunk * rows_per_chunk;
   const int d1 = min(n_dirs, d0 + rows_per_chunk);
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  bool ok[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) ok[q] = c0 + q * kGradThreads < P;
-  int d = d0;
+  const bool ok = c < P;
+  const int64_t cc = ok ? c : 0;
   // an out-of-range offset reads row 0 with a NaN weight: the gradient is poisoned, never a fault
-  auto row = [&](int dd, double& c) {
+  auto row = [&](int dd, double& w) {
     const int64_t off = idx[dd];
     const bool bad = off < 0 || off > max_idx;
-    c = bad ? __builtin_nan("") : coef[dd];
+    w = bad ? __builtin_nan("") : coef[dd];
     return table + (bad ? 0 : off);
   };
-  for (; d + 2 <= d1; d += 2) {  // two rows in flight per iteration
-    double ca, cb;
-    const float* ra = row(d, ca);
-    const float* rb = row(d + 1, cb);
-    float va[4], vb[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      va[q] = ok[q] ? ra[c0 + q * kGradThreads] : 0.f;
-      vb[q] = ok[q] ? rb[c0 + q * kGradThreads] : 0.f;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      acc[q] = fma(ca, (double)va[q], acc[q]);
-      acc[q] = fma(cb, (double)vb[q], acc[q]);
-    }
+  double acc0 = 0.0, acc1 = 0.0;
+  int d = d0;
+  for (; d + 4 <= d1; d += 4) {  // four rows in flight
+    double w0, w1, w2, w3;
+    const float v0 = row(d, w0)[cc], v1 = row(d + 1, w1)[cc];
+    const float v2 = row(d + 2, w2)[cc], v3 = row(d + 3, w3)[cc];
+    acc0 = fma(w0, (double)v0, acc0);
+    acc1 = fma(w1, (double)v1, acc1);
+    acc0 = fma(w2, (double)v2, acc0);
+    acc1 = fma(w3, (double)v3, acc1);
   }
   for (; d < d1; ++d) {
-    double ca;
-    const float* ra = row(d, ca);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (ok[q]) acc[q] = fma(ca, (double)ra[c0 + q * kGradThreads], acc[q]);
+    double w;
+    const float v = row(d, w)[cc];
+    acc0 = fma(w, (double)v, acc0);
   }
-  double* out = partial + (int64_t)chunk * P;
-#pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (ok[q]) out[c0 + q * kGradThreads] = acc[q];
+  if (ok) partial[(int64_t)chunk * P + c] = acc0 + acc1;
 }
 
 __global__ __launch_bounds__(256) void fd_grad_reduce_kernel(const double* __restrict__ partial,

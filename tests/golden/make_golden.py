@@ -403,12 +403,75 @@ def g7_worker_synthetic():
     save("g7_worker_synthetic.npz", **out)
 
 
+def g8_impala():
+    """G3 for the ImpalaCNN (policies/impala.py:48-186): reference module, B=1 sequences.
+
+    Params = 0.1 * table slice (seed 7, size 2^22) so they need not be committed; BN running stats
+    are set to non-trivial values so the eval-mode BN folding is exercised.  Two env sequences of
+    3 steps each (B=1 per call, the reference's own usage -- with B>1 its done-mask uses env 0's
+    flag for every env), one with a mid-sequence done.  Also the entropy pass of worker/agent.py:66
+    (all visited obs as one batch through the end-of-episode LSTM state)."""
+    from policies.impala import ImpalaCNN
+    A = 6
+    torch.manual_seed(124)
+    net = ImpalaCNN(A, use_lstm=True)
+    net.eval()
+    P = sum(p.numel() for p in net.parameters())
+    rs = np.random.RandomState(7)
+    table = rs.randn(2 ** 22).astype(np.float32)
+    flat = (table[1000:1000 + P] * np.float32(0.1)).astype(np.float32)
+    with torch.no_grad():
+        torch.nn.utils.vector_to_parameters(torch.as_tensor(flat), net.parameters())
+        bns = [m for m in net.modules() if isinstance(m, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d))]
+        nbn = sum(m.num_features for m in bns)
+        rm = (table[2000000:2000000 + nbn] * np.float32(0.1)).astype(np.float32)
+        rv = (1.0 + 0.5 * np.abs(table[3000000:3000000 + nbn])).astype(np.float32)
+        off = 0
+        for m in bns:
+            n = m.num_features
+            m.running_mean.copy_(torch.as_tensor(rm[off:off + n]))
+            m.running_var.copy_(torch.as_tensor(rv[off:off + n]))
+            off += n
+    feats = []
+    hook = net.fc[0].register_forward_hook(lambda mod, inp, out: feats.append(inp[0].detach().clone()))
+    frng = np.random.RandomState(5)
+    n_seq, T = 2, 3
+    frames = frng.randint(0, 256, size=(n_seq, T, 3, 64, 64)).astype(np.float32)
+    rewards = np.array([[0.0, 2.5, -0.25], [0.0, -3.0, 0.75]], np.float32)
+    dones = np.array([[False, False, False], [False, True, False]])
+    probs = np.zeros((n_seq, T, A), np.float32)
+    hs = np.zeros((n_seq, T, 256), np.float32)
+    cs = np.zeros((n_seq, T, 256), np.float32)
+    feat = np.zeros((n_seq, T, 2048), np.float32)
+    ent_probs = np.zeros((n_seq, T, A), np.float32)
+    with torch.no_grad():
+        for q in range(n_seq):
+            net.state = net.initial_state()
+            for t in range(T):
+                obs = {"frame": torch.as_tensor(frames[q, t]).view(1, 1, 3, 64, 64),
+                       "reward": torch.as_tensor(rewards[q, t]).view(1, 1),
+                       "done": torch.as_tensor(bool(dones[q, t])).view(1, 1)}
+                logits = net(obs)
+                probs[q, t] = torch.softmax(logits, dim=-1).view(-1).numpy()
+                hs[q, t] = net.state[0].view(-1).numpy()
+                cs[q, t] = net.state[1].view(-1).numpy()
+                feat[q, t] = feats[-1].view(-1).numpy()
+            # entropy pass: every visited obs, one batch, through the end-of-sequence state
+            batch = {"frame": torch.as_tensor(frames[q]).view(T, 1, 3, 64, 64),
+                     "reward": torch.as_tensor(rewards[q]).view(T, 1),
+                     "done": torch.as_tensor(np.zeros(T, bool)).view(T, 1)}
+            ent_probs[q] = torch.softmax(net(batch), dim=-1).view(T, A).numpy()
+    hook.remove()
+    save("g8_impala.npz", A=np.array(A), P=np.array(P), table_seed=np.array(7), param_offset=np.array(1000),
+         rm=rm, rv=rv, frames=frames.astype(np.uint8), rewards=rewards, dones=dones, probs=probs, h=hs, c=cs,
+         feat=feat, ent_probs=ent_probs,
+         param_shapes=np.array([str(tuple(p.shape)) for p in net.parameters()]))
+
+
+GENERATORS = {"g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
+              "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g8": g8_impala}
+
 if __name__ == "__main__":
     torch.set_num_threads(1)
-    g1_noise()
-    g2_perturb()
-    g3_forward()
-    g4_fd_step()
-    g5_trap()
-    g6_runner_trap()
-    g7_worker_synthetic()
+    for name in (sys.argv[1:] or sorted(GENERATORS)):
+        GENERATORS[name]()
