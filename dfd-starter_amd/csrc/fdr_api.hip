@@ -7,6 +7,7 @@
 #include <cstring>
 #include <string>
 
+#include "fdr_impala.h"
 #include "fdr_internal.h"
 
 namespace fdr {
@@ -229,3 +230,94 @@ int fdr_dsgd_step(fdr_ctx* ctx, float* theta, const double* g, int64_t n_params,
 }
 
 }  // extern "C"
+
+// ---- ImpalaPolicy ----------------------------------------------------------------------------
+int64_t fdr_impala_num_params(int32_t n_act) {
+  impala::Layout L;
+  return impala::make_layout(n_act, &L) ? L.P : -1;
+}
+
+int64_t fdr_impala_num_bn_stats(void) {
+  impala::Layout L;
+  impala::make_layout(1, &L);
+  return L.n_bn_stats;
+}
+
+static int impala_layout(const fdr_impala_desc* d, impala::Layout* L) {
+  if (!d) return set_error(FDR_ERR_INVALID, "impala desc is NULL");
+  if (!impala::make_layout(d->n_act, L)) return set_error(FDR_ERR_UNSUPPORTED, "n_act must be in 1..32");
+  if (d->n_params != L->P) return set_error(FDR_ERR_INVALID, "n_params does not match the ImpalaCNN layout");
+  return FDR_OK;
+}
+
+int64_t fdr_impala_workspace_bytes(const fdr_impala_desc* d, int32_t n_lanes) {
+  impala::Layout L;
+  if (!d || n_lanes < 0 || !impala::make_layout(d->n_act, &L)) return -1;
+  return impala::plan(L, n_lanes, d->envs_per_lane, d->episode_len, d->entropy != 0).total;
+}
+
+int fdr_impala_rollout(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lanes_desc* lanes,
+                       int32_t n_lanes, uint64_t seed, int32_t jiggle, double* ret, double* ent,
+                       int32_t* steps, double* norm2, int32_t* actions, float* probs, void* ws,
+                       int64_t ws_bytes, fdr_stream stream) {
+  (void)ctx;
+  impala::Layout L;
+  int rc = impala_layout(d, &L);
+  if (rc) return rc;
+  impala::RolloutCall c{};
+  rc = lanes_args(lanes, n_lanes, L.P, &c.lanes);
+  if (rc) return rc;
+  const int E = d->envs_per_lane;
+  if (E != 1 && E != 2 && E != 4 && E != 8) return set_error(FDR_ERR_UNSUPPORTED, "envs_per_lane must be 1, 2, 4 or 8");
+  if (d->episode_len <= 0 || d->episode_len >= (1 << 20)) return set_error(FDR_ERR_INVALID, "episode_len out of range");
+  if (!ret || !ent || !steps) return set_error(FDR_ERR_INVALID, "NULL output");
+  c.layout = &L;
+  c.n_lanes = n_lanes;
+  c.envs = E;
+  c.T = d->episode_len;
+  c.entropy = d->entropy != 0;
+  c.jiggle = jiggle;
+  c.seed = seed;
+  c.env_seed = d->env_seed;
+  c.bn_mean = d->bn_mean;
+  c.bn_var = d->bn_var;
+  c.ret = ret;
+  c.ent = ent;
+  c.steps = steps;
+  c.norm2 = norm2;
+  c.actions = actions;
+  c.probs = probs;
+  return impala::launch_rollout(c, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int64_t fdr_impala_forward_workspace_bytes(int32_t n_act, int32_t n_envs) {
+  impala::Layout L;
+  if (n_envs < 0 || !impala::make_layout(n_act, &L)) return -1;
+  return impala::forward_workspace_bytes(L, n_envs);
+}
+
+int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* d, const float* theta, int32_t n_envs,
+                       const float* frames, const float* reward, const float* notdone, float* h,
+                       float* c, float* probs, float* feat, void* ws, int64_t ws_bytes,
+                       fdr_stream stream) {
+  (void)ctx;
+  impala::Layout L;
+  int rc = impala_layout(d, &L);
+  if (rc) return rc;
+  if (!theta || !frames || !h || !c || !probs) return set_error(FDR_ERR_INVALID, "NULL pointer");
+  if (n_envs < 0) return set_error(FDR_ERR_INVALID, "n_envs < 0");
+  impala::ForwardCall f{};
+  f.layout = &L;
+  f.theta = theta;
+  f.n_envs = n_envs;
+  f.frames = frames;
+  f.reward = reward;
+  f.notdone = notdone;
+  f.h = h;
+  f.c = c;
+  f.probs = probs;
+  f.feat_out = feat;
+  f.bn_mean = d->bn_mean;
+  f.bn_var = d->bn_var;
+  return impala::launch_forward(f, ws, ws_bytes, (hipStream_t)stream);
+}

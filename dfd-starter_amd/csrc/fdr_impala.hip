@@ -1,0 +1,757 @@
+// fdr_impala.hip -- ImpalaPolicy rollouts (policies/impala.py:8-186) on gfx950.
+//
+// Per rollout:   prep    theta'_l = fl32(theta + fl32(sigma * s_l * eps_l)) gathered once into a
+//                        per-lane pack laid out for the kernels (+ |lambda_l|^2 partials)
+// Per step t:    conv    one workgroup per (lane, env): synthetic frame -> 15 convs on f32 MFMA
+//                        (v_mfma_f32_16x16x4_f32), activations LDS-resident, -> relu'd 2048 feature
+//                core    one workgroup per lane (E envs): BN1d + fc + ReLU, LSTM cell, BN1d + head,
+//                        softmax, action, synthetic reward, return
+// After T steps: replay  the reference's entropy pass (worker/agent.py:60-66): the visited obs
+//                        replayed through the LSTM from the end-of-episode state
+//                finish  jiggle, mean entropy, steps, |lambda|^2
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+#include "fdr_impala.h"
+
+namespace fdr {
+namespace impala {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kCh[3] = {16, 32, 32};
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t kFrameSalt = 0x4652414D45533031ull;  // oracle/impala.py FRAME_SALT
+constexpr uint64_t kRewardSalt = 0x5245574152443031ull; // oracle/impala.py REWARD_SALT
+constexpr float kBnEps = 1e-5f;
+
+// ------------------------------------------------------------------------------------------
+// Host: pack layout.  Walks the reference's parameters() order (feat_convs, resnet1, resnet2,
+// fc, core, policy -- policies/impala.py:60-119) and assigns every tensor a pack section.
+// Conv / BN index = stage * 5 + part, part 0 = stage entry, 1/2 = resnet1 bn0+conv0 / bn1+conv1,
+// 3/4 = resnet2; BN 15 = fc BN1d, 16 = head BN1d.  Running stats follow modules() order, which
+// is the same walk.
+// ------------------------------------------------------------------------------------------
+static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+bool make_layout(int n_act, Layout* L) {
+  if (n_act < 1 || n_act > kMaxAct) return false;
+  *L = Layout{};
+  L->n_act = n_act;
+  int32_t dst = 0, src = 0, stat = 0;
+  auto add = [&](int32_t kind, int32_t len, int32_t a, int32_t b, int32_t src_len) {
+    Section& s = L->sec[L->n_sections++];
+    s = Section{dst, len, src, kind, a, b};
+    const int32_t at = dst;
+    dst += len;
+    src += src_len;
+    return at;
+  };
+  auto bn = [&](int idx, int ch) {
+    L->bn_w[idx] = add(kCopy, 2 * ch, 0, 0, 2 * ch);  // weight then bias, contiguous in theta
+    L->bn_b[idx] = L->bn_w[idx] + ch;
+    L->bn_stat[idx] = stat;
+    stat += ch;
+  };
+  auto conv = [&](int idx, int cin, int cout) {
+    const int kpad = (int)round_up(9 * cin, 4);
+    L->conv_w[idx] = add(kConvFrag, kpad * cout, cin, cout, 9 * cin * cout);
+    L->conv_b[idx] = add(kCopy, cout, 0, 0, cout);
+  };
+  int cin = 3;
+  for (int s = 0; s < 3; ++s) {  // feat_convs[s]: BN2d(cin), Conv2d(cin -> c)
+    bn(s * 5, cin);
+    conv(s * 5, cin, kCh[s]);
+    cin = kCh[s];
+  }
+  for (int r = 0; r < 2; ++r)    // resnet1[s], resnet2[s]: (BN, ReLU, Conv) x 2
+    for (int s = 0; s < 3; ++s)
+      for (int j = 0; j < 2; ++j) {
+        const int idx = s * 5 + 1 + 2 * r + j;
+        bn(idx, kCh[s]);
+        conv(idx, kCh[s], kCh[s]);
+      }
+  bn(15, kFeat);                                                   // fc[0] BatchNorm1d(2048)
+  L->fc_wt = add(kTranspose, kFeat * kHid, kHid, kFeat, kFeat * kHid);  // fc[1].weight -> W^T
+  L->fc_b = add(kCopy, kHid, 0, 0, kHid);
+  L->lstm_wt = add(kTranspose, kCoreIn * kGates, kGates, kCoreIn, kCoreIn * kGates);  // W_ih^T
+  add(kTranspose, kHid * kGates, kGates, kHid, kHid * kGates);                        // W_hh^T
+  L->lstm_bih = add(kCopy, 2 * kGates, 0, 0, 2 * kGates);  // b_ih, b_hh
+  L->lstm_bhh = L->lstm_bih + kGates;
+  bn(16, kHid);                                                    // policy[0] BatchNorm1d(256)
+  L->head_w = add(kCopy, n_act * kHid + n_act, 0, 0, n_act * kHid + n_act);  // weight, bias
+  L->head_b = L->head_w + n_act * kHid;
+  L->P = src;
+  L->pack = round_up(dst, 64);
+  L->n_bn_stats = stat;
+  return true;
+}
+
+constexpr int kPrepThreads = 256;
+constexpr int kPrepPer = 4;
+constexpr int kPrepSpan = kPrepThreads * kPrepPer;
+
+Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy) {
+  Plan p{};
+  const int64_t ne = (int64_t)n_lanes * envs;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) { const int64_t at = o; o += round_up(std::max<int64_t>(bytes, 0), 256); return at; };
+  p.nblk = (int)((L.pack + kPrepSpan - 1) / kPrepSpan);
+  p.pack = take((int64_t)n_lanes * L.pack * 4);
+  p.feat = take(ne * kFeat * 4);
+  p.h = take(ne * kHid * 4);
+  p.c = take(ne * kHid * 4);
+  p.rprev = take(ne * 4);
+  p.ci = take(entropy ? (int64_t)T * ne * kCoreIn * 4 : 0);
+  p.n2 = take((int64_t)n_lanes * p.nblk * 8);
+  p.total = o;
+  return p;
+}
+
+// ------------------------------------------------------------------------------------------
+// prep: pack[lane][j] = theta'_lane[src(j)]  (fl32(theta + fl32(sigma * +-eps)), no contraction)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t section_src(const Section& s, int32_t u) {
+  if (s.kind == kCopy) return (int64_t)s.src + u;
+  if (s.kind == kTranspose) {  // pack = W^T: u = k * rows + r  ->  W[r][k]
+    const int32_t k = u / s.a, r = u - k * s.a;
+    return (int64_t)s.src + (int64_t)r * s.b + k;
+  }
+  // conv B-fragment (v_mfma_f32_16x16x4_f32): u = (kstep * NT + nt) * 64 + l; B[k][n] with
+  // k = 4 * kstep + (l >> 4), n = nt * 16 + (l & 15).  K order: Cin % 4 == 0 -> tap-major,
+  // cin = 4 * (kstep % (Cin/4)) + (l >> 4); Cin = 3 -> k = tap * 3 + cin, zero-padded to 28.
+  const int32_t cin = s.a, cout = s.b, nt_n = cout / 16;
+  const int32_t ks = u / (nt_n * 64), rem = u - ks * nt_n * 64;
+  const int32_t nt = rem >> 6, l = rem & 63;
+  const int32_t n = nt * 16 + (l & 15);
+  int32_t tap, ci;
+  if ((cin & 3) == 0) {
+    const int32_t q = cin >> 2;
+    tap = ks / q;
+    ci = 4 * (ks - tap * q) + (l >> 4);
+  } else {
+    const int32_t k = 4 * ks + (l >> 4);
+    if (k >= 9 * cin) return -1;
+    tap = k / cin;
+    ci = k - tap * cin;
+  }
+  return (int64_t)s.src + ((int64_t)n * cin + ci) * 9 + tap;
+}
+
+__global__ __launch_bounds__(kPrepThreads) void prep_kernel(Layout L, LanesArgs lanes, float* __restrict__ pack,
+                                                            double* __restrict__ n2_part) {
+  const int lane = blockIdx.y;
+  ParamSrc src = lanes.src(lane);
+  const int64_t j0 = (int64_t)blockIdx.x * kPrepSpan + threadIdx.x;
+  float* out = pack + (int64_t)lane * L.pack;
+  double n2 = 0.0;
+  const bool bad = src.n2 != src.n2;  // out-of-range table offset: NaN norm, unperturbed lane
+  src.n2 = 0.0;
+#pragma unroll
+  for (int i = 0; i < kPrepPer; ++i) {
+    const int64_t j = j0 + (int64_t)i * kPrepThreads;
+    if (j >= L.pack) break;
+    int lo = 0, hi = L.n_sections - 1;  // last section with dst <= j
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (L.sec[mid].dst <= j) lo = mid; else hi = mid - 1;
+    }
+    const Section& s = L.sec[lo];
+    const int32_t u = (int32_t)(j - s.dst);
+    const int64_t p = u < s.len ? section_src(s, u) : -1;
+    out[j] = p >= 0 ? src.get(p) : 0.f;
+  }
+  n2 = src.n2;
+  // block reduce (deterministic): wave sums, then wave 0
+  __shared__ double red[kPrepThreads / kWave];
+  n2 = wave_sum(n2);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n2;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kPrepThreads / kWave; ++w) t += red[w];
+    n2_part[(int64_t)lane * gridDim.x + blockIdx.x] = bad ? __builtin_nan("") : t;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// conv stack: one workgroup (8 waves) per (lane, env); everything between the frame and the
+// 2048-feature stays in LDS.
+//   T  (guarded, padded NCHW input of the current conv)  18,496 floats
+//   X  (unpadded stage activation / residual stream)      16,384 floats
+//   S  (5-row band of an entry conv's output, pooled into X) lives in whichever is free
+// ------------------------------------------------------------------------------------------
+constexpr int kConvThreads = 512;
+constexpr int kGuard = 128;          // one padded row above T: the band of conv row -1 reads it
+constexpr int kRT = 16 * 34 * 34;
+constexpr int kRX = 16 * 32 * 32;
+constexpr int kBnTab = 15 * 32;
+constexpr int kConvLds = kGuard + kRT + kRX + 2 * kBnTab;
+
+struct StepArgs {
+  const float* pack;
+  int64_t pack_stride;  // floats between lanes' packs (0: every lane shares one pack)
+  const float* bn_mean;
+  const float* bn_var;
+  int n_lanes, envs, n_act, t, T;
+  int64_t lane_offset;
+  uint64_t fkey, rkey, akey;
+  const float* frames;     // external frames [lane*E+e][3][64][64] (forward API) or NULL
+  float* feat;             // [lane*E+e][2048]
+  // core
+  float* h;
+  float* c;
+  float* rprev;
+  float* ci;               // [t][lane*E+e][257] (entropy replay) or NULL
+  double* ret;
+  double* ent;
+  int32_t* actions;        // [lane*E+e][T] or NULL
+  float* probs;            // rollout: [lane*E+e][T][A]; forward: [lane*E+e][A]; or NULL
+  const int8_t* deterministic;
+  const float* reward_in;  // forward: reward carried by the obs
+  const float* notdone;    // forward: done mask (policies/impala.py:170-176)
+};
+
+__device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
+
+// acc[i] (tile q = wave + 8 i) += A_tile(q) * B(nt = wave % NT) over K = 9 * CIN, A gathered from
+// the padded LDS image Tin ([CIN][*][WP], row 0 = padded row of output row 0).
+template <int CIN, int NT, int TPW, int W, int WP, int PLANE, int MT>
+__device__ __forceinline__ void conv_mfma(const float* Tin, const float* __restrict__ wf, f32x4 (&acc)[TPW],
+                                          int wave, int lane) {
+  constexpr int KS = (9 * CIN + 3) / 4;
+  const int nt = wave % NT;
+  float bf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) bf[s] = wf[(s * NT + nt) * 64 + lane];
+  int base[TPW];
+  const int g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    int mt = (wave + 8 * i) / NT;
+    mt = mt < MT ? mt : MT - 1;
+    const int m = mt * 16 + (lane & 15);
+    base[i] = (m / W) * WP + (m % W);
+    acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if constexpr ((CIN & 3) == 0) {
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) base[i] += g * PLANE;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int tap = s / (CIN / 4);
+      const int off = 4 * (s % (CIN / 4)) * PLANE + (tap / 3) * WP + (tap % 3);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(Tin[base[i] + off], bf[s], acc[i], 0, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int k = 4 * s + g;
+      const int tap = k / CIN, ci = k - tap * CIN;
+      const int off = k < 9 * CIN ? ci * PLANE + (tap / 3) * WP + (tap % 3) : 0;  // pad k: weight 0
+#pragma unroll
+      for (int i = 0; i < TPW; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(Tin[base[i] + off], bf[s], acc[i], 0, 0, 0);
+    }
+  }
+}
+
+// Visit the outputs of conv_mfma: f(n, m, v) for channel n, output pixel m (row-major, width W).
+template <int NT, int TPW, int MT, typename F>
+__device__ __forceinline__ void conv_out(const f32x4 (&acc)[TPW], int wave, int lane, F f) {
+  const int n = (wave % NT) * 16 + (lane & 15);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int q = wave + 8 * i;
+    if (q / NT >= MT) continue;
+    const int m0 = (q / NT) * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f(n, m0 + r, acc[i][r]);
+  }
+}
+
+// T <- BN(X) (optionally ReLU) into the padded image [C][H+2][W+2], zero border.
+template <int C, int H, bool RELU>
+__device__ __forceinline__ void to_padded(const float* X, float* T, const float* sc, const float* sh) {
+  constexpr int WP = H + 2, PLANE = WP * WP;
+  for (int i = threadIdx.x; i < C * PLANE; i += kConvThreads) {
+    const int ch = i / PLANE, rem = i - ch * PLANE;
+    const int y = rem / WP - 1, x = rem % WP - 1;
+    float v = 0.f;
+    if (y >= 0 && y < H && x >= 0 && x < H) {
+      v = fmaf(X[(ch * H + y) * H + x], sc[ch], sh[ch]);
+      if (RELU) v = relu(v);
+    }
+    T[i] = v;
+  }
+}
+
+// Stage entry: X <- maxpool3s2p1(conv3x3(T) + b) in 5-row bands (conv rows 4b-1 .. 4b+3 -> pooled
+// rows 2b, 2b+1) through the scratch S; conv row -1 is read from the guard and never pooled.
+template <int CIN, int COUT, int H>
+__device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, const float* __restrict__ wf,
+                                            const float* __restrict__ bias, int wave, int lane) {
+  constexpr int WP = H + 2, PLANE = WP * WP, NT = COUT / 16, MT = 5 * H / 16;
+  constexpr int TPW = (MT * NT + 7) / 8, HO = H / 2;
+  const float bn_ = bias[(wave % NT) * 16 + (lane & 15)];
+  for (int b = 0; b < H / 4; ++b) {
+    f32x4 acc[TPW];
+    conv_mfma<CIN, NT, TPW, H, WP, PLANE, MT>(T + (4 * b - 1) * WP, wf, acc, wave, lane);
+    conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) { S[n * 5 * H + m] = v + bn_; });
+    __syncthreads();
+    for (int i = threadIdx.x; i < COUT * 2 * HO; i += kConvThreads) {
+      const int ch = i / (2 * HO), rem = i - ch * 2 * HO;
+      const int pr = rem / HO, px = rem % HO;
+      float m = -FLT_MAX;
+#pragma unroll
+      for (int dr = 0; dr < 3; ++dr) {
+        const int r = 2 * pr + dr;  // local band row; conv row 4b - 1 + r
+        if (b == 0 && r == 0) continue;
+#pragma unroll
+        for (int dc = -1; dc <= 1; ++dc) {
+          const int x = 2 * px + dc;
+          if (x < 0 || x >= H) continue;
+          m = fmaxf(m, S[(ch * 5 + r) * H + x]);
+        }
+      }
+      X[(ch * HO + 2 * b + pr) * HO + px] = m;
+    }
+    __syncthreads();
+  }
+}
+
+// Two residual blocks (policies/impala.py:77-105, 152-157) on X [C][H][H], T as scratch.
+template <int C, int H>
+__device__ __forceinline__ void res_blocks(float* T, float* X, const float* __restrict__ pk, const Layout& L,
+                                           int stage, const float* bsc, const float* bsh, int wave, int lane) {
+  constexpr int WP = H + 2, PLANE = WP * WP, NT = C / 16, MT = H * H / 16;
+  constexpr int TPW = (MT * NT + 7) / 8;
+  for (int r = 0; r < 2; ++r) {
+    const int i0 = stage * 5 + 1 + 2 * r, i1 = i0 + 1;
+    to_padded<C, H, true>(X, T, bsc + i0 * 32, bsh + i0 * 32);
+    __syncthreads();
+    f32x4 acc[TPW];
+    conv_mfma<C, NT, TPW, H, WP, PLANE, MT>(T, pk + L.conv_w[i0], acc, wave, lane);
+    const int n_ = (wave % NT) * 16 + (lane & 15);
+    const float b0 = pk[L.conv_b[i0] + n_], s1 = bsc[i1 * 32 + n_], h1 = bsh[i1 * 32 + n_];
+    __syncthreads();  // every wave is done reading T
+    conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) {
+      T[n * PLANE + (m / H + 1) * WP + (m % H) + 1] = relu(fmaf(v + b0, s1, h1));
+    });
+    __syncthreads();
+    conv_mfma<C, NT, TPW, H, WP, PLANE, MT>(T, pk + L.conv_w[i1], acc, wave, lane);
+    const float b1 = pk[L.conv_b[i1] + n_];
+    conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) { X[n * H * H + m] = (v + b1) + X[n * H * H + m]; });
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a) {
+  __shared__ float lds[kConvLds];
+  // XCD-aware: the E workgroups of one lane run on one XCD, back to back (shared weights in L2)
+  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+  const int lane = (slot / a.envs) * 8 + xcd, e = slot % a.envs;
+  if (lane >= a.n_lanes) return;
+  const int wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const int64_t env = (int64_t)lane * a.envs + e;
+  const float* pk = a.pack + (int64_t)lane * a.pack_stride;
+  float* T = lds + kGuard;
+  float* X = T + kRT;
+  float* bsc = X + kRX;
+  float* bsh = bsc + kBnTab;
+
+  // eval-mode BN folded per channel: y = x * (w / sqrt(rv + eps)) + (b - rm * scale)
+  for (int i = threadIdx.x; i < kBnTab; i += kConvThreads) {
+    const int idx = i >> 5, ch = i & 31;
+    const int nch = idx == 0 ? 3 : (idx == 5 ? 16 : (idx < 5 ? 16 : 32));
+    float sc = 0.f, sh = 0.f;
+    if (ch < nch) {
+      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[idx] + ch] : 0.f;
+      const float rv = a.bn_var ? a.bn_var[L.bn_stat[idx] + ch] : 1.f;
+      const float inv = 1.f / sqrtf(rv + kBnEps);
+      sc = pk[L.bn_w[idx] + ch] * inv;
+      sh = pk[L.bn_b[idx] + ch] - rm * sc;
+    }
+    bsc[i] = sc;
+    bsh[i] = sh;
+  }
+  for (int i = threadIdx.x; i < kGuard + kRT; i += kConvThreads) lds[i] = 0.f;
+  __syncthreads();
+
+  // ---- frame (policies/impala.py:147: frame / 255) -> BN2d(3) -> padded [3][66][66] ----
+  constexpr int FW = 66, FPLANE = 66 * 66;
+  if (a.frames) {
+    const float* fr = a.frames + env * kFramePix;
+    for (int p = threadIdx.x; p < kFramePix; p += kConvThreads) {
+      const int ch = p >> 12, y = (p >> 6) & 63, x = p & 63;
+      T[ch * FPLANE + (y + 1) * FW + x + 1] = fmaf(fr[p] / 255.0f, bsc[ch], bsh[ch]);
+    }
+  } else {
+    const uint64_t gid = (uint64_t)(a.lane_offset * a.envs + env);
+    for (int w = threadIdx.x; w < kFramePix / 8; w += kConvThreads) {
+      const uint64_t ctr = (gid << 32) | ((uint64_t)a.t << 11) | (uint64_t)w;
+      const uint64_t hb = mix64(a.fkey + ctr * kGolden);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int p = 8 * w + j, ch = p >> 12, y = (p >> 6) & 63, x = p & 63;
+        const float v = (float)((uint32_t)(hb >> (8 * j)) & 255u);
+        T[ch * FPLANE + (y + 1) * FW + x + 1] = fmaf(v / 255.0f, bsc[ch], bsh[ch]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 1: conv 3->16 @64x64, pool -> X [16][32][32], residual blocks ----
+  stage_entry<3, 16, 64>(T, T + 3 * FPLANE, X, pk + L.conv_w[0], pk + L.conv_b[0], wave, ln);
+  res_blocks<16, 32>(T, X, pk, L, 0, bsc, bsh, wave, ln);
+  // ---- stage 2: BN(X) -> T [16][34][34]; conv 16->32 @32x32, pool -> X [32][16][16] ----
+  to_padded<16, 32, false>(X, T, bsc + 5 * 32, bsh + 5 * 32);
+  __syncthreads();
+  stage_entry<16, 32, 32>(T, X + 32 * 16 * 16, X, pk + L.conv_w[5], pk + L.conv_b[5], wave, ln);
+  res_blocks<32, 16>(T, X, pk, L, 1, bsc, bsh, wave, ln);
+  // ---- stage 3: conv 32->32 @16x16, pool -> X [32][8][8] ----
+  to_padded<32, 16, false>(X, T, bsc + 10 * 32, bsh + 10 * 32);
+  __syncthreads();
+  stage_entry<32, 32, 16>(T, X + 32 * 8 * 8, X, pk + L.conv_w[10], pk + L.conv_b[10], wave, ln);
+  res_blocks<32, 8>(T, X, pk, L, 2, bsc, bsh, wave, ln);
+  // ---- relu + flatten (C, H, W) (policies/impala.py:159-160) ----
+  float* out = a.feat + env * kFeat;
+  for (int i = threadIdx.x; i < kFeat; i += kConvThreads) out[i] = relu(X[i]);
+}
+
+// ------------------------------------------------------------------------------------------
+// core: one workgroup (256 threads) per lane, E envs.  Thread j owns fc unit j and LSTM unit j
+// (gate rows j, 256+j, 512+j, 768+j), so the cell update is thread-local; weights stream from the
+// pack as coalesced rows of W^T, activations are LDS broadcasts.
+// ------------------------------------------------------------------------------------------
+enum CoreMode { kRollout = 0, kReplay = 1, kForward = 2 };
+constexpr int kCoreThreads = 256;
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+template <int E, int MODE>
+__global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a) {
+  __shared__ float xs[kFeat * E];    // BN'd features, [k][e]
+  __shared__ float cis[kCoreIn * E]; // core input, [k][e]
+  __shared__ float hs[kHid * E];     // h (then BN(h')), [k][e]
+  __shared__ float logit[E * kMaxAct];
+  const int lane = blockIdx.x, j = threadIdx.x;
+  const float* pk = a.pack + (int64_t)lane * a.pack_stride;
+  const int64_t e0 = (int64_t)lane * E;
+  const int A = a.n_act;
+
+  if constexpr (MODE != kReplay) {
+    for (int k = j; k < kFeat; k += kCoreThreads) {
+      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + k] : 0.f;
+      const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + k] : 1.f;
+      const float sc = pk[L.bn_w[15] + k] * (1.f / sqrtf(rv + kBnEps));
+      const float sh = pk[L.bn_b[15] + k] - rm * sc;
+#pragma unroll
+      for (int e = 0; e < E; ++e) xs[k * E + e] = fmaf(a.feat[(e0 + e) * kFeat + k], sc, sh);
+    }
+    __syncthreads();
+    float acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = 0.f;
+    const float* w = pk + L.fc_wt + j;
+#pragma unroll 8
+    for (int k = 0; k < kFeat; ++k) {
+      const float wk = w[(int64_t)k * kHid];
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] = fmaf(wk, xs[k * E + e], acc[e]);
+    }
+    const float bj = pk[L.fc_b + j];
+#pragma unroll
+    for (int e = 0; e < E; ++e) cis[j * E + e] = relu(acc[e] + bj);
+    if (j < E) {
+      const float r = MODE == kForward ? (a.reward_in ? a.reward_in[e0 + j] : 0.f) : a.rprev[e0 + j];
+      cis[kHid * E + j] = fminf(fmaxf(r, -1.f), 1.f);
+    }
+    if (MODE == kRollout && a.ci) {
+      __syncthreads();
+      float* dst = a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn;
+      for (int i = j; i < kCoreIn * E; i += kCoreThreads) {
+        const int e = i / kCoreIn, k = i - e * kCoreIn;
+        dst[i] = cis[k * E + e];
+      }
+    }
+  } else {
+    const float* src = a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn;
+    for (int i = j; i < kCoreIn * E; i += kCoreThreads) {
+      const int e = i / kCoreIn, k = i - e * kCoreIn;
+      cis[k * E + e] = src[i];
+    }
+  }
+  float cj[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const float nd = (MODE == kForward && a.notdone) ? a.notdone[e0 + e] : 1.f;
+    hs[j * E + e] = nd * a.h[(e0 + e) * kHid + j];
+    cj[e] = nd * a.c[(e0 + e) * kHid + j];
+  }
+  __syncthreads();
+
+  // LSTM cell (torch gate order i, f, g, o): gates = (W_ih x + b_ih) + (W_hh h + b_hh)
+  float ax[4][E], ah[4][E];
+#pragma unroll
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int e = 0; e < E; ++e) ax[g][e] = ah[g][e] = 0.f;
+  const float* wl = pk + L.lstm_wt + j;
+#pragma unroll 2
+  for (int k = 0; k < kCoreIn; ++k) {
+    const float* wr = wl + (int64_t)k * kGates;
+    const float w0 = wr[0], w1 = wr[kHid], w2 = wr[2 * kHid], w3 = wr[3 * kHid];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float x = cis[k * E + e];
+      ax[0][e] = fmaf(w0, x, ax[0][e]);
+      ax[1][e] = fmaf(w1, x, ax[1][e]);
+      ax[2][e] = fmaf(w2, x, ax[2][e]);
+      ax[3][e] = fmaf(w3, x, ax[3][e]);
+    }
+  }
+#pragma unroll 2
+  for (int k = 0; k < kHid; ++k) {
+    const float* wr = wl + (int64_t)(kCoreIn + k) * kGates;
+    const float w0 = wr[0], w1 = wr[kHid], w2 = wr[2 * kHid], w3 = wr[3 * kHid];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float x = hs[k * E + e];
+      ah[0][e] = fmaf(w0, x, ah[0][e]);
+      ah[1][e] = fmaf(w1, x, ah[1][e]);
+      ah[2][e] = fmaf(w2, x, ah[2][e]);
+      ah[3][e] = fmaf(w3, x, ah[3][e]);
+    }
+  }
+  float hj[E];
+  {
+    float bi[4], bh[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      bi[g] = pk[L.lstm_bih + g * kHid + j];
+      bh[g] = pk[L.lstm_bhh + g * kHid + j];
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float gi = sigm((ax[0][e] + bi[0]) + (ah[0][e] + bh[0]));
+      const float gf = sigm((ax[1][e] + bi[1]) + (ah[1][e] + bh[1]));
+      const float gg = tanhf((ax[2][e] + bi[2]) + (ah[2][e] + bh[2]));
+      const float go = sigm((ax[3][e] + bi[3]) + (ah[3][e] + bh[3]));
+      cj[e] = gf * cj[e] + gi * gg;
+      hj[e] = go * tanhf(cj[e]);
+      a.h[(e0 + e) * kHid + j] = hj[e];
+      a.c[(e0 + e) * kHid + j] = cj[e];
+    }
+  }
+  __syncthreads();  // all reads of the old h are done
+  {
+    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
+    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
+    const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
+    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+#pragma unroll
+    for (int e = 0; e < E; ++e) hs[j * E + e] = fmaf(hj[e], sc, sh);
+  }
+  __syncthreads();
+  if (j < A * E) {  // policy head Linear(256 -> A) (policies/impala.py:122, 184)
+    const int ai = j / E, e = j - ai * E;
+    const float* w = pk + L.head_w + ai * kHid;
+    float s = 0.f;
+    for (int k = 0; k < kHid; ++k) s = fmaf(w[k], hs[k * E + e], s);
+    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
+  }
+  __syncthreads();
+  if (j < E) {
+    const int e = j;
+    const float* lg = logit + e * kMaxAct;
+    float mx = -FLT_MAX;
+    for (int i = 0; i < A; ++i) mx = fmaxf(mx, lg[i]);
+    float p[kMaxAct];
+    float sum = 0.f;
+    for (int i = 0; i < A; ++i) {
+      p[i] = expf(lg[i] - mx);
+      sum += p[i];
+    }
+    const float inv = 1.f / sum;
+    for (int i = 0; i < A; ++i) p[i] *= inv;
+    const int64_t ge = e0 + e;
+    if constexpr (MODE == kForward) {
+      if (a.probs)
+        for (int i = 0; i < A; ++i) a.probs[ge * A + i] = p[i];
+    } else if constexpr (MODE == kReplay) {
+      // torch Categorical(probs).entropy(): normalise, log clamped at float min
+      float tot = 0.f;
+      for (int i = 0; i < A; ++i) tot += p[i];
+      float h = 0.f;
+      for (int i = 0; i < A; ++i) {
+        const float pn = p[i] / tot;
+        const float l = pn > 0.f ? logf(pn) : -FLT_MAX;
+        h -= pn * l;
+      }
+      a.ent[ge] += (double)h;
+    } else {
+      if (a.probs)
+        for (int i = 0; i < A; ++i) a.probs[(ge * a.T + a.t) * A + i] = p[i];
+      const uint64_t gid = (uint64_t)(a.lane_offset * E + ge);
+      int act = 0;
+      const bool det = a.deterministic && a.deterministic[lane];
+      if (det) {
+        float best = p[0];
+        for (int i = 1; i < A; ++i)
+          if (p[i] > best) { best = p[i]; act = i; }
+      } else {  // inverse CDF, sequential f32 cumsum (oracle/policies.py categorical_inverse_cdf)
+        float tot = 0.f;
+        for (int i = 0; i < A; ++i) tot += p[i];
+        const float u = uniform24(hash_ctr(a.akey, gid, (uint64_t)a.t, 0));
+        const float target = u * tot;
+        float cs = 0.f;
+        for (int i = 0; i < A - 1; ++i) {
+          cs += p[i];
+          act += cs <= target ? 1 : 0;
+        }
+      }
+      const uint64_t ctr = (gid << 32) | ((uint64_t)a.t << 11);
+      const int tgt = (int)((mix64(a.rkey + ctr * kGolden) >> 40) % (uint64_t)A);
+      const float r = act == tgt ? 1.f : (act == (tgt + 1) % A ? -1.f : 0.f);
+      a.ret[ge] += (double)r;
+      a.rprev[ge] = r;
+      if (a.actions) a.actions[ge * a.T + a.t] = act;
+    }
+  }
+}
+
+__global__ void init_kernel(int64_t n_env, float* h, float* c, float* rprev, double* ret, double* ent) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_env * kHid) { h[i] = 0.f; c[i] = 0.f; }
+  if (i < n_env) { rprev[i] = 0.f; ret[i] = 0.0; ent[i] = 0.0; }
+}
+
+__global__ void finish_kernel(int n_lanes, int envs, int T, int entropy, int jiggle, uint64_t akey,
+                              int64_t lane_offset, const double* n2_part, int nblk, double* ret,
+                              double* ent, int32_t* steps, double* norm2) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (int64_t)n_lanes * envs) {
+    const uint64_t gid = (uint64_t)(lane_offset * envs + i);
+    if (jiggle) ret[i] += (hash_ctr(akey, gid, kJiggleT, 15) & 1ull) ? 1e-12 : -1e-12;
+    if (ent) ent[i] = entropy ? ent[i] / (double)T : 0.0;
+    if (steps) steps[i] = T;
+  }
+  if (i < n_lanes && norm2) {
+    double s = 0.0;
+    for (int b = 0; b < nblk; ++b) s += n2_part[i * nblk + b];
+    norm2[i] = s;
+  }
+}
+
+template <int E>
+static int launch_steps(const Layout& L, StepArgs a, int entropy, hipStream_t stream) {
+  const int conv_grid = (a.n_lanes + 7) / 8 * 8 * a.envs;
+  for (int t = 0; t < a.T; ++t) {
+    a.t = t;
+    hipLaunchKernelGGL(conv_kernel, dim3(conv_grid), dim3(kConvThreads), 0, stream, L, a);
+    hipLaunchKernelGGL((core_kernel<E, kRollout>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+  }
+  if (entropy)
+    for (int t = 0; t < a.T; ++t) {
+      a.t = t;
+      hipLaunchKernelGGL((core_kernel<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+    }
+  return check_launch("impala step kernels");
+}
+
+int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  const Layout& L = *c.layout;
+  const Plan p = plan(L, c.n_lanes, c.envs, c.T, c.entropy != 0);
+  if (!ws || ws_bytes < p.total) return set_error(FDR_ERR_WORKSPACE, "impala workspace too small");
+  if (c.n_lanes == 0) return FDR_OK;
+  char* w = static_cast<char*>(ws);
+  StepArgs a{};
+  a.pack = reinterpret_cast<float*>(w + p.pack);
+  a.pack_stride = L.pack;
+  a.bn_mean = c.bn_mean;
+  a.bn_var = c.bn_var;
+  a.n_lanes = c.n_lanes;
+  a.envs = c.envs;
+  a.n_act = L.n_act;
+  a.T = c.T;
+  a.lane_offset = c.lanes.lane_offset;
+  a.fkey = mix64(c.env_seed ^ kFrameSalt);
+  a.rkey = mix64(c.env_seed ^ kRewardSalt);
+  a.akey = mix64(c.seed);
+  a.feat = reinterpret_cast<float*>(w + p.feat);
+  a.h = reinterpret_cast<float*>(w + p.h);
+  a.c = reinterpret_cast<float*>(w + p.c);
+  a.rprev = reinterpret_cast<float*>(w + p.rprev);
+  a.ci = c.entropy ? reinterpret_cast<float*>(w + p.ci) : nullptr;
+  a.ret = c.ret;
+  a.ent = c.ent;
+  a.actions = c.actions;
+  a.probs = c.probs;
+  a.deterministic = c.lanes.deterministic;
+  double* n2 = reinterpret_cast<double*>(w + p.n2);
+
+  hipLaunchKernelGGL(prep_kernel, dim3(p.nblk, c.n_lanes), dim3(kPrepThreads), 0, stream, L, c.lanes,
+                     const_cast<float*>(a.pack), n2);
+  const int64_t ne = (int64_t)c.n_lanes * c.envs;
+  hipLaunchKernelGGL(init_kernel, dim3((unsigned)((ne * kHid + 255) / 256)), dim3(256), 0, stream, ne, a.h, a.c,
+                     a.rprev, a.ret, a.ent);
+  int rc = check_launch("impala prep/init");
+  if (rc) return rc;
+  switch (c.envs) {
+    case 1: rc = launch_steps<1>(L, a, c.entropy, stream); break;
+    case 2: rc = launch_steps<2>(L, a, c.entropy, stream); break;
+    case 4: rc = launch_steps<4>(L, a, c.entropy, stream); break;
+    case 8: rc = launch_steps<8>(L, a, c.entropy, stream); break;
+    default: return set_error(FDR_ERR_UNSUPPORTED, "envs_per_lane must be 1, 2, 4 or 8");
+  }
+  if (rc) return rc;
+  const int64_t nmax = std::max<int64_t>(ne, c.n_lanes);
+  hipLaunchKernelGGL(finish_kernel, dim3((unsigned)((nmax + 255) / 256)), dim3(256), 0, stream, c.n_lanes, c.envs,
+                     c.T, c.entropy, c.jiggle, a.akey, c.lanes.lane_offset, n2, p.nblk, c.ret, c.ent, c.steps,
+                     c.norm2);
+  return check_launch("impala finish");
+}
+
+int64_t forward_workspace_bytes(const Layout& L, int n_envs) {
+  const Plan p = plan(L, 1, std::max(n_envs, 0), 0, false);
+  return p.total;
+}
+
+int launch_forward(const ForwardCall& c, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  const Layout& L = *c.layout;
+  const Plan p = plan(L, 1, c.n_envs, 0, false);
+  if (!ws || ws_bytes < p.total) return set_error(FDR_ERR_WORKSPACE, "impala forward workspace too small");
+  if (c.n_envs == 0) return FDR_OK;
+  char* w = static_cast<char*>(ws);
+  LanesArgs lanes{};
+  lanes.base = c.theta;
+  StepArgs a{};
+  a.pack = reinterpret_cast<float*>(w + p.pack);
+  a.pack_stride = 0;  // every env shares the one pack
+  a.bn_mean = c.bn_mean;
+  a.bn_var = c.bn_var;
+  a.n_lanes = c.n_envs;
+  a.envs = 1;
+  a.n_act = L.n_act;
+  a.frames = c.frames;
+  a.feat = c.feat_out ? c.feat_out : reinterpret_cast<float*>(w + p.feat);
+  a.h = c.h;
+  a.c = c.c;
+  a.probs = c.probs;
+  a.reward_in = c.reward;
+  a.notdone = c.notdone;
+  hipLaunchKernelGGL(prep_kernel, dim3(p.nblk, 1), dim3(kPrepThreads), 0, stream, L, lanes,
+                     const_cast<float*>(a.pack), reinterpret_cast<double*>(w + p.n2));
+  hipLaunchKernelGGL(conv_kernel, dim3((c.n_envs + 7) / 8 * 8), dim3(kConvThreads), 0, stream, L, a);
+  hipLaunchKernelGGL((core_kernel<1, kForward>), dim3(c.n_envs), dim3(kCoreThreads), 0, stream, L, a);
+  return check_launch("impala forward");
+}
+
+}  // namespace impala
+}  // namespace fdr

@@ -15,7 +15,9 @@ FDR_ENV_SYNTH, FDR_ENV_TRAP = 0, 1
 
 EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy", "fdr_ctx_device",
            "fdr_perturb", "fdr_policy_forward", "fdr_rollout", "fdr_fd_weights",
-           "fdr_fd_grad_workspace_bytes", "fdr_fd_grad", "fdr_dsgd_workspace_bytes", "fdr_dsgd_step")
+           "fdr_fd_grad_workspace_bytes", "fdr_fd_grad", "fdr_dsgd_workspace_bytes", "fdr_dsgd_step",
+           "fdr_impala_num_params", "fdr_impala_num_bn_stats", "fdr_impala_workspace_bytes",
+           "fdr_impala_rollout", "fdr_impala_forward_workspace_bytes", "fdr_impala_forward")
 
 
 class FDRError(RuntimeError):
@@ -41,6 +43,12 @@ class LanesDesc(ctypes.Structure):
                 ("sigma", ctypes.c_float), ("deterministic", ctypes.c_void_p), ("lane_offset", ctypes.c_int64)]
 
 
+class ImpalaDesc(ctypes.Structure):
+    _fields_ = [("n_act", ctypes.c_int32), ("envs_per_lane", ctypes.c_int32), ("episode_len", ctypes.c_int32),
+                ("entropy", ctypes.c_int32), ("env_seed", ctypes.c_uint64), ("n_params", ctypes.c_int64),
+                ("bn_mean", ctypes.c_void_p), ("bn_var", ctypes.c_void_p)]
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError("libfdr.so not found at %s -- build it with `python -c 'import __graft_entry__ as g; "
@@ -64,6 +72,14 @@ def _load():
         "fdr_fd_grad": (ctypes.c_int, [P, P, I64, P, P, I32, I64, P, P, I64, P]),
         "fdr_dsgd_workspace_bytes": (I64, [I64]),
         "fdr_dsgd_step": (ctypes.c_int, [P, P, P, I64, F64, F64, P, P, I64, P]),
+        "fdr_impala_num_params": (I64, [I32]),
+        "fdr_impala_num_bn_stats": (I64, []),
+        "fdr_impala_workspace_bytes": (I64, [ctypes.POINTER(ImpalaDesc), I32]),
+        "fdr_impala_rollout": (ctypes.c_int, [P, ctypes.POINTER(ImpalaDesc), ctypes.POINTER(LanesDesc), I32, U64,
+                                              I32, P, P, P, P, P, P, P, I64, P]),
+        "fdr_impala_forward_workspace_bytes": (I64, [I32, I32]),
+        "fdr_impala_forward": (ctypes.c_int, [P, ctypes.POINTER(ImpalaDesc), P, I32, P, P, P, P, P, P, P, P, I64,
+                                              P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

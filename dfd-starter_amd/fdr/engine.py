@@ -158,3 +158,83 @@ def dsgd_step(theta, g, lr, lr_scale, out=None):
     check(lib.fdr_dsgd_step(None, _p(theta), _p(g), theta.numel(), float(lr), float(lr_scale), _p(out), _p(ws),
                             ws.numel(), _stream(dev)), "fdr_dsgd_step")
     return out
+
+
+# ---- ImpalaPolicy (policies/impala.py) --------------------------------------------------------
+def impala_num_params(n_act):
+    return int(lib.fdr_impala_num_params(int(n_act)))
+
+
+def impala_num_bn_stats():
+    return int(lib.fdr_impala_num_bn_stats())
+
+
+class ImpalaSpec(object):
+    """Shape of an ImpalaPolicy rollout: A actions, E envs per perturbation, T-step episodes."""
+
+    def __init__(self, n_act, envs_per_lane=1, episode_len=1, entropy=True, env_seed=0):
+        self.n_act, self.envs_per_lane, self.episode_len = int(n_act), int(envs_per_lane), int(episode_len)
+        self.entropy, self.env_seed = bool(entropy), int(env_seed)
+        self.n_params = impala_num_params(n_act)
+        if self.n_params < 0:
+            raise ValueError("n_act out of range")
+
+    def desc(self, bn_mean=None, bn_var=None):
+        _check_dev(bn_mean, bn_var)
+        for t in (bn_mean, bn_var):
+            if t is not None and (t.dtype != torch.float32 or t.numel() != impala_num_bn_stats()):
+                raise ValueError("BN stats must be float32[%d]" % impala_num_bn_stats())
+        return _lib.ImpalaDesc(self.n_act, self.envs_per_lane, self.episode_len, 1 if self.entropy else 0,
+                               self.env_seed & ((1 << 64) - 1), self.n_params,
+                               None if bn_mean is None else bn_mean.data_ptr(),
+                               None if bn_var is None else bn_var.data_ptr())
+
+
+def impala_rollout(spec, lanes, n_lanes, seed, jiggle=True, bn_mean=None, bn_var=None, record=False, out=None,
+                   device=None):
+    """fdr_impala_rollout: returns RolloutResult with per-env [n_lanes*E] fields, norm2 per lane,
+    plus .actions [n_lanes*E, T] / .probs [n_lanes*E, T, A] when record=True."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    n_env = n_lanes * spec.envs_per_lane
+    if out is None:
+        out = RolloutResult(torch.empty(n_env, dtype=torch.float64, device=dev),
+                            torch.empty(n_env, dtype=torch.float64, device=dev),
+                            torch.empty(n_env, dtype=torch.int32, device=dev),
+                            torch.empty(n_lanes, dtype=torch.float64, device=dev))
+    out.actions = torch.empty((n_env, spec.episode_len), dtype=torch.int32, device=dev) if record else None
+    out.probs = torch.empty((n_env, spec.episode_len, spec.n_act), dtype=torch.float32, device=dev) if record \
+        else None
+    d = spec.desc(bn_mean, bn_var)
+    nb = lib.fdr_impala_workspace_bytes(ctypes.byref(d), n_lanes)
+    if nb < 0:
+        raise ValueError("bad impala spec")
+    ws = _workspace("impala", nb, dev)
+    check(lib.fdr_impala_rollout(None, ctypes.byref(d), ctypes.byref(lanes), n_lanes,
+                                 ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(out.reward),
+                                 _p(out.entropy), _p(out.timesteps), _p(out.norm2), _p(out.actions), _p(out.probs),
+                                 _p(ws), ws.numel(), _stream(dev)), "fdr_impala_rollout")
+    return out
+
+
+def impala_forward(spec, theta, frames, h, c, reward=None, notdone=None, bn_mean=None, bn_var=None, feat=False):
+    """One ImpalaCNN step for n envs sharing theta; h, c [n, 256] are updated in place.
+    Returns probs [n, A] (and the relu'd conv features [n, 2048] if feat)."""
+    _check_dev(theta, frames, h, c, reward, notdone)
+    dev = theta.device
+    frames = frames.to(torch.float32).reshape(-1, 3 * 64 * 64).contiguous()
+    n = frames.shape[0]
+    for t in (h, c):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != n * 256:
+            raise ValueError("h / c must be contiguous float32 [n, 256]")
+    if reward is not None:
+        reward = reward.to(torch.float32).reshape(-1).contiguous()
+    if notdone is not None:
+        notdone = notdone.to(torch.float32).reshape(-1).contiguous()
+    probs = torch.empty((n, spec.n_act), dtype=torch.float32, device=dev)
+    f = torch.empty((n, 2048), dtype=torch.float32, device=dev) if feat else None
+    d = spec.desc(bn_mean, bn_var)
+    nb = lib.fdr_impala_forward_workspace_bytes(spec.n_act, n)
+    ws = _workspace("impala_fwd", nb, dev)
+    check(lib.fdr_impala_forward(None, ctypes.byref(d), _p(theta), n, _p(frames), _p(reward), _p(notdone), _p(h),
+                                 _p(c), _p(probs), _p(f), _p(ws), ws.numel(), _stream(dev)), "fdr_impala_forward")
+    return (probs, f) if feat else probs

@@ -149,6 +149,54 @@ int fdr_dsgd_step(fdr_ctx* ctx, float* theta, const double* g, int64_t n_params,
                   double lr_scale, double* out, void* workspace, int64_t workspace_bytes,
                   fdr_stream stream);
 
+/* ---- ImpalaPolicy (policies/impala.py:8-186) on the synthetic frame env --------------------
+ * The IMPALA conv stack runs on f32 MFMA tiles (one workgroup per env, activations resident in
+ * LDS), the fc + LSTM + head per lane; theta'_l is gathered once per rollout into a per-lane
+ * pack in the workspace.  Frames: uint8-valued 3x64x64 counter-hash frames and a +-1/0 reward
+ * (DESIGN.md "Impala path"; oracle/impala.py restates both). */
+typedef struct fdr_impala_desc {
+  int32_t n_act;         /* A = policy output size (env action_space.n), 1..32 */
+  int32_t envs_per_lane; /* E in {1, 2, 4, 8}: envs evaluated with one theta' (BASELINE config 4) */
+  int32_t episode_len;   /* T: fixed-length synthetic episodes */
+  int32_t entropy;       /* 1 = the reference's end-of-episode entropy pass (worker/agent.py:60-66):
+                            every visited obs replayed through the LSTM from the final state;
+                            0 = skip it (ent = 0) */
+  uint64_t env_seed;     /* synthetic frame / reward stream */
+  int64_t n_params;      /* must equal fdr_impala_num_params(n_act) */
+  const float* bn_mean;  /* eval-mode BN running stats, modules() order, concatenated:
+                            fdr_impala_num_bn_stats() floats; NULL = mean 0 */
+  const float* bn_var;   /* NULL = var 1 */
+} fdr_impala_desc;
+
+/* len(ImpalaPolicy.get_trainable_flat()) for n_act actions; -1 if n_act is out of range. */
+int64_t fdr_impala_num_params(int32_t n_act);
+/* total number of BatchNorm running-mean (= running-var) entries of the ImpalaCNN */
+int64_t fdr_impala_num_bn_stats(void);
+
+/* Each lane l evaluates theta'_l (lanes desc as for fdr_rollout) on envs l*E .. l*E+E-1, each one
+ * full episode from reset, returns laid out [n_lanes * E] (lane-major):
+ *   ret, ent (f64), steps (i32) per env; norm2 [n_lanes] f64 per lane;
+ *   actions [n_lanes*E, T] i32 and probs [n_lanes*E, T, A] f32 optional (NULL) per-step traces.
+ * workspace: fdr_impala_workspace_bytes(desc, n_lanes) bytes (theta' packs + per-step state).
+ * Replaces Worker.collect_returns with an ImpalaPolicy (worker/worker.py:20-38). */
+int64_t fdr_impala_workspace_bytes(const fdr_impala_desc* desc, int32_t n_lanes);
+int fdr_impala_rollout(fdr_ctx* ctx, const fdr_impala_desc* desc, const fdr_lanes_desc* lanes,
+                       int32_t n_lanes, uint64_t seed, int32_t jiggle, double* ret, double* ent,
+                       int32_t* steps, double* norm2, int32_t* actions, float* probs, void* workspace,
+                       int64_t workspace_bytes, fdr_stream stream);
+
+/* One step of ImpalaPolicy.forward (policies/impala.py:18-19, 144-186) for n_envs independent
+ * envs sharing theta [P]: frames [n_envs, 3, 64, 64] f32 (0..255), reward [n_envs] (NULL = 0),
+ * notdone [n_envs] (NULL = 1; multiplies the incoming state), h / c [n_envs, 256] updated in
+ * place, probs [n_envs, A] out, feat [n_envs, 2048] out (optional: relu'd conv features).
+ * Only desc->n_act, n_params, bn_mean, bn_var are read.
+ * workspace: fdr_impala_forward_workspace_bytes(n_act, n_envs) bytes. */
+int64_t fdr_impala_forward_workspace_bytes(int32_t n_act, int32_t n_envs);
+int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* desc, const float* theta, int32_t n_envs,
+                       const float* frames, const float* reward, const float* notdone, float* h,
+                       float* c, float* probs, float* feat, void* workspace, int64_t workspace_bytes,
+                       fdr_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,146 @@
+"""GPU parity of the Impala path (fdr_impala_forward / fdr_impala_rollout) against the oracle and the
+reference's own outputs (tests/golden/g8_impala.npz).  Tolerances: features/probs/state 1e-5 abs (f32,
+MFMA vs torch-CPU summation order); sampled actions and integer rewards exact; norm2 rel 1e-9."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import impala as oi
+
+pytestmark = pytest.mark.gpu
+
+ATOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def engine():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from fdr import engine
+    return engine
+
+
+@pytest.fixture(scope="module")
+def g8(golden):
+    return golden("g8_impala.npz")
+
+
+@pytest.fixture(scope="module")
+def table():
+    return np.random.RandomState(124).randn(2 ** 22).astype(np.float32)
+
+
+def test_forward_matches_reference_golden(engine, g8):
+    A, P = int(g8["A"]), int(g8["P"])
+    tab = np.random.RandomState(int(g8["table_seed"])).randn(2 ** 22).astype(np.float32)
+    off = int(g8["param_offset"])
+    theta = torch.tensor((tab[off:off + P] * np.float32(0.1)).astype(np.float32), device="cuda")
+    rm = torch.tensor(g8["rm"], device="cuda")
+    rv = torch.tensor(g8["rv"], device="cuda")
+    spec = engine.ImpalaSpec(A)
+    nq, T = g8["frames"].shape[:2]
+    h = torch.zeros(nq, 256, device="cuda")
+    c = torch.zeros(nq, 256, device="cuda")
+    for t in range(T):
+        fr = torch.tensor(g8["frames"][:, t].astype(np.float32), device="cuda")
+        rw = torch.tensor(g8["rewards"][:, t], device="cuda")
+        nd = torch.tensor(1.0 - g8["dones"][:, t].astype(np.float32), device="cuda")
+        probs, feat = engine.impala_forward(spec, theta, fr, h, c, reward=rw, notdone=nd, bn_mean=rm, bn_var=rv,
+                                            feat=True)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(feat.cpu().numpy(), g8["feat"][:, t], atol=ATOL)
+        np.testing.assert_allclose(h.cpu().numpy(), g8["h"][:, t], atol=ATOL)
+        np.testing.assert_allclose(c.cpu().numpy(), g8["c"][:, t], atol=ATOL)
+        np.testing.assert_allclose(probs.cpu().numpy(), g8["probs"][:, t], atol=ATOL)
+
+
+def _theta(A, seed=124):
+    """A trained-looking theta: torch default init of the reference layout (ImpalaCNN has no normc)."""
+    torch.manual_seed(seed)
+    parts = []
+    for name, shape in oi.layout(A):
+        if name.endswith("bn.w") or ".bn" in name and name.endswith(".w"):
+            parts.append(torch.ones(shape).reshape(-1))
+        elif ".bn" in name or name.startswith("fc.bn") or name.startswith("head.bn"):
+            parts.append(torch.zeros(shape).reshape(-1))
+        else:
+            fan_in = int(np.prod(shape[1:])) if len(shape) > 1 else shape[0]
+            bound = 1.0 / np.sqrt(fan_in)
+            parts.append(torch.empty(shape).uniform_(-bound, bound).reshape(-1))
+    return torch.cat(parts).numpy().astype(np.float32)
+
+
+def _run(engine, table, A, E, T, idx, sign, det, seed=11, env_seed=5, entropy=True, lane_offset=0, rm=None, rv=None):
+    theta = _theta(A)
+    L = len(idx)
+    dev = "cuda"
+    tt = torch.tensor(table, device=dev)
+    th = torch.tensor(theta, device=dev)
+    idx_t = torch.tensor(np.asarray(idx, np.int64), device=dev)
+    sg_t = torch.tensor(np.asarray(sign, np.int8), device=dev)
+    det_t = torch.tensor(np.asarray(det, np.int8), device=dev)
+    lanes = engine.lanes_desc(th, 0, tt, idx_t, sg_t, 0.02, det_t, lane_offset=lane_offset)
+    spec = engine.ImpalaSpec(A, E, T, entropy=entropy, env_seed=env_seed)
+    rm_t = None if rm is None else torch.tensor(rm, device=dev)
+    rv_t = None if rv is None else torch.tensor(rv, device=dev)
+    out = engine.impala_rollout(spec, lanes, L, seed, jiggle=True, bn_mean=rm_t, bn_var=rv_t, record=True)
+    torch.cuda.synchronize()
+    nb = oi.num_bn()
+    ref = oi.evaluate_lanes(theta, table, np.asarray(idx), np.asarray(sign), 0.02, A, E, T, seed, env_seed,
+                            np.zeros(nb, np.float32) if rm is None else rm,
+                            np.ones(nb, np.float32) if rv is None else rv,
+                            deterministic=np.asarray(det, bool), lane_offset=lane_offset, record=True)
+    return out, ref
+
+
+def _compare(out, ref, L, E, T, A, entropy=True):
+    probs = out.probs.cpu().numpy().reshape(L, E, T, A)
+    np.testing.assert_allclose(probs, ref["probs"], atol=ATOL)
+    acts = out.actions.cpu().numpy().reshape(L, E, T)
+    assert (acts == ref["actions"]).mean() == 1.0, np.argwhere(acts != ref["actions"])
+    np.testing.assert_array_equal(out.reward.cpu().numpy().reshape(L, E), ref["ret"])
+    np.testing.assert_array_equal(out.timesteps.cpu().numpy().reshape(L, E), ref["steps"])
+    if entropy:
+        np.testing.assert_allclose(out.entropy.cpu().numpy().reshape(L, E), ref["ent"], atol=ATOL)
+    np.testing.assert_allclose(out.norm2.cpu().numpy(), ref["norm2"], rtol=1e-9)
+
+
+def test_rollout_antithetic_stochastic(engine, table):
+    A, E, T = 6, 2, 4
+    idx = [1234, 1234]
+    out, ref = _run(engine, table, A, E, T, idx, [1, -1], [0, 0])
+    _compare(out, ref, 2, E, T, A)
+
+
+def test_rollout_deterministic_with_bn_stats_and_lane_offset(engine, table):
+    A, E, T = 4, 1, 3
+    rs = np.random.RandomState(3)
+    nb = oi.num_bn()
+    rm = (0.1 * rs.randn(nb)).astype(np.float32)
+    rv = (1.0 + 0.5 * np.abs(rs.randn(nb))).astype(np.float32)
+    idx = [77, 2_000_000, 3_000_000]
+    out, ref = _run(engine, table, A, E, T, idx, [1, 0, -1], [1, 1, 0], lane_offset=5, rm=rm, rv=rv)
+    _compare(out, ref, 3, E, T, A)
+
+
+def test_rollout_four_envs_ragged_lanes(engine, table):
+    """E = 4 (BASELINE config 4's envs per perturbation) with a lane count that is not a multiple of
+    the 8-XCD workgroup grouping."""
+    A, E, T = 6, 4, 2
+    idx = [10, 20, 30]
+    out, ref = _run(engine, table, A, E, T, idx, [1, 1, -1], [0, 0, 0], entropy=False)
+    _compare(out, ref, 3, E, T, A, entropy=False)
+    assert np.all(out.entropy.cpu().numpy() == 0.0)
+
+
+def test_bad_offset_poisons_norm_without_fault(engine, table):
+    A = 6
+    th = torch.tensor(_theta(A), device="cuda")
+    tt = torch.tensor(table, device="cuda")
+    idx = torch.tensor([0, len(table)], dtype=torch.int64, device="cuda")      # second is out of range
+    sg = torch.tensor([1, 1], dtype=torch.int8, device="cuda")
+    lanes = engine.lanes_desc(th, 0, tt, idx, sg, 0.02)
+    out = engine.impala_rollout(engine.ImpalaSpec(A, 1, 1, entropy=False), lanes, 2, 3)
+    torch.cuda.synchronize()
+    n2 = out.norm2.cpu().numpy()
+    assert np.isfinite(n2[0]) and np.isnan(n2[1])
