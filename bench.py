@@ -34,7 +34,16 @@ CONFIGS = {
     # name: (policy kind, n_in, n_act, env shape name, episode_len)
     "halfcheetah": ("mujoco", 17, 6, "halfcheetah", 1000),
     "cartpole": ("discrete", 4, 2, "cartpole", 500),
+    # BASELINE config 4 per GPU: 8192 perturbations x 4 envs over 8 GPUs -> 1024 lanes x 4 envs each
+    "impala": ("impala", (64, 64, 3), 6, "frames", 1000),
 }
+IMPALA_ENVS = 4
+IMPALA_LANES = 1024
+# ImpalaCNN conv stack, algorithmic FLOPs per env step: sum over the 15 convs of 2*Cin*9*Cout*Ho*Wo
+IMPALA_CONV_FLOP = 2 * 9 * (3 * 16 * 64 * 64 + 4 * 16 * 16 * 32 * 32 + 16 * 32 * 32 * 32 + 4 * 32 * 32 * 16 * 16
+                            + 32 * 32 * 16 * 16 + 4 * 32 * 32 * 8 * 8)
+# fc + LSTM + head weights streamed per (lane, step) by the core kernel (f32)
+IMPALA_CORE_BYTES = 4 * (2048 * 256 + 257 * 1024 + 256 * 1024)
 
 
 def lane_step_flops(kind, n_in, n_act):
@@ -48,6 +57,30 @@ def lane_step_flops(kind, n_in, n_act):
 # ------------------------------------------------------------------------------------------------
 # CPU baseline (oracle restatement of the reference's per-lane loop), forked before any GPU use
 # ------------------------------------------------------------------------------------------------
+def _cpu_worker_impala(wid, seconds, T):
+    """Per-env reference loop on one core: ImpalaCNN torch-CPU forward per step (oracle restatement of
+    policies/impala.py + worker/agent.py), perturbed theta, synthetic frames."""
+    import numpy as np
+    import torch
+    from oracle import impala as oi
+    from oracle import rng as crng
+    torch.manual_seed(124)
+    P = oi.num_params(6)
+    theta = (torch.randn(P) * 0.01).numpy()
+    eps = np.random.RandomState(wid).randn(P).astype(np.float32)
+    p = oi.unflatten((theta + np.float32(0.02) * eps).astype(np.float32), 6)
+    bn = oi.split_bn(np.zeros(oi.num_bn(), np.float32), np.ones(oi.num_bn(), np.float32))
+    h, c, r = torch.zeros(1, 256), torch.zeros(1, 256), np.zeros(1, np.float32)
+    steps, t0, t = 0, time.perf_counter(), 0
+    while time.perf_counter() - t0 < seconds:
+        fr = oi.frames(5, [wid], t).astype(np.float32)
+        pr, h, c, _, _ = oi.forward(p, bn, fr, r, h, c)
+        a = oi.categorical_inverse_cdf(pr.numpy()[0], crng.uniform(7, wid, t, 0))
+        r = oi.rewards(5, [wid], t, [a], 6)
+        steps, t = steps + 1, (t + 1) % T
+    return steps, time.perf_counter() - t0
+
+
 def _cpu_worker(args):
     wid, seconds, cfg = args
     import numpy as np
@@ -55,6 +88,8 @@ def _cpu_worker(args):
     torch.set_num_threads(1)
     from oracle import agent, envs, noise, policies
     kind, n_in, n_act, _, T = CONFIGS[cfg]
+    if kind == "impala":
+        return _cpu_worker_impala(wid, seconds, T)
     torch.manual_seed(124)
     pol = policies.TorchPolicy(kind, n_in, n_act, seed=124)
     theta = pol.get_flat()
@@ -107,8 +142,10 @@ def main():
         cores = max(1, min(16, os.cpu_count() or 1))
         v, steps = cpu_baseline(args.config, args.cpu_seconds, cores)
         cpu = {"value": round(v, 1), "unit": "env steps/s", "cores": cores, "kind": "port",
-               "sample": "%d processes x %.0f s of whole episodes (T=%d, +/-eps perturbed %s policy, torch CPU "
-                         "forward per step, 1 thread each): %d env steps" % (cores, args.cpu_seconds, T, kind, steps)}
+               "sample": "%d processes x %.0f s of %s (T=%d, +/-eps perturbed %s policy, torch CPU "
+                         "forward per step, 1 thread each): %d env steps"
+                         % (cores, args.cpu_seconds, "whole episodes" if kind != "impala" else "episode steps",
+                            T, kind, steps)}
 
     import numpy as np
     import torch
@@ -120,16 +157,23 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from dsgd import DSGD
-    from envs import SyntheticEnv
+    from envs import FrameEnv, SyntheticEnv
+    from fdr import engine
     from learner import FiniteDifferences
-    from policies import DiscretePolicy, MujocoPolicy
+    from policies import DiscretePolicy, ImpalaPolicy, MujocoPolicy
     from utils import AdaptiveOmega, SharedNoiseTable
     from worker import Agent, Worker
 
     torch.manual_seed(124)
-    Pol = DiscretePolicy if kind == "discrete" else MujocoPolicy
-    policy = Pol(n_in, n_act, seed=124, device=dev)
-    env = SyntheticEnv.named(env_name, device=dev, episode_len=T)
+    impala = kind == "impala"
+    if impala:
+        policy = ImpalaPolicy(n_in, n_act, seed=124, device=dev)
+        env = FrameEnv(n_act, episode_len=T, envs_per_lane=IMPALA_ENVS, env_seed=5)
+        engine.impala_profile(True)
+    else:
+        Pol = DiscretePolicy if kind == "discrete" else MujocoPolicy
+        policy = Pol(n_in, n_act, seed=124, device=dev)
+        env = SyntheticEnv.named(env_name, device=dev, episode_len=T)
     table = SharedNoiseTable(25_000_000, policy.num_params, random_seed=124)
     table.device_table(dev)
     agent = Agent(policy, env, random_seed=124 + rank)
@@ -137,12 +181,14 @@ def main():
     omega = AdaptiveOmega()
     learner = FiniteDifferences(policy, DSGD(policy.parameters(), lr=0.01), omega, table, noise_std=0.02)
 
-    L = args.perturbations
+    L = args.perturbations if not impala or args.perturbations != 4096 else IMPALA_LANES
+    E = IMPALA_ENVS if impala else 1
     n_dirs_global = (L // 2) * world
     from fdr import dist as fdist
     lane_range = fdist.lane_range(n_dirs_global, 2, world, rank)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     roll_ms = []
+    phase_ms = []
 
     def fd_step(timed):
         if timed:
@@ -151,6 +197,8 @@ def main():
         if timed:
             ev1.record()
         out = learner.step_async(batch, 0.0, 0.0, 0.0)
+        if timed and impala:
+            phase_ms.append(engine.impala_profile_read())
         return out, batch
 
     for _ in range(args.warmup):
@@ -178,15 +226,49 @@ def main():
     upd, gnorm = out.tolist()
     assert gnorm > 0 and np.isfinite(upd)
 
-    lane_steps = L * T * world * args.steps
+    lane_steps = L * E * T * world * args.steps
     value = lane_steps / elapsed
-    flops = lane_step_flops(kind, n_in, n_act) * L * T
-    achieved_tf = flops / (rollout_ms * 1e-3) / 1e12
     traffic = None
     pmc = os.path.join(REPO, "profiles", "pmc_rollout_%s.json" % args.config)
     if os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
+    if impala:
+        conv_ms, core_ms, replay_ms = (float(np.mean([p[i] for p in phase_ms])) for i in range(3))
+        if world > 1:
+            t = torch.tensor([conv_ms, core_ms, replay_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            conv_ms, core_ms, replay_ms = t.tolist()
+        conv_launch_ms = conv_ms / T
+        achieved_tf = IMPALA_CONV_FLOP * L * E / (conv_launch_ms * 1e-3) / 1e12
+        core_gbs = IMPALA_CORE_BYTES * L / (core_ms / T * 1e-3) / 1e9
+        roofline = {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                    "kernel": "impala conv_kernel (15 convs, v_mfma_f32_16x16x4_f32)",
+                    "conv_launch_ms": round(conv_launch_ms, 4), "flop_per_env_step": IMPALA_CONV_FLOP,
+                    "envs_per_launch": L * E, "rollout_ms": round(rollout_ms, 3),
+                    "core_kernel": {"bound": "hbm", "achieved": round(core_gbs, 1), "peak": HBM_PEAK_GBS,
+                                    "unit": "GB/s", "frac": round(core_gbs / HBM_PEAK_GBS, 4),
+                                    "launch_ms": round(core_ms / T, 4), "bytes_per_lane_step": IMPALA_CORE_BYTES},
+                    "entropy_replay_ms": round(replay_ms, 3),
+                    "note": "f32 MFMA peak (= f32 vector peak); conv time from HIP events between the step-loop "
+                            "launches (fdr_impala_profile)"}
+        workload = ("BASELINE config 4 per GPU: ImpalaPolicy(A=%d) P=%d, %d perturbations (%d directions x +/-) x "
+                    "%d envs each, synthetic 3x64x64 frames, T=%d, full FD step (rollout + entropy pass + weights "
+                    "+ gradient + DSGD)" % (n_act, policy.num_params, L, L // 2, E, T))
+    else:
+        flops = lane_step_flops(kind, n_in, n_act) * L * T
+        achieved_tf = flops / (rollout_ms * 1e-3) / 1e12
+        roofline = {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                    "kernel": "rollout_kernel<17,6,mujoco,synth>", "rollout_ms": round(rollout_ms, 4),
+                    "flop_per_lane_step": lane_step_flops(kind, n_in, n_act),
+                    "note": "fp32 VALU/matrix peak; theta' is VGPR-resident for the whole episode, so the "
+                            "kernel is compute-bound (DESIGN.md 'Roofline')"}
+        workload = ("BASELINE config 3: HalfCheetah-shaped synthetic env (obs 17, act 6), MujocoPolicy(17,6) P=%d, "
+                    "%d antithetic perturbations per GPU (%d directions x +/-), T=%d fixed-length episodes, full FD "
+                    "step (rollout + weights + gradient + DSGD)" % (policy.num_params, L, L // 2, T)
+                    if args.config == "halfcheetah" else args.config)
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -201,18 +283,10 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic",
-        "config": {"workload": "BASELINE config 3: HalfCheetah-shaped synthetic env (obs 17, act 6), "
-                               "MujocoPolicy(17,6) P=%d, %d antithetic perturbations per GPU (%d directions x +/-), "
-                               "T=%d fixed-length episodes, full FD step (rollout + weights + gradient + DSGD)"
-                               % (policy.num_params, L, L // 2, T) if args.config == "halfcheetah" else args.config,
-                   "perturbations_per_gpu": L, "global_perturbations": L * world, "episode_len": T,
-                   "n_params": policy.num_params, "parallelism": "dp%d" % world},
-        "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                     "kernel": "rollout_kernel<17,6,mujoco,synth>", "rollout_ms": round(rollout_ms, 4),
-                     "flop_per_lane_step": lane_step_flops(kind, n_in, n_act),
-                     "note": "fp32 VALU/matrix peak; theta' is VGPR-resident for the whole episode, so the "
-                             "kernel is compute-bound (DESIGN.md 'Roofline')"},
+        "config": {"workload": workload, "perturbations_per_gpu": L, "envs_per_perturbation": E,
+                   "global_perturbations": L * world, "episode_len": T, "n_params": policy.num_params,
+                   "parallelism": "dp%d" % world},
+        "roofline": roofline,
         "cpu_baseline": cpu,
         "update_norm": upd,
     }

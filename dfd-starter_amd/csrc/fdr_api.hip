@@ -321,3 +321,18 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* d, const float* thet
   f.bn_var = d->bn_var;
   return impala::launch_forward(f, ws, ws_bytes, (hipStream_t)stream);
 }
+
+int fdr_impala_profile(int32_t enable) {
+  impala::set_profile(enable);
+  return FDR_OK;
+}
+
+int fdr_impala_profile_read(double* ms) {
+  if (!ms) return set_error(FDR_ERR_INVALID, "NULL pointer");
+  return impala::read_profile(ms);
+}
+
+int fdr_impala_debug_clock(uint64_t* buf) {
+  impala::set_debug_clock(buf);
+  return FDR_OK;
+}

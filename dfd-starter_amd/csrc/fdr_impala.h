@@ -74,6 +74,9 @@ struct ForwardCall {
   const float* bn_var;
 };
 int64_t forward_workspace_bytes(const Layout& L, int n_envs);
+void set_profile(int on);
+void set_debug_clock(uint64_t* buf);
+int read_profile(double* out3);
 int launch_forward(const ForwardCall& c, void* ws, int64_t ws_bytes, hipStream_t stream);
 
 }  // namespace impala

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <vector>
 
 #include "fdr_impala.h"
 
@@ -179,17 +180,28 @@ __global__ __launch_bounds__(kPrepThreads) void prep_kernel(Layout L, LanesArgs 
 
 // ------------------------------------------------------------------------------------------
 // conv stack: one workgroup (8 waves) per (lane, env); everything between the frame and the
-// 2048-feature stays in LDS.
-//   T  (guarded, padded NCHW input of the current conv)  18,496 floats
-//   X  (unpadded stage activation / residual stream)      16,384 floats
-//   S  (5-row band of an entry conv's output, pooled into X) lives in whichever is free
+// 2048-feature stays in LDS (all 160 KiB; floats):
+//   [guard 128][TE 23,488: padded input image T of the current conv + band scratch S][X 16,384]
+//   [BN scale/shift 960]
+// Padded planes are strided so the 4 lane groups of an MFMA A-read (4 input channels) start 16
+// banks apart: plane % 64 == 16 (32x32 and 16x16 stages) -> conflict-free ds_read_b32.
 // ------------------------------------------------------------------------------------------
 constexpr int kConvThreads = 512;
-constexpr int kGuard = 128;          // one padded row above T: the band of conv row -1 reads it
-constexpr int kRT = 16 * 34 * 34;
+constexpr int kGuard = 128;          // padded rows above T: the band of conv row -1 reads them
+constexpr int kTE = 23488;
 constexpr int kRX = 16 * 32 * 32;
 constexpr int kBnTab = 15 * 32;
-constexpr int kConvLds = kGuard + kRT + kRX + 2 * kBnTab;
+constexpr int kConvLds = kGuard + kTE + kRX + 2 * kBnTab;  // 40,960 floats = 160 KiB
+constexpr int kBand = 9;             // conv rows per entry-conv band: 4 pooled rows + 1 shared row
+
+template <int H>
+struct Plane {  // padded [H+2][H+2] image, bank-staggered plane stride
+  static constexpr int WP = H + 2;
+  static constexpr int RAW = WP * WP;
+  static constexpr int P = H == 64 ? RAW : RAW + ((16 - RAW % 64) % 64 + 64) % 64 + (H == 8 ? 2 : 0);
+};
+static_assert(Plane<32>::P == 1168 && Plane<16>::P == 336 && Plane<8>::P == 146, "plane strides");
+static_assert(16 * Plane<32>::P <= kTE && 3 * Plane<64>::P + 16 * kBand * 65 <= kTE, "LDS plan");
 
 struct StepArgs {
   const float* pack;
@@ -213,20 +225,34 @@ struct StepArgs {
   const int8_t* deterministic;
   const float* reward_in;  // forward: reward carried by the obs
   const float* notdone;    // forward: done mask (policies/impala.py:170-176)
+  uint64_t* dbg;           // diagnostics: phase clocks of conv workgroup 0 (fdr_impala_debug_clock) or NULL
 };
+
+// phase clock of the first conv workgroup (s_memtime), for the phase breakdown in DESIGN.md
+#define FDR_STAMP(a, k)                                                      \
+  do {                                                                       \
+    if ((a).dbg && blockIdx.x == 0 && threadIdx.x == 0) (a).dbg[k] = clock64(); \
+  } while (0)
 
 __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
 
-// acc[i] (tile q = wave + 8 i) += A_tile(q) * B(nt = wave % NT) over K = 9 * CIN, A gathered from
-// the padded LDS image Tin ([CIN][*][WP], row 0 = padded row of output row 0).
-template <int CIN, int NT, int TPW, int W, int WP, int PLANE, int MT>
-__device__ __forceinline__ void conv_mfma(const float* Tin, const float* __restrict__ wf, f32x4 (&acc)[TPW],
-                                          int wave, int lane) {
+// B fragments of one conv for this wave's N-tile: bf[s] = B[k = 4s + (lane >> 4)][n], one VGPR each.
+template <int CIN, int NT>
+__device__ __forceinline__ void load_frag(const float* __restrict__ wf, float (&bf)[(9 * CIN + 3) / 4], int wave,
+                                          int lane) {
   constexpr int KS = (9 * CIN + 3) / 4;
   const int nt = wave % NT;
-  float bf[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) bf[s] = wf[(s * NT + nt) * 64 + lane];
+}
+
+// acc[i] (tile q = wave + 8 i) = A_tile(q) * B over K = 9 * CIN on v_mfma_f32_16x16x4_f32, A gathered
+// from the padded LDS image Tin ([CIN][*][WP] with plane stride PLANE, row 0 = padded row of output
+// row 0).  M-tile = 16 consecutive output pixels (row-major, width W).
+template <int CIN, int NT, int TPW, int W, int WP, int PLANE, int MT>
+__device__ __forceinline__ void conv_mfma(const float* Tin, const float (&bf)[(9 * CIN + 3) / 4], f32x4 (&acc)[TPW],
+                                          int wave, int lane) {
+  constexpr int KS = (9 * CIN + 3) / 4;
   int base[TPW];
   const int g = lane >> 4;
 #pragma unroll
@@ -275,79 +301,97 @@ __device__ __forceinline__ void conv_out(const f32x4 (&acc)[TPW], int wave, int 
   }
 }
 
-// T <- BN(X) (optionally ReLU) into the padded image [C][H+2][W+2], zero border.
-template <int C, int H, bool RELU>
+// T <- BN(X) (optionally ReLU) into the padded image [C][H+2][H+2] (plane stride Plane<H>::P).
+// BORDER: also write the zero border (needed when T last held another layout).
+template <int C, int H, bool RELU, bool BORDER>
 __device__ __forceinline__ void to_padded(const float* X, float* T, const float* sc, const float* sh) {
-  constexpr int WP = H + 2, PLANE = WP * WP;
-  for (int i = threadIdx.x; i < C * PLANE; i += kConvThreads) {
-    const int ch = i / PLANE, rem = i - ch * PLANE;
-    const int y = rem / WP - 1, x = rem % WP - 1;
-    float v = 0.f;
-    if (y >= 0 && y < H && x >= 0 && x < H) {
-      v = fmaf(X[(ch * H + y) * H + x], sc[ch], sh[ch]);
-      if (RELU) v = relu(v);
+  constexpr int WP = Plane<H>::WP, PL = Plane<H>::P, LH = H == 64 ? 6 : (H == 32 ? 5 : (H == 16 ? 4 : 3));
+  // interior, 4 consecutive x per thread (one ds_read_b128 of X)
+  for (int i = threadIdx.x; i < C * H * H / 4; i += kConvThreads) {
+    const int e = 4 * i, ch = e >> (2 * LH), y = (e >> LH) & (H - 1), x = e & (H - 1);
+    const float4 v = *reinterpret_cast<const float4*>(X + e);
+    const float a = sc[ch], b = sh[ch];
+    float o0 = fmaf(v.x, a, b), o1 = fmaf(v.y, a, b), o2 = fmaf(v.z, a, b), o3 = fmaf(v.w, a, b);
+    if (RELU) { o0 = relu(o0); o1 = relu(o1); o2 = relu(o2); o3 = relu(o3); }
+    float* d = T + ch * PL + (y + 1) * WP + x + 1;
+    d[0] = o0; d[1] = o1; d[2] = o2; d[3] = o3;
+  }
+  if (BORDER) {  // 4 (H + 1) border cells per plane
+    for (int i = threadIdx.x; i < C * 4 * (H + 1); i += kConvThreads) {
+      const int ch = i / (4 * (H + 1)), r = i - ch * 4 * (H + 1), side = r / (H + 1), k = r - side * (H + 1);
+      const int off = side == 0 ? k : side == 1 ? (H + 1) * WP + 1 + k : side == 2 ? (k + 1) * WP : k * WP + WP - 1;
+      T[ch * PL + off] = 0.f;
     }
-    T[i] = v;
   }
 }
 
-// Stage entry: X <- maxpool3s2p1(conv3x3(T) + b) in 5-row bands (conv rows 4b-1 .. 4b+3 -> pooled
-// rows 2b, 2b+1) through the scratch S; conv row -1 is read from the guard and never pooled.
-template <int CIN, int COUT, int H>
-__device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, const float* __restrict__ wf,
+// Stage entry: X <- maxpool3s2p1(conv3x3(T) + b), in bands of 9 conv rows (8b-1 .. 8b+7 -> pooled
+// rows 4b .. 4b+3) through the scratch S [COUT][9][1 + H]: column 0 of S is -inf (the pool's left
+// pad) and conv row -1 of band 0 is stored as -inf, so the pool is branch-free and separable --
+// one thread per (channel, pooled column): 9 horizontal max3, then 4 vertical max3.
+// The B fragments are loaded once, before the caller's barrier, and reused by every band.
+template <int CIN, int COUT, int H, int PLANE>
+__device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, const float (&bf)[(9 * CIN + 3) / 4],
                                             const float* __restrict__ bias, int wave, int lane) {
-  constexpr int WP = H + 2, PLANE = WP * WP, NT = COUT / 16, MT = 5 * H / 16;
-  constexpr int TPW = (MT * NT + 7) / 8, HO = H / 2;
+  constexpr int WP = H + 2, NT = COUT / 16, MT = kBand * H / 16;
+  constexpr int TPW = (MT * NT + 7) / 8, HO = H / 2, SW = H + 1;
   const float bn_ = bias[(wave % NT) * 16 + (lane & 15)];
-  for (int b = 0; b < H / 4; ++b) {
+  for (int i = threadIdx.x; i < COUT * kBand; i += kConvThreads) S[i * SW] = -FLT_MAX;
+  for (int b = 0; b < H / 8; ++b) {
     f32x4 acc[TPW];
-    conv_mfma<CIN, NT, TPW, H, WP, PLANE, MT>(T + (4 * b - 1) * WP, wf, acc, wave, lane);
-    conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) { S[n * 5 * H + m] = v + bn_; });
+    conv_mfma<CIN, NT, TPW, H, WP, PLANE, MT>(T + (8 * b - 1) * WP, bf, acc, wave, lane);
+    conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) {
+      const int r = m / H, x = m % H;
+      S[(n * kBand + r) * SW + 1 + x] = (b == 0 && r == 0) ? -FLT_MAX : v + bn_;
+    });
     __syncthreads();
-    for (int i = threadIdx.x; i < COUT * 2 * HO; i += kConvThreads) {
-      const int ch = i / (2 * HO), rem = i - ch * 2 * HO;
-      const int pr = rem / HO, px = rem % HO;
-      float m = -FLT_MAX;
+    for (int i = threadIdx.x; i < COUT * HO; i += kConvThreads) {
+      const int ch = i / HO, px = i - ch * HO;
+      const float* sc = S + ch * kBand * SW + 2 * px;  // columns 2px-1 .. 2px+1 (+1 for the pad column)
+      float hm[kBand];
 #pragma unroll
-      for (int dr = 0; dr < 3; ++dr) {
-        const int r = 2 * pr + dr;  // local band row; conv row 4b - 1 + r
-        if (b == 0 && r == 0) continue;
+      for (int r = 0; r < kBand; ++r) hm[r] = fmaxf(fmaxf(sc[r * SW], sc[r * SW + 1]), sc[r * SW + 2]);
 #pragma unroll
-        for (int dc = -1; dc <= 1; ++dc) {
-          const int x = 2 * px + dc;
-          if (x < 0 || x >= H) continue;
-          m = fmaxf(m, S[(ch * 5 + r) * H + x]);
-        }
-      }
-      X[(ch * HO + 2 * b + pr) * HO + px] = m;
+      for (int pr = 0; pr < 4; ++pr)
+        X[(ch * HO + 4 * b + pr) * HO + px] = fmaxf(fmaxf(hm[2 * pr], hm[2 * pr + 1]), hm[2 * pr + 2]);
     }
     __syncthreads();
   }
 }
 
-// Two residual blocks (policies/impala.py:77-105, 152-157) on X [C][H][H], T as scratch.
+// Two residual blocks (policies/impala.py:77-105, 152-157) on X [C][H][H], T as scratch.  Each conv's
+// weights are loaded ahead of the barrier that precedes it, so the fetch overlaps LDS work.
 template <int C, int H>
 __device__ __forceinline__ void res_blocks(float* T, float* X, const float* __restrict__ pk, const Layout& L,
-                                           int stage, const float* bsc, const float* bsh, int wave, int lane) {
-  constexpr int WP = H + 2, PLANE = WP * WP, NT = C / 16, MT = H * H / 16;
-  constexpr int TPW = (MT * NT + 7) / 8;
+                                           int stage, const float* bsc, const float* bsh, int wave, int lane,
+                                           const StepArgs& a, int k0) {
+  constexpr int WP = H + 2, PLANE = Plane<H>::P, NT = C / 16, MT = H * H / 16;
+  constexpr int TPW = (MT * NT + 7) / 8, KS = (9 * C + 3) / 4;
+  const int n_ = (wave % NT) * 16 + (lane & 15);
+  float bf[KS];
   for (int r = 0; r < 2; ++r) {
     const int i0 = stage * 5 + 1 + 2 * r, i1 = i0 + 1;
-    to_padded<C, H, true>(X, T, bsc + i0 * 32, bsh + i0 * 32);
+    load_frag<C, NT>(pk + L.conv_w[i0], bf, wave, lane);
+    if (r == 0) to_padded<C, H, true, true>(X, T, bsc + i0 * 32, bsh + i0 * 32);
+    else to_padded<C, H, true, false>(X, T, bsc + i0 * 32, bsh + i0 * 32);
     __syncthreads();
+    FDR_STAMP(a, k0 + 4 * r);
     f32x4 acc[TPW];
-    conv_mfma<C, NT, TPW, H, WP, PLANE, MT>(T, pk + L.conv_w[i0], acc, wave, lane);
-    const int n_ = (wave % NT) * 16 + (lane & 15);
+    conv_mfma<C, NT, TPW, H, WP, PLANE, MT>(T, bf, acc, wave, lane);
     const float b0 = pk[L.conv_b[i0] + n_], s1 = bsc[i1 * 32 + n_], h1 = bsh[i1 * 32 + n_];
+    load_frag<C, NT>(pk + L.conv_w[i1], bf, wave, lane);
     __syncthreads();  // every wave is done reading T
+    FDR_STAMP(a, k0 + 4 * r + 1);
     conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) {
       T[n * PLANE + (m / H + 1) * WP + (m % H) + 1] = relu(fmaf(v + b0, s1, h1));
     });
     __syncthreads();
-    conv_mfma<C, NT, TPW, H, WP, PLANE, MT>(T, pk + L.conv_w[i1], acc, wave, lane);
+    FDR_STAMP(a, k0 + 4 * r + 2);
+    conv_mfma<C, NT, TPW, H, WP, PLANE, MT>(T, bf, acc, wave, lane);
     const float b1 = pk[L.conv_b[i1] + n_];
     conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) { X[n * H * H + m] = (v + b1) + X[n * H * H + m]; });
     __syncthreads();
+    FDR_STAMP(a, k0 + 4 * r + 3);
   }
 }
 
@@ -361,10 +405,14 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
   const int64_t env = (int64_t)lane * a.envs + e;
   const float* pk = a.pack + (int64_t)lane * a.pack_stride;
   float* T = lds + kGuard;
-  float* X = T + kRT;
+  float* X = T + kTE;
   float* bsc = X + kRX;
   float* bsh = bsc + kBnTab;
+  constexpr int FW = 66, FPLANE = Plane<64>::P;
 
+  float bf3[7];
+  load_frag<3, 1>(pk + L.conv_w[0], bf3, wave, ln);
+  FDR_STAMP(a, 0);
   // eval-mode BN folded per channel: y = x * (w / sqrt(rv + eps)) + (b - rm * scale)
   for (int i = threadIdx.x; i < kBnTab; i += kConvThreads) {
     const int idx = i >> 5, ch = i & 31;
@@ -380,11 +428,11 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
     bsc[i] = sc;
     bsh[i] = sh;
   }
-  for (int i = threadIdx.x; i < kGuard + kRT; i += kConvThreads) lds[i] = 0.f;
+  for (int i = threadIdx.x; i < kGuard + 3 * FPLANE; i += kConvThreads) lds[i] = 0.f;
   __syncthreads();
+  FDR_STAMP(a, 1);
 
   // ---- frame (policies/impala.py:147: frame / 255) -> BN2d(3) -> padded [3][66][66] ----
-  constexpr int FW = 66, FPLANE = 66 * 66;
   if (a.frames) {
     const float* fr = a.frames + env * kFramePix;
     for (int p = threadIdx.x; p < kFramePix; p += kConvThreads) {
@@ -405,23 +453,41 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
     }
   }
   __syncthreads();
+  FDR_STAMP(a, 2);
 
-  // ---- stage 1: conv 3->16 @64x64, pool -> X [16][32][32], residual blocks ----
-  stage_entry<3, 16, 64>(T, T + 3 * FPLANE, X, pk + L.conv_w[0], pk + L.conv_b[0], wave, ln);
-  res_blocks<16, 32>(T, X, pk, L, 0, bsc, bsh, wave, ln);
-  // ---- stage 2: BN(X) -> T [16][34][34]; conv 16->32 @32x32, pool -> X [32][16][16] ----
-  to_padded<16, 32, false>(X, T, bsc + 5 * 32, bsh + 5 * 32);
-  __syncthreads();
-  stage_entry<16, 32, 32>(T, X + 32 * 16 * 16, X, pk + L.conv_w[5], pk + L.conv_b[5], wave, ln);
-  res_blocks<32, 16>(T, X, pk, L, 1, bsc, bsh, wave, ln);
-  // ---- stage 3: conv 32->32 @16x16, pool -> X [32][8][8] ----
-  to_padded<32, 16, false>(X, T, bsc + 10 * 32, bsh + 10 * 32);
-  __syncthreads();
-  stage_entry<32, 32, 16>(T, X + 32 * 8 * 8, X, pk + L.conv_w[10], pk + L.conv_b[10], wave, ln);
-  res_blocks<32, 8>(T, X, pk, L, 2, bsc, bsh, wave, ln);
+  // ---- stage 1: conv 3->16 @64x64, pool -> X1 [16][32][32], residual blocks ----
+  stage_entry<3, 16, 64, FPLANE>(T, T + 3 * FPLANE, X, bf3, pk + L.conv_b[0], wave, ln);
+  FDR_STAMP(a, 3);
+  res_blocks<16, 32>(T, X, pk, L, 0, bsc, bsh, wave, ln, a, 4);
+  // ---- stage 2: BN(X1) -> T; conv 16->32 @32x32 with S2 after T, pool -> X2 [32][16][16] ----
+  {
+    float bf[36];
+    load_frag<16, 2>(pk + L.conv_w[5], bf, wave, ln);
+    to_padded<16, 32, false, true>(X, T, bsc + 5 * 32, bsh + 5 * 32);
+    __syncthreads();
+    FDR_STAMP(a, 12);
+    float* S2 = T + 16 * Plane<32>::P;  // overlaps the dead X1
+    stage_entry<16, 32, 32, Plane<32>::P>(T, S2, S2 + 32 * kBand * 33, bf, pk + L.conv_b[5], wave, ln);
+  }
+  float* X2 = T + 16 * Plane<32>::P + 32 * kBand * 33;
+  FDR_STAMP(a, 13);
+  res_blocks<32, 16>(T, X2, pk, L, 1, bsc, bsh, wave, ln, a, 14);
+  // ---- stage 3: BN(X2) -> T; conv 32->32 @16x16, pool -> X3 [32][8][8] ----
+  float* X3 = T + 32 * Plane<16>::P + 32 * kBand * 17;
+  {
+    float bf[72];
+    load_frag<32, 2>(pk + L.conv_w[10], bf, wave, ln);
+    to_padded<32, 16, false, true>(X2, T, bsc + 10 * 32, bsh + 10 * 32);
+    __syncthreads();
+    FDR_STAMP(a, 22);
+    stage_entry<32, 32, 16, Plane<16>::P>(T, T + 32 * Plane<16>::P, X3, bf, pk + L.conv_b[10], wave, ln);
+  }
+  FDR_STAMP(a, 23);
+  res_blocks<32, 8>(T, X3, pk, L, 2, bsc, bsh, wave, ln, a, 24);
   // ---- relu + flatten (C, H, W) (policies/impala.py:159-160) ----
   float* out = a.feat + env * kFeat;
-  for (int i = threadIdx.x; i < kFeat; i += kConvThreads) out[i] = relu(X[i]);
+  for (int i = threadIdx.x; i < kFeat; i += kConvThreads) out[i] = relu(X3[i]);
+  FDR_STAMP(a, 32);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -649,18 +715,74 @@ __global__ void finish_kernel(int n_lanes, int envs, int T, int entropy, int jig
   }
 }
 
+// Opt-in phase timing (fdr_impala_profile): HIP events between the launches of the step loop, so
+// a caller (bench.py) can attribute the rollout's time to conv / core / replay kernels live.
+namespace {
+struct Profile {
+  bool on = false;
+  std::vector<hipEvent_t> ev;
+  int used = 0, T = 0, entropy = 0;
+  hipEvent_t next() {
+    if (used == (int)ev.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      ev.push_back(e);
+    }
+    return ev[used++];
+  }
+};
+Profile g_prof;
+uint64_t* g_dbg = nullptr;
+}  // namespace
+
+void set_debug_clock(uint64_t* buf) { g_dbg = buf; }
+
+static void mark(hipStream_t s) {
+  if (g_prof.on) {
+    hipEvent_t e = g_prof.next();
+    if (e) (void)hipEventRecord(e, s);
+  }
+}
+
+void set_profile(int on) {
+  g_prof.on = on != 0;
+  g_prof.used = 0;
+}
+
+int read_profile(double* out) {
+  out[0] = out[1] = out[2] = 0.0;
+  const int need = 2 * g_prof.T + 1 + (g_prof.entropy ? g_prof.T : 0);
+  if (!g_prof.on || g_prof.used < need) return set_error(FDR_ERR_INVALID, "no profiled impala rollout");
+  if (hipEventSynchronize(g_prof.ev[need - 1]) != hipSuccess) return set_error(FDR_ERR_HIP, "event sync failed");
+  auto ms = [](hipEvent_t a, hipEvent_t b) { float v = 0.f; (void)hipEventElapsedTime(&v, a, b); return (double)v; };
+  for (int t = 0; t < g_prof.T; ++t) {
+    out[0] += ms(g_prof.ev[2 * t], g_prof.ev[2 * t + 1]);
+    out[1] += ms(g_prof.ev[2 * t + 1], g_prof.ev[2 * t + 2]);
+  }
+  for (int t = 0; g_prof.entropy && t < g_prof.T; ++t)
+    out[2] += ms(g_prof.ev[2 * g_prof.T + t], g_prof.ev[2 * g_prof.T + t + 1]);
+  return FDR_OK;
+}
+
 template <int E>
 static int launch_steps(const Layout& L, StepArgs a, int entropy, hipStream_t stream) {
   const int conv_grid = (a.n_lanes + 7) / 8 * 8 * a.envs;
+  g_prof.used = 0;
+  g_prof.T = a.T;
+  g_prof.entropy = entropy;
+  mark(stream);
   for (int t = 0; t < a.T; ++t) {
     a.t = t;
     hipLaunchKernelGGL(conv_kernel, dim3(conv_grid), dim3(kConvThreads), 0, stream, L, a);
+    mark(stream);
     hipLaunchKernelGGL((core_kernel<E, kRollout>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+    mark(stream);
   }
   if (entropy)
     for (int t = 0; t < a.T; ++t) {
       a.t = t;
       hipLaunchKernelGGL((core_kernel<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+      mark(stream);
     }
   return check_launch("impala step kernels");
 }
@@ -694,6 +816,7 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
   a.actions = c.actions;
   a.probs = c.probs;
   a.deterministic = c.lanes.deterministic;
+  a.dbg = g_dbg;
   double* n2 = reinterpret_cast<double*>(w + p.n2);
 
   hipLaunchKernelGGL(prep_kernel, dim3(p.nblk, c.n_lanes), dim3(kPrepThreads), 0, stream, L, c.lanes,

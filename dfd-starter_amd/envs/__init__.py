@@ -12,6 +12,10 @@ into the rollout kernel, so an env here is a *descriptor*: device tensors + shap
       s <- tanh(M s + K a)  (a one-hot for discrete actions);  reward = s[0];  done at t = T.
 * ``TrapEnv`` -- custom_envs/simple_trap_env (environment.py:8-61) on the GPU, integer-exact:
   the reference's walkable bitmap ships as data (custom_envs/simple_trap_env/trap_map.npz).
+* ``FrameEnv`` -- the Atari/procgen-shaped workload of BASELINE configs 4/5 for ImpalaPolicy:
+  uint8-valued 3x64x64 frames from a counter hash of (env, t, pixel), a +1/-1/0 reward for hitting
+  a hashed target action (or its successor), fixed T; ``envs_per_lane`` envs share one theta'.
+  Generated inside the conv kernel (never stored); oracle/impala.py restates it.
 """
 import os
 
@@ -75,3 +79,20 @@ class TrapEnv(object):
     def desc(self):
         return _lib.EnvDesc(_lib.FDR_ENV_TRAP, 2, 9, self.episode_len, None, None, None,
                             self.walkable.data_ptr(), self.map_w, self.map_h)
+
+
+class FrameEnv(object):
+    """Synthetic frame env for ImpalaPolicy rollouts (fdr_impala_rollout)."""
+    obs_shape = (64, 64, 3)
+
+    def __init__(self, n_act, episode_len=1000, envs_per_lane=4, env_seed=0, entropy=True):
+        self.act_dim = int(n_act)
+        self.episode_len = int(episode_len)
+        self.envs_per_lane = int(envs_per_lane)
+        self.env_seed = int(env_seed)
+        self.entropy = bool(entropy)
+
+    def spec(self):
+        from fdr import engine
+        return engine.ImpalaSpec(self.act_dim, self.envs_per_lane, self.episode_len, entropy=self.entropy,
+                                 env_seed=self.env_seed)

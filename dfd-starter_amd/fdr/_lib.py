@@ -17,7 +17,8 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_perturb", "fdr_policy_forward", "fdr_rollout", "fdr_fd_weights",
            "fdr_fd_grad_workspace_bytes", "fdr_fd_grad", "fdr_dsgd_workspace_bytes", "fdr_dsgd_step",
            "fdr_impala_num_params", "fdr_impala_num_bn_stats", "fdr_impala_workspace_bytes",
-           "fdr_impala_rollout", "fdr_impala_forward_workspace_bytes", "fdr_impala_forward")
+           "fdr_impala_rollout", "fdr_impala_forward_workspace_bytes", "fdr_impala_forward",
+           "fdr_impala_profile", "fdr_impala_profile_read", "fdr_impala_debug_clock")
 
 
 class FDRError(RuntimeError):
@@ -78,6 +79,9 @@ def _load():
         "fdr_impala_rollout": (ctypes.c_int, [P, ctypes.POINTER(ImpalaDesc), ctypes.POINTER(LanesDesc), I32, U64,
                                               I32, P, P, P, P, P, P, P, I64, P]),
         "fdr_impala_forward_workspace_bytes": (I64, [I32, I32]),
+        "fdr_impala_profile": (ctypes.c_int, [I32]),
+        "fdr_impala_profile_read": (ctypes.c_int, [P]),
+        "fdr_impala_debug_clock": (ctypes.c_int, [P]),
         "fdr_impala_forward": (ctypes.c_int, [P, ctypes.POINTER(ImpalaDesc), P, I32, P, P, P, P, P, P, P, P, I64,
                                               P]),
     }

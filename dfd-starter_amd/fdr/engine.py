@@ -238,3 +238,14 @@ def impala_forward(spec, theta, frames, h, c, reward=None, notdone=None, bn_mean
     check(lib.fdr_impala_forward(None, ctypes.byref(d), _p(theta), n, _p(frames), _p(reward), _p(notdone), _p(h),
                                  _p(c), _p(probs), _p(f), _p(ws), ws.numel(), _stream(dev)), "fdr_impala_forward")
     return (probs, f) if feat else probs
+
+
+def impala_profile(enable):
+    lib.fdr_impala_profile(1 if enable else 0)
+
+
+def impala_profile_read():
+    """(conv_ms, core_ms, replay_ms) summed over the last profiled fdr_impala_rollout (host sync)."""
+    out = (ctypes.c_double * 3)()
+    check(lib.fdr_impala_profile_read(ctypes.cast(out, ctypes.c_void_p)), "fdr_impala_profile_read")
+    return tuple(out)

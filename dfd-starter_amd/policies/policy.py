@@ -46,7 +46,8 @@ class Policy(nn.Module):
                 p.data = flat[off:off + n].view_as(p)
                 off += n
         self.flat = flat
-        self.spec = engine.PolicySpec(self.KIND, self.input_shape, self.output_shape, self.num_params)
+        if self.KIND in ("discrete", "mujoco"):
+            self.spec = engine.PolicySpec(self.KIND, self.input_shape, self.output_shape, self.num_params)
 
     def _init_params(self):
         self._normc_init()

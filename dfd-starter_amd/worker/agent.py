@@ -50,8 +50,14 @@ class Agent(object):
         lanes = engine.lanes_desc(p.flat, 0, deterministic=det)
         om, osd = self.obs_norm_tensors(mean, std)
         bm, bv = p.bn_stats()
-        res = engine.rollout(p.spec, self.env, lanes, 1, self.next_seed(), jiggle=False, obs_mean=om, obs_std=osd,
-                             bn_mean=bm, bn_var=bv, device=p.flat.device)
+        if p.KIND == "impala":   # one env, one episode of the synthetic frame env
+            spec = engine.ImpalaSpec(p.output_shape, 1, self.env.episode_len, entropy=self.env.entropy,
+                                     env_seed=self.env.env_seed)
+            res = engine.impala_rollout(spec, lanes, 1, self.next_seed(), jiggle=False, bn_mean=bm, bn_var=bv,
+                                        device=p.flat.device)
+        else:
+            res = engine.rollout(p.spec, self.env, lanes, 1, self.next_seed(), jiggle=False, obs_mean=om,
+                                 obs_std=osd, bn_mean=bm, bn_var=bv, device=p.flat.device)
         steps = int(res.timesteps.item())
         self.cumulative_timesteps += steps
         reward = float(res.reward.item()) + self.rng.choice((-1e-12, 1e-12))   # agent.py:69

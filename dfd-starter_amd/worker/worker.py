@@ -63,10 +63,19 @@ class Worker(object):
         det_d = self._to_device(np.asarray(det, np.int8), torch.int8)
         table = self.noise_source.device_table(p.flat.device)
         lanes = engine.lanes_desc(p.flat, 0, table, idx_d, sign_d, self.sigma, det_d, lane_offset)
-        om, osd = self.agent.obs_norm_tensors(self.fixed_obs_stats.mean, self.fixed_obs_stats.std)
         bm, bv = p.bn_stats()
         if seed is None:
             seed = self.agent.next_seed(n)
+        if p.KIND == "impala":
+            # E envs per lane: returns are per (lane, env), lane-major; idx / sign / norm2 repeat per env
+            E = self.agent.env.envs_per_lane
+            res = engine.impala_rollout(self.agent.env.spec(), lanes, n, seed, jiggle=jiggle, bn_mean=bm,
+                                        bn_var=bv, device=p.flat.device)
+            if E > 1:
+                res.norm2 = res.norm2.repeat_interleave(E)
+                idx_d, sign_d = idx_d.repeat_interleave(E), sign_d.repeat_interleave(E)
+            return res, idx_d, sign_d
+        om, osd = self.agent.obs_norm_tensors(self.fixed_obs_stats.mean, self.fixed_obs_stats.std)
         res = engine.rollout(p.spec, self.agent.env, lanes, n, seed, jiggle=jiggle, obs_mean=om, obs_std=osd,
                              bn_mean=bm, bn_var=bv, out=out, device=p.flat.device)
         return res, idx_d, sign_d
@@ -91,9 +100,12 @@ class Worker(object):
         det = np.zeros(len(lidx), np.int8)
         lo = 0 if lane_range is None else lane_range[0]
         res, idx_d, sign_d = self.launch(lidx, sign, det, seed=seed, out=out, lane_offset=lo)
+        E = getattr(self.agent.env, "envs_per_lane", 1)
+        if E > 1:
+            lidx, sign = np.repeat(lidx, E), np.repeat(sign, E)
         self.agent.cumulative_timesteps += int(len(lidx)) * self.agent.env.episode_len
         return FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, lidx, sign, self.epoch,
-                       lanes_per_dir=lpd)
+                       lanes_per_dir=lpd * E)
 
     # ---- reference API ----------------------------------------------------------------------
     @torch.no_grad()
@@ -105,6 +117,9 @@ class Worker(object):
             idx[~is_eval] = self.noise_source.sample_batch(k)
         sign = np.where(is_eval, 0, 1).astype(np.int8)
         res, idx_d, sign_d = self.launch(idx, sign, is_eval.astype(np.int8), jiggle=False)
+        E = getattr(self.agent.env, "envs_per_lane", 1)
+        if E > 1:
+            idx, sign, is_eval = np.repeat(idx, E), np.repeat(sign, E), np.repeat(is_eval, E)
         b = FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, idx, sign, self.epoch,
                     is_eval=is_eval)
         rets = b.to_returns()

@@ -197,6 +197,16 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* desc, const float* t
                        float* c, float* probs, float* feat, void* workspace, int64_t workspace_bytes,
                        fdr_stream stream);
 
+/* Opt-in phase timing of fdr_impala_rollout (process-wide, not thread-safe): when enabled, HIP
+ * events are recorded between the step-loop launches; fdr_impala_profile_read waits for the last
+ * profiled rollout and returns HOST ms[3] = summed conv-stack / core (fc+LSTM+head) / entropy-replay
+ * kernel time.  Used by bench.py for the live roofline figure. */
+int fdr_impala_profile(int32_t enable);
+int fdr_impala_profile_read(double* ms);
+/* Diagnostics: subsequent fdr_impala_rollout launches write s_memtime clocks of conv workgroup 0 at
+ * 33 phase boundaries into the DEVICE buffer buf (u64[33], overwritten each step); NULL = off. */
+int fdr_impala_debug_clock(uint64_t* buf);
+
 #ifdef __cplusplus
 }
 #endif

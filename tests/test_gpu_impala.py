@@ -144,3 +144,64 @@ def test_bad_offset_poisons_norm_without_fault(engine, table):
     torch.cuda.synchronize()
     n2 = out.norm2.cpu().numpy()
     assert np.isfinite(n2[0]) and np.isnan(n2[1])
+
+
+def test_policy_api_matches_reference_golden(engine, g8):
+    """ImpalaPolicy.forward on the reference's obs dicts (utils/impala_env_wrapper.py:25-28)."""
+    from policies import ImpalaPolicy
+    A, P = int(g8["A"]), int(g8["P"])
+    pol = ImpalaPolicy((64, 64, 3), A, seed=124)
+    tab = np.random.RandomState(int(g8["table_seed"])).randn(2 ** 22).astype(np.float32)
+    off = int(g8["param_offset"])
+    pol.set_trainable_flat((tab[off:off + P] * np.float32(0.1)).astype(np.float32))
+    o = 0
+    for m in pol.model.bn_layers():
+        n = m.num_features
+        m.running_mean.copy_(torch.as_tensor(g8["rm"][o:o + n]))
+        m.running_var.copy_(torch.as_tensor(g8["rv"][o:o + n]))
+        o += n
+    for q in range(g8["frames"].shape[0]):
+        pol.reset()
+        for t in range(g8["frames"].shape[1]):
+            obs = {"frame": torch.as_tensor(g8["frames"][q, t].astype(np.float32)).view(1, 1, 3, 64, 64),
+                   "reward": torch.as_tensor(g8["rewards"][q, t]).view(1, 1),
+                   "done": torch.as_tensor(bool(g8["dones"][q, t])).view(1, 1)}
+            probs = pol.forward(obs)
+            assert tuple(probs.shape) == (1, 1, A)
+            np.testing.assert_allclose(probs.view(-1).cpu().numpy(), g8["probs"][q, t], atol=ATOL)
+            np.testing.assert_allclose(pol.state[0].view(-1).cpu().numpy(), g8["h"][q, t], atol=ATOL)
+
+
+def test_worker_and_learner_fd_step(engine):
+    """Worker.evaluate (E = 2 envs per perturbation, antithetic) -> FiniteDifferences.step: the rollout
+    returns match the oracle and the update follows the oracle's FD gradient over the per-env returns."""
+    from dsgd import DSGD
+    from envs import FrameEnv
+    from learner import FiniteDifferences
+    from policies import ImpalaPolicy
+    from utils import AdaptiveOmega, SharedNoiseTable
+    from worker import Agent, Worker
+    from oracle import learner as ol
+    torch.manual_seed(124)
+    pol = ImpalaPolicy((64, 64, 3), 6, seed=124)
+    P = pol.num_params
+    nt = SharedNoiseTable(2 ** 22, P, random_seed=124)
+    env = FrameEnv(6, episode_len=2, envs_per_lane=2, env_seed=5)
+    worker = Worker(pol, Agent(pol, env, random_seed=3), nt, None, sigma=0.02)
+    learner = FiniteDifferences(pol, DSGD(pol.parameters(), lr=0.01), AdaptiveOmega(), nt, noise_std=0.02)
+    theta0 = pol.get_trainable_flat().copy()
+    batch = worker.evaluate(2, antithetic=True, seed=77)
+    assert len(batch) == 8 and batch.lanes_per_dir == 4
+    rew = batch.reward.cpu().numpy()
+    lanes_idx, lanes_sign = batch.idx_host[::2], batch.sign_host[::2]
+    nb = oi.num_bn()
+    ref = oi.evaluate_lanes(theta0, nt._table, lanes_idx, lanes_sign, 0.02, 6, 2, 2, 77, 5,
+                            np.zeros(nb, np.float32), np.ones(nb, np.float32))
+    np.testing.assert_array_equal(rew.reshape(4, 2), ref["ret"])
+    np.testing.assert_allclose(batch.norm2.cpu().numpy(), np.repeat(ref["norm2"], 2), rtol=1e-9)
+    upd = learner.step(batch, 0.0, 0.0, 0.0)
+    g, _ = ol.fd_gradient(nt._table, P, batch.idx_host, batch.sign_host, rew, 0.0, 0.02)
+    d = pol.get_trainable_flat().astype(np.float64) - theta0
+    np.testing.assert_allclose(np.linalg.norm(d), upd, rtol=1e-5)
+    cos = float(np.dot(d, g) / (np.linalg.norm(d) * np.linalg.norm(g)))   # DSGD ascends g
+    assert cos > 1 - 1e-6, cos

@@ -1,0 +1,58 @@
+"""Phase breakdown of the Impala conv kernel (s_memtime clocks of workgroup 0, fdr_impala_debug_clock).
+
+    python tools/impala_phases.py [--lanes 1024 --envs 4]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "dfd-starter_amd"))
+from fdr import engine  # noqa: E402
+from fdr._lib import lib  # noqa: E402
+
+NAMES = {0: "start", 1: "bn table + zero", 2: "frame", 3: "stage1 entry conv+pool"}
+for st, k0, pre in ((1, 4, None), (2, 14, 12), (3, 24, 22)):
+    if pre is not None:
+        NAMES[pre] = "stage%d BN -> padded" % st
+        NAMES[pre + 1] = "stage%d entry conv+pool" % st
+    for r in range(2):
+        NAMES[k0 + 4 * r] = "stage%d res%d bn0+relu" % (st, r)
+        NAMES[k0 + 4 * r + 1] = "stage%d res%d conv0" % (st, r)
+        NAMES[k0 + 4 * r + 2] = "stage%d res%d epilogue" % (st, r)
+        NAMES[k0 + 4 * r + 3] = "stage%d res%d conv1+add" % (st, r)
+NAMES[32] = "relu + store"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lanes", type=int, default=1024)
+    ap.add_argument("--envs", type=int, default=4)
+    args = ap.parse_args()
+    A = 6
+    P = engine.impala_num_params(A)
+    torch.manual_seed(0)
+    theta = (torch.randn(P) * 0.02).cuda()
+    table = torch.randn(P + 4096).cuda()
+    idx = torch.randint(0, 4096, (args.lanes,), dtype=torch.int64).cuda()
+    sign = torch.ones(args.lanes, dtype=torch.int8).cuda()
+    lanes = engine.lanes_desc(theta, 0, table, idx, sign, 0.02)
+    dbg = torch.zeros(33, dtype=torch.int64).cuda()
+    lib.fdr_impala_debug_clock(ctypes.c_void_p(dbg.data_ptr()))
+    spec = engine.ImpalaSpec(A, args.envs, 2, entropy=False)
+    engine.impala_rollout(spec, lanes, args.lanes, 1)
+    torch.cuda.synchronize()
+    lib.fdr_impala_debug_clock(None)
+    c = dbg.cpu().numpy().astype(np.int64)
+    tot = c[32] - c[0]
+    order = sorted(NAMES)
+    print("conv workgroup 0: %d clocks total" % tot)
+    for a, b in zip(order[:-1], order[1:]):
+        print("%-28s %9d  %5.1f%%" % (NAMES[b], c[b] - c[a], 100.0 * (c[b] - c[a]) / tot))
+
+
+if __name__ == "__main__":
+    main()
