@@ -44,6 +44,7 @@ bool make_layout(int n_act, Layout* L) {
   L->n_act = n_act;
   int32_t dst = 0, src = 0, stat = 0;
   auto add = [&](int32_t kind, int32_t len, int32_t a, int32_t b, int32_t src_len) {
+    dst = (int32_t)round_up(dst, 16);  // 64-byte aligned sections: float4 streaming in the core kernel
     Section& s = L->sec[L->n_sections++];
     s = Section{dst, len, src, kind, a, b};
     const int32_t at = dst;
@@ -502,7 +503,9 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); 
 
 template <int E, int MODE>
 __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a) {
-  __shared__ float xs[kFeat * E];    // BN'd features, [k][e]
+  // xw: the BN'd features xs [2048][E] during the fc, then the fc partial sums [4][256][E], then the
+  // LSTM gate pre-activations [1024][E] -- each phase separated by a barrier.
+  __shared__ float xw[kFeat * E];
   __shared__ float cis[kCoreIn * E]; // core input, [k][e]
   __shared__ float hs[kHid * E];     // h (then BN(h')), [k][e]
   __shared__ float logit[E * kMaxAct];
@@ -510,6 +513,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
   const float* pk = a.pack + (int64_t)lane * a.pack_stride;
   const int64_t e0 = (int64_t)lane * E;
   const int A = a.n_act;
+  const int c4 = j & 63, wq = j >> 6;  // float4 column group, wave index
 
   if constexpr (MODE != kReplay) {
     for (int k = j; k < kFeat; k += kCoreThreads) {
@@ -518,22 +522,40 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
       const float sc = pk[L.bn_w[15] + k] * (1.f / sqrtf(rv + kBnEps));
       const float sh = pk[L.bn_b[15] + k] - rm * sc;
 #pragma unroll
-      for (int e = 0; e < E; ++e) xs[k * E + e] = fmaf(a.feat[(e0 + e) * kFeat + k], sc, sh);
+      for (int e = 0; e < E; ++e) xw[k * E + e] = fmaf(a.feat[(e0 + e) * kFeat + k], sc, sh);
     }
     __syncthreads();
-    float acc[E];
+    // fc (2048 -> 256): wave wq streams rows [512 wq, 512 wq + 512) of W^T as float4 (1 KiB / wave-load)
+    float acc[4][E];
 #pragma unroll
-    for (int e = 0; e < E; ++e) acc[e] = 0.f;
-    const float* w = pk + L.fc_wt + j;
-#pragma unroll 8
-    for (int k = 0; k < kFeat; ++k) {
-      const float wk = w[(int64_t)k * kHid];
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int e = 0; e < E; ++e) acc[e] = fmaf(wk, xs[k * E + e], acc[e]);
+      for (int e = 0; e < E; ++e) acc[c][e] = 0.f;
+    const float4* w4 = reinterpret_cast<const float4*>(pk + L.fc_wt) + c4;
+#pragma unroll 4
+    for (int k = wq * (kFeat / 4); k < (wq + 1) * (kFeat / 4); ++k) {
+      const float4 w = w4[(int64_t)k * (kHid / 4)];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const float x = xw[k * E + e];
+        acc[0][e] = fmaf(w.x, x, acc[0][e]);
+        acc[1][e] = fmaf(w.y, x, acc[1][e]);
+        acc[2][e] = fmaf(w.z, x, acc[2][e]);
+        acc[3][e] = fmaf(w.w, x, acc[3][e]);
+      }
     }
+    __syncthreads();  // xs is dead
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < E; ++e) xw[(wq * kHid + 4 * c4 + c) * E + e] = acc[c][e];
+    __syncthreads();
     const float bj = pk[L.fc_b + j];
 #pragma unroll
-    for (int e = 0; e < E; ++e) cis[j * E + e] = relu(acc[e] + bj);
+    for (int e = 0; e < E; ++e) {
+      const float y = ((xw[j * E + e] + xw[(kHid + j) * E + e]) + xw[(2 * kHid + j) * E + e]) + xw[(3 * kHid + j) * E + e];
+      cis[j * E + e] = relu(y + bj);
+    }
     if (j < E) {
       const float r = MODE == kForward ? (a.reward_in ? a.reward_in[e0 + j] : 0.f) : a.rprev[e0 + j];
       cis[kHid * E + j] = fminf(fmaxf(r, -1.f), 1.f);
@@ -562,61 +584,62 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
   }
   __syncthreads();
 
-  // LSTM cell (torch gate order i, f, g, o): gates = (W_ih x + b_ih) + (W_hh h + b_hh)
-  float ax[4][E], ah[4][E];
+  // LSTM gates (torch order i, f, g, o): thread j streams columns 4j .. 4j+3 of [W_ih | W_hh]^T, so
+  // wave wq computes gate wq; gates = (W_ih x + b_ih) + (W_hh h + b_hh)
+  {
+    float ax[4][E], ah[4][E];
 #pragma unroll
-  for (int g = 0; g < 4; ++g)
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int e = 0; e < E; ++e) ax[g][e] = ah[g][e] = 0.f;
-  const float* wl = pk + L.lstm_wt + j;
-#pragma unroll 2
-  for (int k = 0; k < kCoreIn; ++k) {
-    const float* wr = wl + (int64_t)k * kGates;
-    const float w0 = wr[0], w1 = wr[kHid], w2 = wr[2 * kHid], w3 = wr[3 * kHid];
+      for (int e = 0; e < E; ++e) ax[c][e] = ah[c][e] = 0.f;
+    const float4* wl = reinterpret_cast<const float4*>(pk + L.lstm_wt) + j;
+#pragma unroll 4
+    for (int k = 0; k < kCoreIn; ++k) {
+      const float4 w = wl[(int64_t)k * (kGates / 4)];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const float x = cis[k * E + e];
-      ax[0][e] = fmaf(w0, x, ax[0][e]);
-      ax[1][e] = fmaf(w1, x, ax[1][e]);
-      ax[2][e] = fmaf(w2, x, ax[2][e]);
-      ax[3][e] = fmaf(w3, x, ax[3][e]);
+      for (int e = 0; e < E; ++e) {
+        const float x = cis[k * E + e];
+        ax[0][e] = fmaf(w.x, x, ax[0][e]);
+        ax[1][e] = fmaf(w.y, x, ax[1][e]);
+        ax[2][e] = fmaf(w.z, x, ax[2][e]);
+        ax[3][e] = fmaf(w.w, x, ax[3][e]);
+      }
     }
-  }
-#pragma unroll 2
-  for (int k = 0; k < kHid; ++k) {
-    const float* wr = wl + (int64_t)(kCoreIn + k) * kGates;
-    const float w0 = wr[0], w1 = wr[kHid], w2 = wr[2 * kHid], w3 = wr[3 * kHid];
+#pragma unroll 4
+    for (int k = 0; k < kHid; ++k) {
+      const float4 w = wl[(int64_t)(kCoreIn + k) * (kGates / 4)];
 #pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const float x = hs[k * E + e];
-      ah[0][e] = fmaf(w0, x, ah[0][e]);
-      ah[1][e] = fmaf(w1, x, ah[1][e]);
-      ah[2][e] = fmaf(w2, x, ah[2][e]);
-      ah[3][e] = fmaf(w3, x, ah[3][e]);
+      for (int e = 0; e < E; ++e) {
+        const float x = hs[k * E + e];
+        ah[0][e] = fmaf(w.x, x, ah[0][e]);
+        ah[1][e] = fmaf(w.y, x, ah[1][e]);
+        ah[2][e] = fmaf(w.z, x, ah[2][e]);
+        ah[3][e] = fmaf(w.w, x, ah[3][e]);
+      }
     }
+    const float4 bi = reinterpret_cast<const float4*>(pk + L.lstm_bih)[j];
+    const float4 bh = reinterpret_cast<const float4*>(pk + L.lstm_bhh)[j];
+    const float bif[4] = {bi.x, bi.y, bi.z, bi.w}, bhf[4] = {bh.x, bh.y, bh.z, bh.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < E; ++e) xw[(4 * j + c) * E + e] = (ax[c][e] + bif[c]) + (ah[c][e] + bhf[c]);
   }
+  __syncthreads();  // gates complete; all reads of the old h are done
   float hj[E];
-  {
-    float bi[4], bh[4];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      bi[g] = pk[L.lstm_bih + g * kHid + j];
-      bh[g] = pk[L.lstm_bhh + g * kHid + j];
-    }
-#pragma unroll
-    for (int e = 0; e < E; ++e) {
-      const float gi = sigm((ax[0][e] + bi[0]) + (ah[0][e] + bh[0]));
-      const float gf = sigm((ax[1][e] + bi[1]) + (ah[1][e] + bh[1]));
-      const float gg = tanhf((ax[2][e] + bi[2]) + (ah[2][e] + bh[2]));
-      const float go = sigm((ax[3][e] + bi[3]) + (ah[3][e] + bh[3]));
-      cj[e] = gf * cj[e] + gi * gg;
-      hj[e] = go * tanhf(cj[e]);
-      a.h[(e0 + e) * kHid + j] = hj[e];
-      a.c[(e0 + e) * kHid + j] = cj[e];
-    }
+  for (int e = 0; e < E; ++e) {
+    const float gi = sigm(xw[j * E + e]);
+    const float gf = sigm(xw[(kHid + j) * E + e]);
+    const float gg = tanhf(xw[(2 * kHid + j) * E + e]);
+    const float go = sigm(xw[(3 * kHid + j) * E + e]);
+    cj[e] = gf * cj[e] + gi * gg;
+    hj[e] = go * tanhf(cj[e]);
+    a.h[(e0 + e) * kHid + j] = hj[e];
+    a.c[(e0 + e) * kHid + j] = cj[e];
   }
-  __syncthreads();  // all reads of the old h are done
   {
+
     const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
     const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
     const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));

@@ -21,4 +21,7 @@ run pmc_fetch --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_f
 run pmc_write --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run -- python3 $BENCH
 run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace \
     --output-format csv -d "$OUT/pmc_sq" -o run -- python3 $BENCH
+if [ -n "${MFMA_PMC:-}" ]; then
+  run pmc_mfma --pmc $MFMA_PMC --kernel-trace --output-format csv -d "$OUT/pmc_mfma" -o run -- python3 $BENCH
+fi
 ls -R "$OUT" | head -50

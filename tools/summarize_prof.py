@@ -1,7 +1,7 @@
 """Summarise a tools/profile.sh output directory into profiles/<tag>_summary.md + the PMC json
 bench.py reads (profiles/pmc_rollout_<config>.json).
 
-    python tools/summarize_prof.py gpurun_out/prof_r01 r01 [config]
+    python tools/summarize_prof.py gpurun_out/prof_r01 r01 [config [kernel-substring]]
 
 HBM bytes per launch = FETCH_SIZE*1024*2 + WRITE_SIZE*1024: MI355X_MICROARCH.md section HBM --
 on gfx950 FETCH_SIZE reports half of a wide coalesced read; that x2 correction is applied to the
@@ -22,14 +22,14 @@ def per_kernel(path, counter=None):
     return out
 
 
-def main(d, tag, config="halfcheetah"):
+def main(d, tag, config="halfcheetah", dominant="rollout_kernel"):
     stats = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
     fetch = per_kernel(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(d, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
     sq = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in csv.DictReader(open(os.path.join(d, "pmc_sq", "run_counter_collection.csv"))):
         sq[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    lines = ["# rocprofv3 summary -- %s (bench.py --steps 20 --warmup 3, 1x MI355X)" % tag, "",
+    lines = ["# rocprofv3 summary -- %s (bench.py config %s, 1x MI355X)" % (tag, config), "",
              "Kernel stats (`rocprofv3 --kernel-trace --stats`):", "",
              "| kernel | calls | total ms | avg us | pct |", "|---|---|---|---|---|"]
     for s in stats:
@@ -47,18 +47,18 @@ def main(d, tag, config="halfcheetah"):
         lines.append("| %s | %.1f | %.1f | %.0f | %.0f | %.0f | %.0f | %.0f |" % (
             k[:70], f, w, hbm, q.get("SQ_INSTS_VALU", 0), q.get("SQ_INSTS_LDS", 0), q.get("SQ_WAVES", 0),
             q.get("GRBM_GUI_ACTIVE", 0)))
-        if "rollout_kernel" in k:
+        if dominant in k:
             rollout = dict(kernel=k, fetch_size_kb=f, write_size_kb=w, hbm_bytes_per_launch=hbm, sq=q)
     if rollout:
-        st = [s for s in stats if "rollout_kernel" in s["Name"]][0]
+        st = [s for s in stats if dominant in s["Name"]][0]
         avg_ns = float(st["AverageNs"])
         q = rollout["sq"]
         clk = q.get("GRBM_GUI_ACTIVE", 0) / 8 / (avg_ns * 1e-9) / 1e9 if avg_ns else 0
         rollout["avg_duration_us"] = avg_ns / 1e3
         rollout["effective_clock_ghz"] = clk
-        lines += ["", "Rollout kernel: avg %.1f us, effective clock %.2f GHz (GRBM_GUI_ACTIVE/8/duration), "
+        lines += ["", "Dominant kernel (%s): avg %.1f us, effective clock %.2f GHz (GRBM_GUI_ACTIVE/8/duration), "
                       "VALU instructions per wave-step %.1f, LDS per wave-step %.1f." % (
-                          avg_ns / 1e3, clk, q.get("SQ_INSTS_VALU", 0) / max(1, q.get("SQ_WAVES", 1)) / 1000,
+                          dominant, avg_ns / 1e3, clk, q.get("SQ_INSTS_VALU", 0) / max(1, q.get("SQ_WAVES", 1)) / 1000,
                           q.get("SQ_INSTS_LDS", 0) / max(1, q.get("SQ_WAVES", 1)) / 1000)]
         with open(os.path.join("profiles", "pmc_rollout_%s.json" % config), "w") as fh:
             json.dump(dict(rollout, source=d, tag=tag), fh, indent=1)
