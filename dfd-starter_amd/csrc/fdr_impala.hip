@@ -326,56 +326,59 @@ __device__ __forceinline__ void to_padded(const float* X, float* T, const float*
   }
 }
 
-// Stage entry: X <- maxpool3s2p1(conv3x3(T) + b), in bands of 9 conv rows (8b-1 .. 8b+7 -> pooled
-// rows 4b .. 4b+3) through the scratch S [COUT][9][1 + H]: column 0 of S is -inf (the pool's left
-// pad) and conv row -1 of band 0 is stored as -inf, so the pool is branch-free and separable --
-// one thread per (channel, pooled column): 9 horizontal max3, then 4 vertical max3.
-// The B fragments are loaded once, before the caller's barrier, and reused by every band.
-template <int CIN, int COUT, int H, int PLANE>
+// Stage entry: X <- maxpool3s2p1(conv3x3(T) + b), in bands of BR conv rows ((BR-1) b - 1 .. (BR-1) b + BR - 2
+// -> pooled rows (BR-1)/2 * b ..) through the scratch S [COUT][BR][1 + H]: column 0 of S is -inf (the
+// pool's left pad) and conv row -1 of band 0 is stored as -inf, so the pool is branch-free and
+// separable -- one thread per (channel, pooled column): BR horizontal max3, then vertical max3.
+// The B fragments are loaded by the caller and reused by every band.
+template <int CIN, int COUT, int H, int PLANE, int BR>
 __device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, const float (&bf)[(9 * CIN + 3) / 4],
                                             const float* __restrict__ bias, int wave, int lane) {
-  constexpr int WP = H + 2, NT = COUT / 16, MT = kBand * H / 16;
+  constexpr int WP = H + 2, NT = COUT / 16, MT = BR * H / 16, PRB = (BR - 1) / 2;
   constexpr int TPW = (MT * NT + 7) / 8, HO = H / 2, SW = H + 1;
+  static_assert((BR * H) % 16 == 0 && H % (BR - 1) == 0, "band shape");
   const float bn_ = bias[(wave % NT) * 16 + (lane & 15)];
-  for (int i = threadIdx.x; i < COUT * kBand; i += kConvThreads) S[i * SW] = -FLT_MAX;
-  for (int b = 0; b < H / 8; ++b) {
+  for (int i = threadIdx.x; i < COUT * BR; i += kConvThreads) S[i * SW] = -FLT_MAX;
+  for (int b = 0; b < H / (BR - 1); ++b) {
     f32x4 acc[TPW];
-    conv_mfma<CIN, NT, TPW, H, WP, PLANE, MT>(T + (8 * b - 1) * WP, bf, acc, wave, lane);
+    conv_mfma<CIN, NT, TPW, H, WP, PLANE, MT>(T + ((BR - 1) * b - 1) * WP, bf, acc, wave, lane);
     conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) {
       const int r = m / H, x = m % H;
-      S[(n * kBand + r) * SW + 1 + x] = (b == 0 && r == 0) ? -FLT_MAX : v + bn_;
+      S[(n * BR + r) * SW + 1 + x] = (b == 0 && r == 0) ? -FLT_MAX : v + bn_;
     });
     __syncthreads();
     for (int i = threadIdx.x; i < COUT * HO; i += kConvThreads) {
       const int ch = i / HO, px = i - ch * HO;
-      const float* sc = S + ch * kBand * SW + 2 * px;  // columns 2px-1 .. 2px+1 (+1 for the pad column)
-      float hm[kBand];
+      const float* sc = S + ch * BR * SW + 2 * px;  // columns 2px-1 .. 2px+1 (+1 for the pad column)
+      float hm[BR];
 #pragma unroll
-      for (int r = 0; r < kBand; ++r) hm[r] = fmaxf(fmaxf(sc[r * SW], sc[r * SW + 1]), sc[r * SW + 2]);
+      for (int r = 0; r < BR; ++r) hm[r] = fmaxf(fmaxf(sc[r * SW], sc[r * SW + 1]), sc[r * SW + 2]);
 #pragma unroll
-      for (int pr = 0; pr < 4; ++pr)
-        X[(ch * HO + 4 * b + pr) * HO + px] = fmaxf(fmaxf(hm[2 * pr], hm[2 * pr + 1]), hm[2 * pr + 2]);
+      for (int pr = 0; pr < PRB; ++pr)
+        X[(ch * HO + PRB * b + pr) * HO + px] = fmaxf(fmaxf(hm[2 * pr], hm[2 * pr + 1]), hm[2 * pr + 2]);
     }
     __syncthreads();
   }
 }
 
-// Two residual blocks (policies/impala.py:77-105, 152-157) on X [C][H][H], T as scratch.  Each conv's
-// weights are loaded ahead of the barrier that precedes it, so the fetch overlaps LDS work.
-template <int C, int H>
-__device__ __forceinline__ void res_blocks(float* T, float* X, const float* __restrict__ pk, const Layout& L,
-                                           int stage, const float* bsc, const float* bsh, int wave, int lane,
-                                           const StepArgs& a, int k0) {
+// Two residual blocks (policies/impala.py:77-105, 152-157) on X [C][H][H], T [C][H+2][H+2] as the conv
+// input.  On entry T must hold relu(bn0(X)) of block 0 with a zero border, and bf the B fragments of
+// block 0's first conv.  Every BN (+ReLU) that follows a conv is fused into that conv's epilogue:
+//   block 0 conv1 epilogue: X <- X + conv + b; T <- relu(bn0_block1(X))
+//   block 1 conv1 epilogue: LAST == 0: T <- bn_entry(stage+1)(X + conv + b)  (the next stage's input,
+//                           same padded geometry); LAST == 1: out <- relu(X + conv + b) (the features)
+// Weights of the next conv are fetched right after the MFMAs that last read bf, ahead of the barrier.
+template <int C, int H, int LAST>
+__device__ __forceinline__ void res_blocks(float* T, float* X, float (&bf)[(9 * C + 3) / 4], const float* __restrict__ pk,
+                                           const Layout& L, int stage, const float* bsc, const float* bsh, int wave,
+                                           int lane, const StepArgs& a, int k0, float* __restrict__ out) {
   constexpr int WP = H + 2, PLANE = Plane<H>::P, NT = C / 16, MT = H * H / 16;
-  constexpr int TPW = (MT * NT + 7) / 8, KS = (9 * C + 3) / 4;
+  constexpr int TPW = (MT * NT + 7) / 8;
   const int n_ = (wave % NT) * 16 + (lane & 15);
-  float bf[KS];
+  auto tpos = [&](int n, int m) { return n * PLANE + (m / H + 1) * WP + (m % H) + 1; };
+#pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int i0 = stage * 5 + 1 + 2 * r, i1 = i0 + 1;
-    load_frag<C, NT>(pk + L.conv_w[i0], bf, wave, lane);
-    if (r == 0) to_padded<C, H, true, true>(X, T, bsc + i0 * 32, bsh + i0 * 32);
-    else to_padded<C, H, true, false>(X, T, bsc + i0 * 32, bsh + i0 * 32);
-    __syncthreads();
     FDR_STAMP(a, k0 + 4 * r);
     f32x4 acc[TPW];
     conv_mfma<C, NT, TPW, H, WP, PLANE, MT>(T, bf, acc, wave, lane);
@@ -383,16 +386,43 @@ __device__ __forceinline__ void res_blocks(float* T, float* X, const float* __re
     load_frag<C, NT>(pk + L.conv_w[i1], bf, wave, lane);
     __syncthreads();  // every wave is done reading T
     FDR_STAMP(a, k0 + 4 * r + 1);
-    conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) {
-      T[n * PLANE + (m / H + 1) * WP + (m % H) + 1] = relu(fmaf(v + b0, s1, h1));
-    });
+    conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) { T[tpos(n, m)] = relu(fmaf(v + b0, s1, h1)); });
     __syncthreads();
     FDR_STAMP(a, k0 + 4 * r + 2);
     conv_mfma<C, NT, TPW, H, WP, PLANE, MT>(T, bf, acc, wave, lane);
     const float b1 = pk[L.conv_b[i1] + n_];
-    conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) { X[n * H * H + m] = (v + b1) + X[n * H * H + m]; });
-    __syncthreads();
+    // BN that consumes this block's output: block 1's bn0, or the next stage's entry BN
+    const int inext = r == 0 ? i1 + 1 : (stage + 1) * 5;
+    const float s2 = (r == 1 && LAST) ? 0.f : bsc[inext * 32 + n_];
+    const float h2 = (r == 1 && LAST) ? 0.f : bsh[inext * 32 + n_];
+    __syncthreads();  // every wave is done reading T
     FDR_STAMP(a, k0 + 4 * r + 3);
+    if (r == 0) {
+      // two passes over the accumulators (X update, then T) keep the live set small
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        const int q = wave + 8 * i;
+        if (q / NT >= MT) continue;
+        const int m0 = (q / NT) * 16 + (lane >> 4) * 4;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const float xn = (acc[i][rr] + b1) + X[n_ * H * H + m0 + rr];
+          X[n_ * H * H + m0 + rr] = xn;
+          acc[i][rr] = xn;
+        }
+      }
+      conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) { T[tpos(n, m)] = relu(fmaf(v, s2, h2)); });
+      load_frag<C, NT>(pk + L.conv_w[i1 + 1], bf, wave, lane);  // block 1's first conv
+    } else if (!LAST) {
+      conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) {
+        T[tpos(n, m)] = fmaf((v + b1) + X[n * H * H + m], s2, h2);
+      });
+    } else {
+      conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) {
+        out[n * H * H + m] = relu((v + b1) + X[n * H * H + m]);   // flatten (C, H, W), impala.py:159-160
+      });
+    }
+    __syncthreads();
   }
 }
 
@@ -457,37 +487,48 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
   FDR_STAMP(a, 2);
 
   // ---- stage 1: conv 3->16 @64x64, pool -> X1 [16][32][32], residual blocks ----
-  stage_entry<3, 16, 64, FPLANE>(T, T + 3 * FPLANE, X, bf3, pk + L.conv_b[0], wave, ln);
-  FDR_STAMP(a, 3);
-  res_blocks<16, 32>(T, X, pk, L, 0, bsc, bsh, wave, ln, a, 4);
-  // ---- stage 2: BN(X1) -> T; conv 16->32 @32x32 with S2 after T, pool -> X2 [32][16][16] ----
+  stage_entry<3, 16, 64, FPLANE, kBand>(T, T + 3 * FPLANE, X, bf3, pk + L.conv_b[0], wave, ln);
+  {
+    float bf[36];
+    load_frag<16, 1>(pk + L.conv_w[1], bf, wave, ln);
+    to_padded<16, 32, true, true>(X, T, bsc + 1 * 32, bsh + 1 * 32);
+    __syncthreads();
+    FDR_STAMP(a, 3);
+    res_blocks<16, 32, 0>(T, X, bf, pk, L, 0, bsc, bsh, wave, ln, a, 4, nullptr);  // ends with T = BN5(X1)
+  }
+  // ---- stage 2: conv 16->32 @32x32 (S2 after T, over the dead X1), pool -> X2 [32][16][16] ----
+  float* X2 = T + 16 * Plane<32>::P + 32 * kBand * 33;
   {
     float bf[36];
     load_frag<16, 2>(pk + L.conv_w[5], bf, wave, ln);
-    to_padded<16, 32, false, true>(X, T, bsc + 5 * 32, bsh + 5 * 32);
-    __syncthreads();
     FDR_STAMP(a, 12);
-    float* S2 = T + 16 * Plane<32>::P;  // overlaps the dead X1
-    stage_entry<16, 32, 32, Plane<32>::P>(T, S2, S2 + 32 * kBand * 33, bf, pk + L.conv_b[5], wave, ln);
+    stage_entry<16, 32, 32, Plane<32>::P, kBand>(T, T + 16 * Plane<32>::P, X2, bf, pk + L.conv_b[5], wave, ln);
   }
-  float* X2 = T + 16 * Plane<32>::P + 32 * kBand * 33;
-  FDR_STAMP(a, 13);
-  res_blocks<32, 16>(T, X2, pk, L, 1, bsc, bsh, wave, ln, a, 14);
-  // ---- stage 3: BN(X2) -> T; conv 32->32 @16x16, pool -> X3 [32][8][8] ----
-  float* X3 = T + 32 * Plane<16>::P + 32 * kBand * 17;
+  {
+    float bf[72];
+    load_frag<32, 2>(pk + L.conv_w[6], bf, wave, ln);
+    to_padded<32, 16, true, true>(X2, T, bsc + 6 * 32, bsh + 6 * 32);
+    __syncthreads();
+    FDR_STAMP(a, 13);
+    res_blocks<32, 16, 0>(T, X2, bf, pk, L, 1, bsc, bsh, wave, ln, a, 14, nullptr);  // ends with T = BN10(X2)
+  }
+  // ---- stage 3: conv 32->32 @16x16 in one 17-row band, pool -> X3 [32][8][8] ----
+  float* X3 = T + 32 * Plane<16>::P + 32 * 17 * 17;
   {
     float bf[72];
     load_frag<32, 2>(pk + L.conv_w[10], bf, wave, ln);
-    to_padded<32, 16, false, true>(X2, T, bsc + 10 * 32, bsh + 10 * 32);
-    __syncthreads();
     FDR_STAMP(a, 22);
-    stage_entry<32, 32, 16, Plane<16>::P>(T, T + 32 * Plane<16>::P, X3, bf, pk + L.conv_b[10], wave, ln);
+    stage_entry<32, 32, 16, Plane<16>::P, 17>(T, T + 32 * Plane<16>::P, X3, bf, pk + L.conv_b[10], wave, ln);
   }
-  FDR_STAMP(a, 23);
-  res_blocks<32, 8>(T, X3, pk, L, 2, bsc, bsh, wave, ln, a, 24);
-  // ---- relu + flatten (C, H, W) (policies/impala.py:159-160) ----
-  float* out = a.feat + env * kFeat;
-  for (int i = threadIdx.x; i < kFeat; i += kConvThreads) out[i] = relu(X3[i]);
+  {
+    float bf[72];
+    load_frag<32, 2>(pk + L.conv_w[11], bf, wave, ln);
+    to_padded<32, 8, true, true>(X3, T, bsc + 11 * 32, bsh + 11 * 32);
+    __syncthreads();
+    FDR_STAMP(a, 23);
+    // ---- relu + flatten (C, H, W) fused into the last epilogue (policies/impala.py:159-160) ----
+    res_blocks<32, 8, 1>(T, X3, bf, pk, L, 2, bsc, bsh, wave, ln, a, 24, a.feat + env * kFeat);
+  }
   FDR_STAMP(a, 32);
 }
 

@@ -14,17 +14,17 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from fdr import engine  # noqa: E402
 from fdr._lib import lib  # noqa: E402
 
-NAMES = {0: "start", 1: "bn table + zero", 2: "frame", 3: "stage1 entry conv+pool"}
-for st, k0, pre in ((1, 4, None), (2, 14, 12), (3, 24, 22)):
-    if pre is not None:
-        NAMES[pre] = "stage%d BN -> padded" % st
-        NAMES[pre + 1] = "stage%d entry conv+pool" % st
+NAMES = {0: "start", 1: "bn table + zero", 2: "frame"}
+for st, pre, k0 in ((1, 2, 4), (2, 12, 14), (3, 22, 24)):
+    NAMES[pre + 1] = "stage%d entry conv+pool+bn" % st
     for r in range(2):
-        NAMES[k0 + 4 * r] = "stage%d res%d bn0+relu" % (st, r)
+        NAMES[k0 + 4 * r] = "stage%d res%d (launch)" % (st, r) if r == 0 else "stage%d res0 conv1 epilogue" % st
         NAMES[k0 + 4 * r + 1] = "stage%d res%d conv0" % (st, r)
-        NAMES[k0 + 4 * r + 2] = "stage%d res%d epilogue" % (st, r)
-        NAMES[k0 + 4 * r + 3] = "stage%d res%d conv1+add" % (st, r)
-NAMES[32] = "relu + store"
+        NAMES[k0 + 4 * r + 2] = "stage%d res%d epilogue0" % (st, r)
+        NAMES[k0 + 4 * r + 3] = "stage%d res%d conv1" % (st, r)
+NAMES[12] = "stage1 res1 conv1 epilogue"
+NAMES[22] = "stage2 res1 conv1 epilogue"
+NAMES[32] = "stage3 res1 conv1 epilogue (features)"
 
 
 def main():
