@@ -38,6 +38,8 @@ int64_t grad_workspace_bytes(int n_dirs, int64_t P);
 int launch_fd_grad(const float* table, int64_t table_size, const int64_t* idx, const double* coef,
                    int n_dirs, int64_t P, double* g, void* ws, int64_t ws_bytes, hipStream_t stream);
 int64_t dsgd_workspace_bytes(int64_t P);
+int launch_strategy_dist(const float* S, int n, const float* B, int H, int Z, int D, int kind, double* dists,
+                         double* min_d, int32_t* arg, hipStream_t stream);
 int launch_dsgd(float* theta, const double* g, int64_t P, double lr, double lr_scale, double* out,
                 void* ws, int64_t ws_bytes, hipStream_t stream);
 
@@ -133,6 +135,14 @@ int fdr_rollout(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc*
                 const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
                 const float* obs_mean, const float* obs_std, double* ret, double* ent,
                 int32_t* steps, double* norm2, fdr_stream stream) {
+  return fdr_rollout_states(ctx, policy, env, lanes, n_lanes, seed, jiggle, obs_mean, obs_std, ret, ent, steps,
+                            norm2, nullptr, stream);
+}
+
+int fdr_rollout_states(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc* env,
+                       const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
+                       const float* obs_mean, const float* obs_std, double* ret, double* ent,
+                       int32_t* steps, double* norm2, float* states, fdr_stream stream) {
   (void)ctx;
   PolicyKey k;
   int rc = policy_key(policy, &k);
@@ -181,6 +191,7 @@ int fdr_rollout(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc*
   a.ent = ent;
   a.steps = steps;
   a.norm2 = norm2;
+  a.states = states;
   return launch_rollout(k, env->kind, a, (hipStream_t)stream);
 }
 
@@ -335,4 +346,17 @@ int fdr_impala_profile_read(double* ms) {
 int fdr_impala_debug_clock(uint64_t* buf) {
   impala::set_debug_clock(buf);
   return FDR_OK;
+}
+
+int fdr_strategy_distances(fdr_ctx* ctx, const float* strategies, int32_t n, const float* archive, int32_t n_archive,
+                           int32_t n_states, int32_t dim, int32_t kind, double* dists, double* min_dist,
+                           int32_t* argmin, fdr_stream stream) {
+  (void)ctx;
+  if (n < 0 || n_archive <= 0 || n_states <= 0 || dim <= 0) return set_error(FDR_ERR_INVALID, "bad sizes");
+  if (n > 0 && (!strategies || !archive)) return set_error(FDR_ERR_INVALID, "NULL pointer");
+  if (kind != FDR_DIST_L2 && kind != FDR_DIST_TVD && kind != FDR_DIST_W2)
+    return set_error(FDR_ERR_INVALID, "unknown distance kind");
+  if (kind == FDR_DIST_W2 && (dim & 1)) return set_error(FDR_ERR_INVALID, "W2 needs dim = 2k ([mean | std])");
+  return launch_strategy_dist(strategies, n, archive, n_archive, n_states, dim, kind, dists, min_dist, argmin,
+                              (hipStream_t)stream);
 }

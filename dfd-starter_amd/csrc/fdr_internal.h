@@ -73,6 +73,7 @@ struct RolloutArgs {
   double* ent;
   int32_t* steps;
   double* norm2;
+  float* states;  // NULL, or [n_lanes, T, n_in] visited raw observations (fdr_rollout_states)
 };
 
 int launch_policy_forward(const PolicyKey& k, const LanesArgs& lanes, int n_lanes,

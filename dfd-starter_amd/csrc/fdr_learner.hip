@@ -274,3 +274,73 @@ int launch_dsgd(float* theta, const double* g, int64_t P, double lr, double lr_s
 }
 
 }  // namespace fdr
+
+namespace fdr {
+
+// ------------------------------------------------------------------------------------------
+// Strategy distances / novelty (utils/math_helpers.py:147-222, strategy/*): one 256-thread block
+// per strategy i holds it in LDS; each wave walks archive entries h = w, w+4, ..., its lanes over
+// the probe states z, f64 accumulation, fixed reduction order.  d[i][h] = mean_z term(a_iz, b_hz).
+// ------------------------------------------------------------------------------------------
+constexpr int kNovThreads = 256;
+constexpr int kNovMaxZD = 8192;  // floats of one strategy held in LDS (32 KiB)
+
+__global__ __launch_bounds__(kNovThreads) void strategy_dist_kernel(const float* __restrict__ S, const float* __restrict__ B,
+                                                                   int H, int Z, int D, int kind, double* __restrict__ dists,
+                                                                   double* __restrict__ min_d, int32_t* __restrict__ arg) {
+  __shared__ float a[kNovMaxZD];
+  __shared__ double wmin[kNovThreads / kWave];
+  __shared__ int warg[kNovThreads / kWave];
+  const int i = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ZD = Z * D;
+  for (int t = threadIdx.x; t < ZD; t += kNovThreads) a[t] = S[(int64_t)i * ZD + t];
+  __syncthreads();
+  double best = __builtin_inf();
+  int best_h = -1;
+  const int k = D / 2;
+  for (int h = wave; h < H; h += kNovThreads / kWave) {
+    const float* b = B + (int64_t)h * ZD;
+    double acc = 0.0;
+    for (int z = lane; z < Z; z += kWave) {
+      const float* az = a + z * D;
+      const float* bz = b + z * D;
+      double term = 0.0;
+      if (kind == FDR_DIST_TVD) {
+        for (int d = 0; d < D; ++d) term += fabs((double)az[d] - (double)bz[d]);
+      } else if (kind == FDR_DIST_L2) {
+        for (int d = 0; d < D; ++d) { const double df = (double)bz[d] - (double)az[d]; term += df * df; }
+        term = sqrt(term);
+      } else {  // FDR_DIST_W2: [mean | std]
+        for (int d = 0; d < k; ++d) {
+          const double dm = (double)az[d] - (double)bz[d];
+          const double s1 = az[k + d], s2 = bz[k + d];
+          term += dm * dm + (s1 + s2 - 2.0 * sqrt(s1 * s2));
+        }
+      }
+      acc += term;
+    }
+    acc = wave_sum(acc) / (double)Z;
+    if (dists && lane == 0) dists[(int64_t)i * H + h] = acc;
+    if (acc < best) { best = acc; best_h = h; }  // h increases: first minimum kept
+  }
+  if (lane == 0) { wmin[wave] = best; warg[wave] = best_h; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = __builtin_inf();
+    int am = -1;
+    for (int w = 0; w < kNovThreads / kWave; ++w)
+      if (warg[w] >= 0 && (wmin[w] < m || (wmin[w] == m && warg[w] < am))) { m = wmin[w]; am = warg[w]; }
+    if (min_d) min_d[i] = m;
+    if (arg) arg[i] = am;
+  }
+}
+
+int launch_strategy_dist(const float* S, int n, const float* B, int H, int Z, int D, int kind, double* dists,
+                         double* min_d, int32_t* arg, hipStream_t stream) {
+  if ((int64_t)Z * D > kNovMaxZD) return set_error(FDR_ERR_UNSUPPORTED, "Z * D exceeds 8192");
+  if (n == 0) return FDR_OK;
+  hipLaunchKernelGGL(strategy_dist_kernel, dim3(n), dim3(kNovThreads), 0, stream, S, B, H, Z, D, kind, dists, min_d, arg);
+  return check_launch("strategy_dist_kernel");
+}
+
+}  // namespace fdr

@@ -223,7 +223,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock) void policy_forward_kernel(
 // ---------------------------------------------------------------------------------------------
 // Whole-episode rollout: fdr_rollout
 // ---------------------------------------------------------------------------------------------
-template <int NIN, int NA, bool DISC, int ENV>
+template <int NIN, int NA, bool DISC, int ENV, bool REC>
 __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(RolloutArgs a) {
   using Lane = MlpLane<NIN, NA, DISC>;
   constexpr int NQI = Lane::NQI;
@@ -287,6 +287,9 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
       const int ds = j / kDrawsPerStep, dk = j % kDrawsPerStep;
       const uint64_t h = hash_ctr(key, ulane, (uint64_t)(t + ds), (uint64_t)dk);
       rbuf = DISC ? uniform24(h) : normal_bm(h);
+    }
+    if constexpr (REC) {  // visited (raw) observations, worker/agent.py:36 / 58-59 (save_states)
+      if (j < NIN) a.states[((int64_t)lane * T + t) * NIN + j] = s;
     }
     float X[NQI];
     row_allgather<NQI>(policy_input(s), X);
@@ -419,12 +422,18 @@ int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hi
     if (Layout<NIN, NA, DISC>::P != k.n_params)                                                 \
       return set_error(FDR_ERR_INVALID, "n_params does not match the policy layout");           \
     if (env_kind == FDR_ENV_SYNTH) {                                                            \
-      hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, FDR_ENV_SYNTH>), grid, block, 0, stream, args); \
+      if (args.states)                                                                          \
+        hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, FDR_ENV_SYNTH, true>), grid, block, 0, stream, args); \
+      else                                                                                      \
+        hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, FDR_ENV_SYNTH, false>), grid, block, 0, stream, args); \
       return check_launch("rollout_kernel<synth>");                                             \
     }                                                                                           \
     if constexpr (NIN == 2 && NA == 9 && DISC) {                                                \
       if (env_kind == FDR_ENV_TRAP) {                                                           \
-        hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, FDR_ENV_TRAP>), grid, block, 0, stream, args); \
+        if (args.states)                                                                        \
+          hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, FDR_ENV_TRAP, true>), grid, block, 0, stream, args); \
+        else                                                                                    \
+          hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, FDR_ENV_TRAP, false>), grid, block, 0, stream, args); \
         return check_launch("rollout_kernel<trap>");                                            \
       }                                                                                         \
     }                                                                                           \

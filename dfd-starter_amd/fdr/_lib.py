@@ -12,13 +12,15 @@ LIB_PATH = os.environ.get("FDR_LIB", os.path.join(_HERE, "libfdr.so"))
 FDR_OK, FDR_ERR_INVALID, FDR_ERR_UNSUPPORTED, FDR_ERR_HIP, FDR_ERR_WORKSPACE = 0, 1, 2, 3, 4
 FDR_POLICY_DISCRETE, FDR_POLICY_MUJOCO = 0, 1
 FDR_ENV_SYNTH, FDR_ENV_TRAP = 0, 1
+FDR_DIST_L2, FDR_DIST_TVD, FDR_DIST_W2 = 0, 1, 2
 
 EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy", "fdr_ctx_device",
            "fdr_perturb", "fdr_policy_forward", "fdr_rollout", "fdr_fd_weights",
            "fdr_fd_grad_workspace_bytes", "fdr_fd_grad", "fdr_dsgd_workspace_bytes", "fdr_dsgd_step",
            "fdr_impala_num_params", "fdr_impala_num_bn_stats", "fdr_impala_workspace_bytes",
            "fdr_impala_rollout", "fdr_impala_forward_workspace_bytes", "fdr_impala_forward",
-           "fdr_impala_profile", "fdr_impala_profile_read", "fdr_impala_debug_clock")
+           "fdr_impala_profile", "fdr_impala_profile_read", "fdr_impala_debug_clock",
+           "fdr_strategy_distances", "fdr_rollout_states")
 
 
 class FDRError(RuntimeError):
@@ -68,6 +70,8 @@ def _load():
                                               P, P, P]),
         "fdr_rollout": (ctypes.c_int, [P, ctypes.POINTER(PolicyDesc), ctypes.POINTER(EnvDesc),
                                        ctypes.POINTER(LanesDesc), I32, U64, I32, P, P, P, P, P, P, P]),
+        "fdr_rollout_states": (ctypes.c_int, [P, ctypes.POINTER(PolicyDesc), ctypes.POINTER(EnvDesc),
+                                              ctypes.POINTER(LanesDesc), I32, U64, I32, P, P, P, P, P, P, P, P]),
         "fdr_fd_weights": (ctypes.c_int, [P, P, I32, F64, I32, I32, P, P, I32, F32, P, P]),
         "fdr_fd_grad_workspace_bytes": (I64, [I32, I64]),
         "fdr_fd_grad": (ctypes.c_int, [P, P, I64, P, P, I32, I64, P, P, I64, P]),
@@ -82,6 +86,7 @@ def _load():
         "fdr_impala_profile": (ctypes.c_int, [I32]),
         "fdr_impala_profile_read": (ctypes.c_int, [P]),
         "fdr_impala_debug_clock": (ctypes.c_int, [P]),
+        "fdr_strategy_distances": (ctypes.c_int, [P, P, I32, P, I32, I32, I32, I32, P, P, P, P]),
         "fdr_impala_forward": (ctypes.c_int, [P, ctypes.POINTER(ImpalaDesc), P, I32, P, P, P, P, P, P, P, P, I64,
                                               P]),
     }

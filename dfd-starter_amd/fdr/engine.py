@@ -94,7 +94,8 @@ class RolloutResult(object):
 
 
 def rollout(spec, env, lanes, n_lanes, seed, jiggle=True, obs_mean=None, obs_std=None,
-            bn_mean=None, bn_var=None, out=None, device=None):
+            bn_mean=None, bn_var=None, out=None, device=None, states=None):
+    """fdr_rollout; with states (f32 [n_lanes, T, n_in] device tensor) fdr_rollout_states."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     _check_dev(obs_mean, obs_std, bn_mean, bn_var)
     if out is None:
@@ -104,6 +105,16 @@ def rollout(spec, env, lanes, n_lanes, seed, jiggle=True, obs_mean=None, obs_std
                             torch.empty(n_lanes, dtype=torch.float64, device=dev))
     pd = spec.desc(bn_mean, bn_var)
     ed = env.desc()
+    if states is not None:
+        _check_dev(states)
+        if states.dtype != torch.float32 or not states.is_contiguous() or \
+                states.numel() != n_lanes * env.episode_len * spec.n_in:
+            raise ValueError("states must be contiguous float32 [n_lanes, T, n_in]")
+        check(lib.fdr_rollout_states(None, ctypes.byref(pd), ctypes.byref(ed), ctypes.byref(lanes), n_lanes,
+                                     ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(obs_mean),
+                                     _p(obs_std), _p(out.reward), _p(out.entropy), _p(out.timesteps),
+                                     _p(out.norm2), _p(states), _stream(dev)), "fdr_rollout_states")
+        return out
     check(lib.fdr_rollout(None, ctypes.byref(pd), ctypes.byref(ed), ctypes.byref(lanes), n_lanes,
                           ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(obs_mean),
                           _p(obs_std), _p(out.reward), _p(out.entropy), _p(out.timesteps), _p(out.norm2),
@@ -249,3 +260,38 @@ def impala_profile_read():
     out = (ctypes.c_double * 3)()
     check(lib.fdr_impala_profile_read(ctypes.cast(out, ctypes.c_void_p)), "fdr_impala_profile_read")
     return tuple(out)
+
+
+# ---- strategy distances / novelty (utils/math_helpers.py:147-222) ---------------------------------
+DIST_KINDS = {"l2": _lib.FDR_DIST_L2, "tvd": _lib.FDR_DIST_TVD, "w2": _lib.FDR_DIST_W2}
+
+
+def strategy_distances(strategies, archive, kind, full=False):
+    """strategies [n, Z, D], archive [H, Z, D] (f32 device) -> (min [n] f64, argmin [n] i32[, dists [n, H]])."""
+    _check_dev(strategies, archive)
+    S = strategies.to(torch.float32).contiguous()
+    B = archive.to(torch.float32).contiguous()
+    n, Z, D = S.shape
+    H = B.shape[0]
+    if tuple(B.shape[1:]) != (Z, D):
+        raise ValueError("archive shape %s does not match strategies %s" % (tuple(B.shape), tuple(S.shape)))
+    dev = S.device
+    mn = torch.empty(n, dtype=torch.float64, device=dev)
+    am = torch.empty(n, dtype=torch.int32, device=dev)
+    dd = torch.empty((n, H), dtype=torch.float64, device=dev) if full else None
+    check(lib.fdr_strategy_distances(None, _p(S), n, _p(B), H, Z, D, DIST_KINDS[kind], _p(dd), _p(mn), _p(am),
+                                     _stream(dev)), "fdr_strategy_distances")
+    return (mn, am, dd) if full else (mn, am)
+
+
+def lane_strategies(spec, lanes_fn, n_lanes, zeta, bn_mean=None, bn_var=None):
+    """get_strategy (discrete: probs; mujoco: [mean | std]) of n_lanes policies over the Z probe
+    states zeta -> f32 [n_lanes, Z, D].  lanes_fn(Z) must return a lanes descriptor of n_lanes * Z
+    (policy, state) pairs, policy-major (every lane field repeated Z times)."""
+    _check_dev(zeta)
+    Z = zeta.shape[0]
+    x = zeta.to(torch.float32).reshape(Z, -1).repeat(n_lanes, 1).contiguous()
+    out = policy_forward(spec, lanes_fn(Z), n_lanes * Z, x, bn_mean, bn_var)
+    if isinstance(out, tuple):
+        out = torch.cat(out, dim=-1)
+    return out.reshape(n_lanes, Z, -1)

@@ -65,7 +65,8 @@ class FDBatch(object):
         ent = self.entropy.double().cpu().numpy()
         ts = self.timesteps.cpu().numpy()
         n2 = self.norm2.cpu().numpy() if self.norm2 is not None else [None] * len(rew)
-        nov = np.zeros(len(rew)) if self.novelty is None else np.asarray(self.novelty)
+        nov = np.zeros(len(rew)) if self.novelty is None else \
+            (self.novelty.double().cpu().numpy() if torch.is_tensor(self.novelty) else np.asarray(self.novelty))
         out = []
         for i in range(len(rew)):
             r = FDReturn()

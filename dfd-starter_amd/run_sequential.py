@@ -79,6 +79,8 @@ class SequentialRunner(object):
         self.policy_reward = 0
         self.policy_entropy = 0
         self.policy_novelty = 0
+        self.zeta = np.zeros((0, self.policy.input_shape), np.float32)
+        self.zeta_idxs = []
         self.vbn_buffer = None
         if vbn_buffer_size > 0:
             # run_sequential.py:198-213 samples the buffer from env steps; the GPU envs expose no host
@@ -89,6 +91,20 @@ class SequentialRunner(object):
         self.current_state.policy_params = self.policy.get_trainable_flat()
         self.current_state.epoch = 0
         self.history = []
+
+    def _update_zeta(self, eval_states):
+        """run_sequential.py:142-143: shuffled slots of the probe set zeta take an eval episode's states.
+        The reference starts from zeta = [] (so the fancy-index assignment raises); here the first eval
+        episode seeds zeta with its first zeta_size states."""
+        if eval_states is None or len(eval_states) == 0:
+            return
+        if len(self.zeta) == 0:
+            self.zeta = np.array(eval_states[:self.zeta_size], np.float32)
+            self.zeta_idxs = list(range(len(self.zeta)))
+            return
+        self.rng.shuffle(self.zeta_idxs)
+        new = np.asarray(eval_states[:self.zeta_size], np.float32)
+        self.zeta[self.zeta_idxs[:len(new)]] = new[:len(self.zeta_idxs)]
 
     def _schedule(self):
         """Eval coins in the reference's order until batch_size training returns (run_sequential.py:134)."""
@@ -116,15 +132,21 @@ class SequentialRunner(object):
                                    else np.ones(n_dirs, np.int8), np.zeros(int(is_eval.sum()), np.int8)])
             det = (sign == 0).astype(np.int8)
             res, idx_d, sign_d = self.worker.launch(lidx, sign, det, jiggle=False)
+            nov = self.worker.lane_novelty(idx_d, sign_d)          # worker.py:53, every lane at once
+            nov = np.zeros(len(lidx)) if nov is None else nov.cpu().numpy()
             rew = res.reward.cpu().numpy() + np.array([self.agent.rng.choice((-1e-12, 1e-12)) for _ in lidx])
             ent = res.entropy.cpu().numpy()
             steps = int(res.timesteps.sum().item())
             self.agent.cumulative_timesteps += steps
             n_train = n_dirs * lpd
-            for r, e in zip(rew[n_train:], ent[n_train:]):
+            eval_states = self.worker.eval_states() if is_eval.any() else None
+            for r, e, nv in zip(rew[n_train:], ent[n_train:], nov[n_train:]):
                 self.policy_reward = self.policy_reward * 0.9 + r * 0.1
                 self.policy_entropy = self.policy_entropy * 0.9 + e * 0.1
+                self.policy_novelty = self.policy_novelty * 0.9 + nv * 0.1
+                self._update_zeta(eval_states)
             if is_eval.any():
+                self.strategy_handler.set_zeta(self.zeta)
                 self.omega.step(float(np.mean(rew[:n_train])))
             dev = self.policy.flat.device
             batch = FDBatch(torch.as_tensor(rew[:n_train], device=dev), res.entropy[:n_train],
@@ -134,6 +156,9 @@ class SequentialRunner(object):
             if self.vbn_buffer is not None:
                 self.policy.compute_vbn(self.vbn_buffer)
             if update_magnitude > 0:
+                self.strategy_handler.add_policy(self.policy)                   # run_sequential.py:160
+                self.current_state.strategy_frames = self.zeta
+                self.current_state.strategy_history = self.strategy_handler.strategy_tensor
                 self.current_state.policy_params = self.policy.get_trainable_flat()
                 self.current_state.epoch = self.learner.epoch
                 self.worker.update(self.current_state)
@@ -144,7 +169,7 @@ class SequentialRunner(object):
                           "Policy Entropy": self.policy_entropy,
                           "Policy Novelty": self.policy_novelty,
                           "Noisy Reward": float(np.mean(rew[:n_train])),
-                          "Noisy Novelty": 0.0,
+                          "Noisy Novelty": float(np.mean(nov[:n_train])),
                           "Update Magnitude": update_magnitude,
                           "Omega": self.omega.omega}
                 self.history.append(dict(report, idx=idx_dirs, rewards=rew[:n_train]))

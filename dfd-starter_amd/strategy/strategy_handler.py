@@ -1,62 +1,142 @@
-"""Novelty archive -- the API of strategy/strategy_handler.py:6-31 (not a hot-path row).
+"""Novelty archive -- strategy/strategy_handler.py:6-31 + sparse_history_manager.py:6-148 on the GPU
+(SURVEY 8f.2).
 
-A strategy is policy.get_strategy(zeta) (the HIP forward over the probe states zeta); novelty is
-the minimum distance to the archived strategies (utils/math_helpers.py:147-155).  When the archive
-is full, a new point replaces one member of the closest pair if it is more novel than that pair's
-distance (sparse_history_manager.py:73-109, simplified bookkeeping).  Novelty is reported but, as in
-the reference, not used by the objective (learner/finite_differences.py:48).
+A strategy is ``policy.get_strategy(zeta)`` over the probe states zeta (discrete: probs; mujoco:
+[mean | std]); the archive holds up to ``max_history_size`` strategies as ONE device tensor
+[H, Z, D].  Strategies come from the HIP policy forward over (policy, state) pairs
+(``engine.lane_strategies``), distances and novelty from ``fdr_strategy_distances`` (the reference's
+``l2_dist`` / ``categorical_tvd`` / ``gaussian_wasserstein_dist_from_strategies``, f64 accumulation).
+``lane_novelty`` scores every perturbed lane of a batch in two launches -- the batched form of
+``Worker._build_ret``'s per-return ``compute_novelty`` (worker/worker.py:53), which the reference
+evaluates on the perturbed policy.  Replacement when full follows ``_replace_point`` /
+``_update_strategy_point_dists`` (sparse_history_manager.py:73-148) on the pairwise distance table.
 """
 import numpy as np
+import torch
 
-from utils import math_helpers
+from fdr import engine
+
+# reference distance functions -> fdr_strategy_distances kinds (SURVEY finding 6: the reference's
+# run_sequential passes gaussian_wasserstein_dist where the *_from_strategies form is meant)
+KIND_BY_NAME = {"l2_dist": "l2", "categorical_tvd": "tvd", "gaussian_wasserstein_dist_from_strategies": "w2",
+                "gaussian_wasserstein_dist": "w2"}
 
 
 class StrategyHandler(object):
-    def __init__(self, policy, strategy_distance_fn, max_history_size=200):
+    def __init__(self, policy, strategy_distance_fn=None, max_history_size=200):
         self.policy = policy
         self.strategy_distance_fn = strategy_distance_fn
+        name = getattr(strategy_distance_fn, "__name__", "l2_dist") if strategy_distance_fn is not None \
+            else "l2_dist"                     # compute_strategy_novelty's default (math_helpers.py:148-149)
+        if name not in KIND_BY_NAME:
+            raise ValueError("unsupported strategy distance %r" % name)
+        self.kind = KIND_BY_NAME[name]
         self.max_history_size = max_history_size
-        self.points = []              # flat parameter vectors (host)
-        self.strategy_tensor = np.zeros(0)
-        self.zeta = None
+        self.points = []              # archived flat parameter vectors (host, as StrategyPoint.flat)
+        self.archive = None           # device f32 [H, Z, D]
+        self.pair = None              # host f64 [H, H] known distances (inf on the diagonal)
+        self.worst_point_idx = 0
+        self.zeta = None              # device f32 [Z, n_in]
 
-    def _strategy(self, flat):
-        old = self.policy.get_trainable_flat()
-        self.policy.set_trainable_flat(flat)
-        s = self.policy.get_strategy(self.zeta)
-        self.policy.set_trainable_flat(old)
-        return s
+    # ---- strategies on the device ------------------------------------------------------------
+    def _dev(self):
+        return self.policy.flat.device
 
-    def add_policy(self, policy):
-        flat = policy.get_trainable_flat()
-        if len(self.points) < self.max_history_size or self.zeta is None or len(self.zeta) == 0:
-            self.points.append(flat)
-            if self.zeta is not None and len(self.zeta):
-                self.set_zeta(self.zeta)
-            return None
-        s = self._strategy(flat)
-        nov, dists = math_helpers.compute_strategy_novelty(s, self.strategy_tensor, True, self.strategy_distance_fn)
-        n = len(self.points)
-        pair = np.array([[math_helpers.compute_strategy_distance(self.strategy_tensor[i], self.strategy_tensor[j],
-                                                                 self.strategy_distance_fn) if i != j else np.inf
-                          for j in range(n)] for i in range(n)])
-        i, j = np.unravel_index(np.argmin(pair), pair.shape)
-        if nov > pair[i, j]:
-            second = np.sort(pair, axis=1)[:, 1] if n > 2 else np.zeros(n)
-            k = i if second[i] <= second[j] else j
-            self.points[k] = flat
-            self.strategy_tensor[k] = s
-            return k
-        return -1
+    def _strategies_of_flat(self, flat):
+        """get_strategy(zeta) of one parameter vector -> [1, Z, D]."""
+        p = self.policy
+        base = torch.as_tensor(np.asarray(flat, np.float32), device=self._dev()).contiguous()
+        bm, bv = p.bn_stats()
+        return engine.lane_strategies(p.spec, lambda Z: engine.lanes_desc(base, 0), 1, self.zeta, bm, bv)
 
+    def lane_strategies(self, table, idx, sign, sigma):
+        """Strategies of the perturbed lanes theta + sign * sigma * table[idx:] -> [n, Z, D]."""
+        p = self.policy
+        n = idx.numel()
+        bm, bv = p.bn_stats()
+
+        def lanes(Z):
+            return engine.lanes_desc(p.flat, 0, table, idx.repeat_interleave(Z), sign.repeat_interleave(Z), sigma)
+        return engine.lane_strategies(p.spec, lanes, n, self.zeta, bm, bv)
+
+    @property
+    def strategy_tensor(self):
+        """The reference attribute (run_sequential.py:107,162): the archive as a host array."""
+        return np.zeros(0) if self.archive is None else self.archive.cpu().numpy()
+
+    def _ready(self):
+        return self.zeta is not None and self.archive is not None and self.archive.shape[0] >= 2
+
+    # ---- reference API -----------------------------------------------------------------------
     def set_zeta(self, zeta):
+        """strategy_handler.py:19-24 -> evaluate_strategies + _construct_table (:33-71)."""
         if zeta is None or len(zeta) == 0:
             return
-        self.zeta = np.asarray(zeta)
-        self.strategy_tensor = np.asarray([self._strategy(f) for f in self.points])
+        z = torch.as_tensor(np.asarray(zeta, np.float32), device=self._dev())
+        self.zeta = z.reshape(z.shape[0], -1).contiguous()
+        if not self.points:
+            return
+        self.archive = torch.cat([self._strategies_of_flat(f) for f in self.points]).contiguous()
+        self._construct_table()
+
+    def _construct_table(self):
+        H = self.archive.shape[0]
+        _, _, d = engine.strategy_distances(self.archive, self.archive, self.kind, full=True)
+        self.pair = d.cpu().numpy()
+        self.pair[np.arange(H), np.arange(H)] = np.inf
+        self._update_worst()
+
+    def _update_worst(self):
+        """_update_strategy_point_dists (:110-148): closest / second-closest per point, then the less
+        novel member of the closest pair (first strict minimum in index order, as the reference)."""
+        D = self.pair
+        n = D.shape[0]
+        if n < 2:
+            self.worst_point_idx = 0
+            return
+        closest = np.argmin(D, axis=1)
+        cd = D[np.arange(n), closest]
+        second = np.sort(D, axis=1)[:, 1] if n > 2 else np.full(n, np.inf)
+        worst, worst_dist = 0, np.inf
+        for i in range(n):
+            if cd[i] < worst_dist:
+                j = closest[i]
+                worst_dist = cd[i]
+                worst = i if second[i] < second[j] else j
+        self.worst_point_idx = int(worst)
+
+    def add_policy(self, policy):
+        """strategy_handler.py:16-17 -> submit_policy (:17-30) / _replace_point (:73-108)."""
+        flat = np.asarray(policy.get_trainable_flat(), np.float32).copy()
+        if len(self.points) < self.max_history_size or self.zeta is None or self.archive is None:
+            self.points.append(flat)   # the archive is re-evaluated at the next set_zeta, as the reference
+            return None
+        s = self._strategies_of_flat(flat)
+        mn, _, d = engine.strategy_distances(s, self.archive, self.kind, full=True)
+        novelty, dists = float(mn.item()), d[0].cpu().numpy()
+        idx = self.worst_point_idx
+        current_worst = self.pair[idx].min()
+        if novelty > current_worst or current_worst == np.inf:
+            self.points[idx] = flat
+            self.archive[idx] = s[0]
+            others = np.arange(self.pair.shape[0]) != idx
+            self.pair[idx, others] = dists[others]
+            self.pair[others, idx] = dists[others]
+            self._update_worst()
+            return idx
+        return -1
 
     def compute_novelty(self, policy):
-        if self.zeta is None or len(self.zeta) == 0 or self.strategy_tensor is None or len(self.strategy_tensor) < 2:
+        """strategy_handler.py:26-31: min distance of policy's strategy to the archive (0 if not ready)."""
+        if not self._ready():
             return 0
-        s = policy.get_strategy(self.zeta)
-        return math_helpers.compute_strategy_novelty(s, self.strategy_tensor, distance_fn=self.strategy_distance_fn)
+        mn, _ = engine.strategy_distances(self._strategies_of_flat(policy.get_trainable_flat()), self.archive,
+                                          self.kind)
+        return float(mn.item())
+
+    def lane_novelty(self, table, idx, sign, sigma):
+        """Novelty of every perturbed lane (device f64 [n]); zeros if the archive is not ready."""
+        if not self._ready():
+            return torch.zeros(idx.numel(), dtype=torch.float64, device=self._dev())
+        mn, _ = engine.strategy_distances(self.lane_strategies(table, idx, sign, sigma), self.archive, self.kind)
+        return mn

@@ -80,8 +80,9 @@ class Worker(object):
                              bn_mean=bm, bn_var=bv, out=out, device=p.flat.device)
         return res, idx_d, sign_d
 
-    def evaluate(self, n_dirs, antithetic=True, seed=None, lane_range=None, out=None):
+    def evaluate(self, n_dirs, antithetic=True, seed=None, lane_range=None, out=None, novelty=False):
         """n_dirs perturbation directions (x2 lanes if antithetic) -> FDBatch on the device.
+        novelty=True also scores every lane against the strategy archive (FDBatch.novelty, device f64).
 
         lane_range=(lo, hi) evaluates only that slice of the lanes (multi-GPU sharding: every rank
         draws the full index list, in order, and keeps its contiguous share)."""
@@ -104,8 +105,9 @@ class Worker(object):
         if E > 1:
             lidx, sign = np.repeat(lidx, E), np.repeat(sign, E)
         self.agent.cumulative_timesteps += int(len(lidx)) * self.agent.env.episode_len
+        nov = self.lane_novelty(idx_d, sign_d) if novelty else None
         return FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, lidx, sign, self.epoch,
-                       lanes_per_dir=lpd * E)
+                       lanes_per_dir=lpd * E, novelty=nov)
 
     # ---- reference API ----------------------------------------------------------------------
     @torch.no_grad()
@@ -117,18 +119,48 @@ class Worker(object):
             idx[~is_eval] = self.noise_source.sample_batch(k)
         sign = np.where(is_eval, 0, 1).astype(np.int8)
         res, idx_d, sign_d = self.launch(idx, sign, is_eval.astype(np.int8), jiggle=False)
+        nov = self.lane_novelty(idx_d, sign_d)
         E = getattr(self.agent.env, "envs_per_lane", 1)
         if E > 1:
             idx, sign, is_eval = np.repeat(idx, E), np.repeat(sign, E), np.repeat(is_eval, E)
+        eval_states = self.eval_states() if is_eval.any() else None
         b = FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, idx, sign, self.epoch,
                     is_eval=is_eval)
+        b.novelty = None if nov is None else nov.cpu().numpy()
         rets = b.to_returns()
         for r in rets:
             r.reward += self.agent.rng.choice((-1e-12, 1e-12))     # agent.py:69
             self.agent.cumulative_timesteps += r.timesteps
-            r.novelty = self.strategy_handler.compute_novelty(self.policy) if self.strategy_handler else 0
+            if r.is_eval and eval_states is not None:
+                r.eval_states = list(eval_states)                   # worker.py:35 (agent.saved_states)
             r.obs_stats_update = self.agent.obs_stats.serialize()
         return rets
+
+    # ---- novelty path -----------------------------------------------------------
+    def lane_novelty(self, idx_d, sign_d):
+        """compute_novelty of every lane's (perturbed) policy, worker.py:53, batched on the device
+        (f64 [n]); None without a strategy handler."""
+        h = self.strategy_handler
+        if h is None or self.policy.KIND == "impala":
+            return None
+        return h.lane_novelty(self.noise_source.device_table(self.policy.flat.device), idx_d, sign_d, self.sigma)
+
+    def eval_states(self):
+        """Visited raw observations of the deterministic unperturbed episode (agent.py:36,58-59 with
+        save_states=True) -> host f32 [T, n_in].  Every eval episode of an epoch starts from reset
+        with theta and deterministic actions, so one recorded lane serves all of them."""
+        p = self.policy
+        if p.KIND == "impala":
+            return None
+        dev = p.flat.device
+        T = self.agent.env.episode_len
+        states = torch.empty((1, T, p.input_shape), dtype=torch.float32, device=dev)
+        det = torch.ones(1, dtype=torch.int8, device=dev)
+        om, osd = self.agent.obs_norm_tensors(self.fixed_obs_stats.mean, self.fixed_obs_stats.std)
+        bm, bv = p.bn_stats()
+        engine.rollout(p.spec, self.agent.env, engine.lanes_desc(p.flat, 0, deterministic=det), 1, 0, jiggle=False,
+                       obs_mean=om, obs_std=osd, bn_mean=bm, bn_var=bv, device=dev, states=states)
+        return states[0].cpu().numpy()
 
     def update(self, state):
         # worker.py:40-43, with SURVEY finding 1 fixed: policy_params is the trainable flat vector

@@ -118,6 +118,13 @@ int fdr_rollout(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc*
                 const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
                 const float* obs_mean, const float* obs_std, double* ret, double* ent,
                 int32_t* steps, double* norm2, fdr_stream stream);
+/* Same as fdr_rollout, and also writes every visited raw observation (before normalisation) to
+ * states [n_lanes, T, n_in] f32 -- Agent.collect_return(save_states=True), worker/agent.py:36,58-59,
+ * the eval states run_sequential.py:143 feeds into the novelty probe set zeta. */
+int fdr_rollout_states(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc* env,
+                       const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
+                       const float* obs_mean, const float* obs_std, double* ret, double* ent,
+                       int32_t* steps, double* norm2, float* states, fdr_stream stream);
 
 /* ---- FD weighting (learner/finite_differences.py:40-49, utils/math_helpers.py:127-134) --
  * z = standardize(rewards_all - policy_reward) over ALL n_all lanes (f64, population std,
@@ -148,6 +155,22 @@ int64_t fdr_dsgd_workspace_bytes(int64_t n_params);
 int fdr_dsgd_step(fdr_ctx* ctx, float* theta, const double* g, int64_t n_params, double lr,
                   double lr_scale, double* out, void* workspace, int64_t workspace_bytes,
                   fdr_stream stream);
+
+/* ---- strategy distances / novelty (utils/math_helpers.py:147-222, strategy/) -----------------
+ * strategies [n, Z, D] f32 = get_strategy over the Z probe states for n policies (e.g. every
+ * perturbed lane); archive [H, Z, D] f32.  d[i][h] = mean over z of
+ *   FDR_DIST_L2   || b - a ||_2                                   (l2_dist :166-170)
+ *   FDR_DIST_TVD  sum_d |a - b|                                   (categorical_tvd :216-219)
+ *   FDR_DIST_W2   ||m_a - m_b||^2 + sum(s_a + s_b - 2 sqrt(s_a s_b)), D = 2k = [mean | std]
+ *                 (gaussian_wasserstein_dist_from_strategies :202-213)
+ * f64 accumulation.  Outputs (each nullable): dists [n, H] f64; min_dist [n] f64 = the novelty of
+ * compute_strategy_novelty (:147-155); argmin [n] i32 (first minimum).  Z * D <= 8192. */
+#define FDR_DIST_L2 0
+#define FDR_DIST_TVD 1
+#define FDR_DIST_W2 2
+int fdr_strategy_distances(fdr_ctx* ctx, const float* strategies, int32_t n, const float* archive, int32_t n_archive,
+                           int32_t n_states, int32_t dim, int32_t kind, double* dists, double* min_dist,
+                           int32_t* argmin, fdr_stream stream);
 
 /* ---- ImpalaPolicy (policies/impala.py:8-186) on the synthetic frame env --------------------
  * The IMPALA conv stack runs on f32 MFMA tiles (one workgroup per env, activations resident in

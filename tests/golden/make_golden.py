@@ -468,8 +468,32 @@ def g8_impala():
          param_shapes=np.array([str(tuple(p.shape)) for p in net.parameters()]))
 
 
+def g9_novelty():
+    """Strategy distances / novelty (utils/math_helpers.py:147-222) on seeded strategies."""
+    rs = np.random.RandomState(9)
+    out = {}
+    Z, A, K, H = 7, 5, 3, 6
+    p = rs.rand(Z, A).astype(np.float32); p /= p.sum(-1, keepdims=True)
+    P = rs.rand(H, Z, A).astype(np.float32); P /= P.sum(-1, keepdims=True)
+    g = np.concatenate([rs.randn(Z, K), 0.1 + rs.rand(Z, K)], -1).astype(np.float32)
+    G = np.concatenate([rs.randn(H, Z, K), 0.1 + rs.rand(H, Z, K)], -1).astype(np.float32)
+    out.update(cat_a=p, cat_b=P, gau_a=g, gau_b=G)
+    out["tvd"] = np.asarray(math_helpers.categorical_tvd(p, P))
+    out["l2"] = np.asarray(math_helpers.l2_dist(p, P))
+    out["w2"] = np.asarray(math_helpers.gaussian_wasserstein_dist_from_strategies(g, G))
+    out["nov_tvd"] = np.asarray(math_helpers.compute_strategy_novelty(p, P, distance_fn=math_helpers.categorical_tvd))
+    out["nov_l2"] = np.asarray(math_helpers.compute_strategy_novelty(p, P))
+    out["nov_w2"] = np.asarray(math_helpers.compute_strategy_novelty(
+        g, G, distance_fn=math_helpers.gaussian_wasserstein_dist_from_strategies))
+    # pairwise archive distances as SparseHistoryManager._construct_table computes them (:55-66)
+    out["pair_tvd"] = np.array([[math_helpers.compute_strategy_distance(P[i], P[j], distance_fn=math_helpers.categorical_tvd)
+                                 for j in range(H)] for i in range(H)])
+    save("g9_novelty.npz", **out)
+
+
 GENERATORS = {"g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
-              "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g8": g8_impala}
+              "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g8": g8_impala,
+              "g9": g9_novelty}
 
 if __name__ == "__main__":
     torch.set_num_threads(1)
