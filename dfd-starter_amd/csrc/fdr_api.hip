@@ -143,6 +143,25 @@ int fdr_rollout_states(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_en
                        const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
                        const float* obs_mean, const float* obs_std, double* ret, double* ent,
                        int32_t* steps, double* norm2, float* states, fdr_stream stream) {
+  fdr_rollout_extras x{};
+  x.states = states;
+  return fdr_rollout_ex(ctx, policy, env, lanes, n_lanes, seed, jiggle, obs_mean, obs_std, ret, ent, steps, norm2,
+                        &x, stream);
+}
+
+int fdr_obs_stats_merge(fdr_ctx* ctx, const float* mean, const float* m2, const int32_t* count, int32_t n, int32_t dim,
+                        float* acc_mean, float* acc_m2, int64_t* acc_count, fdr_stream stream) {
+  (void)ctx;
+  if (n < 0 || dim <= 0) return set_error(FDR_ERR_INVALID, "bad sizes");
+  if ((n > 0 && (!mean || !m2 || !count)) || !acc_mean || !acc_m2 || !acc_count)
+    return set_error(FDR_ERR_INVALID, "NULL pointer");
+  return launch_obs_stats_merge(mean, m2, count, n, dim, acc_mean, acc_m2, acc_count, (hipStream_t)stream);
+}
+
+int fdr_rollout_ex(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc* env,
+                   const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
+                   const float* obs_mean, const float* obs_std, double* ret, double* ent, int32_t* steps,
+                   double* norm2, const fdr_rollout_extras* extras, fdr_stream stream) {
   (void)ctx;
   PolicyKey k;
   int rc = policy_key(policy, &k);
@@ -191,7 +210,17 @@ int fdr_rollout_states(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_en
   a.ent = ent;
   a.steps = steps;
   a.norm2 = norm2;
-  a.states = states;
+  if (extras) {
+    a.states = extras->states;
+    if (extras->obs_mean || extras->obs_m2 || extras->obs_count) {
+      if (!extras->obs_mean || !extras->obs_m2 || !extras->obs_count)
+        return set_error(FDR_ERR_INVALID, "obs_mean, obs_m2 and obs_count must be given together");
+      a.os_mean = extras->obs_mean;
+      a.os_m2 = extras->obs_m2;
+      a.os_count = extras->obs_count;
+      a.os_chance = extras->obs_chance;
+    }
+  }
   return launch_rollout(k, env->kind, a, (hipStream_t)stream);
 }
 

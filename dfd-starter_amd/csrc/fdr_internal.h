@@ -74,11 +74,18 @@ struct RolloutArgs {
   int32_t* steps;
   double* norm2;
   float* states;  // NULL, or [n_lanes, T, n_in] visited raw observations (fdr_rollout_states)
+  // NULL, or per-lane Welford obs statistics (fdr_rollout_obs_stats)
+  float* os_mean;
+  float* os_m2;
+  int32_t* os_count;
+  float os_chance;
 };
 
 int launch_policy_forward(const PolicyKey& k, const LanesArgs& lanes, int n_lanes,
                           const float* bn_mean, const float* bn_var, const float* x, float* out0,
                           float* out1, hipStream_t stream);
 int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream);
+int launch_obs_stats_merge(const float* mean, const float* m2, const int32_t* count, int n, int d, float* acc_mean,
+                           float* acc_m2, int64_t* acc_count, hipStream_t stream);
 
 }  // namespace fdr

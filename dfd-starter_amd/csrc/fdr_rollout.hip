@@ -223,7 +223,8 @@ __global__ __launch_bounds__(64 * kLanesPerBlock) void policy_forward_kernel(
 // ---------------------------------------------------------------------------------------------
 // Whole-episode rollout: fdr_rollout
 // ---------------------------------------------------------------------------------------------
-template <int NIN, int NA, bool DISC, int ENV, bool REC>
+// FEAT bit 0: record visited observations (fdr_rollout_states); bit 1: Welford obs statistics
+template <int NIN, int NA, bool DISC, int ENV, int FEAT>
 __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(RolloutArgs a) {
   using Lane = MlpLane<NIN, NA, DISC>;
   constexpr int NQI = Lane::NQI;
@@ -280,6 +281,9 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
   constexpr int kDrawsPerStep = DISC ? 1 : NA;
   constexpr int kStepsPerBatch = 64 / kDrawsPerStep;
   float rbuf = 0.f;
+  uint64_t os_mask = 0;  // obs-stat coins of the current 64-step batch (wave-uniform)
+  int os_n = 0;
+  float os_mean = 0.f, os_m2 = 0.f;
 
   for (int t = 0; t < T; ++t) {
     const int tb = t % kStepsPerBatch;
@@ -288,8 +292,26 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
       const uint64_t h = hash_ctr(key, ulane, (uint64_t)(t + ds), (uint64_t)dk);
       rbuf = DISC ? uniform24(h) : normal_bm(h);
     }
-    if constexpr (REC) {  // visited (raw) observations, worker/agent.py:36 / 58-59 (save_states)
+    if constexpr (FEAT & 1) {  // visited (raw) observations, worker/agent.py:36 / 58-59 (save_states)
       if (j < NIN) a.states[((int64_t)lane * T + t) * NIN + j] = s;
+    }
+    if constexpr (FEAT & 2) {
+      // worker/agent.py:37-39: with probability obs_stats_update_chance the raw obs enters the lane's
+      // WelfordRunningStat (utils/math_helpers.py:29-38, f32, same operation order, no contraction).
+      // Coins come 64 steps at a time: lane i draws step t + i (counter k = 14), one ballot.
+      if ((t & 63) == 0) {
+        const float u = uniform24(hash_ctr(key, ulane, (uint64_t)(t + j), 14));
+        os_mask = __ballot(u < a.os_chance);
+      }
+      if ((os_mask >> (t & 63)) & 1ull) {
+#pragma clang fp contract(off)
+        const int cc = os_n;
+        os_n += 1;
+        const float delta = s - os_mean;
+        const float delta_n = delta / (float)os_n;
+        os_mean += delta_n;
+        os_m2 += (delta * delta_n) * (float)cc;
+      }
     }
     float X[NQI];
     row_allgather<NQI>(policy_input(s), X);
@@ -385,6 +407,13 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
     a.steps[lane] = T;
     if (a.norm2) a.norm2[lane] = n2;
   }
+  if constexpr (FEAT & 2) {
+    if (j < NIN) {
+      a.os_mean[(int64_t)lane * NIN + j] = os_mean;
+      a.os_m2[(int64_t)lane * NIN + j] = os_m2;
+    }
+    if (j == 0) a.os_count[lane] = os_n;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -415,6 +444,17 @@ int launch_policy_forward(const PolicyKey& k, const LanesArgs& lanes, int n_lane
   return set_error(FDR_ERR_UNSUPPORTED, "no compiled policy_forward for this (kind, n_in, n_act)");
 }
 
+template <int NIN, int NA, bool DISC, int ENV>
+static void launch_feat(const RolloutArgs& args, dim3 grid, dim3 block, hipStream_t stream) {
+  const int feat = (args.states ? 1 : 0) | (args.os_mean ? 2 : 0);
+  switch (feat) {
+    case 0: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, 0>), grid, block, 0, stream, args); break;
+    case 1: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, 1>), grid, block, 0, stream, args); break;
+    case 2: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, 2>), grid, block, 0, stream, args); break;
+    default: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, 3>), grid, block, 0, stream, args); break;
+  }
+}
+
 int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream) {
   const dim3 grid((args.n_lanes + kLanesPerBlock - 1) / kLanesPerBlock), block(64 * kLanesPerBlock);
 #define FDR_ROLL(NIN, NA, DISC)                                                                 \
@@ -422,18 +462,12 @@ int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hi
     if (Layout<NIN, NA, DISC>::P != k.n_params)                                                 \
       return set_error(FDR_ERR_INVALID, "n_params does not match the policy layout");           \
     if (env_kind == FDR_ENV_SYNTH) {                                                            \
-      if (args.states)                                                                          \
-        hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, FDR_ENV_SYNTH, true>), grid, block, 0, stream, args); \
-      else                                                                                      \
-        hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, FDR_ENV_SYNTH, false>), grid, block, 0, stream, args); \
+      launch_feat<NIN, NA, DISC, FDR_ENV_SYNTH>(args, grid, block, stream);                     \
       return check_launch("rollout_kernel<synth>");                                             \
     }                                                                                           \
     if constexpr (NIN == 2 && NA == 9 && DISC) {                                                \
       if (env_kind == FDR_ENV_TRAP) {                                                           \
-        if (args.states)                                                                        \
-          hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, FDR_ENV_TRAP, true>), grid, block, 0, stream, args); \
-        else                                                                                    \
-          hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, FDR_ENV_TRAP, false>), grid, block, 0, stream, args); \
+        launch_feat<NIN, NA, DISC, FDR_ENV_TRAP>(args, grid, block, stream);                    \
         return check_launch("rollout_kernel<trap>");                                            \
       }                                                                                         \
     }                                                                                           \
@@ -442,6 +476,52 @@ int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hi
   FDR_SHAPES(FDR_ROLL)
 #undef FDR_ROLL
   return set_error(FDR_ERR_UNSUPPORTED, "no compiled rollout for this (kind, n_in, n_act)");
+}
+
+}  // namespace fdr
+
+namespace fdr {
+
+// ---------------------------------------------------------------------------------------------
+// Welford merge (utils/math_helpers.py:68-87, increment_from_obs_stats_update): the lanes' partial
+// statistics folded into the accumulator in lane order, f32, the reference's operation order.
+// One thread per observation dimension; lanes with count 0 are skipped, as the reference.
+// ---------------------------------------------------------------------------------------------
+__global__ void obs_stats_merge_kernel(const float* __restrict__ mean, const float* __restrict__ m2,
+                                       const int32_t* __restrict__ count, int n, int d, float* acc_mean,
+                                       float* acc_m2, int64_t* acc_count) {
+#pragma clang fp contract(off)
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t c = *acc_count;
+  float m = j < d ? acc_mean[j] : 0.f, v = j < d ? acc_m2[j] : 0.f;
+  for (int i = 0; i < n; ++i) {
+    const int64_t oc = count[i];
+    if (oc == 0) continue;
+    const int64_t cnt = c + oc;
+    if (j < d) {
+      const float om = mean[(int64_t)i * d + j], ov = m2[(int64_t)i * d + j];
+      const float md = om - m;
+      const float mds = md * md;
+      const float cm = ((float)c * m + (float)oc * om) / (float)cnt;
+      v = (v + ov) + ((mds * (float)c) * (float)oc) / (float)cnt;
+      m = cm;
+    }
+    c = cnt;
+  }
+  if (j < d) {
+    acc_mean[j] = m;
+    acc_m2[j] = v;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) *acc_count = c;
+}
+
+int launch_obs_stats_merge(const float* mean, const float* m2, const int32_t* count, int n, int d, float* acc_mean,
+                           float* acc_m2, int64_t* acc_count, hipStream_t stream) {
+  if (d > 1024) return set_error(FDR_ERR_UNSUPPORTED, "obs_dim > 1024");
+  hipLaunchKernelGGL(obs_stats_merge_kernel, dim3(1), dim3(1024), 0, stream, mean, m2, count, n, d, acc_mean, acc_m2,
+                     acc_count);
+  return check_launch("obs_stats_merge_kernel");
 }
 
 }  // namespace fdr

@@ -20,7 +20,7 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_impala_num_params", "fdr_impala_num_bn_stats", "fdr_impala_workspace_bytes",
            "fdr_impala_rollout", "fdr_impala_forward_workspace_bytes", "fdr_impala_forward",
            "fdr_impala_profile", "fdr_impala_profile_read", "fdr_impala_debug_clock",
-           "fdr_strategy_distances", "fdr_rollout_states")
+           "fdr_strategy_distances", "fdr_rollout_states", "fdr_rollout_ex", "fdr_obs_stats_merge")
 
 
 class FDRError(RuntimeError):
@@ -44,6 +44,11 @@ class LanesDesc(ctypes.Structure):
     _fields_ = [("base", ctypes.c_void_p), ("base_stride", ctypes.c_int64), ("table", ctypes.c_void_p),
                 ("table_size", ctypes.c_int64), ("idx", ctypes.c_void_p), ("sign", ctypes.c_void_p),
                 ("sigma", ctypes.c_float), ("deterministic", ctypes.c_void_p), ("lane_offset", ctypes.c_int64)]
+
+
+class RolloutExtras(ctypes.Structure):
+    _fields_ = [("states", ctypes.c_void_p), ("obs_mean", ctypes.c_void_p), ("obs_m2", ctypes.c_void_p),
+                ("obs_count", ctypes.c_void_p), ("obs_chance", ctypes.c_float)]
 
 
 class ImpalaDesc(ctypes.Structure):
@@ -72,6 +77,10 @@ def _load():
                                        ctypes.POINTER(LanesDesc), I32, U64, I32, P, P, P, P, P, P, P]),
         "fdr_rollout_states": (ctypes.c_int, [P, ctypes.POINTER(PolicyDesc), ctypes.POINTER(EnvDesc),
                                               ctypes.POINTER(LanesDesc), I32, U64, I32, P, P, P, P, P, P, P, P]),
+        "fdr_rollout_ex": (ctypes.c_int, [P, ctypes.POINTER(PolicyDesc), ctypes.POINTER(EnvDesc),
+                                          ctypes.POINTER(LanesDesc), I32, U64, I32, P, P, P, P, P, P,
+                                          ctypes.POINTER(RolloutExtras), P]),
+        "fdr_obs_stats_merge": (ctypes.c_int, [P, P, P, P, I32, I32, P, P, P, P]),
         "fdr_fd_weights": (ctypes.c_int, [P, P, I32, F64, I32, I32, P, P, I32, F32, P, P]),
         "fdr_fd_grad_workspace_bytes": (I64, [I32, I64]),
         "fdr_fd_grad": (ctypes.c_int, [P, P, I64, P, P, I32, I64, P, P, I64, P]),

@@ -94,8 +94,9 @@ class RolloutResult(object):
 
 
 def rollout(spec, env, lanes, n_lanes, seed, jiggle=True, obs_mean=None, obs_std=None,
-            bn_mean=None, bn_var=None, out=None, device=None, states=None):
-    """fdr_rollout; with states (f32 [n_lanes, T, n_in] device tensor) fdr_rollout_states."""
+            bn_mean=None, bn_var=None, out=None, device=None, states=None, obs_stats=None):
+    """fdr_rollout; fdr_rollout_ex when states (f32 [n_lanes, T, n_in] device tensor) is given or
+    obs_stats = the per-step sampling chance (-> out.obs_mean / obs_m2 / obs_count per lane)."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     _check_dev(obs_mean, obs_std, bn_mean, bn_var)
     if out is None:
@@ -105,15 +106,26 @@ def rollout(spec, env, lanes, n_lanes, seed, jiggle=True, obs_mean=None, obs_std
                             torch.empty(n_lanes, dtype=torch.float64, device=dev))
     pd = spec.desc(bn_mean, bn_var)
     ed = env.desc()
-    if states is not None:
-        _check_dev(states)
-        if states.dtype != torch.float32 or not states.is_contiguous() or \
-                states.numel() != n_lanes * env.episode_len * spec.n_in:
-            raise ValueError("states must be contiguous float32 [n_lanes, T, n_in]")
-        check(lib.fdr_rollout_states(None, ctypes.byref(pd), ctypes.byref(ed), ctypes.byref(lanes), n_lanes,
-                                     ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(obs_mean),
-                                     _p(obs_std), _p(out.reward), _p(out.entropy), _p(out.timesteps),
-                                     _p(out.norm2), _p(states), _stream(dev)), "fdr_rollout_states")
+    if states is not None or obs_stats is not None:
+        x = _lib.RolloutExtras(None, None, None, None, 0.0)
+        if states is not None:
+            _check_dev(states)
+            if states.dtype != torch.float32 or not states.is_contiguous() or \
+                    states.numel() != n_lanes * env.episode_len * spec.n_in:
+                raise ValueError("states must be contiguous float32 [n_lanes, T, n_in]")
+            x.states = states.data_ptr()
+        if obs_stats is not None:
+            chance = float(obs_stats)
+            out.obs_mean = torch.empty((n_lanes, spec.n_in), dtype=torch.float32, device=dev)
+            out.obs_m2 = torch.empty_like(out.obs_mean)
+            out.obs_count = torch.empty(n_lanes, dtype=torch.int32, device=dev)
+            x.obs_mean, x.obs_m2, x.obs_count = out.obs_mean.data_ptr(), out.obs_m2.data_ptr(), \
+                out.obs_count.data_ptr()
+            x.obs_chance = chance
+        check(lib.fdr_rollout_ex(None, ctypes.byref(pd), ctypes.byref(ed), ctypes.byref(lanes), n_lanes,
+                                 ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(obs_mean),
+                                 _p(obs_std), _p(out.reward), _p(out.entropy), _p(out.timesteps),
+                                 _p(out.norm2), ctypes.byref(x), _stream(dev)), "fdr_rollout_ex")
         return out
     check(lib.fdr_rollout(None, ctypes.byref(pd), ctypes.byref(ed), ctypes.byref(lanes), n_lanes,
                           ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(obs_mean),
@@ -295,3 +307,11 @@ def lane_strategies(spec, lanes_fn, n_lanes, zeta, bn_mean=None, bn_var=None):
     if isinstance(out, tuple):
         out = torch.cat(out, dim=-1)
     return out.reshape(n_lanes, Z, -1)
+
+
+def obs_stats_merge(mean, m2, count, acc_mean, acc_m2, acc_count):
+    """Fold per-lane Welford partials into the device accumulator (in place, lane order)."""
+    _check_dev(mean, m2, count, acc_mean, acc_m2, acc_count)
+    n, d = mean.shape
+    check(lib.fdr_obs_stats_merge(None, _p(mean), _p(m2), _p(count), n, d, _p(acc_mean), _p(acc_m2), _p(acc_count),
+                                  _stream(mean.device)), "fdr_obs_stats_merge")

@@ -46,6 +46,7 @@ class FDBatch(object):
         self.lanes_per_dir = lanes_per_dir
         self.is_eval = np.zeros(len(self.sign_host), bool) if is_eval is None else np.asarray(is_eval)
         self.novelty = novelty
+        self.obs_stats = None   # (mean [n, d], m2 [n, d], count [n]) device Welford partials, or None
 
     def __len__(self):
         return len(self.sign_host)
@@ -67,6 +68,7 @@ class FDBatch(object):
         n2 = self.norm2.cpu().numpy() if self.norm2 is not None else [None] * len(rew)
         nov = np.zeros(len(rew)) if self.novelty is None else \
             (self.novelty.double().cpu().numpy() if torch.is_tensor(self.novelty) else np.asarray(self.novelty))
+        os_host = None if self.obs_stats is None else tuple(t.cpu().numpy() for t in self.obs_stats)
         out = []
         for i in range(len(rew)):
             r = FDReturn()
@@ -76,6 +78,8 @@ class FDBatch(object):
             r.sign = int(self.sign_host[i])
             r.reward, r.entropy, r.timesteps = float(rew[i]), float(ent[i]), int(ts[i])
             r.novelty = float(nov[i])
+            if os_host is not None:     # WelfordRunningStat.serialize() of this episode (worker.py:56)
+                r.obs_stats_update = os_host[0][i].tolist() + os_host[1][i].tolist() + [int(os_host[2][i])]
             r.norm2 = None if n2[i] is None else float(n2[i])
             out.append(r)
         return out

@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from dsgd import DSGD
+from fdr import engine
 from envs import SyntheticEnv, TrapEnv
 from learner import FDBatch, FDState, FiniteDifferences
 from policies import DiscretePolicy, MujocoPolicy
@@ -80,6 +81,14 @@ class SequentialRunner(object):
         self.policy_entropy = 0
         self.policy_novelty = 0
         self.zeta = np.zeros((0, self.policy.input_shape), np.float32)
+        # run_server.py:94,143,196: every return's obs-stat update is merged into one global Welford
+        # accumulator that the workers normalise with next epoch (device, fdr_obs_stats_merge)
+        self.global_obs = None
+        if normalize_obs:
+            d = self.policy.input_shape
+            self.global_obs = (torch.zeros(d, dtype=torch.float32, device=self.device),
+                               torch.zeros(d, dtype=torch.float32, device=self.device),
+                               torch.zeros(1, dtype=torch.int64, device=self.device))
         self.zeta_idxs = []
         self.vbn_buffer = None
         if vbn_buffer_size > 0:
@@ -132,6 +141,8 @@ class SequentialRunner(object):
                                    else np.ones(n_dirs, np.int8), np.zeros(int(is_eval.sum()), np.int8)])
             det = (sign == 0).astype(np.int8)
             res, idx_d, sign_d = self.worker.launch(lidx, sign, det, jiggle=False)
+            if self.global_obs is not None and getattr(res, "obs_mean", None) is not None:
+                engine.obs_stats_merge(res.obs_mean, res.obs_m2, res.obs_count, *self.global_obs)
             nov = self.worker.lane_novelty(idx_d, sign_d)          # worker.py:53, every lane at once
             nov = np.zeros(len(lidx)) if nov is None else nov.cpu().numpy()
             rew = res.reward.cpu().numpy() + np.array([self.agent.rng.choice((-1e-12, 1e-12)) for _ in lidx])
@@ -160,6 +171,9 @@ class SequentialRunner(object):
                 self.current_state.strategy_frames = self.zeta
                 self.current_state.strategy_history = self.strategy_handler.strategy_tensor
                 self.current_state.policy_params = self.policy.get_trainable_flat()
+                if self.global_obs is not None:
+                    m, v, c = (t.cpu().numpy() for t in self.global_obs)
+                    self.current_state.obs_stats = m.tolist() + v.tolist() + [int(c[0])]
                 self.current_state.epoch = self.learner.epoch
                 self.worker.update(self.current_state)
                 report = {"Epoch": self.learner.epoch,

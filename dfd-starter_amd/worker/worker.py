@@ -18,6 +18,12 @@ from learner.fd_return import FDBatch
 from utils.math_helpers import WelfordRunningStat
 
 
+def obs_partials(res):
+    """(mean [n, d], m2 [n, d], count [n]) device partials of a rollout run with obs statistics."""
+    m = getattr(res, "obs_mean", None)
+    return None if m is None else (res.obs_mean, res.obs_m2, res.obs_count)
+
+
 class Worker(object):
     def __init__(self, policy, agent, noise_source, strategy_handler, sigma=0.02, eval_prob=0.1, random_seed=123):
         self.policy = policy
@@ -76,8 +82,10 @@ class Worker(object):
                 idx_d, sign_d = idx_d.repeat_interleave(E), sign_d.repeat_interleave(E)
             return res, idx_d, sign_d
         om, osd = self.agent.obs_norm_tensors(self.fixed_obs_stats.mean, self.fixed_obs_stats.std)
+        # agent.py:37-39: with normalize_obs every episode also samples raw obs into its Welford stats
+        chance = self.agent.obs_stats_update_chance if self.agent.normalize_obs else None
         res = engine.rollout(p.spec, self.agent.env, lanes, n, seed, jiggle=jiggle, obs_mean=om, obs_std=osd,
-                             bn_mean=bm, bn_var=bv, out=out, device=p.flat.device)
+                             bn_mean=bm, bn_var=bv, out=out, device=p.flat.device, obs_stats=chance)
         return res, idx_d, sign_d
 
     def evaluate(self, n_dirs, antithetic=True, seed=None, lane_range=None, out=None, novelty=False):
@@ -106,8 +114,10 @@ class Worker(object):
             lidx, sign = np.repeat(lidx, E), np.repeat(sign, E)
         self.agent.cumulative_timesteps += int(len(lidx)) * self.agent.env.episode_len
         nov = self.lane_novelty(idx_d, sign_d) if novelty else None
-        return FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, lidx, sign, self.epoch,
-                       lanes_per_dir=lpd * E, novelty=nov)
+        b = FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, lidx, sign, self.epoch,
+                    lanes_per_dir=lpd * E, novelty=nov)
+        b.obs_stats = obs_partials(res)
+        return b
 
     # ---- reference API ----------------------------------------------------------------------
     @torch.no_grad()
@@ -127,13 +137,15 @@ class Worker(object):
         b = FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, idx, sign, self.epoch,
                     is_eval=is_eval)
         b.novelty = None if nov is None else nov.cpu().numpy()
+        b.obs_stats = obs_partials(res)
         rets = b.to_returns()
         for r in rets:
             r.reward += self.agent.rng.choice((-1e-12, 1e-12))     # agent.py:69
             self.agent.cumulative_timesteps += r.timesteps
             if r.is_eval and eval_states is not None:
                 r.eval_states = list(eval_states)                   # worker.py:35 (agent.saved_states)
-            r.obs_stats_update = self.agent.obs_stats.serialize()
+            if r.obs_stats_update is None or len(r.obs_stats_update) == 0:
+                r.obs_stats_update = self.agent.obs_stats.serialize()
         return rets
 
     # ---- novelty path -----------------------------------------------------------

@@ -126,6 +126,31 @@ int fdr_rollout_states(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_en
                        const float* obs_mean, const float* obs_std, double* ret, double* ent,
                        int32_t* steps, double* norm2, float* states, fdr_stream stream);
 
+/* General form: optional per-lane side outputs of the same episodes (each field NULL = off).
+ *   states        [n_lanes, T, n_in] f32  visited raw observations (save_states)
+ *   obs_mean/obs_m2 [n_lanes, n_in] f32, obs_count [n_lanes] i32: each lane's WelfordRunningStat
+ *                 (utils/math_helpers.py:29-38) of the raw observations sampled with probability
+ *                 obs_chance per step (worker/agent.py:37-39; coin = counter stream, k = 14);
+ *                 merge them with fdr_obs_stats_merge. */
+typedef struct fdr_rollout_extras {
+  float* states;
+  float* obs_mean;
+  float* obs_m2;
+  int32_t* obs_count;
+  float obs_chance;
+} fdr_rollout_extras;
+int fdr_rollout_ex(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc* env,
+                   const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
+                   const float* obs_mean, const float* obs_std, double* ret, double* ent, int32_t* steps,
+                   double* norm2, const fdr_rollout_extras* extras, fdr_stream stream);
+
+/* ---- obs statistics merge (utils/math_helpers.py:68-87, increment_from_obs_stats_update) --------
+ * Folds n partial Welford statistics (mean/m2 [n, dim] f32, count [n] i32, e.g. from
+ * fdr_rollout_ex) into the accumulator (acc_mean/acc_m2 [dim] f32, acc_count [1] i64, device,
+ * in/out) in index order with the reference's f32 formulas; zero-count partials are skipped. */
+int fdr_obs_stats_merge(fdr_ctx* ctx, const float* mean, const float* m2, const int32_t* count, int32_t n, int32_t dim,
+                        float* acc_mean, float* acc_m2, int64_t* acc_count, fdr_stream stream);
+
 /* ---- FD weighting (learner/finite_differences.py:40-49, utils/math_helpers.py:127-134) --
  * z = standardize(rewards_all - policy_reward) over ALL n_all lanes (f64, population std,
  * unchanged if std == 0); for the local lanes [lane_lo, lane_lo + n_local):

@@ -19,6 +19,7 @@ per-step policy entropies (same probabilities as the reference's end-of-episode 
 """
 import numpy as np
 
+from . import obs_stats
 from . import policies as pol
 from . import rng as crng
 from .noise import perturb
@@ -46,8 +47,10 @@ def collect_return(policy, env, obs, deterministic, noise_fn, jiggle_fn, mean=No
 
 
 def evaluate_lanes(kind, n_in, n_act, theta, table, idx, sign, sigma, env, seed,
-                   deterministic=False, bn_stats=None, obs_mean=None, obs_std=None, jiggle=True):
-    """Batched numpy reference of fdr_rollout (synthetic env).  Returns ret, ent, steps, norm2."""
+                   deterministic=False, bn_stats=None, obs_mean=None, obs_std=None, jiggle=True,
+                   obs_chance=None, record_states=False):
+    """Batched numpy reference of fdr_rollout (synthetic env).  Returns ret, ent, steps, norm2
+    (+ the per-lane Welford statistics if obs_chance, + states [L, T, n_in] if record_states)."""
     L = len(idx)
     thetas = perturb(theta, table, idx, sign, sigma)
     # squared norm of lambda = sign * fl32(sigma * eps) -- what the FD learner divides by
@@ -62,7 +65,15 @@ def evaluate_lanes(kind, n_in, n_act, theta, table, idx, sign, sigma, env, seed,
     ent = np.zeros(L, dtype=np.float64)
     det = np.broadcast_to(np.asarray(deterministic, dtype=bool), (L,))
     T = env.episode_len
+    stats = [obs_stats.Welford(n_in) for _ in range(L)] if obs_chance is not None else None
+    states = np.zeros((L, T, n_in), np.float32) if record_states else None
     for t in range(T):
+        if record_states:
+            states[:, t] = obs
+        if stats is not None:   # worker/agent.py:37-39 (raw obs, before normalisation)
+            coin = obs_stats.lane_coins(seed, lanes, t, obs_chance)
+            for l in np.nonzero(coin)[0]:
+                stats[l].update(obs[l])
         x = obs
         if obs_mean is not None:
             x = np.clip((x - obs_mean) / obs_std, -10, 10).astype(np.float32)
@@ -82,4 +93,9 @@ def evaluate_lanes(kind, n_in, n_act, theta, table, idx, sign, sigma, env, seed,
     ent /= T
     if jiggle:
         ret += crng.jiggle(seed, lanes)
-    return ret, ent, np.full(L, T, dtype=np.int32), norm2
+    out = (ret, ent, np.full(L, T, dtype=np.int32), norm2)
+    if stats is not None:
+        out = out + (stats,)
+    if record_states:
+        out = out + (states,)
+    return out

@@ -491,9 +491,34 @@ def g9_novelty():
     save("g9_novelty.npz", **out)
 
 
+def g10_welford():
+    """WelfordRunningStat (utils/math_helpers.py:7-124): sequential updates, std/mean properties and the
+    increment_from_obs_stats_update merge that run_server.py:143 applies to every return."""
+    rs = np.random.RandomState(10)
+    d = 5
+    parts = []
+    for n in (0, 1, 3, 7, 12):
+        w = math_helpers.WelfordRunningStat(d)
+        xs = (rs.randn(n, d) * 3 + 1).astype(np.float32)
+        for x in xs:
+            w.increment(x, 1)
+        parts.append((xs, w.serialize()))
+    acc = math_helpers.WelfordRunningStat(d)
+    for _, ser in parts:
+        acc.increment_from_obs_stats_update(ser)
+    out = {"d": np.array(d)}
+    for i, (xs, ser) in enumerate(parts):
+        out["x%d" % i] = xs
+        out["ser%d" % i] = np.asarray(ser, np.float64)
+    out["acc_ser"] = np.asarray(acc.serialize(), np.float64)
+    out["acc_mean"] = np.asarray(acc.mean, np.float32)
+    out["acc_std"] = np.asarray(acc.std, np.float32)
+    save("g10_welford.npz", **out)
+
+
 GENERATORS = {"g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
               "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g8": g8_impala,
-              "g9": g9_novelty}
+              "g9": g9_novelty, "g10": g10_welford}
 
 if __name__ == "__main__":
     torch.set_num_threads(1)
