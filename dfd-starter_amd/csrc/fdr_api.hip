@@ -389,3 +389,50 @@ int fdr_strategy_distances(fdr_ctx* ctx, const float* strategies, int32_t n, con
   return launch_strategy_dist(strategies, n, archive, n_archive, n_states, dim, kind, dists, min_dist, argmin,
                               (hipStream_t)stream);
 }
+
+static int lambda_row(const float* table, int64_t table_size, const int64_t* idx, const int8_t* sign,
+                      const int32_t* slot, int32_t n, int64_t P, float sigma, const float* drift, int32_t n_slots,
+                      LambdaRow* R) {
+  if (n < 0 || P <= 0 || table_size < P) return set_error(FDR_ERR_INVALID, "bad sizes");
+  if (n > 0 && (!table || !idx)) return set_error(FDR_ERR_INVALID, "NULL pointer");
+  if (n_slots < 0 || (n_slots > 0 && !drift)) return set_error(FDR_ERR_INVALID, "drift missing");
+  *R = LambdaRow{table, table_size - P, idx, sign, slot, drift, n_slots, P, sigma};
+  return FDR_OK;
+}
+
+int fdr_fd_lambda_norms(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx, const int8_t* sign,
+                        const int32_t* slot, int32_t n, int64_t n_params, float sigma, const float* drift,
+                        int32_t n_slots, double* norm2, fdr_stream stream) {
+  (void)ctx;
+  LambdaRow R;
+  int rc = lambda_row(table, table_size, idx, sign, slot, n, n_params, sigma, drift, n_slots, &R);
+  if (rc) return rc;
+  if (!norm2) return set_error(FDR_ERR_INVALID, "NULL output");
+  return launch_lambda_norms(R, n, norm2, (hipStream_t)stream);
+}
+
+int fdr_fd_grad_lambda(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx, const int8_t* sign,
+                       const int32_t* slot, const double* coef, int32_t n, int64_t n_params, float sigma,
+                       const float* drift, int32_t n_slots, double* g, void* ws, int64_t ws_bytes,
+                       fdr_stream stream) {
+  (void)ctx;
+  LambdaRow R;
+  int rc = lambda_row(table, table_size, idx, sign, slot, n, n_params, sigma, drift, n_slots, &R);
+  if (rc) return rc;
+  if (!g || (n > 0 && !coef)) return set_error(FDR_ERR_INVALID, "NULL pointer");
+  if (n == 0) return set_error(FDR_ERR_INVALID, "no returns");
+  return launch_lambda_grad(R, coef, n, g, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int64_t fdr_bn_refresh_workspace_bytes(int32_t n) { return n < 0 ? -1 : bn_refresh_workspace_bytes(n); }
+
+int fdr_bn_refresh(fdr_ctx* ctx, const fdr_policy_desc* policy, const float* theta, const float* x, int32_t n,
+                   float momentum, float* bn_mean, float* bn_var, void* ws, int64_t ws_bytes, fdr_stream stream) {
+  (void)ctx;
+  if (!policy || policy->kind != FDR_POLICY_DISCRETE || policy->hidden != kHidden)
+    return set_error(FDR_ERR_UNSUPPORTED, "BN refresh is defined for the DiscretePolicy (hidden 64)");
+  if (policy->n_in <= 0 || policy->n_in > 64) return set_error(FDR_ERR_UNSUPPORTED, "n_in must be in 1..64");
+  if (!theta || !x || !bn_mean || !bn_var) return set_error(FDR_ERR_INVALID, "NULL pointer");
+  if (n < 2) return set_error(FDR_ERR_INVALID, "train-mode BatchNorm needs n >= 2 samples");
+  return launch_bn_refresh(policy->n_in, theta, x, n, momentum, bn_mean, bn_var, ws, ws_bytes, (hipStream_t)stream);
+}

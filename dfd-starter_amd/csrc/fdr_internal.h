@@ -85,6 +85,43 @@ int launch_policy_forward(const PolicyKey& k, const LanesArgs& lanes, int n_lane
                           const float* bn_mean, const float* bn_var, const float* x, float* out0,
                           float* out1, hipStream_t stream);
 int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream);
+
+// Delayed-return perturbation rows (fdr_fd_lambda_norms / fdr_fd_grad_lambda), by value to kernels.
+int64_t bn_refresh_workspace_bytes(int n);
+int launch_bn_refresh(int n_in, const float* theta, const float* x, int n, float momentum, float* rm, float* rv,
+                      void* ws, int64_t ws_bytes, hipStream_t stream);
+
+struct LambdaRow {
+  const float* table;
+  int64_t max_idx;
+  const int64_t* idx;
+  const int8_t* sign;
+  const int32_t* slot;
+  const float* drift;
+  int n_slots;
+  int64_t P;
+  float sigma;
+
+  // pointer to eps_i (row 0 if the offset is out of range: the caller poisons that row with NaN)
+  __device__ __forceinline__ const float* eps(int i, bool& bad) const {
+    const int64_t off = idx[i];
+    bad = off < 0 || off > max_idx;
+    return table + (bad ? 0 : off);
+  }
+  __device__ __forceinline__ const float* dr(int i) const {
+    const int s = slot ? slot[i] : -1;
+    return (s >= 0 && s < n_slots) ? drift + (int64_t)s * P : nullptr;
+  }
+  __device__ __forceinline__ float value(const float* e, const float* d, int sg, int64_t p) const {
+#pragma clang fp contract(off)
+    float v = sigma * e[p];
+    v = sg < 0 ? -v : v;
+    return d ? v + d[p] : v;
+  }
+};
+int launch_lambda_norms(const LambdaRow& R, int n, double* n2, hipStream_t stream);
+int launch_lambda_grad(const LambdaRow& R, const double* coef, int n, double* g, void* ws, int64_t ws_bytes,
+                       hipStream_t stream);
 int launch_obs_stats_merge(const float* mean, const float* m2, const int32_t* count, int n, int d, float* acc_mean,
                            float* acc_m2, int64_t* acc_count, hipStream_t stream);
 

@@ -191,6 +191,84 @@ int launch_fd_grad(const float* table, int64_t table_size, const int64_t* idx, c
 }
 
 // ------------------------------------------------------------------------------------------
+// Delayed returns (learner/finite_differences.py:66-73, 80-114): the perturbation of return i is
+//   lambda_i[p] = fl32( sign_i * fl32(sigma * eps_i[p]) + D_{slot_i}[p] ),  D = dist_map[epoch_i]
+// (theta of that epoch minus the current theta; slot < 0: current epoch, D = 0).  Norms and the
+// gradient g = sum_i coef_i * lambda_i run over returns, in the fd_grad tiling, f64 accumulation.
+// ------------------------------------------------------------------------------------------
+
+__global__ __launch_bounds__(256) void lambda_norm_kernel(LambdaRow R, double* __restrict__ n2) {
+  const int i = blockIdx.x;
+  bool bad;
+  const float* e = R.eps(i, bad);
+  const float* d = R.dr(i);
+  const int sg = R.sign ? (int)R.sign[i] : 1;
+  double acc = 0.0;
+  for (int64_t p = threadIdx.x; p < R.P; p += 256) {
+    const double v = R.value(e, d, sg, p);
+    acc = fma(v, v, acc);
+  }
+  __shared__ double red[256 / kWave];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < 256 / kWave; ++w) t += red[w];
+    n2[i] = bad ? __builtin_nan("") : t;
+  }
+}
+
+__global__ __launch_bounds__(kGradThreads) void lambda_grad_partial_kernel(LambdaRow R, const double* __restrict__ coef,
+                                                                          int n, int rows_per_chunk,
+                                                                          double* __restrict__ partial) {
+  const int64_t c = (int64_t)blockIdx.x * kGradThreads + threadIdx.x;
+  const int chunk = blockIdx.y;
+  const int d0 = chunk * rows_per_chunk, d1 = min(n, d0 + rows_per_chunk);
+  const bool ok = c < R.P;
+  const int64_t cc = ok ? c : 0;
+  double acc0 = 0.0, acc1 = 0.0;
+  int i = d0;
+  for (; i + 2 <= d1; i += 2) {
+    bool b0, b1;
+    const float* e0 = R.eps(i, b0);
+    const float* e1 = R.eps(i + 1, b1);
+    const float v0 = R.value(e0, R.dr(i), R.sign ? (int)R.sign[i] : 1, cc);
+    const float v1 = R.value(e1, R.dr(i + 1), R.sign ? (int)R.sign[i + 1] : 1, cc);
+    acc0 = fma(b0 ? __builtin_nan("") : coef[i], (double)v0, acc0);
+    acc1 = fma(b1 ? __builtin_nan("") : coef[i + 1], (double)v1, acc1);
+  }
+  for (; i < d1; ++i) {
+    bool b;
+    const float* e = R.eps(i, b);
+    const float v = R.value(e, R.dr(i), R.sign ? (int)R.sign[i] : 1, cc);
+    acc0 = fma(b ? __builtin_nan("") : coef[i], (double)v, acc0);
+  }
+  if (ok) partial[(int64_t)chunk * R.P + c] = acc0 + acc1;
+}
+
+int launch_lambda_norms(const LambdaRow& R, int n, double* n2, hipStream_t stream) {
+  if (n == 0) return FDR_OK;
+  hipLaunchKernelGGL(lambda_norm_kernel, dim3(n), dim3(256), 0, stream, R, n2);
+  return check_launch("lambda_norm_kernel");
+}
+
+int launch_lambda_grad(const LambdaRow& R, const double* coef, int n, double* g, void* ws, int64_t ws_bytes,
+                       hipStream_t stream) {
+  const GradPlan pl = grad_plan(n, R.P);
+  if (ws_bytes < grad_workspace_bytes(n, R.P) || ws == nullptr)
+    return set_error(FDR_ERR_WORKSPACE, "fd_grad workspace too small");
+  double* partial = static_cast<double*>(ws);
+  hipLaunchKernelGGL(lambda_grad_partial_kernel, dim3(pl.col_blocks, pl.n_chunks), dim3(kGradThreads), 0, stream,
+                     R, coef, n, pl.rows_per_chunk, partial);
+  int rc = check_launch("lambda_grad_partial_kernel");
+  if (rc) return rc;
+  const int rb = (int)std::min<int64_t>((R.P + 255) / 256, 2048);
+  hipLaunchKernelGGL(fd_grad_reduce_kernel, dim3(rb), dim3(256), 0, stream, partial, pl.n_chunks, R.P, g);
+  return check_launch("fd_grad_reduce_kernel");
+}
+
+// ------------------------------------------------------------------------------------------
 // DSGD (dsgd/dynamic_sgd.py:19-39)
 // ------------------------------------------------------------------------------------------
 constexpr int kDsgdBlocks = 256;
@@ -341,6 +419,108 @@ int launch_strategy_dist(const float* S, int n, const float* B, int H, int Z, in
   if (n == 0) return FDR_OK;
   hipLaunchKernelGGL(strategy_dist_kernel, dim3(n), dim3(kNovThreads), 0, stream, S, B, H, Z, D, kind, dists, min_d, arg);
   return check_launch("strategy_dist_kernel");
+}
+
+}  // namespace fdr
+
+namespace fdr {
+
+// ------------------------------------------------------------------------------------------
+// BatchNorm running-stat refresh of the DiscretePolicy (policies/policy.py:31-34 compute_vbn,
+// policies/discrete.py:34-48): one train-mode pass of the buffer; each BN normalises with its batch
+// statistics (biased variance) and folds mean / unbiased variance into its running stats.
+// ------------------------------------------------------------------------------------------
+constexpr float kVbnEps = 1e-5f;
+
+__global__ __launch_bounds__(256) void col_stats_kernel(const float* __restrict__ X, int n, int C,
+                                                        double* __restrict__ mean, double* __restrict__ var) {
+  const int c = blockIdx.x;
+  __shared__ double red[256 / kWave];
+  __shared__ double mu;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) s += X[(int64_t)i * C + c];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) mu = (red[0] + red[1] + red[2] + red[3]) / n;
+  __syncthreads();
+  double q = 0.0;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const double d = X[(int64_t)i * C + c] - mu;
+    q = fma(d, d, q);
+  }
+  q = wave_sum(q);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mean[c] = mu;
+    var[c] = (red[0] + red[1] + red[2] + red[3]) / n;  // biased: what train-mode BN normalises with
+  }
+}
+
+// Y[i][j] = relu(b_j + sum_k W[j][k] * BN_batch(X[i][k]))
+__global__ __launch_bounds__(256) void bn_linear_relu_kernel(const float* __restrict__ X, int n, int Cin,
+                                                             const double* __restrict__ mean, const double* __restrict__ var,
+                                                             const float* __restrict__ bw, const float* __restrict__ bb,
+                                                             const float* __restrict__ W, const float* __restrict__ b,
+                                                             int Cout, float* __restrict__ Y) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)n * Cout) return;
+  const int i = (int)(t / Cout), j = (int)(t % Cout);
+  float acc = b[j];
+  for (int k = 0; k < Cin; ++k) {
+    const float inv = 1.f / sqrtf((float)var[k] + kVbnEps);
+    const float xn = ((X[(int64_t)i * Cin + k] - (float)mean[k]) * inv) * bw[k] + bb[k];
+    acc = fmaf(W[j * Cin + k], xn, acc);
+  }
+  Y[t] = acc > 0.f ? acc : 0.f;
+}
+
+__global__ void bn_running_update_kernel(int C, int n, float momentum, const double* __restrict__ mean,
+                                         const double* __restrict__ var, float* __restrict__ rm,
+                                         float* __restrict__ rv) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float unb = (float)(var[c] * (double)n / (double)(n - 1));
+  rm[c] = momentum * (float)mean[c] + (1.f - momentum) * rm[c];
+  rv[c] = momentum * unb + (1.f - momentum) * rv[c];
+}
+
+int64_t bn_refresh_workspace_bytes(int n) { return (int64_t)n * 64 * 4 * 2 + 6 * 64 * 8 + 256; }
+
+int launch_bn_refresh(int n_in, const float* theta, const float* x, int n, float momentum, float* rm, float* rv,
+                      void* ws, int64_t ws_bytes, hipStream_t stream) {
+  if (ws_bytes < bn_refresh_workspace_bytes(n) || !ws) return set_error(FDR_ERR_WORKSPACE, "bn refresh workspace too small");
+  constexpr int H = kHidden;
+  float* h1 = static_cast<float*>(ws);
+  float* h2 = h1 + (int64_t)n * H;
+  double* st = reinterpret_cast<double*>(h2 + (int64_t)n * H);  // [3 layers][mean 64 | var 64]
+  // theta layout (policies/discrete.py:34-48, parameters() order)
+  const float* bn0w = theta;
+  const float* bn0b = bn0w + n_in;
+  const float* l1w = bn0b + n_in;
+  const float* l1b = l1w + H * n_in;
+  const float* bn1w = l1b + H;
+  const float* bn1b = bn1w + H;
+  const float* l2w = bn1b + H;
+  const float* l2b = l2w + H * H;
+  const float* bn2w = l2b + H;
+  (void)bn2w;
+  const int nb = (int)(((int64_t)n * H + 255) / 256);
+  hipLaunchKernelGGL(col_stats_kernel, dim3(n_in), dim3(256), 0, stream, x, n, n_in, st, st + 64);
+  hipLaunchKernelGGL(bn_linear_relu_kernel, dim3(nb), dim3(256), 0, stream, x, n, n_in, st, st + 64, bn0w, bn0b, l1w,
+                     l1b, H, h1);
+  hipLaunchKernelGGL(col_stats_kernel, dim3(H), dim3(256), 0, stream, h1, n, H, st + 128, st + 192);
+  hipLaunchKernelGGL(bn_linear_relu_kernel, dim3(nb), dim3(256), 0, stream, h1, n, H, st + 128, st + 192, bn1w, bn1b,
+                     l2w, l2b, H, h2);
+  hipLaunchKernelGGL(col_stats_kernel, dim3(H), dim3(256), 0, stream, h2, n, H, st + 256, st + 320);
+  hipLaunchKernelGGL(bn_running_update_kernel, dim3(1), dim3(64), 0, stream, n_in, n, momentum, st, st + 64, rm, rv);
+  hipLaunchKernelGGL(bn_running_update_kernel, dim3(1), dim3(64), 0, stream, H, n, momentum, st + 128, st + 192,
+                     rm + n_in, rv + n_in);
+  hipLaunchKernelGGL(bn_running_update_kernel, dim3(1), dim3(64), 0, stream, H, n, momentum, st + 256, st + 320,
+                     rm + n_in + H, rv + n_in + H);
+  return check_launch("bn refresh kernels");
 }
 
 }  // namespace fdr

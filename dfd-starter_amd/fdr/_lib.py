@@ -20,7 +20,8 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_impala_num_params", "fdr_impala_num_bn_stats", "fdr_impala_workspace_bytes",
            "fdr_impala_rollout", "fdr_impala_forward_workspace_bytes", "fdr_impala_forward",
            "fdr_impala_profile", "fdr_impala_profile_read", "fdr_impala_debug_clock",
-           "fdr_strategy_distances", "fdr_rollout_states", "fdr_rollout_ex", "fdr_obs_stats_merge")
+           "fdr_strategy_distances", "fdr_rollout_states", "fdr_rollout_ex", "fdr_obs_stats_merge",
+           "fdr_fd_lambda_norms", "fdr_fd_grad_lambda", "fdr_bn_refresh_workspace_bytes", "fdr_bn_refresh")
 
 
 class FDRError(RuntimeError):
@@ -81,6 +82,10 @@ def _load():
                                           ctypes.POINTER(LanesDesc), I32, U64, I32, P, P, P, P, P, P,
                                           ctypes.POINTER(RolloutExtras), P]),
         "fdr_obs_stats_merge": (ctypes.c_int, [P, P, P, P, I32, I32, P, P, P, P]),
+        "fdr_fd_lambda_norms": (ctypes.c_int, [P, P, I64, P, P, P, I32, I64, F32, P, I32, P, P]),
+        "fdr_fd_grad_lambda": (ctypes.c_int, [P, P, I64, P, P, P, P, I32, I64, F32, P, I32, P, P, I64, P]),
+        "fdr_bn_refresh_workspace_bytes": (I64, [I32]),
+        "fdr_bn_refresh": (ctypes.c_int, [P, ctypes.POINTER(PolicyDesc), P, P, I32, F32, P, P, P, I64, P]),
         "fdr_fd_weights": (ctypes.c_int, [P, P, I32, F64, I32, I32, P, P, I32, F32, P, P]),
         "fdr_fd_grad_workspace_bytes": (I64, [I32, I64]),
         "fdr_fd_grad": (ctypes.c_int, [P, P, I64, P, P, I32, I64, P, P, I64, P]),

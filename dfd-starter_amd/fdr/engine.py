@@ -315,3 +315,42 @@ def obs_stats_merge(mean, m2, count, acc_mean, acc_m2, acc_count):
     n, d = mean.shape
     check(lib.fdr_obs_stats_merge(None, _p(mean), _p(m2), _p(count), n, d, _p(acc_mean), _p(acc_m2), _p(acc_count),
                                   _stream(mean.device)), "fdr_obs_stats_merge")
+
+
+# ---- delayed returns: lambda with policy drift (learner/finite_differences.py:66-114) -------------
+def fd_lambda_norms(table, idx, sign, slot, sigma, drift, n_params):
+    """||fl32(sign * fl32(sigma * eps_i) + D[slot_i])||^2 per return (f64 [n])."""
+    _check_dev(table, idx, sign, slot, drift)
+    n = idx.numel()
+    n2 = torch.empty(n, dtype=torch.float64, device=table.device)
+    ns = 0 if drift is None else drift.shape[0]
+    check(lib.fdr_fd_lambda_norms(None, _p(table), table.numel(), _p(idx), _p(sign), _p(slot), n, n_params,
+                                  float(sigma), _p(drift), ns, _p(n2), _stream(table.device)), "fdr_fd_lambda_norms")
+    return n2
+
+
+def fd_grad_lambda(table, idx, sign, slot, coef, sigma, drift, n_params, g=None):
+    """g = sum_i coef_i * lambda_i (f64 [P])."""
+    _check_dev(table, idx, sign, slot, coef, drift)
+    dev = table.device
+    n = idx.numel()
+    if g is None:
+        g = torch.empty(n_params, dtype=torch.float64, device=dev)
+    ns = 0 if drift is None else drift.shape[0]
+    nb = lib.fdr_fd_grad_workspace_bytes(n, n_params)
+    ws = _workspace("grad", nb, dev)
+    check(lib.fdr_fd_grad_lambda(None, _p(table), table.numel(), _p(idx), _p(sign), _p(slot), _p(coef), n, n_params,
+                                 float(sigma), _p(drift), ns, _p(g), _p(ws), ws.numel(), _stream(dev)),
+          "fdr_fd_grad_lambda")
+    return g
+
+
+def bn_refresh(spec, theta, x, bn_mean, bn_var, momentum=0.1):
+    """compute_vbn on the device: updates bn_mean / bn_var (f32, [n_in | 64 | 64]) in place."""
+    _check_dev(theta, x, bn_mean, bn_var)
+    x = x.to(torch.float32).reshape(-1, spec.n_in).contiguous()
+    n = x.shape[0]
+    pd = spec.desc(None, None)
+    ws = _workspace("vbn", lib.fdr_bn_refresh_workspace_bytes(n), x.device)
+    check(lib.fdr_bn_refresh(None, ctypes.byref(pd), _p(theta), _p(x), n, float(momentum), _p(bn_mean), _p(bn_var),
+                             _p(ws), ws.numel(), _stream(x.device)), "fdr_bn_refresh")

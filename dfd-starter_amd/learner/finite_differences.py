@@ -127,27 +127,29 @@ class FiniteDifferences(object):
         sigma32 = np.float32(self.noise_std)
         current = [r for r in keep if self.dist_map[r.epoch] is None]
         stale = [r for r in keep if self.dist_map[r.epoch] is not None]
-        # z-score over ALL kept returns (finite_differences.py:40-43)
-        order = current + stale
-        rewards = torch.as_tensor([r.reward for r in order], dtype=torch.float64, device=dev)
-        extra = None
         if stale and self._distributed():
             raise NotImplementedError("stale (delayed) returns are a single-process path; the sharded "
                                       "engine is synchronous and never produces them")
         if stale:
-            z = torch.as_tensor(math_helpers.standardize_arr(np.subtract([r.reward for r in order], policy_reward)),
-                                dtype=torch.float64, device=dev)
-            extra = torch.zeros(P, dtype=torch.float64, device=dev)
-            for k, r in enumerate(stale):
-                i = int(r.encoded_noise)
-                lam = table[i:i + P] * torch.tensor(sigma32, device=dev) * float(getattr(r, "sign", 1) or 1)
-                lam = lam + self.dist_map[r.epoch]
-                nrm = torch.linalg.vector_norm(lam)
-                extra += z[len(current) + k] * (lam / (nrm * nrm)).double()
-        if not current:
-            g = extra
+            # finite_differences.py:88-114 on the device: lambda_i = sigma * eps_i + dist_map[epoch_i],
+            # v_i = lambda_i / ||lambda_i||^2, z-score over all kept returns, g = z . V
+            epochs = sorted({r.epoch for r in stale})
+            drift = torch.stack([self.dist_map[e] for e in epochs]).contiguous()
+            slot_of = {e: k for k, e in enumerate(epochs)}
+            idx = np.array([int(r.encoded_noise) for r in keep], dtype=np.int64)
+            sign = np.array([int(getattr(r, "sign", 1) or 1) for r in keep], dtype=np.int8)
+            slot = np.array([slot_of.get(r.epoch, -1) if self.dist_map[r.epoch] is not None else -1 for r in keep],
+                            dtype=np.int32)
+            idx_d, sign_d, slot_d = (torch.as_tensor(a, device=dev) for a in (idx, sign, slot))
+            rewards = torch.as_tensor([r.reward for r in keep], dtype=torch.float64, device=dev)
+            n2 = engine.fd_lambda_norms(table, idx_d, sign_d, slot_d, self.noise_std, drift, P)
+            ones = torch.ones(len(keep), dtype=torch.int8, device=dev)
+            coef = engine.fd_weights(rewards, policy_reward, 0, ones, n2, 1, 1.0)
+            g = engine.fd_grad_lambda(table, idx_d, sign_d, slot_d, coef, self.noise_std, drift, P,
+                                      self.gradient_memory)
             fdist.allreduce_grad(g, self.process_group)
             return self._apply(g)
+        rewards = torch.as_tensor([r.reward for r in current], dtype=torch.float64, device=dev)
         idx = np.array([int(r.encoded_noise) for r in current], dtype=np.int64)
         sign = np.array([int(getattr(r, "sign", 1) or 1) for r in current], dtype=np.int8)
         idx_d = torch.as_tensor(idx, device=dev)
@@ -155,15 +157,6 @@ class FiniteDifferences(object):
         if all(getattr(r, "norm2", None) is not None for r in current):
             n2 = torch.as_tensor([r.norm2 for r in current], dtype=torch.float64, device=dev)
         else:
-            rows = torch.stack([table[i:i + P] for i in idx])
-            lam = (rows * torch.tensor(sigma32, device=dev)).double()
-            n2 = (lam * lam).sum(dim=1)
-        b = FDBatch(rewards[:len(current)], None, None, n2, idx_d, sign_d, idx, sign, self.epoch)
-        if stale:
-            # weights over the full set: pass every reward, local lanes = the current ones
-            coef = engine.fd_weights(rewards, policy_reward, 0, b.sign, b.norm2, 1, self.noise_std)
-            g = engine.fd_grad(table, b.idx, coef, P, self.gradient_memory)
-            g.add_(extra)
-            fdist.allreduce_grad(g, self.process_group)
-            return self._apply(g)
+            n2 = engine.fd_lambda_norms(table, idx_d, sign_d, None, self.noise_std, None, P)
+        b = FDBatch(rewards, None, None, n2, idx_d, sign_d, idx, sign, self.epoch)
         return self._step_batch(b, policy_reward)

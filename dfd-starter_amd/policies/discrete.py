@@ -4,6 +4,7 @@ import torch
 import torch.nn as nn
 from torch.distributions import Categorical
 
+from fdr import engine
 from .policy import Policy
 
 
@@ -30,6 +31,22 @@ class DiscretePolicy(Policy):
     @torch.no_grad()
     def get_strategy(self, x):
         return self.forward(np.asarray(x)).cpu().numpy()                # discrete.py:31-32
+
+    @torch.no_grad()
+    def compute_vbn(self, buffer):
+        """policies/policy.py:31-34 on the device: fdr_bn_refresh runs the train-mode pass (batch-stat
+        normalisation + running-stat update of the 3 BatchNorm1d) -- no torch compute."""
+        x = torch.as_tensor(np.asarray(buffer), dtype=torch.float32).reshape(-1, self.input_shape)
+        bns = [m for m in self.model if isinstance(m, nn.BatchNorm1d)]
+        bm, bv = self.bn_stats()
+        engine.bn_refresh(self.spec, self.flat, x.to(self.flat.device), bm, bv, momentum=bns[0].momentum)
+        off = 0
+        for m in bns:
+            n = m.num_features
+            m.running_mean.copy_(bm[off:off + n])
+            m.running_var.copy_(bv[off:off + n])
+            m.num_batches_tracked += 1
+            off += n
 
     def _build_model(self):
         h1 = h2 = 64                                                    # discrete.py:34-48

@@ -170,6 +170,34 @@ int fdr_fd_grad(fdr_ctx* ctx, const float* table, int64_t table_size, const int6
                 const double* coef, int32_t n_dirs, int64_t n_params, double* g, void* workspace,
                 int64_t workspace_bytes, fdr_stream stream);
 
+/* ---- delayed returns: lambda with policy drift (learner/finite_differences.py:66-73, 80-114) -----
+ * Return i's perturbation lambda_i = fl32(sign_i * fl32(sigma * table[idx_i + p]) + D[slot_i][p]),
+ * D = drift [n_slots, P] f32 (dist_map: theta of the return's epoch minus the current theta;
+ * slot_i < 0 or slot == NULL: the current epoch, D = 0; sign == NULL: +1).
+ *   fdr_fd_lambda_norms: norm2[i] = ||lambda_i||^2 (f64); NaN for an out-of-range offset.
+ *   fdr_fd_grad_lambda:  g[p] = sum_i coef[i] * lambda_i[p] (f64, fixed order); with
+ *                        coef = fdr_fd_weights(sign = +1, sigma = 1, lanes_per_dir = 1) this is
+ *                        np.dot(z, lambda / ||lambda||^2).  workspace: fdr_fd_grad_workspace_bytes(n, P). */
+int fdr_fd_lambda_norms(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx, const int8_t* sign,
+                        const int32_t* slot, int32_t n, int64_t n_params, float sigma, const float* drift,
+                        int32_t n_slots, double* norm2, fdr_stream stream);
+int fdr_fd_grad_lambda(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx, const int8_t* sign,
+                       const int32_t* slot, const double* coef, int32_t n, int64_t n_params, float sigma,
+                       const float* drift, int32_t n_slots, double* g, void* workspace, int64_t workspace_bytes,
+                       fdr_stream stream);
+
+/* ---- BN running-stat refresh (policies/policy.py:31-34 compute_vbn, run_sequential.py:156-157) ------
+ * DiscretePolicy only (the policy with BatchNorm1d layers): one train-mode pass of the buffer
+ * x [n, n_in] through BN0-L1-ReLU-BN1-L2-ReLU-BN2 with theta; every BN normalises with its batch
+ * statistics (biased variance) and updates its running stats in place:
+ *   rm <- momentum * mean + (1 - momentum) * rm,  rv <- momentum * var * n / (n - 1) + (1 - momentum) * rv
+ * bn_mean / bn_var: the [n_in | 64 | 64] f32 stats of fdr_policy_desc (torch momentum = 0.1); n >= 2.
+ * workspace: fdr_bn_refresh_workspace_bytes(n) bytes. */
+int64_t fdr_bn_refresh_workspace_bytes(int32_t n);
+int fdr_bn_refresh(fdr_ctx* ctx, const fdr_policy_desc* policy, const float* theta, const float* x, int32_t n,
+                   float momentum, float* bn_mean, float* bn_var, void* workspace, int64_t workspace_bytes,
+                   fdr_stream stream);
+
 /* ---- DSGD update (dsgd/dynamic_sgd.py:19-51, policies/policy.py:63-70) -----------------
  * grad = fl32(-g); norm = ||grad||; coef = lr * sqrt(P) * lr_scale / norm;
  * theta <- fl32(theta - fl32(fl32(coef) * grad)).

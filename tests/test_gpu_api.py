@@ -192,3 +192,26 @@ def test_sequential_runner_antithetic_cheetah():
     assert len(r.history) == 3
     for h in r.history:
         assert np.isfinite(h["Noisy Reward"]) and h["Update Magnitude"] > 0
+
+
+def test_compute_vbn_on_device_vs_torch_train_mode():
+    """fdr_bn_refresh == one train-mode torch pass of the DiscretePolicy (policies/policy.py:31-34)."""
+    import torch.nn as nn
+    from policies import DiscretePolicy
+    from oracle import policies as opol
+    torch.manual_seed(124)
+    pol = DiscretePolicy(4, 2, seed=124)
+    ref = opol.TorchPolicy("discrete", 4, 2, seed=124)
+    ref.set_flat(pol.get_trainable_flat())
+    buf = (np.random.RandomState(3).randn(500, 4) * 2 + 0.5).astype(np.float32)
+    for _ in range(2):                      # twice: the second pass starts from refreshed stats
+        pol.compute_vbn(buf)
+        ref.model.train()
+        with torch.no_grad():
+            ref.model(torch.as_tensor(buf))
+        ref.model.eval()
+    got = [m for m in pol.model if isinstance(m, nn.BatchNorm1d)]
+    want = [m for m in ref.model if isinstance(m, nn.BatchNorm1d)]
+    for g, w in zip(got, want):
+        np.testing.assert_allclose(g.running_mean.cpu().numpy(), w.running_mean.numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(g.running_var.cpu().numpy(), w.running_var.numpy(), rtol=1e-5, atol=1e-6)

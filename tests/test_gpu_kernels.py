@@ -303,3 +303,25 @@ def _oracle_lanes_with_ids(kind, n_in, n_act, theta, tab, idx, sign, env, seed, 
         obs, r = env.step((mean + std * z).astype(np.float32))
         ret += r
     return ret + crng.jiggle(seed, lanes)
+
+
+def test_lambda_drift_norms_and_grad_vs_oracle(eng):
+    """Delayed returns (finite_differences.py:88-114): lambda = sign * fl32(sigma eps) + dist_map[epoch]."""
+    P = 6092
+    t, tab = table(P)
+    rs = np.random.RandomState(4)
+    n = 10
+    idx = t.sample_indices(n)
+    sign = rs.choice([-1, 1], n).astype(np.int8)
+    drift = (rs.randn(2, P) * 0.01).astype(np.float32)
+    slot = rs.choice([-1, 0, 1], n).astype(np.int32)
+    s32 = np.float32(0.02)
+    lam = np.stack([(np.float32(sg) * (t.table[i:i + P] * s32).astype(np.float32)).astype(np.float32)
+                    + (drift[sl] if sl >= 0 else np.float32(0)) for i, sg, sl in zip(idx, sign, slot)]).astype(np.float32)
+    n2_ref = (lam.astype(np.float64) ** 2).sum(1)
+    n2 = eng.fd_lambda_norms(tab, dev(idx, torch.int64), dev(sign), dev(slot), 0.02, dev(drift), P).cpu().numpy()
+    np.testing.assert_allclose(n2, n2_ref, rtol=1e-12)
+    coef = rs.randn(n)
+    g = eng.fd_grad_lambda(tab, dev(idx, torch.int64), dev(sign), dev(slot), dev(coef), 0.02, dev(drift), P)
+    g_ref = coef @ lam.astype(np.float64)
+    assert np.linalg.norm(g.cpu().numpy() - g_ref) <= 1e-12 * np.linalg.norm(g_ref)
