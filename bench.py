@@ -28,6 +28,7 @@ for _p in (REPO, PKG):
 
 METRIC = "env steps/sec (whole node) + sec/FD-grad-step, 4096 antithetic perturbations"
 FP32_PEAK_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 vector = FP32 matrix peak
+FP16_PEAK_TFLOPS = 2516.6         # MI355X_MICROARCH.md: dense FP16/BF16 MFMA peak (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 CONFIGS = {
@@ -36,6 +37,8 @@ CONFIGS = {
     "cartpole": ("discrete", 4, 2, "cartpole", 500),
     # BASELINE config 4 per GPU: 8192 perturbations x 4 envs over 8 GPUs -> 1024 lanes x 4 envs each
     "impala": ("impala", (64, 64, 3), 6, "frames", 1000),
+    # BASELINE config 5 per GPU: as config 4 with A = 4 and fp16 rollouts
+    "impala_fp16": ("impala", (64, 64, 3), 4, "frames", 1000),
 }
 IMPALA_ENVS = 4
 IMPALA_LANES = 1024
@@ -166,9 +169,11 @@ def main():
 
     torch.manual_seed(124)
     impala = kind == "impala"
+    fp16 = False
     if impala:
         policy = ImpalaPolicy(n_in, n_act, seed=124, device=dev)
-        env = FrameEnv(n_act, episode_len=T, envs_per_lane=IMPALA_ENVS, env_seed=5)
+        fp16 = args.config == "impala_fp16"
+        env = FrameEnv(n_act, episode_len=T, envs_per_lane=IMPALA_ENVS, env_seed=5, fp16=fp16)
         engine.impala_profile(True)
     else:
         Pol = DiscretePolicy if kind == "discrete" else MujocoPolicy
@@ -241,21 +246,25 @@ def main():
             conv_ms, core_ms, replay_ms = t.tolist()
         conv_launch_ms = conv_ms / T
         achieved_tf = IMPALA_CONV_FLOP * L * E / (conv_launch_ms * 1e-3) / 1e12
-        core_gbs = IMPALA_CORE_BYTES * L / (core_ms / T * 1e-3) / 1e9
-        roofline = {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                    "kernel": "impala conv_kernel (15 convs, v_mfma_f32_16x16x4_f32)",
+        core_bytes = IMPALA_CORE_BYTES // (2 if fp16 else 1)
+        core_gbs = core_bytes * L / (core_ms / T * 1e-3) / 1e9
+        peak = FP16_PEAK_TFLOPS if fp16 else FP32_PEAK_TFLOPS
+        roofline = {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(achieved_tf / peak, 4), "traffic": traffic,
+                    "kernel": "impala conv_kernel_h (15 convs, v_mfma_f32_16x16x32_f16)" if fp16 else
+                              "impala conv_kernel (15 convs, v_mfma_f32_16x16x4_f32)",
                     "conv_launch_ms": round(conv_launch_ms, 4), "flop_per_env_step": IMPALA_CONV_FLOP,
                     "envs_per_launch": L * E, "rollout_ms": round(rollout_ms, 3),
                     "core_kernel": {"bound": "hbm", "achieved": round(core_gbs, 1), "peak": HBM_PEAK_GBS,
                                     "unit": "GB/s", "frac": round(core_gbs / HBM_PEAK_GBS, 4),
-                                    "launch_ms": round(core_ms / T, 4), "bytes_per_lane_step": IMPALA_CORE_BYTES},
+                                    "launch_ms": round(core_ms / T, 4), "bytes_per_lane_step": core_bytes},
                     "entropy_replay_ms": round(replay_ms, 3),
-                    "note": "f32 MFMA peak (= f32 vector peak); conv time from HIP events between the step-loop "
-                            "launches (fdr_impala_profile)"}
-        workload = ("BASELINE config 4 per GPU: ImpalaPolicy(A=%d) P=%d, %d perturbations (%d directions x +/-) x "
-                    "%d envs each, synthetic 3x64x64 frames, T=%d, full FD step (rollout + entropy pass + weights "
-                    "+ gradient + DSGD)" % (n_act, policy.num_params, L, L // 2, E, T))
+                    "note": ("dense f16 MFMA peak" if fp16 else "f32 MFMA peak (= f32 vector peak)") +
+                            "; conv time from HIP events between the step-loop launches (fdr_impala_profile)"}
+        workload = ("BASELINE config %d per GPU: ImpalaPolicy(A=%d) P=%d, %d perturbations (%d directions x +/-) x "
+                    "%d envs each, synthetic 3x64x64 frames, T=%d, %s, full FD step (rollout + entropy pass + "
+                    "weights + gradient + DSGD)" % (5 if fp16 else 4, n_act, policy.num_params, L, L // 2, E, T,
+                                                    "fp16 rollouts" if fp16 else "f32"))
     else:
         flops = lane_step_flops(kind, n_in, n_act) * L * T
         achieved_tf = flops / (rollout_ms * 1e-3) / 1e12
@@ -281,7 +290,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f16" if (impala and fp16) else "f32",
         "data": "synthetic",
         "config": {"workload": workload, "perturbations_per_gpu": L, "envs_per_perturbation": E,
                    "global_perturbations": L * world, "episode_len": T, "n_params": policy.num_params,

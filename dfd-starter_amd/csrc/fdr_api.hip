@@ -293,7 +293,7 @@ static int impala_layout(const fdr_impala_desc* d, impala::Layout* L) {
 int64_t fdr_impala_workspace_bytes(const fdr_impala_desc* d, int32_t n_lanes) {
   impala::Layout L;
   if (!d || n_lanes < 0 || !impala::make_layout(d->n_act, &L)) return -1;
-  return impala::plan(L, n_lanes, d->envs_per_lane, d->episode_len, d->entropy != 0).total;
+  return impala::plan(L, n_lanes, d->envs_per_lane, d->episode_len, d->entropy != 0, d->fp16 != 0).total;
 }
 
 int fdr_impala_rollout(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lanes_desc* lanes,
@@ -317,6 +317,7 @@ int fdr_impala_rollout(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lanes_d
   c.T = d->episode_len;
   c.entropy = d->entropy != 0;
   c.jiggle = jiggle;
+  c.fp16 = d->fp16 != 0;
   c.seed = seed;
   c.env_seed = d->env_seed;
   c.bn_mean = d->bn_mean;
@@ -330,10 +331,10 @@ int fdr_impala_rollout(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lanes_d
   return impala::launch_rollout(c, ws, ws_bytes, (hipStream_t)stream);
 }
 
-int64_t fdr_impala_forward_workspace_bytes(int32_t n_act, int32_t n_envs) {
+int64_t fdr_impala_forward_workspace_bytes(int32_t n_act, int32_t n_envs, int32_t fp16) {
   impala::Layout L;
   if (n_envs < 0 || !impala::make_layout(n_act, &L)) return -1;
-  return impala::forward_workspace_bytes(L, n_envs);
+  return impala::forward_workspace_bytes(L, n_envs, fp16 != 0);
 }
 
 int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* d, const float* theta, int32_t n_envs,
@@ -348,6 +349,7 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* d, const float* thet
   if (n_envs < 0) return set_error(FDR_ERR_INVALID, "n_envs < 0");
   impala::ForwardCall f{};
   f.layout = &L;
+  f.fp16 = d->fp16 != 0;
   f.theta = theta;
   f.n_envs = n_envs;
   f.frames = frames;

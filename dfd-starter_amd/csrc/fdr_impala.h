@@ -1,5 +1,7 @@
 // Internal (non-ABI) declarations of the ImpalaPolicy path (fdr_impala.hip).
 #pragma once
+#include <cfloat>
+
 #include "fdr_internal.h"
 
 namespace fdr {
@@ -16,7 +18,7 @@ constexpr int kMaxSections = 64;
 constexpr int kFramePix = 3 * 64 * 64;
 
 // One contiguous run of the per-lane parameter pack: pack[dst + u] = theta'[src + f(u)].
-enum SectionKind : int32_t { kCopy = 0, kConvFrag = 1, kTranspose = 2 };
+enum SectionKind : int32_t { kCopy = 0, kConvFrag = 1, kTranspose = 2, kConvFragH = 3 };
 struct Section {
   int32_t dst, len, src, kind, a, b;  // conv frag: a = Cin, b = Cout; transpose: a = rows, b = cols of W
 };
@@ -33,20 +35,137 @@ struct Layout {
   int32_t fc_wt, fc_b, lstm_wt, lstm_bih, lstm_bhh, head_w, head_b;
   int32_t n_bn_stats;
   Section sec[kMaxSections];
+  // fp16 mode (BASELINE config 5): a second, half-precision pack of the MFMA/streamed weights
+  int64_t hpack;                  // halves per lane (multiple of 64)
+  int32_t conv_h[kConvs];         // f16 MFMA A-fragments of each conv (v_mfma_f32_16x16x32_f16)
+  int32_t fc_wt_h, lstm_wt_h;     // W^T of fc / [W_ih | W_hh] in f16
+  int32_t n_hsections;
+  Section hsec[24];
 };
 
 bool make_layout(int n_act, Layout* out);
 
+struct StepArgs {
+  const float* pack;
+  int64_t pack_stride;  // floats between lanes' packs (0: every lane shares one pack)
+  _Float16* hpack;      // fp16 mode: half pack (conv A-fragments, fc / LSTM W^T), or NULL
+  int64_t hpack_stride;
+  const float* bn_mean;
+  const float* bn_var;
+  int n_lanes, envs, n_act, t, T;
+  int64_t lane_offset;
+  uint64_t fkey, rkey, akey;
+  const float* frames;     // external frames [lane*E+e][3][64][64] (forward API) or NULL
+  float* feat;             // [lane*E+e][2048]
+  // core
+  float* h;
+  float* c;
+  float* rprev;
+  float* ci;               // [t][lane*E+e][257] (entropy replay) or NULL
+  double* ret;
+  double* ent;
+  int32_t* actions;        // [lane*E+e][T] or NULL
+  float* probs;            // rollout: [lane*E+e][T][A]; forward: [lane*E+e][A]; or NULL
+  const int8_t* deterministic;
+  const float* reward_in;  // forward: reward carried by the obs
+  const float* notdone;    // forward: done mask (policies/impala.py:170-176)
+  uint64_t* dbg;           // diagnostics: phase clocks of conv workgroup 0 (fdr_impala_debug_clock) or NULL
+};
+
+// phase clock of the first conv workgroup (s_memtime), for the phase breakdown in DESIGN.md
+#define FDR_STAMP(a, k)                                                      \
+  do {                                                                       \
+    if ((a).dbg && blockIdx.x == 0 && threadIdx.x == 0) (a).dbg[k] = clock64(); \
+  } while (0)
+
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
+constexpr float kBnEps = 1e-5f;
+enum CoreMode { kRollout = 0, kReplay = 1, kForward = 2 };
+constexpr int kCoreThreads = 256;
+constexpr int kBnTab = 15 * 32;
+
+__device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+// Softmax, action (argmax / inverse CDF on the counter stream), synthetic reward and return, or the
+// entropy term (replay), or the probabilities (forward), for env e of lane `lane` (thread e < E).
+template <int E, int MODE>
+__device__ __forceinline__ void core_finish(const StepArgs& a, const float* logit, int lane, int j) {
+  const int A = a.n_act;
+  const int64_t e0 = (int64_t)lane * E;
+    const int e = j;
+    const float* lg = logit + e * kMaxAct;
+    float mx = -FLT_MAX;
+    for (int i = 0; i < A; ++i) mx = fmaxf(mx, lg[i]);
+    float p[kMaxAct];
+    float sum = 0.f;
+    for (int i = 0; i < A; ++i) {
+      p[i] = expf(lg[i] - mx);
+      sum += p[i];
+    }
+    const float inv = 1.f / sum;
+    for (int i = 0; i < A; ++i) p[i] *= inv;
+    const int64_t ge = e0 + e;
+    if constexpr (MODE == kForward) {
+      if (a.probs)
+        for (int i = 0; i < A; ++i) a.probs[ge * A + i] = p[i];
+    } else if constexpr (MODE == kReplay) {
+      // torch Categorical(probs).entropy(): normalise, log clamped at float min
+      float tot = 0.f;
+      for (int i = 0; i < A; ++i) tot += p[i];
+      float h = 0.f;
+      for (int i = 0; i < A; ++i) {
+        const float pn = p[i] / tot;
+        const float l = pn > 0.f ? logf(pn) : -FLT_MAX;
+        h -= pn * l;
+      }
+      a.ent[ge] += (double)h;
+    } else {
+      if (a.probs)
+        for (int i = 0; i < A; ++i) a.probs[(ge * a.T + a.t) * A + i] = p[i];
+      const uint64_t gid = (uint64_t)(a.lane_offset * E + ge);
+      int act = 0;
+      const bool det = a.deterministic && a.deterministic[lane];
+      if (det) {
+        float best = p[0];
+        for (int i = 1; i < A; ++i)
+          if (p[i] > best) { best = p[i]; act = i; }
+      } else {  // inverse CDF, sequential f32 cumsum (oracle/policies.py categorical_inverse_cdf)
+        float tot = 0.f;
+        for (int i = 0; i < A; ++i) tot += p[i];
+        const float u = uniform24(hash_ctr(a.akey, gid, (uint64_t)a.t, 0));
+        const float target = u * tot;
+        float cs = 0.f;
+        for (int i = 0; i < A - 1; ++i) {
+          cs += p[i];
+          act += cs <= target ? 1 : 0;
+        }
+      }
+      const uint64_t ctr = (gid << 32) | ((uint64_t)a.t << 11);
+      const int tgt = (int)((mix64(a.rkey + ctr * kGolden) >> 40) % (uint64_t)A);
+      const float r = act == tgt ? 1.f : (act == (tgt + 1) % A ? -1.f : 0.f);
+      a.ret[ge] += (double)r;
+      a.rprev[ge] = r;
+      if (a.actions) a.actions[ge * a.T + a.t] = act;
+    }
+}
+
+// fp16 mode kernels (fdr_impala_h.hip)
+__global__ void conv_kernel_h(Layout L, StepArgs a);
+template <int E, int MODE>
+__global__ void core_kernel_h(Layout L, StepArgs a);
+constexpr int kHThreads = 512;
+
 struct Plan {  // workspace carve-up (byte offsets)
-  int64_t pack, feat, h, c, rprev, ci, n2, total;
+  int64_t pack, hpack, feat, h, c, rprev, ci, n2, total;
   int nblk;    // prep blocks per lane
 };
-Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy);
+Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16 = false);
 
 struct RolloutCall {
   const Layout* layout;
   LanesArgs lanes;
-  int n_lanes, envs, T, entropy, jiggle;
+  int n_lanes, envs, T, entropy, jiggle, fp16;
   uint64_t seed, env_seed;
   const float* bn_mean;
   const float* bn_var;
@@ -61,6 +180,7 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
 
 struct ForwardCall {
   const Layout* layout;
+  int fp16;
   const float* theta;
   int n_envs;
   const float* frames;
@@ -73,7 +193,7 @@ struct ForwardCall {
   const float* bn_mean;
   const float* bn_var;
 };
-int64_t forward_workspace_bytes(const Layout& L, int n_envs);
+int64_t forward_workspace_bytes(const Layout& L, int n_envs, bool fp16 = false);
 void set_profile(int on);
 void set_debug_clock(uint64_t* buf);
 int read_profile(double* out3);

@@ -24,10 +24,8 @@ namespace impala {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kCh[3] = {16, 32, 32};
-constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
 constexpr uint64_t kFrameSalt = 0x4652414D45533031ull;  // oracle/impala.py FRAME_SALT
 constexpr uint64_t kRewardSalt = 0x5245574152443031ull; // oracle/impala.py REWARD_SALT
-constexpr float kBnEps = 1e-5f;
 
 // ------------------------------------------------------------------------------------------
 // Host: pack layout.  Walks the reference's parameters() order (feat_convs, resnet1, resnet2,
@@ -89,6 +87,31 @@ bool make_layout(int n_act, Layout* L) {
   L->P = src;
   L->pack = round_up(dst, 64);
   L->n_bn_stats = stat;
+
+  // half pack: walk the same source offsets again
+  int32_t hdst = 0;
+  auto hadd = [&](int32_t kind, int32_t len, int32_t a, int32_t b, int32_t s0) {
+    hdst = (int32_t)round_up(hdst, 64);
+    Section& h = L->hsec[L->n_hsections++];
+    h = Section{hdst, len, s0, kind, a, b};
+    const int32_t at = hdst;
+    hdst += len;
+    return at;
+  };
+  for (int i = 0; i < L->n_sections; ++i) {
+    const Section& q = L->sec[i];
+    if (q.kind == kConvFrag) {
+      const int cin = q.a, cout = q.b;
+      const int ks = cin == 3 ? 2 : (9 * cin + 31) / 32;      // k-steps of 32
+      const int idx = [&] { for (int c = 0; c < kConvs; ++c) if (L->conv_w[c] == q.dst) return c; return -1; }();
+      L->conv_h[idx] = hadd(kConvFragH, ks * (cout / 16) * 64 * 8, cin, cout, q.src);
+    } else if (q.kind == kTranspose) {
+      const int32_t at = hadd(kTranspose, q.len, q.a, q.b, q.src);
+      if (q.dst == L->fc_wt) L->fc_wt_h = at;
+      if (q.dst == L->lstm_wt) L->lstm_wt_h = at;
+    }
+  }
+  L->hpack = round_up(hdst, 64);
   return true;
 }
 
@@ -96,13 +119,14 @@ constexpr int kPrepThreads = 256;
 constexpr int kPrepPer = 4;
 constexpr int kPrepSpan = kPrepThreads * kPrepPer;
 
-Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy) {
+Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16) {
   Plan p{};
   const int64_t ne = (int64_t)n_lanes * envs;
   int64_t o = 0;
   auto take = [&](int64_t bytes) { const int64_t at = o; o += round_up(std::max<int64_t>(bytes, 0), 256); return at; };
   p.nblk = (int)((L.pack + kPrepSpan - 1) / kPrepSpan);
   p.pack = take((int64_t)n_lanes * L.pack * 4);
+  p.hpack = take(fp16 ? (int64_t)n_lanes * L.hpack * 2 : 0);
   p.feat = take(ne * kFeat * 4);
   p.h = take(ne * kHid * 4);
   p.c = take(ne * kHid * 4);
@@ -121,6 +145,28 @@ __device__ __forceinline__ int64_t section_src(const Section& s, int32_t u) {
   if (s.kind == kTranspose) {  // pack = W^T: u = k * rows + r  ->  W[r][k]
     const int32_t k = u / s.a, r = u - k * s.a;
     return (int64_t)s.src + (int64_t)r * s.b + k;
+  }
+  if (s.kind == kConvFragH) {
+    // f16 A-fragment (v_mfma_f32_16x16x32_f16, weights as A): u = ((kstep * NT + nt) * 64 + l) * 8 + jj,
+    // A[i = nt*16 + (l & 15)][k = 8 (l >> 4) + jj].  K order per k-step of 32: Cin % 8 == 0 -> lane group
+    // g = l >> 4 holds 8 consecutive channels of one tap (taps per k-step 32 / Cin); Cin = 3 (frame image
+    // with 4 channel slots) -> group g holds taps 8 kstep + 2g, +1 with 4 channel slots each.
+    const int32_t cin = s.a, nt_n = s.b / 16;
+    const int32_t jj = u & 7, l = (u >> 3) & 63, rest = u >> 9;
+    const int32_t nt = rest % nt_n, ks = rest / nt_n;
+    const int32_t i = nt * 16 + (l & 15), g = l >> 4;
+    int32_t tap, ci;
+    if (cin == 3) {
+      tap = 8 * ks + 2 * g + (jj >> 2);
+      ci = jj & 3;
+      if (ci >= 3) return -1;
+    } else {
+      const int32_t cpg = cin / 8, tpk = 32 / cin;
+      tap = ks * tpk + g / cpg;
+      ci = 8 * (g % cpg) + jj;
+    }
+    if (tap >= 9) return -1;
+    return (int64_t)s.src + ((int64_t)i * cin + ci) * 9 + tap;
   }
   // conv B-fragment (v_mfma_f32_16x16x4_f32): u = (kstep * NT + nt) * 64 + l; B[k][n] with
   // k = 4 * kstep + (l >> 4), n = nt * 16 + (l & 15).  K order: Cin % 4 == 0 -> tap-major,
@@ -143,30 +189,34 @@ __device__ __forceinline__ int64_t section_src(const Section& s, int32_t u) {
   return (int64_t)s.src + ((int64_t)n * cin + ci) * 9 + tap;
 }
 
-__global__ __launch_bounds__(kPrepThreads) void prep_kernel(Layout L, LanesArgs lanes, float* __restrict__ pack,
-                                                            double* __restrict__ n2_part) {
+template <typename OUT>
+__global__ __launch_bounds__(kPrepThreads) void prep_kernel(Layout L, LanesArgs lanes, OUT* __restrict__ pack,
+                                                            double* __restrict__ n2_part, int half) {
   const int lane = blockIdx.y;
   ParamSrc src = lanes.src(lane);
   const int64_t j0 = (int64_t)blockIdx.x * kPrepSpan + threadIdx.x;
-  float* out = pack + (int64_t)lane * L.pack;
-  double n2 = 0.0;
+  const int64_t len = half ? L.hpack : L.pack;
+  const Section* sec = half ? L.hsec : L.sec;
+  const int nsec = half ? L.n_hsections : L.n_sections;
+  OUT* out = pack + (int64_t)lane * len;
   const bool bad = src.n2 != src.n2;  // out-of-range table offset: NaN norm, unperturbed lane
   src.n2 = 0.0;
 #pragma unroll
   for (int i = 0; i < kPrepPer; ++i) {
     const int64_t j = j0 + (int64_t)i * kPrepThreads;
-    if (j >= L.pack) break;
-    int lo = 0, hi = L.n_sections - 1;  // last section with dst <= j
+    if (j >= len) break;
+    int lo = 0, hi = nsec - 1;  // last section with dst <= j
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (L.sec[mid].dst <= j) lo = mid; else hi = mid - 1;
+      if (sec[mid].dst <= j) lo = mid; else hi = mid - 1;
     }
-    const Section& s = L.sec[lo];
+    const Section& s = sec[lo];
     const int32_t u = (int32_t)(j - s.dst);
-    const int64_t p = u < s.len ? section_src(s, u) : -1;
-    out[j] = p >= 0 ? src.get(p) : 0.f;
+    const int64_t p = (j >= s.dst && u < s.len) ? section_src(s, u) : -1;
+    out[j] = (OUT)(p >= 0 ? (half ? src.get_nocount(p) : src.get(p)) : 0.f);
   }
-  n2 = src.n2;
+  if (half) return;
+  double n2 = src.n2;
   // block reduce (deterministic): wave sums, then wave 0
   __shared__ double red[kPrepThreads / kWave];
   n2 = wave_sum(n2);
@@ -191,7 +241,6 @@ constexpr int kConvThreads = 512;
 constexpr int kGuard = 128;          // padded rows above T: the band of conv row -1 reads them
 constexpr int kTE = 23488;
 constexpr int kRX = 16 * 32 * 32;
-constexpr int kBnTab = 15 * 32;
 constexpr int kConvLds = kGuard + kTE + kRX + 2 * kBnTab;  // 40,960 floats = 160 KiB
 constexpr int kBand = 9;             // conv rows per entry-conv band: 4 pooled rows + 1 shared row
 
@@ -204,38 +253,6 @@ struct Plane {  // padded [H+2][H+2] image, bank-staggered plane stride
 static_assert(Plane<32>::P == 1168 && Plane<16>::P == 336 && Plane<8>::P == 146, "plane strides");
 static_assert(16 * Plane<32>::P <= kTE && 3 * Plane<64>::P + 16 * kBand * 65 <= kTE, "LDS plan");
 
-struct StepArgs {
-  const float* pack;
-  int64_t pack_stride;  // floats between lanes' packs (0: every lane shares one pack)
-  const float* bn_mean;
-  const float* bn_var;
-  int n_lanes, envs, n_act, t, T;
-  int64_t lane_offset;
-  uint64_t fkey, rkey, akey;
-  const float* frames;     // external frames [lane*E+e][3][64][64] (forward API) or NULL
-  float* feat;             // [lane*E+e][2048]
-  // core
-  float* h;
-  float* c;
-  float* rprev;
-  float* ci;               // [t][lane*E+e][257] (entropy replay) or NULL
-  double* ret;
-  double* ent;
-  int32_t* actions;        // [lane*E+e][T] or NULL
-  float* probs;            // rollout: [lane*E+e][T][A]; forward: [lane*E+e][A]; or NULL
-  const int8_t* deterministic;
-  const float* reward_in;  // forward: reward carried by the obs
-  const float* notdone;    // forward: done mask (policies/impala.py:170-176)
-  uint64_t* dbg;           // diagnostics: phase clocks of conv workgroup 0 (fdr_impala_debug_clock) or NULL
-};
-
-// phase clock of the first conv workgroup (s_memtime), for the phase breakdown in DESIGN.md
-#define FDR_STAMP(a, k)                                                      \
-  do {                                                                       \
-    if ((a).dbg && blockIdx.x == 0 && threadIdx.x == 0) (a).dbg[k] = clock64(); \
-  } while (0)
-
-__device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
 
 // B fragments of one conv for this wave's N-tile: bf[s] = B[k = 4s + (lane >> 4)][n], one VGPR each.
 template <int CIN, int NT>
@@ -537,10 +554,7 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
 // (gate rows j, 256+j, 512+j, 768+j), so the cell update is thread-local; weights stream from the
 // pack as coalesced rows of W^T, activations are LDS broadcasts.
 // ------------------------------------------------------------------------------------------
-enum CoreMode { kRollout = 0, kReplay = 1, kForward = 2 };
-constexpr int kCoreThreads = 256;
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
 template <int E, int MODE>
 __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a) {
@@ -697,63 +711,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
     logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
   }
   __syncthreads();
-  if (j < E) {
-    const int e = j;
-    const float* lg = logit + e * kMaxAct;
-    float mx = -FLT_MAX;
-    for (int i = 0; i < A; ++i) mx = fmaxf(mx, lg[i]);
-    float p[kMaxAct];
-    float sum = 0.f;
-    for (int i = 0; i < A; ++i) {
-      p[i] = expf(lg[i] - mx);
-      sum += p[i];
-    }
-    const float inv = 1.f / sum;
-    for (int i = 0; i < A; ++i) p[i] *= inv;
-    const int64_t ge = e0 + e;
-    if constexpr (MODE == kForward) {
-      if (a.probs)
-        for (int i = 0; i < A; ++i) a.probs[ge * A + i] = p[i];
-    } else if constexpr (MODE == kReplay) {
-      // torch Categorical(probs).entropy(): normalise, log clamped at float min
-      float tot = 0.f;
-      for (int i = 0; i < A; ++i) tot += p[i];
-      float h = 0.f;
-      for (int i = 0; i < A; ++i) {
-        const float pn = p[i] / tot;
-        const float l = pn > 0.f ? logf(pn) : -FLT_MAX;
-        h -= pn * l;
-      }
-      a.ent[ge] += (double)h;
-    } else {
-      if (a.probs)
-        for (int i = 0; i < A; ++i) a.probs[(ge * a.T + a.t) * A + i] = p[i];
-      const uint64_t gid = (uint64_t)(a.lane_offset * E + ge);
-      int act = 0;
-      const bool det = a.deterministic && a.deterministic[lane];
-      if (det) {
-        float best = p[0];
-        for (int i = 1; i < A; ++i)
-          if (p[i] > best) { best = p[i]; act = i; }
-      } else {  // inverse CDF, sequential f32 cumsum (oracle/policies.py categorical_inverse_cdf)
-        float tot = 0.f;
-        for (int i = 0; i < A; ++i) tot += p[i];
-        const float u = uniform24(hash_ctr(a.akey, gid, (uint64_t)a.t, 0));
-        const float target = u * tot;
-        float cs = 0.f;
-        for (int i = 0; i < A - 1; ++i) {
-          cs += p[i];
-          act += cs <= target ? 1 : 0;
-        }
-      }
-      const uint64_t ctr = (gid << 32) | ((uint64_t)a.t << 11);
-      const int tgt = (int)((mix64(a.rkey + ctr * kGolden) >> 40) % (uint64_t)A);
-      const float r = act == tgt ? 1.f : (act == (tgt + 1) % A ? -1.f : 0.f);
-      a.ret[ge] += (double)r;
-      a.rprev[ge] = r;
-      if (a.actions) a.actions[ge * a.T + a.t] = act;
-    }
-  }
+  if (j < E) core_finish<E, MODE>(a, logit, lane, j);
 }
 
 __global__ void init_kernel(int64_t n_env, float* h, float* c, float* rprev, double* ret, double* ent) {
@@ -831,21 +789,31 @@ int read_profile(double* out) {
 template <int E>
 static int launch_steps(const Layout& L, StepArgs a, int entropy, hipStream_t stream) {
   const int conv_grid = (a.n_lanes + 7) / 8 * 8 * a.envs;
+  const bool h = a.hpack != nullptr;
   g_prof.used = 0;
   g_prof.T = a.T;
   g_prof.entropy = entropy;
   mark(stream);
   for (int t = 0; t < a.T; ++t) {
     a.t = t;
-    hipLaunchKernelGGL(conv_kernel, dim3(conv_grid), dim3(kConvThreads), 0, stream, L, a);
+    if (h)
+      hipLaunchKernelGGL(conv_kernel_h, dim3(conv_grid), dim3(kHThreads), 0, stream, L, a);
+    else
+      hipLaunchKernelGGL(conv_kernel, dim3(conv_grid), dim3(kConvThreads), 0, stream, L, a);
     mark(stream);
-    hipLaunchKernelGGL((core_kernel<E, kRollout>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+    if (h)
+      hipLaunchKernelGGL((core_kernel_h<E, kRollout>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+    else
+      hipLaunchKernelGGL((core_kernel<E, kRollout>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
     mark(stream);
   }
   if (entropy)
     for (int t = 0; t < a.T; ++t) {
       a.t = t;
-      hipLaunchKernelGGL((core_kernel<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+      if (h)
+        hipLaunchKernelGGL((core_kernel_h<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+      else
+        hipLaunchKernelGGL((core_kernel<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
       mark(stream);
     }
   return check_launch("impala step kernels");
@@ -853,7 +821,7 @@ static int launch_steps(const Layout& L, StepArgs a, int entropy, hipStream_t st
 
 int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t stream) {
   const Layout& L = *c.layout;
-  const Plan p = plan(L, c.n_lanes, c.envs, c.T, c.entropy != 0);
+  const Plan p = plan(L, c.n_lanes, c.envs, c.T, c.entropy != 0, c.fp16 != 0);
   if (!ws || ws_bytes < p.total) return set_error(FDR_ERR_WORKSPACE, "impala workspace too small");
   if (c.n_lanes == 0) return FDR_OK;
   char* w = static_cast<char*>(ws);
@@ -883,8 +851,14 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
   a.dbg = g_dbg;
   double* n2 = reinterpret_cast<double*>(w + p.n2);
 
-  hipLaunchKernelGGL(prep_kernel, dim3(p.nblk, c.n_lanes), dim3(kPrepThreads), 0, stream, L, c.lanes,
-                     const_cast<float*>(a.pack), n2);
+  hipLaunchKernelGGL(prep_kernel<float>, dim3(p.nblk, c.n_lanes), dim3(kPrepThreads), 0, stream, L, c.lanes,
+                     const_cast<float*>(a.pack), n2, 0);
+  if (c.fp16) {
+    a.hpack = reinterpret_cast<_Float16*>(w + p.hpack);
+    a.hpack_stride = L.hpack;
+    hipLaunchKernelGGL(prep_kernel<_Float16>, dim3((int)((L.hpack + kPrepSpan - 1) / kPrepSpan), c.n_lanes),
+                       dim3(kPrepThreads), 0, stream, L, c.lanes, a.hpack, n2, 1);
+  }
   const int64_t ne = (int64_t)c.n_lanes * c.envs;
   hipLaunchKernelGGL(init_kernel, dim3((unsigned)((ne * kHid + 255) / 256)), dim3(256), 0, stream, ne, a.h, a.c,
                      a.rprev, a.ret, a.ent);
@@ -905,14 +879,14 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
   return check_launch("impala finish");
 }
 
-int64_t forward_workspace_bytes(const Layout& L, int n_envs) {
-  const Plan p = plan(L, 1, std::max(n_envs, 0), 0, false);
+int64_t forward_workspace_bytes(const Layout& L, int n_envs, bool fp16) {
+  const Plan p = plan(L, 1, std::max(n_envs, 0), 0, false, fp16);
   return p.total;
 }
 
 int launch_forward(const ForwardCall& c, void* ws, int64_t ws_bytes, hipStream_t stream) {
   const Layout& L = *c.layout;
-  const Plan p = plan(L, 1, c.n_envs, 0, false);
+  const Plan p = plan(L, 1, c.n_envs, 0, false, c.fp16 != 0);
   if (!ws || ws_bytes < p.total) return set_error(FDR_ERR_WORKSPACE, "impala forward workspace too small");
   if (c.n_envs == 0) return FDR_OK;
   char* w = static_cast<char*>(ws);
@@ -933,10 +907,21 @@ int launch_forward(const ForwardCall& c, void* ws, int64_t ws_bytes, hipStream_t
   a.probs = c.probs;
   a.reward_in = c.reward;
   a.notdone = c.notdone;
-  hipLaunchKernelGGL(prep_kernel, dim3(p.nblk, 1), dim3(kPrepThreads), 0, stream, L, lanes,
-                     const_cast<float*>(a.pack), reinterpret_cast<double*>(w + p.n2));
-  hipLaunchKernelGGL(conv_kernel, dim3((c.n_envs + 7) / 8 * 8), dim3(kConvThreads), 0, stream, L, a);
-  hipLaunchKernelGGL((core_kernel<1, kForward>), dim3(c.n_envs), dim3(kCoreThreads), 0, stream, L, a);
+  hipLaunchKernelGGL(prep_kernel<float>, dim3(p.nblk, 1), dim3(kPrepThreads), 0, stream, L, lanes,
+                     const_cast<float*>(a.pack), reinterpret_cast<double*>(w + p.n2), 0);
+  if (c.fp16) {
+    a.hpack = reinterpret_cast<_Float16*>(w + p.hpack);
+    a.hpack_stride = 0;
+    hipLaunchKernelGGL(prep_kernel<_Float16>, dim3((int)((L.hpack + kPrepSpan - 1) / kPrepSpan), 1),
+                       dim3(kPrepThreads), 0, stream, L, lanes, a.hpack, reinterpret_cast<double*>(w + p.n2), 1);
+  }
+  if (c.fp16) {
+    hipLaunchKernelGGL(conv_kernel_h, dim3((c.n_envs + 7) / 8 * 8), dim3(kHThreads), 0, stream, L, a);
+    hipLaunchKernelGGL((core_kernel_h<1, kForward>), dim3(c.n_envs), dim3(kCoreThreads), 0, stream, L, a);
+  } else {
+    hipLaunchKernelGGL(conv_kernel, dim3((c.n_envs + 7) / 8 * 8), dim3(kConvThreads), 0, stream, L, a);
+    hipLaunchKernelGGL((core_kernel<1, kForward>), dim3(c.n_envs), dim3(kCoreThreads), 0, stream, L, a);
+  }
   return check_launch("impala forward");
 }
 

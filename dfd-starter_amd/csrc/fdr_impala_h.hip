@@ -1,0 +1,553 @@
+// fdr_impala_h.hip -- fp16 mode of the ImpalaPolicy path (BASELINE config 5: "impala policy fp16
+// rollouts").  Same network and step structure as fdr_impala.hip; what changes:
+//   * weights: theta' (computed in f32, bit-exact) rounded once to f16 into the half pack;
+//   * conv stack: activations f16 in LDS, HWC layout, v_mfma_f32_16x16x32_f16 with f32 accumulation;
+//     BN / bias / ReLU / residual adds in f32, rounded to f16 when stored;
+//   * fc + LSTM: f16 weights streamed (half the HBM bytes), f32 activations and accumulation.
+// Orientation: the WEIGHTS are the MFMA A operand (16 output channels x 32 K), the pixels the B
+// operand (32 K x 16 pixels), so a lane's 4 results are 4 consecutive channels of one pixel -> one
+// 8-byte LDS store, and one 16-byte pixel fragment feeds both output-channel tiles.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cmath>
+
+#include "fdr_impala.h"
+
+namespace fdr {
+namespace impala {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// pixel stride (halves) of an MFMA input image: +8 halves keeps the 16 lanes of a fragment read on
+// disjoint banks (48 B / 80 B pixel pitch); the frame image keeps its 4 channel slots
+template <int C>
+struct Pix {
+  static constexpr int CS = C == 3 ? 4 : C + 8;
+};
+
+constexpr int kHGuard = 832;  // halves: one padded row of the widest image (34 * 24) + slack
+constexpr int kBR1 = 33, kBR2 = 17, kBR3 = 17;   // entry-conv band heights (conv rows) per stage
+// region offsets (halves) inside R = lds_h + kHGuard  (DESIGN.md "fp16 mode")
+constexpr int kFrame = 66 * 66 * 4;              // stage-1 input image [66][66][4]
+constexpr int kT1 = 34 * 34 * Pix<16>::CS;       // stage-1 res / stage-2 entry input [34][34][24]
+constexpr int kT2 = 18 * 18 * Pix<32>::CS;       // stage-2 res / stage-3 entry input [18][18][40]
+constexpr int kS1 = kFrame;                       // S1 [33][64][16] after the frame
+constexpr int kX1 = kS1 + kBR1 * 64 * 16;         // X1 [32][32][16]
+constexpr int kS2 = kT1;                          // S2 [17][32][32] after T1
+constexpr int kX2 = kS2 + kBR2 * 32 * 32;         // X2 [16][16][32] (over the dead X1)
+constexpr int kS3 = kT2;                          // S3 [17][16][32] after T2
+constexpr int kX3 = kS3 + kBR3 * 16 * 32;         // X3 [8][8][32]
+constexpr int kRegion = kX1 + 32 * 32 * 16;       // max extent
+static_assert(kT1 <= kX1 && kX2 + 16 * 16 * 32 <= kRegion && kX3 + 8 * 8 * 32 <= kX2, "fp16 LDS plan");
+constexpr int kHLdsBytes = (kHGuard + kRegion) * 2 + 2 * kBnTab * 4;
+static_assert(kHLdsBytes <= 160 * 1024, "fp16 conv LDS");
+
+// ---- conv on f16 MFMA ---------------------------------------------------------------------------
+template <int CIN>
+struct KSteps {
+  static constexpr int N = CIN == 3 ? 2 : (9 * CIN + 31) / 32;
+};
+
+// A fragments of one conv for ALL output-channel tiles: af[s][nt] (4 VGPRs each)
+template <int CIN, int NT>
+__device__ __forceinline__ void load_af(const _Float16* __restrict__ wf, h8 (&af)[KSteps<CIN>::N][NT], int lane) {
+#pragma unroll
+  for (int s = 0; s < KSteps<CIN>::N; ++s)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) af[s][nt] = *reinterpret_cast<const h8*>(wf + (((s * NT + nt) * 64) + lane) * 8);
+}
+
+// offset (halves) of this lane's 8 K-elements of k-step s inside the receptive field of a pixel
+template <int CIN, int CS, int WP>
+__device__ __forceinline__ int k_offset(int s, int g, int part) {
+  int tap;
+  int ch = 0;
+  if (CIN == 3) {
+    tap = 8 * s + 2 * g + part;
+  } else {
+    constexpr int cpg = CIN / 8, tpk = 32 / CIN;
+    tap = s * tpk + g / cpg;
+    ch = 8 * (g % cpg);
+  }
+  if (tap >= 9) tap = 0;  // zero weights: any in-bounds pixel
+  return ((tap / 3) * WP + tap % 3) * CS + ch;
+}
+
+// acc[i][nt] += W(nt) * P(tile q = wave + 8 i) over the whole K; Tin = padded HWC image whose row 0 is
+// the padded row of output row 0 (callers offset it for bands).  Pixel tile = 16 consecutive output
+// pixels (row-major, width W).
+template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT>
+__device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KSteps<CIN>::N][NT],
+                                       f32x4 (&acc)[TPW][NT], int wave, int lane) {
+  constexpr int KS = KSteps<CIN>::N;
+  const int g = lane >> 4;
+  int base[TPW];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    int mt = wave + 8 * i;
+    mt = mt < MT ? mt : MT - 1;
+    const int m = mt * 16 + (lane & 15);
+    base[i] = ((m / W) * WP + (m % W)) * CS;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[i][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if constexpr (CIN == 3) {
+      const int o0 = k_offset<CIN, CS, WP>(s, g, 0), o1 = k_offset<CIN, CS, WP>(s, g, 1);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        const h4 lo = *reinterpret_cast<const h4*>(Tin + base[i] + o0);
+        const h4 hi = *reinterpret_cast<const h4*>(Tin + base[i] + o1);
+        const h8 b = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b, acc[i][nt], 0, 0, 0);
+      }
+    } else {
+      const int o = k_offset<CIN, CS, WP>(s, g, 0);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        const h8 b = *reinterpret_cast<const h8*>(Tin + base[i] + o);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b, acc[i][nt], 0, 0, 0);
+      }
+    }
+  }
+}
+
+// Visit the outputs: f(ch0, m, v4) -- channels ch0 .. ch0+3 of output pixel m
+template <int NT, int TPW, int MT, typename F>
+__device__ __forceinline__ void conv_out_h(const f32x4 (&acc)[TPW][NT], int wave, int lane, F f) {
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int mt = wave + 8 * i;
+    if (mt >= MT) continue;
+    const int m = mt * 16 + (lane & 15);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) f(nt * 16 + 4 * (lane >> 4), m, acc[i][nt]);
+  }
+}
+
+__device__ __forceinline__ h4 to_h4(float a, float b, float c, float d) {
+  return h4{(_Float16)a, (_Float16)b, (_Float16)c, (_Float16)d};
+}
+
+// T <- BN(X) (optionally ReLU): X [H][H][C] f16 -> padded image [H+2][H+2][CS]; BORDER: zero border.
+template <int C, int H, bool RELU, bool BORDER>
+__device__ __forceinline__ void to_padded_h(const _Float16* X, _Float16* T, const float* sc, const float* sh) {
+  constexpr int CS = Pix<C>::CS, WP = H + 2, G = C / 8;
+  for (int i = threadIdx.x; i < H * H * G; i += kHThreads) {
+    const int pix = i / G, cg = i - pix * G, y = pix / H, x = pix % H;
+    const h8 v = *reinterpret_cast<const h8*>(X + pix * C + 8 * cg);
+    h8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float f = fmaf((float)v[k], sc[8 * cg + k], sh[8 * cg + k]);
+      if (RELU) f = relu(f);
+      o[k] = (_Float16)f;
+    }
+    *reinterpret_cast<h8*>(T + ((y + 1) * WP + x + 1) * CS + 8 * cg) = o;
+  }
+  if (BORDER) {
+    const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = threadIdx.x; i < 4 * (H + 1) * G; i += kHThreads) {
+      const int cg = i % G, r = i / G, side = r / (H + 1), k = r - side * (H + 1);
+      const int pix = side == 0 ? k : side == 1 ? (H + 1) * WP + 1 + k : side == 2 ? (k + 1) * WP : k * WP + WP - 1;
+      *reinterpret_cast<h8*>(T + pix * CS + 8 * cg) = z;
+    }
+  }
+}
+
+// Stage entry: X <- maxpool3s2p1(conv3x3(T) + b) in bands of BR conv rows through S [BR][H][COUT]
+// (conv row -1 of band 0 stored as -inf); pool: one thread per (pooled pixel, 8-channel group).
+template <int CIN, int COUT, int H, int BR>
+__device__ __forceinline__ void stage_entry_h(const _Float16* T, _Float16* S, _Float16* X,
+                                              const h8 (&af)[KSteps<CIN>::N][COUT / 16],
+                                              const float* __restrict__ bias, int wave, int lane) {
+  constexpr int CS = Pix<CIN>::CS, WP = H + 2, NT = COUT / 16, MT = BR * H / 16;
+  constexpr int TPW = (MT + 7) / 8, HO = H / 2, PRB = (BR - 1) / 2, G = COUT / 8;
+  float bz[NT][4];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bz[nt][r] = bias[nt * 16 + 4 * (lane >> 4) + r];
+  for (int b = 0; b < H / (BR - 1); ++b) {
+    f32x4 acc[TPW][NT];
+    conv_h<CIN, CS, NT, TPW, H, WP, MT>(T + ((BR - 1) * b - 1) * WP * CS, af, acc, wave, lane);
+    conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
+      const int nt = ch0 >> 4;
+      const bool neg = b == 0 && m < H;  // conv row -1
+      const float ninf = -INFINITY;
+      *reinterpret_cast<h4*>(S + m * COUT + ch0) =
+          neg ? to_h4(ninf, ninf, ninf, ninf)
+              : to_h4(v[0] + bz[nt][0], v[1] + bz[nt][1], v[2] + bz[nt][2], v[3] + bz[nt][3]);
+    });
+    __syncthreads();
+    for (int i = threadIdx.x; i < PRB * HO * G; i += kHThreads) {
+      const int cg = i % G, r = i / G, px = r % HO, pr = r / HO;
+      h8 mx;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) mx[k] = (_Float16)(-INFINITY);
+#pragma unroll
+      for (int dr = 0; dr < 3; ++dr)
+#pragma unroll
+        for (int dc = -1; dc <= 1; ++dc) {
+          const int x = 2 * px + dc;
+          if (x < 0 || x >= H) continue;
+          const h8 v = *reinterpret_cast<const h8*>(S + ((2 * pr + dr) * H + x) * COUT + 8 * cg);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) mx[k] = v[k] > mx[k] ? v[k] : mx[k];
+        }
+      *reinterpret_cast<h8*>(X + ((PRB * b + pr) * HO + px) * COUT + 8 * cg) = mx;
+    }
+    __syncthreads();
+  }
+}
+
+// Two residual blocks; same fusion as the f32 path (fdr_impala.hip res_blocks).  af holds block 0's
+// first conv on entry; T holds relu(bn0(X)) with a zero border.
+template <int C, int H, int LAST>
+__device__ __forceinline__ void res_blocks_h(_Float16* T, _Float16* X, h8 (&af)[KSteps<C>::N][C / 16],
+                                             const _Float16* __restrict__ hp, const float* __restrict__ pk,
+                                             const Layout& L, int stage, const float* bsc, const float* bsh, int wave,
+                                             int lane, const StepArgs& a, int k0, float* __restrict__ out) {
+  constexpr int CS = Pix<C>::CS, WP = H + 2, NT = C / 16, MT = H * H / 16;
+  constexpr int TPW = (MT + 7) / 8;
+  auto tpos = [&](int m) { return ((m / H + 1) * WP + (m % H) + 1) * CS; };
+  const int cl = 4 * (lane >> 4);  // this lane's 4 channels within an output-channel tile
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int i0 = stage * 5 + 1 + 2 * r, i1 = i0 + 1;
+    const int inext = r == 0 ? i1 + 1 : (stage + 1) * 5;
+    // per-lane epilogue constants: bias of both convs, BN after conv0, BN after conv1
+    float b0[NT][4], s1[NT][4], h1[NT][4], b1[NT][4], s2[NT][4], h2[NT][4];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ch = nt * 16 + cl + k;
+        b0[nt][k] = pk[L.conv_b[i0] + ch];
+        b1[nt][k] = pk[L.conv_b[i1] + ch];
+        s1[nt][k] = bsc[i1 * 32 + ch];
+        h1[nt][k] = bsh[i1 * 32 + ch];
+        s2[nt][k] = (r == 1 && LAST) ? 0.f : bsc[inext * 32 + ch];
+        h2[nt][k] = (r == 1 && LAST) ? 0.f : bsh[inext * 32 + ch];
+      }
+    FDR_STAMP(a, k0 + 4 * r);
+    f32x4 acc[TPW][NT];
+    conv_h<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
+    load_af<C, NT>(hp + L.conv_h[i1], af, lane);
+    __syncthreads();  // every wave is done reading T
+    FDR_STAMP(a, k0 + 4 * r + 1);
+    conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
+      const int nt = ch0 >> 4;
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = relu(fmaf(v[k] + b0[nt][k], s1[nt][k], h1[nt][k]));
+      *reinterpret_cast<h4*>(T + tpos(m) + ch0) = to_h4(o[0], o[1], o[2], o[3]);
+    });
+    __syncthreads();
+    FDR_STAMP(a, k0 + 4 * r + 2);
+    conv_h<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
+    __syncthreads();  // every wave is done reading T
+    FDR_STAMP(a, k0 + 4 * r + 3);
+    conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
+      const int nt = ch0 >> 4;
+      const h4 xo = *reinterpret_cast<const h4*>(X + m * C + ch0);
+      float xn[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xn[k] = (float)(_Float16)((v[k] + b1[nt][k]) + (float)xo[k]);
+      if (r == 0) {
+        *reinterpret_cast<h4*>(X + m * C + ch0) = to_h4(xn[0], xn[1], xn[2], xn[3]);
+        float t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = relu(fmaf(xn[k], s2[nt][k], h2[nt][k]));
+        *reinterpret_cast<h4*>(T + tpos(m) + ch0) = to_h4(t[0], t[1], t[2], t[3]);
+      } else if (!LAST) {
+        float t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = fmaf(xn[k], s2[nt][k], h2[nt][k]);
+        *reinterpret_cast<h4*>(T + tpos(m) + ch0) = to_h4(t[0], t[1], t[2], t[3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[(ch0 + k) * H * H + m] = relu(xn[k]);  // flatten (C,H,W)
+      }
+    });
+    if (r == 0) load_af<C, NT>(hp + L.conv_h[i1 + 1], af, lane);
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kHLdsBytes];
+  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+  const int lane = (slot / a.envs) * 8 + xcd, e = slot % a.envs;
+  if (lane >= a.n_lanes) return;
+  const int wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const int64_t env = (int64_t)lane * a.envs + e;
+  const float* pk = a.pack + (int64_t)lane * a.pack_stride;
+  const _Float16* hp = a.hpack + (int64_t)lane * a.hpack_stride;
+  float* bsc = reinterpret_cast<float*>(smem);
+  float* bsh = bsc + kBnTab;
+  _Float16* R = reinterpret_cast<_Float16*>(smem + 2 * kBnTab * 4) + kHGuard;
+
+  h8 af3[KSteps<3>::N][1];
+  load_af<3, 1>(hp + L.conv_h[0], af3, ln);
+  FDR_STAMP(a, 0);
+  for (int i = threadIdx.x; i < kBnTab; i += kHThreads) {
+    const int idx = i >> 5, ch = i & 31;
+    const int nch = idx == 0 ? 3 : (idx == 5 ? 16 : (idx < 5 ? 16 : 32));
+    float sc = 0.f, sh = 0.f;
+    if (ch < nch) {
+      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[idx] + ch] : 0.f;
+      const float rv = a.bn_var ? a.bn_var[L.bn_stat[idx] + ch] : 1.f;
+      const float inv = 1.f / sqrtf(rv + kBnEps);
+      sc = pk[L.bn_w[idx] + ch] * inv;
+      sh = pk[L.bn_b[idx] + ch] - rm * sc;
+    }
+    bsc[i] = sc;
+    bsh[i] = sh;
+  }
+  {  // zero the guard + frame image (its border and 4th channel slot stay 0)
+    uint4* z = reinterpret_cast<uint4*>(R - kHGuard);
+    for (int i = threadIdx.x; i < (kHGuard + kFrame) / 8; i += kHThreads) z[i] = uint4{0, 0, 0, 0};
+  }
+  __syncthreads();
+  FDR_STAMP(a, 1);
+
+  // ---- frame -> BN2d(3) -> padded HWC [66][66][4] f16: one thread per 8 consecutive pixels ----
+  {
+    const int w = threadIdx.x;  // 512 threads x 8 pixels = 64 x 64
+    const int y = w >> 3, x0 = (w & 7) * 8;
+    float v[3][8];
+    if (a.frames) {
+      const float* fr = a.frames + env * kFramePix;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = fr[c * 4096 + y * 64 + x0 + j];
+    } else {
+      const uint64_t gid = (uint64_t)(a.lane_offset * a.envs + env);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const uint64_t word = (uint64_t)(c * 512 + w);
+        const uint64_t hb = mix64(a.fkey + ((gid << 32) | ((uint64_t)a.t << 11) | word) * kGolden);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = (float)((uint32_t)(hb >> (8 * j)) & 255u);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      h4 o;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) o[c] = (_Float16)fmaf(v[c][j] / 255.0f, bsc[c], bsh[c]);
+      o[3] = (_Float16)0.f;
+      *reinterpret_cast<h4*>(R + ((y + 1) * 66 + x0 + j + 1) * 4) = o;
+    }
+  }
+  __syncthreads();
+  FDR_STAMP(a, 2);
+
+  // ---- stage 1 ----
+  stage_entry_h<3, 16, 64, kBR1>(R, R + kS1, R + kX1, af3, pk + L.conv_b[0], wave, ln);
+  {
+    h8 af[KSteps<16>::N][1];
+    load_af<16, 1>(hp + L.conv_h[1], af, ln);
+    to_padded_h<16, 32, true, true>(R + kX1, R, bsc + 1 * 32, bsh + 1 * 32);
+    __syncthreads();
+    FDR_STAMP(a, 3);
+    res_blocks_h<16, 32, 0>(R, R + kX1, af, hp, pk, L, 0, bsc, bsh, wave, ln, a, 4, nullptr);
+  }
+  // ---- stage 2 ----
+  {
+    h8 af[KSteps<16>::N][2];
+    load_af<16, 2>(hp + L.conv_h[5], af, ln);
+    FDR_STAMP(a, 12);
+    stage_entry_h<16, 32, 32, kBR2>(R, R + kS2, R + kX2, af, pk + L.conv_b[5], wave, ln);
+  }
+  {
+    h8 af[KSteps<32>::N][2];
+    load_af<32, 2>(hp + L.conv_h[6], af, ln);
+    to_padded_h<32, 16, true, true>(R + kX2, R, bsc + 6 * 32, bsh + 6 * 32);
+    __syncthreads();
+    FDR_STAMP(a, 13);
+    res_blocks_h<32, 16, 0>(R, R + kX2, af, hp, pk, L, 1, bsc, bsh, wave, ln, a, 14, nullptr);
+  }
+  // ---- stage 3 ----
+  {
+    h8 af[KSteps<32>::N][2];
+    load_af<32, 2>(hp + L.conv_h[10], af, ln);
+    FDR_STAMP(a, 22);
+    stage_entry_h<32, 32, 16, kBR3>(R, R + kS3, R + kX3, af, pk + L.conv_b[10], wave, ln);
+  }
+  {
+    h8 af[KSteps<32>::N][2];
+    load_af<32, 2>(hp + L.conv_h[11], af, ln);
+    to_padded_h<32, 8, true, true>(R + kX3, R, bsc + 11 * 32, bsh + 11 * 32);
+    __syncthreads();
+    FDR_STAMP(a, 23);
+    res_blocks_h<32, 8, 1>(R, R + kX3, af, hp, pk, L, 2, bsc, bsh, wave, ln, a, 24, a.feat + env * kFeat);
+  }
+  FDR_STAMP(a, 32);
+}
+
+// ---- core (fc + LSTM + head) with f16 weights ------------------------------------------------------
+template <int E, int MODE>
+__global__ __launch_bounds__(kCoreThreads) void core_kernel_h(Layout L, StepArgs a) {
+  __shared__ float xw[kFeat * E];  // xs [2048][E] -> fc partials [8][256][E] -> gates [x|h][1024][E]
+  __shared__ float cis[kCoreIn * E];
+  __shared__ float hs[kHid * E];
+  __shared__ float logit[E * kMaxAct];
+  const int lane = blockIdx.x, j = threadIdx.x;
+  const float* pk = a.pack + (int64_t)lane * a.pack_stride;
+  const _Float16* hp = a.hpack + (int64_t)lane * a.hpack_stride;
+  const int64_t e0 = (int64_t)lane * E;
+  const int A = a.n_act;
+
+  if constexpr (MODE != kReplay) {
+    for (int k = j; k < kFeat; k += kCoreThreads) {
+      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + k] : 0.f;
+      const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + k] : 1.f;
+      const float sc = pk[L.bn_w[15] + k] * (1.f / sqrtf(rv + kBnEps));
+      const float sh = pk[L.bn_b[15] + k] - rm * sc;
+#pragma unroll
+      for (int e = 0; e < E; ++e) xw[k * E + e] = fmaf(a.feat[(e0 + e) * kFeat + k], sc, sh);
+    }
+    __syncthreads();
+    // fc: thread = (8 columns, one of 8 K-slices of 256 rows); f16 W^T rows, 16 B per lane
+    const int c8 = j & 31, ks = j >> 5;
+    float acc[8][E];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[c][e] = 0.f;
+    const h8* w8 = reinterpret_cast<const h8*>(hp + L.fc_wt_h) + c8;
+#pragma unroll 4
+    for (int k = ks * 256; k < ks * 256 + 256; ++k) {
+      const h8 w = w8[(int64_t)k * (kHid / 8)];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const float x = xw[k * E + e];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[c][e] = fmaf((float)w[c], x, acc[c][e]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int e = 0; e < E; ++e) xw[(ks * kHid + 8 * c8 + c) * E + e] = acc[c][e];
+    __syncthreads();
+    const float bj = pk[L.fc_b + j];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      float y = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) y += xw[(q * kHid + j) * E + e];
+      cis[j * E + e] = relu(y + bj);
+    }
+    if (j < E) {
+      const float r = MODE == kForward ? (a.reward_in ? a.reward_in[e0 + j] : 0.f) : a.rprev[e0 + j];
+      cis[kHid * E + j] = fminf(fmaxf(r, -1.f), 1.f);
+    }
+    if (MODE == kRollout && a.ci) {
+      __syncthreads();
+      float* dst = a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn;
+      for (int i = j; i < kCoreIn * E; i += kCoreThreads) {
+        const int e = i / kCoreIn, k = i - e * kCoreIn;
+        dst[i] = cis[k * E + e];
+      }
+    }
+  } else {
+    const float* src = a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn;
+    for (int i = j; i < kCoreIn * E; i += kCoreThreads) {
+      const int e = i / kCoreIn, k = i - e * kCoreIn;
+      cis[k * E + e] = src[i];
+    }
+  }
+  float cj[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const float nd = (MODE == kForward && a.notdone) ? a.notdone[e0 + e] : 1.f;
+    hs[j * E + e] = nd * a.h[(e0 + e) * kHid + j];
+    cj[e] = nd * a.c[(e0 + e) * kHid + j];
+  }
+  __syncthreads();
+  {  // gates: threads 0..127 stream W_ih^T (x part), 128..255 W_hh^T (h part), 8 columns each
+    const int cg = j & 127, part = j >> 7;
+    float acc[8][E];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[c][e] = 0.f;
+    const int k_lo = part ? kCoreIn : 0, k_n = part ? kHid : kCoreIn;
+    const float* xin = part ? hs : cis;
+    const h8* w8 = reinterpret_cast<const h8*>(hp + L.lstm_wt_h) + cg;
+#pragma unroll 4
+    for (int k = 0; k < k_n; ++k) {
+      const h8 w = w8[(int64_t)(k_lo + k) * (kGates / 8)];
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const float x = xin[k * E + e];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[c][e] = fmaf((float)w[c], x, acc[c][e]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int e = 0; e < E; ++e) xw[(part * kGates + 8 * cg + c) * E + e] = acc[c][e];
+  }
+  __syncthreads();
+  float hj[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    float pre[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int col = g * kHid + j;
+      pre[g] = (xw[col * E + e] + pk[L.lstm_bih + col]) + (xw[(kGates + col) * E + e] + pk[L.lstm_bhh + col]);
+    }
+    const float gi = sigm(pre[0]), gf = sigm(pre[1]), gg = tanhf(pre[2]), go = sigm(pre[3]);
+    cj[e] = gf * cj[e] + gi * gg;
+    hj[e] = go * tanhf(cj[e]);
+    a.h[(e0 + e) * kHid + j] = hj[e];
+    a.c[(e0 + e) * kHid + j] = cj[e];
+  }
+  {
+    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
+    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
+    const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
+    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+#pragma unroll
+    for (int e = 0; e < E; ++e) hs[j * E + e] = fmaf(hj[e], sc, sh);
+  }
+  __syncthreads();
+  if (j < A * E) {  // head in f32 (A x 256, tiny)
+    const int ai = j / E, e = j - ai * E;
+    const float* w = pk + L.head_w + ai * kHid;
+    float s = 0.f;
+    for (int k = 0; k < kHid; ++k) s = fmaf(w[k], hs[k * E + e], s);
+    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
+  }
+  __syncthreads();
+  if (j < E) core_finish<E, MODE>(a, logit, lane, j);
+}
+
+template __global__ void core_kernel_h<1, kRollout>(Layout, StepArgs);
+template __global__ void core_kernel_h<1, kReplay>(Layout, StepArgs);
+template __global__ void core_kernel_h<1, kForward>(Layout, StepArgs);
+template __global__ void core_kernel_h<2, kRollout>(Layout, StepArgs);
+template __global__ void core_kernel_h<2, kReplay>(Layout, StepArgs);
+template __global__ void core_kernel_h<4, kRollout>(Layout, StepArgs);
+template __global__ void core_kernel_h<4, kReplay>(Layout, StepArgs);
+template __global__ void core_kernel_h<8, kRollout>(Layout, StepArgs);
+template __global__ void core_kernel_h<8, kReplay>(Layout, StepArgs);
+
+int conv_h_lds_bytes() { return kHLdsBytes; }
+
+}  // namespace impala
+}  // namespace fdr

@@ -85,7 +85,8 @@ class FrameEnv(object):
     """Synthetic frame env for ImpalaPolicy rollouts (fdr_impala_rollout)."""
     obs_shape = (64, 64, 3)
 
-    def __init__(self, n_act, episode_len=1000, envs_per_lane=4, env_seed=0, entropy=True):
+    def __init__(self, n_act, episode_len=1000, envs_per_lane=4, env_seed=0, entropy=True, fp16=False):
+        self.fp16 = bool(fp16)
         self.act_dim = int(n_act)
         self.episode_len = int(episode_len)
         self.envs_per_lane = int(envs_per_lane)
@@ -95,4 +96,4 @@ class FrameEnv(object):
     def spec(self):
         from fdr import engine
         return engine.ImpalaSpec(self.act_dim, self.envs_per_lane, self.episode_len, entropy=self.entropy,
-                                 env_seed=self.env_seed)
+                                 env_seed=self.env_seed, fp16=self.fp16)

@@ -55,7 +55,7 @@ class RolloutExtras(ctypes.Structure):
 class ImpalaDesc(ctypes.Structure):
     _fields_ = [("n_act", ctypes.c_int32), ("envs_per_lane", ctypes.c_int32), ("episode_len", ctypes.c_int32),
                 ("entropy", ctypes.c_int32), ("env_seed", ctypes.c_uint64), ("n_params", ctypes.c_int64),
-                ("bn_mean", ctypes.c_void_p), ("bn_var", ctypes.c_void_p)]
+                ("bn_mean", ctypes.c_void_p), ("bn_var", ctypes.c_void_p), ("fp16", ctypes.c_int32)]
 
 
 def _load():
@@ -96,7 +96,7 @@ def _load():
         "fdr_impala_workspace_bytes": (I64, [ctypes.POINTER(ImpalaDesc), I32]),
         "fdr_impala_rollout": (ctypes.c_int, [P, ctypes.POINTER(ImpalaDesc), ctypes.POINTER(LanesDesc), I32, U64,
                                               I32, P, P, P, P, P, P, P, I64, P]),
-        "fdr_impala_forward_workspace_bytes": (I64, [I32, I32]),
+        "fdr_impala_forward_workspace_bytes": (I64, [I32, I32, I32]),
         "fdr_impala_profile": (ctypes.c_int, [I32]),
         "fdr_impala_profile_read": (ctypes.c_int, [P]),
         "fdr_impala_debug_clock": (ctypes.c_int, [P]),

@@ -195,9 +195,9 @@ def impala_num_bn_stats():
 class ImpalaSpec(object):
     """Shape of an ImpalaPolicy rollout: A actions, E envs per perturbation, T-step episodes."""
 
-    def __init__(self, n_act, envs_per_lane=1, episode_len=1, entropy=True, env_seed=0):
+    def __init__(self, n_act, envs_per_lane=1, episode_len=1, entropy=True, env_seed=0, fp16=False):
         self.n_act, self.envs_per_lane, self.episode_len = int(n_act), int(envs_per_lane), int(episode_len)
-        self.entropy, self.env_seed = bool(entropy), int(env_seed)
+        self.entropy, self.env_seed, self.fp16 = bool(entropy), int(env_seed), bool(fp16)
         self.n_params = impala_num_params(n_act)
         if self.n_params < 0:
             raise ValueError("n_act out of range")
@@ -210,7 +210,7 @@ class ImpalaSpec(object):
         return _lib.ImpalaDesc(self.n_act, self.envs_per_lane, self.episode_len, 1 if self.entropy else 0,
                                self.env_seed & ((1 << 64) - 1), self.n_params,
                                None if bn_mean is None else bn_mean.data_ptr(),
-                               None if bn_var is None else bn_var.data_ptr())
+                               None if bn_var is None else bn_var.data_ptr(), 1 if self.fp16 else 0)
 
 
 def impala_rollout(spec, lanes, n_lanes, seed, jiggle=True, bn_mean=None, bn_var=None, record=False, out=None,
@@ -256,7 +256,7 @@ def impala_forward(spec, theta, frames, h, c, reward=None, notdone=None, bn_mean
     probs = torch.empty((n, spec.n_act), dtype=torch.float32, device=dev)
     f = torch.empty((n, 2048), dtype=torch.float32, device=dev) if feat else None
     d = spec.desc(bn_mean, bn_var)
-    nb = lib.fdr_impala_forward_workspace_bytes(spec.n_act, n)
+    nb = lib.fdr_impala_forward_workspace_bytes(spec.n_act, n, 1 if spec.fp16 else 0)
     ws = _workspace("impala_fwd", nb, dev)
     check(lib.fdr_impala_forward(None, ctypes.byref(d), _p(theta), n, _p(frames), _p(reward), _p(notdone), _p(h),
                                  _p(c), _p(probs), _p(f), _p(ws), ws.numel(), _stream(dev)), "fdr_impala_forward")

@@ -242,6 +242,9 @@ typedef struct fdr_impala_desc {
   const float* bn_mean;  /* eval-mode BN running stats, modules() order, concatenated:
                             fdr_impala_num_bn_stats() floats; NULL = mean 0 */
   const float* bn_var;   /* NULL = var 1 */
+  int32_t fp16;          /* 1 = fp16 mode (BASELINE config 5): theta' rounded to f16 for the convs, fc and
+                            LSTM; f16 activations in the conv stack on f16 MFMA, f32 accumulation, state
+                            and head (DESIGN.md "fp16 mode"); 0 = f32 throughout */
 } fdr_impala_desc;
 
 /* len(ImpalaPolicy.get_trainable_flat()) for n_act actions; -1 if n_act is out of range. */
@@ -267,7 +270,7 @@ int fdr_impala_rollout(fdr_ctx* ctx, const fdr_impala_desc* desc, const fdr_lane
  * place, probs [n_envs, A] out, feat [n_envs, 2048] out (optional: relu'd conv features).
  * Only desc->n_act, n_params, bn_mean, bn_var are read.
  * workspace: fdr_impala_forward_workspace_bytes(n_act, n_envs) bytes. */
-int64_t fdr_impala_forward_workspace_bytes(int32_t n_act, int32_t n_envs);
+int64_t fdr_impala_forward_workspace_bytes(int32_t n_act, int32_t n_envs, int32_t fp16);
 int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* desc, const float* theta, int32_t n_envs,
                        const float* frames, const float* reward, const float* notdone, float* h,
                        float* c, float* probs, float* feat, void* workspace, int64_t workspace_bytes,

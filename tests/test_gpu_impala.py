@@ -205,3 +205,54 @@ def test_worker_and_learner_fd_step(engine):
     np.testing.assert_allclose(np.linalg.norm(d), upd, rtol=1e-5)
     cos = float(np.dot(d, g) / (np.linalg.norm(d) * np.linalg.norm(g)))   # DSGD ascends g
     assert cos > 1 - 1e-6, cos
+
+
+# ---- fp16 mode (BASELINE config 5): parity against the f32 reference within the fp16 tolerance ------
+F16_RTOL = 2e-2   # "fp16 mode <= 2e-2 relative"
+
+
+def test_fp16_forward_vs_reference_golden(engine, g8):
+    A, P = int(g8["A"]), int(g8["P"])
+    tab = np.random.RandomState(int(g8["table_seed"])).randn(2 ** 22).astype(np.float32)
+    off = int(g8["param_offset"])
+    theta = torch.tensor((tab[off:off + P] * np.float32(0.1)).astype(np.float32), device="cuda")
+    rm = torch.tensor(g8["rm"], device="cuda")
+    rv = torch.tensor(g8["rv"], device="cuda")
+    spec = engine.ImpalaSpec(A, fp16=True)
+    nq, T = g8["frames"].shape[:2]
+    h = torch.zeros(nq, 256, device="cuda")
+    c = torch.zeros(nq, 256, device="cuda")
+    for t in range(T):
+        fr = torch.tensor(g8["frames"][:, t].astype(np.float32), device="cuda")
+        rw = torch.tensor(g8["rewards"][:, t], device="cuda")
+        nd = torch.tensor(1.0 - g8["dones"][:, t].astype(np.float32), device="cuda")
+        probs, feat = engine.impala_forward(spec, theta, fr, h, c, reward=rw, notdone=nd, bn_mean=rm, bn_var=rv,
+                                            feat=True)
+        torch.cuda.synchronize()
+        f = feat.cpu().numpy()
+        scale = np.abs(g8["feat"][:, t]).max()
+        assert np.abs(f - g8["feat"][:, t]).max() <= F16_RTOL * scale
+        np.testing.assert_allclose(h.cpu().numpy(), g8["h"][:, t], atol=F16_RTOL * np.abs(g8["h"][:, t]).max())
+        np.testing.assert_allclose(probs.cpu().numpy(), g8["probs"][:, t], rtol=F16_RTOL)
+
+
+def test_fp16_rollout_first_step_vs_oracle(engine, table):
+    """Step 0 sees identical inputs in both precisions: probabilities within the fp16 tolerance, the
+    theta' norms identical to the f32 path (they come from the same f32 perturbation)."""
+    A, E, T = 6, 2, 3
+    theta = _theta(A)
+    idx = [77, 2_000_000, 3_000_000]
+    sign = [1, -1, 1]
+    dev = "cuda"
+    lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
+                              torch.tensor(np.asarray(idx, np.int64), device=dev),
+                              torch.tensor(np.asarray(sign, np.int8), device=dev), 0.02)
+    out16 = engine.impala_rollout(engine.ImpalaSpec(A, E, T, env_seed=5, fp16=True), lanes, 3, 11, record=True)
+    out32 = engine.impala_rollout(engine.ImpalaSpec(A, E, T, env_seed=5), lanes, 3, 11, record=True)
+    torch.cuda.synchronize()
+    p16 = out16.probs.cpu().numpy()[:, 0]
+    p32 = out32.probs.cpu().numpy()[:, 0]
+    np.testing.assert_allclose(p16, p32, rtol=F16_RTOL)
+    np.testing.assert_array_equal(out16.norm2.cpu().numpy(), out32.norm2.cpu().numpy())
+    assert np.all(np.isfinite(out16.reward.cpu().numpy())) and np.all(np.isfinite(out16.entropy.cpu().numpy()))
+    np.testing.assert_allclose(out16.entropy.cpu().numpy(), out32.entropy.cpu().numpy(), rtol=F16_RTOL)

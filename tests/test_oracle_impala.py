@@ -83,10 +83,12 @@ def test_abi_impala_layout_queries():
     assert _lib.lib.fdr_impala_num_params(15) == oi.num_params(15)
     assert _lib.lib.fdr_impala_num_params(0) == -1
     assert _lib.lib.fdr_impala_num_bn_stats() == oi.num_bn()
-    d = _lib.ImpalaDesc(6, 4, 1000, 1, 0, oi.num_params(6), None, None)
+    d = _lib.ImpalaDesc(6, 4, 1000, 1, 0, oi.num_params(6), None, None, 0)
     nb = _lib.lib.fdr_impala_workspace_bytes(ctypes.byref(d), 1024)
     assert nb > 1024 * oi.num_params(6) * 4                       # the theta' packs at least
-    bad = _lib.ImpalaDesc(6, 3, 10, 0, 0, oi.num_params(6), None, None)   # E = 3 unsupported
+    d16 = _lib.ImpalaDesc(6, 4, 1000, 1, 0, oi.num_params(6), None, None, 1)
+    assert _lib.lib.fdr_impala_workspace_bytes(ctypes.byref(d16), 1024) > nb + 1024 * oi.num_params(6) * 2 * 0.9
+    bad = _lib.ImpalaDesc(6, 3, 10, 0, 0, oi.num_params(6), None, None, 0)   # E = 3 unsupported
     ld = _lib.LanesDesc(1, 0, None, 0, None, None, 0.0, None, 0)
     rc = _lib.lib.fdr_impala_rollout(None, ctypes.byref(bad), ctypes.byref(ld), 1, 0, 0, 1, 1, 1, None, None,
                                      None, 1, 1 << 40, None)

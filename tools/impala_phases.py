@@ -31,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lanes", type=int, default=1024)
     ap.add_argument("--envs", type=int, default=4)
+    ap.add_argument("--fp16", action="store_true")
     args = ap.parse_args()
     A = 6
     P = engine.impala_num_params(A)
@@ -42,7 +43,7 @@ def main():
     lanes = engine.lanes_desc(theta, 0, table, idx, sign, 0.02)
     dbg = torch.zeros(33, dtype=torch.int64).cuda()
     lib.fdr_impala_debug_clock(ctypes.c_void_p(dbg.data_ptr()))
-    spec = engine.ImpalaSpec(A, args.envs, 2, entropy=False)
+    spec = engine.ImpalaSpec(A, args.envs, 2, entropy=False, fp16=args.fp16)
     engine.impala_rollout(spec, lanes, args.lanes, 1)
     torch.cuda.synchronize()
     lib.fdr_impala_debug_clock(None)
