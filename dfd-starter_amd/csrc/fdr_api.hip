@@ -11,6 +11,19 @@
 #include "fdr_internal.h"
 
 namespace fdr {
+namespace atari {
+int64_t num_params(int n_act);
+int64_t workspace_bytes(int n_act, int n_lanes, int envs);
+int64_t forward_workspace_bytes(int n_act, int n);
+int launch_rollout(int n_act, int envs, int T, uint64_t env_seed, const LanesArgs& lanes, int n_lanes, uint64_t seed,
+                   int jiggle, const float* bn_mean, const float* bn_var, double* ret, double* ent, int32_t* steps,
+                   double* norm2, int32_t* actions, float* probs, void* ws, int64_t ws_bytes, hipStream_t stream);
+int launch_forward(int n_act, const float* theta, int n, const float* frames, const float* bn_mean,
+                   const float* bn_var, float* probs, float* feat, void* ws, int64_t ws_bytes, hipStream_t stream);
+}  // namespace atari
+}  // namespace fdr
+
+namespace fdr {
 
 static thread_local std::string g_err;
 
@@ -437,4 +450,47 @@ int fdr_bn_refresh(fdr_ctx* ctx, const fdr_policy_desc* policy, const float* the
   if (!theta || !x || !bn_mean || !bn_var) return set_error(FDR_ERR_INVALID, "NULL pointer");
   if (n < 2) return set_error(FDR_ERR_INVALID, "train-mode BatchNorm needs n >= 2 samples");
   return launch_bn_refresh(policy->n_in, theta, x, n, momentum, bn_mean, bn_var, ws, ws_bytes, (hipStream_t)stream);
+}
+
+// ---- AtariPolicy ---------------------------------------------------------------------------------------
+int64_t fdr_atari_num_params(int32_t n_act) { return atari::num_params(n_act); }
+
+int64_t fdr_atari_workspace_bytes(const fdr_atari_desc* d, int32_t n_lanes) {
+  if (!d || n_lanes < 0) return -1;
+  return atari::workspace_bytes(d->n_act, n_lanes, d->envs_per_lane);
+}
+
+int fdr_atari_rollout(fdr_ctx* ctx, const fdr_atari_desc* d, const fdr_lanes_desc* lanes, int32_t n_lanes,
+                      uint64_t seed, int32_t jiggle, double* ret, double* ent, int32_t* steps, double* norm2,
+                      int32_t* actions, float* probs, void* ws, int64_t ws_bytes, fdr_stream stream) {
+  (void)ctx;
+  if (!d) return set_error(FDR_ERR_INVALID, "atari desc is NULL");
+  const int64_t P = atari::num_params(d->n_act);
+  if (P < 0) return set_error(FDR_ERR_UNSUPPORTED, "n_act must be in 1..32");
+  if (d->n_params != P) return set_error(FDR_ERR_INVALID, "n_params does not match the AtariPolicy layout");
+  const int E = d->envs_per_lane;
+  if (E != 1 && E != 2 && E != 4) return set_error(FDR_ERR_UNSUPPORTED, "envs_per_lane must be 1, 2 or 4");
+  if (d->episode_len <= 0 || d->episode_len >= (1 << 20)) return set_error(FDR_ERR_INVALID, "episode_len out of range");
+  if (!ret || !ent || !steps) return set_error(FDR_ERR_INVALID, "NULL output");
+  LanesArgs la;
+  int rc = lanes_args(lanes, n_lanes, P, &la);
+  if (rc) return rc;
+  return atari::launch_rollout(d->n_act, E, d->episode_len, d->env_seed, la, n_lanes, seed, jiggle, d->bn_mean,
+                               d->bn_var, ret, ent, steps, norm2, actions, probs, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int64_t fdr_atari_forward_workspace_bytes(int32_t n_act, int32_t n) {
+  return n < 0 ? -1 : atari::forward_workspace_bytes(n_act, n);
+}
+
+int fdr_atari_forward(fdr_ctx* ctx, const fdr_atari_desc* d, const float* theta, int32_t n, const float* frames,
+                      float* probs, float* feat, void* ws, int64_t ws_bytes, fdr_stream stream) {
+  (void)ctx;
+  if (!d) return set_error(FDR_ERR_INVALID, "atari desc is NULL");
+  const int64_t P = atari::num_params(d->n_act);
+  if (P < 0) return set_error(FDR_ERR_UNSUPPORTED, "n_act must be in 1..32");
+  if (d->n_params != P) return set_error(FDR_ERR_INVALID, "n_params does not match the AtariPolicy layout");
+  if (!theta || !frames || !probs || n < 0) return set_error(FDR_ERR_INVALID, "NULL pointer / bad n");
+  return atari::launch_forward(d->n_act, theta, n, frames, d->bn_mean, d->bn_var, probs, feat, ws, ws_bytes,
+                               (hipStream_t)stream);
 }

@@ -90,7 +90,8 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); 
 // Softmax, action (argmax / inverse CDF on the counter stream), synthetic reward and return, or the
 // entropy term (replay), or the probabilities (forward), for env e of lane `lane` (thread e < E).
 template <int E, int MODE>
-__device__ __forceinline__ void core_finish(const StepArgs& a, const float* logit, int lane, int j) {
+__device__ __forceinline__ void core_finish(const StepArgs& a, const float* logit, int lane, int j,
+                                            bool step_entropy = false) {
   const int A = a.n_act;
   const int64_t e0 = (int64_t)lane * E;
     const int e = j;
@@ -145,10 +146,30 @@ __device__ __forceinline__ void core_finish(const StepArgs& a, const float* logi
       const int tgt = (int)((mix64(a.rkey + ctr * kGolden) >> 40) % (uint64_t)A);
       const float r = act == tgt ? 1.f : (act == (tgt + 1) % A ? -1.f : 0.f);
       a.ret[ge] += (double)r;
-      a.rprev[ge] = r;
+      if (a.rprev) a.rprev[ge] = r;
       if (a.actions) a.actions[ge * a.T + a.t] = act;
+      if (step_entropy) {  // stateless policies: the mean per-step entropy equals the batched one
+        float tot = 0.f;
+        for (int i = 0; i < A; ++i) tot += p[i];
+        float hh = 0.f;
+        for (int i = 0; i < A; ++i) {
+          const float pn = p[i] / tot;
+          const float l = pn > 0.f ? logf(pn) : -FLT_MAX;
+          hh -= pn * l;
+        }
+        a.ent[ge] += (double)hh;
+      }
     }
 }
+
+// shared launch helpers of the pack-based policies (defined in fdr_impala.hip)
+int launch_prep(const Layout& L, const LanesArgs& lanes, float* pack, double* n2_part, int n_lanes,
+                hipStream_t stream);
+int prep_blocks(const Layout& L);
+__global__ void init_kernel(int64_t n_env, float* h, float* c, float* rprev, double* ret, double* ent);
+__global__ void finish_kernel(int n_lanes, int envs, int T, int entropy, int jiggle, uint64_t akey,
+                              int64_t lane_offset, const double* n2_part, int nblk, double* ret,
+                              double* ent, int32_t* steps, double* norm2);
 
 // fp16 mode kernels (fdr_impala_h.hip)
 __global__ void conv_kernel_h(Layout L, StepArgs a);

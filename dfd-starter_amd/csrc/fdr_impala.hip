@@ -171,7 +171,8 @@ __device__ __forceinline__ int64_t section_src(const Section& s, int32_t u) {
   // conv B-fragment (v_mfma_f32_16x16x4_f32): u = (kstep * NT + nt) * 64 + l; B[k][n] with
   // k = 4 * kstep + (l >> 4), n = nt * 16 + (l & 15).  K order: Cin % 4 == 0 -> tap-major,
   // cin = 4 * (kstep % (Cin/4)) + (l >> 4); Cin = 3 -> k = tap * 3 + cin, zero-padded to 28.
-  const int32_t cin = s.a, cout = s.b, nt_n = cout / 16;
+  const int32_t cin = s.a & 255, cout = s.b, nt_n = cout / 16;
+  const int32_t ntaps = (s.a >> 8) ? (s.a >> 8) : 9;  // AtariPolicy convs: 8x8 / 4x4 kernels
   const int32_t ks = u / (nt_n * 64), rem = u - ks * nt_n * 64;
   const int32_t nt = rem >> 6, l = rem & 63;
   const int32_t n = nt * 16 + (l & 15);
@@ -186,7 +187,8 @@ __device__ __forceinline__ int64_t section_src(const Section& s, int32_t u) {
     tap = k / cin;
     ci = k - tap * cin;
   }
-  return (int64_t)s.src + ((int64_t)n * cin + ci) * 9 + tap;
+  if (tap >= ntaps) return -1;
+  return (int64_t)s.src + ((int64_t)n * cin + ci) * ntaps + tap;
 }
 
 template <typename OUT>
@@ -716,8 +718,21 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
 
 __global__ void init_kernel(int64_t n_env, float* h, float* c, float* rprev, double* ret, double* ent) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n_env * kHid) { h[i] = 0.f; c[i] = 0.f; }
-  if (i < n_env) { rprev[i] = 0.f; ret[i] = 0.0; ent[i] = 0.0; }
+  if (h && i < n_env * kHid) { h[i] = 0.f; c[i] = 0.f; }
+  if (i < n_env) {
+    if (rprev) rprev[i] = 0.f;
+    ret[i] = 0.0;
+    ent[i] = 0.0;
+  }
+}
+
+int prep_blocks(const Layout& L) { return (int)((L.pack + kPrepSpan - 1) / kPrepSpan); }
+
+int launch_prep(const Layout& L, const LanesArgs& lanes, float* pack, double* n2_part, int n_lanes,
+                hipStream_t stream) {
+  hipLaunchKernelGGL(prep_kernel<float>, dim3(prep_blocks(L), n_lanes), dim3(kPrepThreads), 0, stream, L, lanes,
+                     pack, n2_part, 0);
+  return check_launch("prep_kernel");
 }
 
 __global__ void finish_kernel(int n_lanes, int envs, int T, int entropy, int jiggle, uint64_t akey,

@@ -12,6 +12,7 @@ into the rollout kernel, so an env here is a *descriptor*: device tensors + shap
       s <- tanh(M s + K a)  (a one-hot for discrete actions);  reward = s[0];  done at t = T.
 * ``TrapEnv`` -- custom_envs/simple_trap_env (environment.py:8-61) on the GPU, integer-exact:
   the reference's walkable bitmap ships as data (custom_envs/simple_trap_env/trap_map.npz).
+* ``StackedFrameEnv`` -- the same hash frames as 4 x 84 x 84 stacks for AtariPolicy (fdr_atari_rollout).
 * ``FrameEnv`` -- the Atari/procgen-shaped workload of BASELINE configs 4/5 for ImpalaPolicy:
   uint8-valued 3x64x64 frames from a counter hash of (env, t, pixel), a +1/-1/0 reward for hitting
   a hashed target action (or its successor), fixed T; ``envs_per_lane`` envs share one theta'.
@@ -97,3 +98,12 @@ class FrameEnv(object):
         from fdr import engine
         return engine.ImpalaSpec(self.act_dim, self.envs_per_lane, self.episode_len, entropy=self.entropy,
                                  env_seed=self.env_seed, fp16=self.fp16)
+
+
+class StackedFrameEnv(FrameEnv):
+    """Synthetic 4 x 84 x 84 frame stacks for AtariPolicy rollouts (fdr_atari_rollout)."""
+    obs_shape = (84, 84, 4)
+
+    def spec(self):
+        from fdr import engine
+        return engine.AtariSpec(self.act_dim, self.envs_per_lane, self.episode_len, env_seed=self.env_seed)

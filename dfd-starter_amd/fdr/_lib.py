@@ -21,7 +21,9 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_impala_rollout", "fdr_impala_forward_workspace_bytes", "fdr_impala_forward",
            "fdr_impala_profile", "fdr_impala_profile_read", "fdr_impala_debug_clock",
            "fdr_strategy_distances", "fdr_rollout_states", "fdr_rollout_ex", "fdr_obs_stats_merge",
-           "fdr_fd_lambda_norms", "fdr_fd_grad_lambda", "fdr_bn_refresh_workspace_bytes", "fdr_bn_refresh")
+           "fdr_fd_lambda_norms", "fdr_fd_grad_lambda", "fdr_bn_refresh_workspace_bytes", "fdr_bn_refresh",
+           "fdr_atari_num_params", "fdr_atari_workspace_bytes", "fdr_atari_rollout",
+           "fdr_atari_forward_workspace_bytes", "fdr_atari_forward")
 
 
 class FDRError(RuntimeError):
@@ -50,6 +52,12 @@ class LanesDesc(ctypes.Structure):
 class RolloutExtras(ctypes.Structure):
     _fields_ = [("states", ctypes.c_void_p), ("obs_mean", ctypes.c_void_p), ("obs_m2", ctypes.c_void_p),
                 ("obs_count", ctypes.c_void_p), ("obs_chance", ctypes.c_float)]
+
+
+class AtariDesc(ctypes.Structure):
+    _fields_ = [("n_act", ctypes.c_int32), ("envs_per_lane", ctypes.c_int32), ("episode_len", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("env_seed", ctypes.c_uint64), ("n_params", ctypes.c_int64),
+                ("bn_mean", ctypes.c_void_p), ("bn_var", ctypes.c_void_p)]
 
 
 class ImpalaDesc(ctypes.Structure):
@@ -86,6 +94,12 @@ def _load():
         "fdr_fd_grad_lambda": (ctypes.c_int, [P, P, I64, P, P, P, P, I32, I64, F32, P, I32, P, P, I64, P]),
         "fdr_bn_refresh_workspace_bytes": (I64, [I32]),
         "fdr_bn_refresh": (ctypes.c_int, [P, ctypes.POINTER(PolicyDesc), P, P, I32, F32, P, P, P, I64, P]),
+        "fdr_atari_num_params": (I64, [I32]),
+        "fdr_atari_workspace_bytes": (I64, [ctypes.POINTER(AtariDesc), I32]),
+        "fdr_atari_rollout": (ctypes.c_int, [P, ctypes.POINTER(AtariDesc), ctypes.POINTER(LanesDesc), I32, U64, I32,
+                                             P, P, P, P, P, P, P, I64, P]),
+        "fdr_atari_forward_workspace_bytes": (I64, [I32, I32]),
+        "fdr_atari_forward": (ctypes.c_int, [P, ctypes.POINTER(AtariDesc), P, I32, P, P, P, P, I64, P]),
         "fdr_fd_weights": (ctypes.c_int, [P, P, I32, F64, I32, I32, P, P, I32, F32, P, P]),
         "fdr_fd_grad_workspace_bytes": (I64, [I32, I64]),
         "fdr_fd_grad": (ctypes.c_int, [P, P, I64, P, P, I32, I64, P, P, I64, P]),

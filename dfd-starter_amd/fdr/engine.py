@@ -354,3 +354,60 @@ def bn_refresh(spec, theta, x, bn_mean, bn_var, momentum=0.1):
     ws = _workspace("vbn", lib.fdr_bn_refresh_workspace_bytes(n), x.device)
     check(lib.fdr_bn_refresh(None, ctypes.byref(pd), _p(theta), _p(x), n, float(momentum), _p(bn_mean), _p(bn_var),
                              _p(ws), ws.numel(), _stream(x.device)), "fdr_bn_refresh")
+
+
+# ---- AtariPolicy (policies/atari.py) -------------------------------------------------------------------
+def atari_num_params(n_act):
+    return int(lib.fdr_atari_num_params(int(n_act)))
+
+
+class AtariSpec(object):
+    def __init__(self, n_act, envs_per_lane=1, episode_len=1, env_seed=0):
+        self.n_act, self.envs_per_lane, self.episode_len = int(n_act), int(envs_per_lane), int(episode_len)
+        self.env_seed = int(env_seed)
+        self.n_params = atari_num_params(n_act)
+        if self.n_params < 0:
+            raise ValueError("n_act out of range")
+
+    def desc(self, bn_mean=None, bn_var=None):
+        _check_dev(bn_mean, bn_var)
+        for t in (bn_mean, bn_var):
+            if t is not None and (t.dtype != torch.float32 or t.numel() != 16 + 32 + 256):
+                raise ValueError("BN stats must be float32[304]")
+        return _lib.AtariDesc(self.n_act, self.envs_per_lane, self.episode_len, 0, self.env_seed & ((1 << 64) - 1),
+                              self.n_params, None if bn_mean is None else bn_mean.data_ptr(),
+                              None if bn_var is None else bn_var.data_ptr())
+
+
+def atari_rollout(spec, lanes, n_lanes, seed, jiggle=True, bn_mean=None, bn_var=None, record=False, device=None):
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    n_env = n_lanes * spec.envs_per_lane
+    out = RolloutResult(torch.empty(n_env, dtype=torch.float64, device=dev),
+                        torch.empty(n_env, dtype=torch.float64, device=dev),
+                        torch.empty(n_env, dtype=torch.int32, device=dev),
+                        torch.empty(n_lanes, dtype=torch.float64, device=dev))
+    out.actions = torch.empty((n_env, spec.episode_len), dtype=torch.int32, device=dev) if record else None
+    out.probs = torch.empty((n_env, spec.episode_len, spec.n_act), dtype=torch.float32, device=dev) if record \
+        else None
+    d = spec.desc(bn_mean, bn_var)
+    nb = lib.fdr_atari_workspace_bytes(ctypes.byref(d), n_lanes)
+    ws = _workspace("atari", nb, dev)
+    check(lib.fdr_atari_rollout(None, ctypes.byref(d), ctypes.byref(lanes), n_lanes,
+                                ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(out.reward),
+                                _p(out.entropy), _p(out.timesteps), _p(out.norm2), _p(out.actions), _p(out.probs),
+                                _p(ws), ws.numel(), _stream(dev)), "fdr_atari_rollout")
+    return out
+
+
+def atari_forward(spec, theta, frames, bn_mean=None, bn_var=None, feat=False):
+    _check_dev(theta, frames)
+    frames = frames.to(torch.float32).reshape(-1, 4 * 84 * 84).contiguous()
+    n = frames.shape[0]
+    dev = theta.device
+    probs = torch.empty((n, spec.n_act), dtype=torch.float32, device=dev)
+    f = torch.empty((n, 2592), dtype=torch.float32, device=dev) if feat else None
+    d = spec.desc(bn_mean, bn_var)
+    ws = _workspace("atari_fwd", lib.fdr_atari_forward_workspace_bytes(spec.n_act, n), dev)
+    check(lib.fdr_atari_forward(None, ctypes.byref(d), _p(theta), n, _p(frames), _p(probs), _p(f), _p(ws), ws.numel(),
+                                _stream(dev)), "fdr_atari_forward")
+    return (probs, f) if feat else probs

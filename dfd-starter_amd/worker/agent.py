@@ -52,9 +52,13 @@ class Agent(object):
         bm, bv = p.bn_stats()
         if p.KIND == "impala":   # one env, one episode of the synthetic frame env
             spec = engine.ImpalaSpec(p.output_shape, 1, self.env.episode_len, entropy=self.env.entropy,
-                                     env_seed=self.env.env_seed)
+                                     env_seed=self.env.env_seed, fp16=getattr(self.env, "fp16", False))
             res = engine.impala_rollout(spec, lanes, 1, self.next_seed(), jiggle=False, bn_mean=bm, bn_var=bv,
                                         device=p.flat.device)
+        elif p.KIND == "atari":
+            spec = engine.AtariSpec(p.output_shape, 1, self.env.episode_len, env_seed=self.env.env_seed)
+            res = engine.atari_rollout(spec, lanes, 1, self.next_seed(), jiggle=False, bn_mean=bm, bn_var=bv,
+                                       device=p.flat.device)
         else:
             res = engine.rollout(p.spec, self.env, lanes, 1, self.next_seed(), jiggle=False, obs_mean=om,
                                  obs_std=osd, bn_mean=bm, bn_var=bv, device=p.flat.device)

@@ -72,11 +72,12 @@ class Worker(object):
         bm, bv = p.bn_stats()
         if seed is None:
             seed = self.agent.next_seed(n)
-        if p.KIND == "impala":
+        if p.KIND in ("impala", "atari"):
             # E envs per lane: returns are per (lane, env), lane-major; idx / sign / norm2 repeat per env
             E = self.agent.env.envs_per_lane
-            res = engine.impala_rollout(self.agent.env.spec(), lanes, n, seed, jiggle=jiggle, bn_mean=bm,
-                                        bn_var=bv, device=p.flat.device)
+            roll = engine.impala_rollout if p.KIND == "impala" else engine.atari_rollout
+            res = roll(self.agent.env.spec(), lanes, n, seed, jiggle=jiggle, bn_mean=bm, bn_var=bv,
+                       device=p.flat.device)
             if E > 1:
                 res.norm2 = res.norm2.repeat_interleave(E)
                 idx_d, sign_d = idx_d.repeat_interleave(E), sign_d.repeat_interleave(E)
@@ -153,7 +154,7 @@ class Worker(object):
         """compute_novelty of every lane's (perturbed) policy, worker.py:53, batched on the device
         (f64 [n]); None without a strategy handler."""
         h = self.strategy_handler
-        if h is None or self.policy.KIND == "impala":
+        if h is None or self.policy.KIND in ("impala", "atari"):
             return None
         return h.lane_novelty(self.noise_source.device_table(self.policy.flat.device), idx_d, sign_d, self.sigma)
 
@@ -162,7 +163,7 @@ class Worker(object):
         save_states=True) -> host f32 [T, n_in].  Every eval episode of an epoch starts from reset
         with theta and deterministic actions, so one recorded lane serves all of them."""
         p = self.policy
-        if p.KIND == "impala":
+        if p.KIND in ("impala", "atari"):
             return None
         dev = p.flat.device
         T = self.agent.env.episode_len

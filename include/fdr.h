@@ -264,6 +264,32 @@ int fdr_impala_rollout(fdr_ctx* ctx, const fdr_impala_desc* desc, const fdr_lane
                        int32_t* steps, double* norm2, int32_t* actions, float* probs, void* workspace,
                        int64_t workspace_bytes, fdr_stream stream);
 
+/* ---- AtariPolicy (policies/atari.py:7-51) on the synthetic stacked-frame env ------------
+ * 4 x 84 x 84 counter-hash frames (oracle/atari.py), the reward of the Impala frame env; conv 8x8 s4 and
+ * 4x4 s2 on f32 MFMA with BN + ReLU in LDS, fc 2592 -> 256 + BN1d + ReLU + head per lane.
+ * bn_mean / bn_var: running stats [16 | 32 | 256] (NULL = 0 / 1).  Outputs as fdr_impala_rollout;
+ * entropy = mean per-step Categorical entropy (stateless policy).  envs_per_lane in {1, 2, 4}. */
+typedef struct fdr_atari_desc {
+  int32_t n_act;
+  int32_t envs_per_lane;
+  int32_t episode_len;
+  int32_t reserved;
+  uint64_t env_seed;
+  int64_t n_params;       /* must equal fdr_atari_num_params(n_act) */
+  const float* bn_mean;
+  const float* bn_var;
+} fdr_atari_desc;
+int64_t fdr_atari_num_params(int32_t n_act);
+int64_t fdr_atari_workspace_bytes(const fdr_atari_desc* desc, int32_t n_lanes);
+int fdr_atari_rollout(fdr_ctx* ctx, const fdr_atari_desc* desc, const fdr_lanes_desc* lanes, int32_t n_lanes,
+                      uint64_t seed, int32_t jiggle, double* ret, double* ent, int32_t* steps, double* norm2,
+                      int32_t* actions, float* probs, void* workspace, int64_t workspace_bytes, fdr_stream stream);
+/* AtariPolicy.forward for n frames [n, 4, 84, 84] (f32, raw 0..255 as the reference feeds them):
+ * probs [n, A]; feat [n, 2592] optional.  workspace: fdr_atari_forward_workspace_bytes(n_act, n). */
+int64_t fdr_atari_forward_workspace_bytes(int32_t n_act, int32_t n);
+int fdr_atari_forward(fdr_ctx* ctx, const fdr_atari_desc* desc, const float* theta, int32_t n, const float* frames,
+                      float* probs, float* feat, void* workspace, int64_t workspace_bytes, fdr_stream stream);
+
 /* One step of ImpalaPolicy.forward (policies/impala.py:18-19, 144-186) for n_envs independent
  * envs sharing theta [P]: frames [n_envs, 3, 64, 64] f32 (0..255), reward [n_envs] (NULL = 0),
  * notdone [n_envs] (NULL = 1; multiplies the incoming state), h / c [n_envs, 256] updated in

@@ -516,9 +516,46 @@ def g10_welford():
     save("g10_welford.npz", **out)
 
 
+def g11_atari():
+    """AtariPolicy (policies/atari.py:7-51): normc init fingerprint (policy.py:88-115 over conv, BN and
+    linear weights) and eval-mode forwards.  The reference's Policy.forward views non-tensor input with
+    a tuple input_shape (policy.py:27-28), which torch rejects, so the forward is fed tensors."""
+    from policies import AtariPolicy
+    A = 6
+    torch.manual_seed(124)
+    pol = AtariPolicy((84, 84), A, seed=124)
+    flat = pol.get_trainable_flat().copy()
+    P = flat.size
+    rs = np.random.RandomState(11)
+    # forward at the (normc) init theta: every layer with a weight is normc'd and its bias zeroed, so
+    # theta depends on RandomState(seed) only and the oracle can rebuild it
+    bns = [m for m in pol.model if isinstance(m, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d))]
+    nbn = sum(m.num_features for m in bns)
+    scale = np.concatenate([np.full(16, 3e3), np.full(32, 3e2), np.full(256, 1.0)]).astype(np.float32)
+    rm = (rs.randn(nbn) * scale).astype(np.float32)
+    rv = ((1.0 + rs.rand(nbn)) * scale * scale).astype(np.float32)
+    off = 0
+    with torch.no_grad():
+        for m in bns:
+            n = m.num_features
+            m.running_mean.copy_(torch.as_tensor(rm[off:off + n]))
+            m.running_var.copy_(torch.as_tensor(rv[off:off + n]))
+            off += n
+    frames = rs.randint(0, 256, size=(5, 4, 84, 84)).astype(np.float32)
+    feats = []
+    hook = pol.model[7].register_forward_hook(lambda mod, inp, out: feats.append(inp[0].detach().clone()))
+    with torch.no_grad():
+        probs = pol.forward(torch.as_tensor(frames)).numpy()
+    hook.remove()
+    save("g11_atari.npz", A=np.array(A), P=np.array(P), init_sha=np.array(sha(flat)), init_head=flat[:64],
+         init_tail=flat[-64:], init_sum=np.array(float(np.float64(flat).sum())), rm=rm, rv=rv,
+         frames=frames.astype(np.uint8), probs=probs, feat=feats[0].numpy(),
+         param_shapes=np.array([str(tuple(p.shape)) for p in pol.parameters()]))
+
+
 GENERATORS = {"g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
               "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g8": g8_impala,
-              "g9": g9_novelty, "g10": g10_welford}
+              "g9": g9_novelty, "g10": g10_welford, "g11": g11_atari}
 
 if __name__ == "__main__":
     torch.set_num_threads(1)
