@@ -28,6 +28,12 @@ namespace fdr {
 
 constexpr int kLanesPerBlock = 4;
 
+#ifdef FDR_PHASE_STAMPS
+// diagnostics build only (make stamps): s_memtime cycles per step phase of wave 0 of block 0
+// -- policy L1, L2, head, action, env -- summed over the episode (tools/rollout_phases.py)
+__device__ unsigned long long g_phase_stamps[5];
+#endif
+
 __host__ __device__ constexpr int round4(int x) { return (x + 3) / 4 * 4; }
 
 // Flat parameter layout = nn.Module.parameters() order (policies/policy.py:36-42).
@@ -77,49 +83,138 @@ __device__ __forceinline__ void bn_fold(float w, float b, float rm, float rv, fl
 }
 
 // ---------------------------------------------------------------------------------------------
-// One lane's policy, register resident.  Wave lane j = 16 r + c.
+// One lane's policy, register resident.
+//
+// Matvecs run on packed f32 FMAs (v_pk_fma_f32, two MACs per instruction) over operands that sit
+// in the lane's own registers -- DPP-operand FMAs issue at ~4.7 cycles per wave-instruction on
+// gfx950 (tools/probes/valu_probe.hip) and were the rollout's bottleneck.  Activations cross lanes
+// through a 1 KiB per-wave LDS scratch: one ds_write_b32 per lane, broadcast ds_read_b128 back.
+//
+//   L1 (NIN -> 64)  broadcast input (LDS), lane j: row j of W1 (VGPR pairs, or the per-wave LDS
+//                   tile when NIN > 8; bias folded into the padding column); output j in lane j.
+//   env (M s + K a) the state row-gathered by two permlane swaps, DPP row_newbcast FMAs against
+//                   this lane's row of [M | K] (LDS): no broadcast copy, few VGPRs.
+//   L2 (64 -> 64)   8 x 8 lane blocks: lane (r = j/8, c = j%8) holds W2[8r + pi_c(i)][8c + k]
+//                   (i, k < 8; 64 VGPRs), reads x[8c .. 8c + 7] (two b128), accumulates 8
+//                   partial outputs in 4 packed pairs, then a 3-level reduce-scatter over the 8
+//                   lanes of its half-row (DPP half_mirror, quad xor 2, quad xor 1: 7 adds)
+//                   leaves output 8r + c = j in lane j.  pi_c(i) = c ^ sigma(i),
+//                   sigma = (0 1 2 3 7 6 5 4), is the register order that makes every level send
+//                   the partner exactly the outputs it keeps.
+//   head (64 -> NOUT <= 16)  lane (q = j/16, o = j%16): W3[o][16q .. 16q + 15] against the
+//                   broadcast h[16q ..], then the 4-row all-reduce (two permlane swaps).
 // ---------------------------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+__host__ __device__ constexpr int l2_sigma(int i) { return i < 4 ? i : 11 - i; }
+
+// per-wave LDS scratch for the cross-lane hand-offs of one step (16-B aligned slots)
+// (LDS ops of one wave complete in order, so the step's input x can share h2's slot: it is read
+// before h2 is written, and h2 is read before the next step's x is written)
+struct alignas(16) WaveScratch {
+  float h1[kHidden];
+  union {
+    float x[kWave];  // policy input (+ the 1 of the folded bias column), written by every lane
+    float h2[kHidden];
+  };
+};
+
+template <int N>
+__device__ __forceinline__ void lds_bcast(const float* v, float (&x)[N]) {  // N % 4 == 0
+  const float4* v4 = reinterpret_cast<const float4*>(v);
+#pragma unroll
+  for (int q = 0; q < N / 4; ++q) {
+    const float4 t = v4[q];
+    x[4 * q] = t.x;
+    x[4 * q + 1] = t.y;
+    x[4 * q + 2] = t.z;
+    x[4 * q + 3] = t.w;
+  }
+}
+
+// sum_k w[k] x[k] over a 16-B aligned LDS row (N % 4 == 0), two packed partial sums
+template <int N>
+__device__ __forceinline__ float dot_lds_row(const float* w, const float (&x)[N], float init) {
+  const float4* w4 = reinterpret_cast<const float4*>(w);
+  f2 acc = {init, 0.f};
+#pragma unroll
+  for (int q = 0; q < N / 4; ++q) {
+    const float4 t = w4[q];
+    acc = pk_fma(f2{t.x, t.y}, f2{x[4 * q], x[4 * q + 1]}, acc);
+    acc = pk_fma(f2{t.z, t.w}, f2{x[4 * q + 2], x[4 * q + 3]}, acc);
+  }
+  return acc.x + acc.y;
+}
+
 template <int NIN, int NA, bool DISC>
 struct MlpLane {
   using L = Layout<NIN, NA, DISC>;
+  using Scratch = WaveScratch;
   static constexpr int NOUT = L::NOUT;
-  static constexpr int NQI = (NIN + 15) / 16;  // gathered rows of the input vector
-  // Wide inputs keep W1 in a per-wave LDS tile [k][64] (lane-contiguous, conflict-free
-  // ds_read_b32) instead of NIN persistent VGPRs: keeps the rollout at <= 128 VGPRs.
+  static constexpr int NX = round4(NIN);
+  static constexpr bool kBiasCol = NIN < NX;  // b1 sits in W1 column NIN (input NIN == 1)
+  // Per-wave LDS tile of lane-private weights, float4 chunks laid out [chunk][lane] (conflict-free
+  // b128): W1 row j when NIN > 8 (bias folded into column NIN), then W3[o][16q .. 16q + 15].
+  // Keeping them out of VGPRs leaves room for whole-row loads in flight (<= 128 VGPRs, 4 waves/SIMD);
+  // the W3 chunks are read in the same LDS round trip as the head's input.
   static constexpr bool kW1Lds = NIN > 8;
-  static constexpr int kW1Regs = kW1Lds ? 1 : NIN;
-  static constexpr int kLdsFloats = kW1Lds ? NIN * kWave : 0;
-  float w1[kW1Regs], b1;
-  float* w1s;  // LDS tile (kW1Lds)
-  float w2[kHidden], b2;
-  float w3[16], b3;  // W3[o = c][16 r .. 16 r + 15]
+  static constexpr int kW1Chunks = kW1Lds ? NX / 4 : 0;
+  static constexpr int kTileF4 = (kW1Chunks + 4) * kWave;  // float4 per wave
+  f2 w1[kW1Lds ? 1 : NX / 2];
+  float b1;
+  const float4* tile;  // this lane's column of the tile (chunk m at tile[m * kWave])
+  f2 w2[32];           // w2[p * 8 + k] = (W2[8r + pi_c(2p)][8c + k], W2[8r + pi_c(2p + 1)][8c + k])
+  float b2;
+  float b3;
   float a0, c0, a1, c1, a2, c2;  // discrete: folded BN for input j / hidden unit j
 
   __device__ __forceinline__ void load(ParamSrc& src, int j, const float* bn_mean,
-                                       const float* bn_var, float* lds_tile) {
-    const int o = j & 15, r = j >> 4;
-    w1s = lds_tile;
+                                       const float* bn_var, float4* lds_tile) {
+    const int r = j >> 3, c = j & 7, o = j & 15, q = j >> 4;
+    tile = lds_tile + j;
+    float4* my = lds_tile + j;
+    auto w1v = [&](int k) {
+      return k < NIN ? src.get(L::L1W + (int64_t)j * NIN + k) : (k == NIN ? src.get(L::L1B + j) : 0.f);
+    };
     if constexpr (kW1Lds) {
 #pragma unroll
-      for (int k = 0; k < NIN; ++k) w1s[k * kWave + j] = src.get(L::L1W + (int64_t)j * NIN + k);
-      wave_lds_sync();
+      for (int m = 0; m < kW1Chunks; ++m) {
+        const float e0 = w1v(4 * m), e1 = w1v(4 * m + 1), e2 = w1v(4 * m + 2), e3 = w1v(4 * m + 3);
+        my[m * kWave] = float4{e0, e1, e2, e3};
+      }
     } else {
 #pragma unroll
-      for (int k = 0; k < NIN; ++k) w1[k] = src.get(L::L1W + (int64_t)j * NIN + k);
+      for (int p = 0; p < NX / 2; ++p) {
+        const float e0 = w1v(2 * p), e1 = w1v(2 * p + 1);
+        w1[p] = f2{e0, e1};
+      }
     }
-    b1 = src.get(L::L1B + j);
+    b1 = kBiasCol ? 0.f : src.get(L::L1B + j);
 #pragma unroll
-    for (int k = 0; k < kHidden; ++k) w2[k] = src.get(L::L2W + (int64_t)j * kHidden + k);
+    for (int p = 0; p < 4; ++p) {
+      const int row0 = 8 * r + (c ^ l2_sigma(2 * p)), row1 = 8 * r + (c ^ l2_sigma(2 * p + 1));
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        w2[p * 8 + k] = f2{src.get(L::L2W + (int64_t)row0 * kHidden + 8 * c + k),
+                           src.get(L::L2W + (int64_t)row1 * kHidden + 8 * c + k)};
+    }
     b2 = src.get(L::L2B + j);
     if (o < NOUT) {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) w3[k] = src.get(L::L3W + (int64_t)o * kHidden + 16 * r + k);
-      b3 = r == 0 ? src.get(L::L3B + o) : src.get_nocount(L::L3B + o);
+      for (int m = 0; m < 4; ++m) {
+        const int64_t base = L::L3W + (int64_t)o * kHidden + 16 * q + 4 * m;
+        const float e0 = src.get(base), e1 = src.get(base + 1), e2 = src.get(base + 2), e3 = src.get(base + 3);
+        my[(kW1Chunks + m) * kWave] = float4{e0, e1, e2, e3};
+      }
+      b3 = q == 0 ? src.get(L::L3B + o) : src.get_nocount(L::L3B + o);
     } else {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) w3[k] = 0.f;
+      for (int m = 0; m < 4; ++m) my[(kW1Chunks + m) * kWave] = float4{0.f, 0.f, 0.f, 0.f};
       b3 = 0.f;
     }
+    wave_lds_sync();
     a0 = c0 = a1 = c1 = a2 = c2 = 0.f;
     if constexpr (DISC) {
       if (j < NIN) {
@@ -147,34 +242,100 @@ struct MlpLane {
     }
   }
 
-  // Both hidden layers and the head: returns the head pre-activation for output o = j & 15
-  // (identical in the 4 rows).  X = row all-gather of the policy input.
-  __device__ __forceinline__ float forward(const float (&X)[NQI], int j) const {
-    float z;
+  // First hidden layer of unit j from the row all-gather X of the input (fdr_wave.h): every MAC a
+  // DPP row_newbcast FMA against the lane's W1 row -- no broadcast copy of the input.
+  static constexpr int NQI = (NIN + 15) / 16;
+  __device__ __forceinline__ float layer1_dpp(const float (&X)[NQI]) const {
+    float w[NX];
     if constexpr (kW1Lds) {
-      float wt[NIN];
 #pragma unroll
-      for (int k = 0; k < NIN; ++k) wt[k] = w1s[k * kWave + j];
-      z = dot_gathered<NIN>(X, wt, b1);
+      for (int q = 0; q < NX / 4; ++q) {
+        const float4 t = tile[q * kWave];
+        w[4 * q] = t.x;
+        w[4 * q + 1] = t.y;
+        w[4 * q + 2] = t.z;
+        w[4 * q + 3] = t.w;
+      }
     } else {
-      z = dot_gathered<NIN>(X, w1, b1);
+#pragma unroll
+      for (int p = 0; p < NX / 2; ++p) {
+        w[2 * p] = w1[p].x;
+        w[2 * p + 1] = w1[p].y;
+      }
     }
-    float h;
+    const float z = dot_gathered<NIN>(X, w, kBiasCol ? w[NIN] : b1);
     if constexpr (DISC) {
-      h = fmaf(fmaxf(z, 0.f), a1, c1);
+      return fmaf(fmaxf(z, 0.f), a1, c1);
     } else {
-      h = tanh_fast(z);
+      return tanh_fast(z);
     }
-    float Hq[4];
-    row_allgather<4>(h, Hq);
-    z = dot_gathered<kHidden>(Hq, w2, b2);
+  }
+
+  // First hidden layer of unit j against the broadcast input xs (xs[NIN] == 1 picks up the folded
+  // bias).
+  __device__ __forceinline__ float layer1(const float (&xs)[NX]) const {
+    f2 acc = {b1, 0.f};
+    if constexpr (kW1Lds) {
+#pragma unroll
+      for (int q = 0; q < NX / 4; ++q) {
+        const float4 w = tile[q * kWave];
+        acc = pk_fma(f2{w.x, w.y}, f2{xs[4 * q], xs[4 * q + 1]}, acc);
+        acc = pk_fma(f2{w.z, w.w}, f2{xs[4 * q + 2], xs[4 * q + 3]}, acc);
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < NX / 2; ++p) acc = pk_fma(w1[p], f2{xs[2 * p], xs[2 * p + 1]}, acc);
+    }
+    const float z = acc.x + acc.y;
     if constexpr (DISC) {
-      h = fmaf(fmaxf(z, 0.f), a2, c2);
+      return fmaf(fmaxf(z, 0.f), a1, c1);
     } else {
-      h = tanh_fast(z);
+      return tanh_fast(z);
     }
-    const float y = dot_row16(h, w3, 0.f);  // row r: inputs 16 r .. 16 r + 15 are its own lanes
-    return row_allreduce_sum(y) + b3;
+  }
+
+  // second hidden layer and the head: h = layer-1 output of unit j; returns the head
+  // pre-activation for output o = j & 15 (identical in the 4 rows).
+  template <class Mark>
+  __device__ __forceinline__ float layers23(float h, Scratch* sc, int j, Mark&& mark) const {
+    const int c = j & 7, q = j >> 4;
+    sc->h1[j] = h;
+    wave_lds_sync();
+    float x[8];
+    lds_bcast<8>(sc->h1 + 8 * c, x);
+    f2 acc[4] = {f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) acc[p] = pk_fma(w2[p * 8 + k], f2{x[k], x[k]}, acc[p]);
+    // reduce-scatter over the 8 lanes of the half-row: slot i = acc[i / 2][i % 2]
+    const float q0 = acc[0].x + dpp_mov<kDppHalfMirror>(acc[2].x);
+    const float q1 = acc[0].y + dpp_mov<kDppHalfMirror>(acc[2].y);
+    const float q2 = acc[1].x + dpp_mov<kDppHalfMirror>(acc[3].x);
+    const float q3 = acc[1].y + dpp_mov<kDppHalfMirror>(acc[3].y);
+    const float r0 = q0 + dpp_mov<kDppQuadXor2>(q2);
+    const float r1 = q1 + dpp_mov<kDppQuadXor2>(q3);
+    const float z = (r0 + dpp_mov<kDppQuadXor1>(r1)) + b2;
+    float h2;
+    if constexpr (DISC) {
+      h2 = fmaf(fmaxf(z, 0.f), a2, c2);
+    } else {
+      h2 = tanh_fast(z);
+    }
+    mark(1, h2);
+    sc->h2[j] = h2;
+    wave_lds_sync();
+    const float4* hv = reinterpret_cast<const float4*>(sc->h2 + 16 * q);
+    f2 a3 = {0.f, 0.f}, a4 = {0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float4 u = hv[m], w = tile[(kW1Chunks + m) * kWave];
+      a3 = pk_fma(f2{w.x, w.y}, f2{u.x, u.y}, a3);
+      a4 = pk_fma(f2{w.z, w.w}, f2{u.z, u.w}, a4);
+    }
+    const float out = row_allreduce_sum((a3.x + a3.y) + (a4.x + a4.y)) + b3;
+    mark(2, out);
+    return out;
   }
 
   // Discrete: softmax across the row (o = j & 15 < NA); returns p_o, 0 for o >= NA.
@@ -196,17 +357,20 @@ __global__ __launch_bounds__(64 * kLanesPerBlock) void policy_forward_kernel(
     const float* __restrict__ bn_var, const float* __restrict__ x, float* __restrict__ out0,
     float* __restrict__ out1) {
   using Lane = MlpLane<NIN, NA, DISC>;
-  __shared__ float w1tile[kLanesPerBlock * (Lane::kLdsFloats > 0 ? Lane::kLdsFloats : 1)];
+  __shared__ float4 wtile[kLanesPerBlock * Lane::kTileF4];
+  __shared__ typename Lane::Scratch scratch[kLanesPerBlock];
   const int j = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int lane = blockIdx.x * kLanesPerBlock + wv;
   if (lane >= n_lanes) return;
   ParamSrc src = lanes.src(lane);
   Lane pl;
-  pl.load(src, j, bn_mean, bn_var, w1tile + wv * Lane::kLdsFloats);
-  const float xin = j < NIN ? pl.input_transform(x[(int64_t)lane * NIN + j]) : 0.f;
-  float X[Lane::NQI];
-  row_allgather<Lane::NQI>(xin, X);
-  const float y = pl.forward(X, j);
+  pl.load(src, j, bn_mean, bn_var, wtile + wv * Lane::kTileF4);
+  auto* sc = &scratch[wv];
+  sc->x[j] = j < NIN ? pl.input_transform(x[(int64_t)lane * NIN + j]) : (j == NIN ? 1.f : 0.f);
+  wave_lds_sync();
+  float xb[Lane::NX];
+  lds_bcast<Lane::NX>(sc->x, xb);
+  const float y = pl.layers23(pl.layer1(xb), sc, j, [](int, float) {});
   if constexpr (DISC) {
     const float p = pl.softmax(y, j);
     if (j < NA) out0[(int64_t)lane * NA + j] = p;
@@ -223,23 +387,28 @@ __global__ __launch_bounds__(64 * kLanesPerBlock) void policy_forward_kernel(
 // ---------------------------------------------------------------------------------------------
 // Whole-episode rollout: fdr_rollout
 // ---------------------------------------------------------------------------------------------
-// FEAT bit 0: record visited observations (fdr_rollout_states); bit 1: Welford obs statistics
+// FEAT bit 0: record visited observations (fdr_rollout_states); bit 1: Welford obs statistics;
+// bit 2: observation normalisation (obs_mean / obs_std given)
 template <int NIN, int NA, bool DISC, int ENV, int FEAT>
 __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(RolloutArgs a) {
   using Lane = MlpLane<NIN, NA, DISC>;
-  constexpr int NQI = Lane::NQI;
-  constexpr int MS = (round4(NIN) % 8 == 0) ? round4(NIN) + 4 : round4(NIN);  // M row stride
-  constexpr int KS = round4(NA) + ((round4(NA) % 8 == 0) ? 4 : 0);             // K row stride
-  __shared__ float4 env4[(ENV == FDR_ENV_SYNTH) ? (NIN * MS + NIN * KS + 3) / 4 : 1];
-  __shared__ float w1tile[kLanesPerBlock * (Lane::kLdsFloats > 0 ? Lane::kLdsFloats : 1)];
-  float* envM = reinterpret_cast<float*>(env4);
-  float* envK = envM + NIN * MS;
+  constexpr int NX = Lane::NX;
+  // env rows [M[i] (NX) | K[i] (one column per action)], stride MKS (b128 rows)
+  constexpr int NQI = Lane::NQI;  // row-gathered registers of the input / state
+  constexpr int NMK = NX + round4(NA);
+  constexpr int MKS = NMK % 8 == 0 ? NMK + 4 : NMK;
+  __shared__ float4 env4[(ENV == FDR_ENV_SYNTH) ? NIN * MKS / 4 : 1];
+  __shared__ float4 wtile[kLanesPerBlock * Lane::kTileF4];
+  __shared__ typename Lane::Scratch scratch[kLanesPerBlock];
+  float* envMK = reinterpret_cast<float*>(env4);
 
   const int j = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int lane = blockIdx.x * kLanesPerBlock + wv;
   if constexpr (ENV == FDR_ENV_SYNTH) {
-    for (int e = threadIdx.x; e < NIN * NIN; e += blockDim.x) envM[(e / NIN) * MS + e % NIN] = a.M[e];
-    for (int e = threadIdx.x; e < NIN * NA; e += blockDim.x) envK[(e / NA) * KS + e % NA] = a.K[e];
+    for (int e = threadIdx.x; e < NIN * MKS; e += blockDim.x) {  // padding columns zero (b128 row reads)
+      const int i = e / MKS, k = e % MKS;
+      envMK[e] = k < NIN ? a.M[i * NIN + k] : (k >= NX && k < NX + NA ? a.K[i * NA + k - NX] : 0.f);
+    }
     __syncthreads();  // the only cross-wave hand-off: shared env matrices
   }
   if (lane >= a.n_lanes) return;
@@ -247,11 +416,11 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
   ParamSrc src = a.lanes.src(lane);
   const bool det = a.lanes.deterministic ? a.lanes.deterministic[lane] != 0 : false;
   Lane pl;
-  pl.load(src, j, a.bn_mean, a.bn_var, w1tile + wv * Lane::kLdsFloats);
+  pl.load(src, j, a.bn_mean, a.bn_var, wtile + wv * Lane::kTileF4);
   const double n2 = wave_sum(src.n2);
 
   const int ji = j < NIN ? j : NIN - 1;
-  const bool norm_obs = a.obs_mean != nullptr;
+  constexpr bool norm_obs = (FEAT & 4) != 0;
   const float om = norm_obs ? a.obs_mean[ji] : 0.f;
   const float osd = norm_obs ? a.obs_std[ji] : 1.f;
   auto policy_input = [&](float s) {
@@ -285,13 +454,35 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
   int os_n = 0;
   float os_mean = 0.f, os_m2 = 0.f;
 
+#ifdef FDR_PHASE_STAMPS
+  uint64_t ph_acc[5] = {0, 0, 0, 0, 0};
+  uint64_t ph_last = 0;
+  auto mark = [&](int k, float dep) {
+    uint64_t now;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now) : "v"(dep));
+    if (k >= 0) ph_acc[k] += now - ph_last;
+    ph_last = now;
+  };
+#else
+  auto mark = [](int, float) {};
+#endif
+  // Draw batch starting at step t (lane-parallel), and the normal of step t for action dim o.
+  auto draw = [&](int t) {
+    const int ds = j / kDrawsPerStep, dk = j % kDrawsPerStep;
+    const uint64_t h = hash_ctr(key, ulane, (uint64_t)(t + ds), (uint64_t)dk);
+    rbuf = DISC ? uniform24(h) : normal_bm(h);
+  };
+  auto fetch_z = [&](int t) {
+    return DISC ? 0.f : __shfl(rbuf, (t % kStepsPerBatch) * NA + (o < NA ? o : 0), kWave);
+  };
   for (int t = 0; t < T; ++t) {
+    // The W1 / M / K rows are loop-invariant LDS data; hoisting their loads out of the loop would
+    // pin ~46 more VGPRs (and spill W2).  Keep them per-step reads.
+    asm volatile("" ::: "memory");
+    mark(-1, s);
     const int tb = t % kStepsPerBatch;
-    if (!det && tb == 0) {
-      const int ds = j / kDrawsPerStep, dk = j % kDrawsPerStep;
-      const uint64_t h = hash_ctr(key, ulane, (uint64_t)(t + ds), (uint64_t)dk);
-      rbuf = DISC ? uniform24(h) : normal_bm(h);
-    }
+    if (!det && tb == 0) draw(t);
+    const float zt = fetch_z(t);  // this step's normal for action dim o (continuous)
     if constexpr (FEAT & 1) {  // visited (raw) observations, worker/agent.py:36 / 58-59 (save_states)
       if (j < NIN) a.states[((int64_t)lane * T + t) * NIN + j] = s;
     }
@@ -313,9 +504,30 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
         os_m2 += (delta * delta_n) * (float)cc;
       }
     }
+    // policy input row-gathered into NQI registers (two permlane swaps)
+    auto* sc = &scratch[wv];
+    constexpr bool kSame = !DISC && !norm_obs;  // mujoco: policy input == env state
     float X[NQI];
     row_allgather<NQI>(policy_input(s), X);
-    const float y = pl.forward(X, j);
+    const float h1 = pl.layer1_dpp(X);
+    // env dynamics M s: independent of the action, issued beside the first layer
+    const float* mrow = envMK + ji * MKS;
+    float pre = 0.f;
+    if constexpr (ENV == FDR_ENV_SYNTH) {
+      float S[NQI];
+      if constexpr (kSame) {
+#pragma unroll
+        for (int q = 0; q < NQI; ++q) S[q] = X[q];
+      } else {
+        row_allgather<NQI>(s, S);
+      }
+      float mr[NIN];
+#pragma unroll
+      for (int k = 0; k < NIN; ++k) mr[k] = mrow[k];
+      pre = dot_gathered<NIN>(S, mr, 0.f);
+    }
+    mark(0, h1);
+    const float y = pl.layers23(h1, sc, j, mark);
     int act_d = 0;
     float act_c = 0.f;
     if constexpr (DISC) {
@@ -352,32 +564,19 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
     } else {
       const float th = tanh_fast(y);
       const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
-      eacc += (j < NA) ? __logf(sd) : 0.f;
-      const float z = __shfl(rbuf, tb * NA + (o < NA ? o : 0), kWave);  // normal (t, o)
-      act_c = det ? th : gauss_action(th, sd, z);
+      eacc += (j < NA) ? __builtin_amdgcn_logf(sd) * 0.693147180559945309f : 0.f;  // v_log_f32: sd in [0.1, 1]
+      act_c = det ? th : gauss_action(th, sd, zt);
     }
 
+    mark(3, DISC ? (float)act_d : act_c);
     // ---- env step ----
     if constexpr (ENV == FDR_ENV_SYNTH) {
-      float S[NQI];
-      if (!DISC && !norm_obs) {
-#pragma unroll
-        for (int q = 0; q < NQI; ++q) S[q] = X[q];  // policy input == env state: reuse the gather
-      } else {
-        row_allgather<NQI>(s, S);
-      }
-      const float* mrow = envM + ji * MS;
-      float mr[NIN];
-#pragma unroll
-      for (int k = 0; k < NIN; ++k) mr[k] = mrow[k];
-      float pre = dot_gathered<NIN>(S, mr, 0.f);
       if constexpr (DISC) {
-        pre += envK[ji * KS + act_d];
+        pre += mrow[NX + act_d];
       } else {
-        const float* krow = envK + ji * KS;
         float kr[NA];
 #pragma unroll
-        for (int m = 0; m < NA; ++m) kr[m] = krow[m];
+        for (int m = 0; m < NA; ++m) kr[m] = mrow[NX + m];
         dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in lane m of every row
       }
       s = tanh_fast(pre);
@@ -393,7 +592,12 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
       racc += (double)(col * 7 - prev_x);
       s = trap_obs(j, col, row);
     }
+    mark(4, s);
   }
+#ifdef FDR_PHASE_STAMPS
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int k = 0; k < 5; ++k) g_phase_stamps[k] = ph_acc[k];
+#endif
 
   // ---- epilogue ----
   const double esum = wave_sum((j < NA) ? (double)eacc : 0.0);
@@ -446,13 +650,14 @@ int launch_policy_forward(const PolicyKey& k, const LanesArgs& lanes, int n_lane
 
 template <int NIN, int NA, bool DISC, int ENV>
 static void launch_feat(const RolloutArgs& args, dim3 grid, dim3 block, hipStream_t stream) {
-  const int feat = (args.states ? 1 : 0) | (args.os_mean ? 2 : 0);
+  const int feat = (args.states ? 1 : 0) | (args.os_mean ? 2 : 0) | (args.obs_mean ? 4 : 0);
+#define FDR_FEAT_CASE(F) \
+  case F: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, F>), grid, block, 0, stream, args); break;
   switch (feat) {
-    case 0: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, 0>), grid, block, 0, stream, args); break;
-    case 1: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, 1>), grid, block, 0, stream, args); break;
-    case 2: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, 2>), grid, block, 0, stream, args); break;
-    default: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, 3>), grid, block, 0, stream, args); break;
+    FDR_FEAT_CASE(0) FDR_FEAT_CASE(1) FDR_FEAT_CASE(2) FDR_FEAT_CASE(3)
+    FDR_FEAT_CASE(4) FDR_FEAT_CASE(5) FDR_FEAT_CASE(6) FDR_FEAT_CASE(7)
   }
+#undef FDR_FEAT_CASE
 }
 
 int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream) {
@@ -525,3 +730,10 @@ int launch_obs_stats_merge(const float* mean, const float* m2, const int32_t* co
 }
 
 }  // namespace fdr
+
+#ifdef FDR_PHASE_STAMPS
+extern "C" int fdr_debug_phase_read(unsigned long long* out5) {
+  return hipMemcpyFromSymbol(out5, HIP_SYMBOL(fdr::g_phase_stamps), 5 * sizeof(unsigned long long)) == hipSuccess
+             ? 0 : -1;
+}
+#endif
