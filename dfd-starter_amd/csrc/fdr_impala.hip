@@ -352,11 +352,13 @@ __device__ __forceinline__ void to_padded(const float* X, float* T, const float*
 // The B fragments are loaded by the caller and reused by every band.
 template <int CIN, int COUT, int H, int PLANE, int BR>
 __device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, const float (&bf)[(9 * CIN + 3) / 4],
-                                            const float* __restrict__ bias, int wave, int lane) {
+                                            const float* __restrict__ bias, int wave, int lane, const StepArgs& a,
+                                            int kst) {
   constexpr int WP = H + 2, NT = COUT / 16, MT = BR * H / 16, PRB = (BR - 1) / 2;
   constexpr int TPW = (MT * NT + 7) / 8, HO = H / 2, SW = H + 1;
   static_assert((BR * H) % 16 == 0 && H % (BR - 1) == 0, "band shape");
   const float bn_ = bias[(wave % NT) * 16 + (lane & 15)];
+  uint64_t t_conv = 0, t_pool = 0, t0 = a.dbg ? clock64() : 0;  // diagnostics (fdr_impala_debug_clock)
   for (int i = threadIdx.x; i < COUT * BR; i += kConvThreads) S[i * SW] = -FLT_MAX;
   for (int b = 0; b < H / (BR - 1); ++b) {
     f32x4 acc[TPW];
@@ -366,6 +368,11 @@ __device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, 
       S[(n * BR + r) * SW + 1 + x] = (b == 0 && r == 0) ? -FLT_MAX : v + bn_;
     });
     __syncthreads();
+    if (a.dbg) {
+      const uint64_t t1 = clock64();
+      t_conv += t1 - t0;
+      t0 = t1;
+    }
     for (int i = threadIdx.x; i < COUT * HO; i += kConvThreads) {
       const int ch = i / HO, px = i - ch * HO;
       const float* sc = S + ch * BR * SW + 2 * px;  // columns 2px-1 .. 2px+1 (+1 for the pad column)
@@ -377,6 +384,15 @@ __device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, 
         X[(ch * HO + PRB * b + pr) * HO + px] = fmaxf(fmaxf(hm[2 * pr], hm[2 * pr + 1]), hm[2 * pr + 2]);
     }
     __syncthreads();
+    if (a.dbg) {
+      const uint64_t t1 = clock64();
+      t_pool += t1 - t0;
+      t0 = t1;
+    }
+  }
+  if (a.dbg && blockIdx.x == 0 && threadIdx.x == 0) {  // summed over the bands
+    a.dbg[kst] = t_conv;
+    a.dbg[kst + 1] = t_pool;
   }
 }
 
@@ -506,7 +522,7 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
   FDR_STAMP(a, 2);
 
   // ---- stage 1: conv 3->16 @64x64, pool -> X1 [16][32][32], residual blocks ----
-  stage_entry<3, 16, 64, FPLANE, kBand>(T, T + 3 * FPLANE, X, bf3, pk + L.conv_b[0], wave, ln);
+  stage_entry<3, 16, 64, FPLANE, kBand>(T, T + 3 * FPLANE, X, bf3, pk + L.conv_b[0], wave, ln, a, 40);
   {
     float bf[36];
     load_frag<16, 1>(pk + L.conv_w[1], bf, wave, ln);
@@ -521,7 +537,7 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
     float bf[36];
     load_frag<16, 2>(pk + L.conv_w[5], bf, wave, ln);
     FDR_STAMP(a, 12);
-    stage_entry<16, 32, 32, Plane<32>::P, kBand>(T, T + 16 * Plane<32>::P, X2, bf, pk + L.conv_b[5], wave, ln);
+    stage_entry<16, 32, 32, Plane<32>::P, kBand>(T, T + 16 * Plane<32>::P, X2, bf, pk + L.conv_b[5], wave, ln, a, 48);
   }
   {
     float bf[72];
@@ -537,7 +553,7 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
     float bf[72];
     load_frag<32, 2>(pk + L.conv_w[10], bf, wave, ln);
     FDR_STAMP(a, 22);
-    stage_entry<32, 32, 16, Plane<16>::P, 17>(T, T + 32 * Plane<16>::P, X3, bf, pk + L.conv_b[10], wave, ln);
+    stage_entry<32, 32, 16, Plane<16>::P, 17>(T, T + 32 * Plane<16>::P, X3, bf, pk + L.conv_b[10], wave, ln, a, 56);
   }
   {
     float bf[72];

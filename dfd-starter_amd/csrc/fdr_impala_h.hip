@@ -139,13 +139,25 @@ __device__ __forceinline__ h4 to_h4(float a, float b, float c, float d) {
 template <int C, int H, bool RELU, bool BORDER>
 __device__ __forceinline__ void to_padded_h(const _Float16* X, _Float16* T, const float* sc, const float* sh) {
   constexpr int CS = Pix<C>::CS, WP = H + 2, G = C / 8;
-  for (int i = threadIdx.x; i < H * H * G; i += kHThreads) {
-    const int pix = i / G, cg = i - pix * G, y = pix / H, x = pix % H;
+  static_assert(kHThreads % G == 0, "a thread keeps one 8-channel group");
+  constexpr int PPI = kHThreads / G, NP = H * H, IT = (NP + PPI - 1) / PPI;
+  const int cg = threadIdx.x % G;
+  float scv[8], shv[8];  // this thread's channels: loaded once, not per pixel
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    scv[k] = sc[8 * cg + k];
+    shv[k] = sh[8 * cg + k];
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int pix = threadIdx.x / G + it * PPI;
+    if (NP % PPI != 0 && pix >= NP) break;
+    const int y = pix / H, x = pix % H;
     const h8 v = *reinterpret_cast<const h8*>(X + pix * C + 8 * cg);
     h8 o;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float f = fmaf((float)v[k], sc[8 * cg + k], sh[8 * cg + k]);
+      float f = fmaf((float)v[k], scv[k], shv[k]);
       if (RELU) f = relu(f);
       o[k] = (_Float16)f;
     }
@@ -166,7 +178,8 @@ __device__ __forceinline__ void to_padded_h(const _Float16* X, _Float16* T, cons
 template <int CIN, int COUT, int H, int BR>
 __device__ __forceinline__ void stage_entry_h(const _Float16* T, _Float16* S, _Float16* X,
                                               const h8 (&af)[KSteps<CIN>::N][COUT / 16],
-                                              const float* __restrict__ bias, int wave, int lane) {
+                                              const float* __restrict__ bias, int wave, int lane,
+                                              const StepArgs& a, int kst) {
   constexpr int CS = Pix<CIN>::CS, WP = H + 2, NT = COUT / 16, MT = BR * H / 16;
   constexpr int TPW = (MT + 7) / 8, HO = H / 2, PRB = (BR - 1) / 2, G = COUT / 8;
   float bz[NT][4];
@@ -186,24 +199,32 @@ __device__ __forceinline__ void stage_entry_h(const _Float16* T, _Float16* S, _F
               : to_h4(v[0] + bz[nt][0], v[1] + bz[nt][1], v[2] + bz[nt][2], v[3] + bz[nt][3]);
     });
     __syncthreads();
-    for (int i = threadIdx.x; i < PRB * HO * G; i += kHThreads) {
+    FDR_STAMP(a, kst + 2 * b);  // diagnostics: band b conv + store done
+    // 3x3 / stride-2 max pool, branch-free (the left tap of column 0 is clamped onto column 0,
+    // which the window holds anyway) and fully unrolled so every load of a thread is in flight
+    constexpr int NI = PRB * HO * G, IT = (NI + kHThreads - 1) / kHThreads;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = threadIdx.x + it * kHThreads;
+      if (NI % kHThreads != 0 && i >= NI) break;
       const int cg = i % G, r = i / G, px = r % HO, pr = r / HO;
-      h8 mx;
+      const _Float16* base = S + (2 * pr * H) * COUT + 8 * cg;
+      const int xl = 2 * px > 0 ? 2 * px - 1 : 0;
+      h8 v[9];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) mx[k] = (_Float16)(-INFINITY);
-#pragma unroll
-      for (int dr = 0; dr < 3; ++dr)
-#pragma unroll
-        for (int dc = -1; dc <= 1; ++dc) {
-          const int x = 2 * px + dc;
-          if (x < 0 || x >= H) continue;
-          const h8 v = *reinterpret_cast<const h8*>(S + ((2 * pr + dr) * H + x) * COUT + 8 * cg);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) mx[k] = v[k] > mx[k] ? v[k] : mx[k];
-        }
+      for (int dr = 0; dr < 3; ++dr) {
+        v[3 * dr] = *reinterpret_cast<const h8*>(base + (dr * H + xl) * COUT);
+        v[3 * dr + 1] = *reinterpret_cast<const h8*>(base + (dr * H + 2 * px) * COUT);
+        v[3 * dr + 2] = *reinterpret_cast<const h8*>(base + (dr * H + 2 * px + 1) * COUT);
+      }
+      const h8 m01 = __builtin_elementwise_max(v[0], v[1]), m23 = __builtin_elementwise_max(v[2], v[3]);
+      const h8 m45 = __builtin_elementwise_max(v[4], v[5]), m67 = __builtin_elementwise_max(v[6], v[7]);
+      const h8 mx = __builtin_elementwise_max(
+          __builtin_elementwise_max(__builtin_elementwise_max(m01, m23), __builtin_elementwise_max(m45, m67)), v[8]);
       *reinterpret_cast<h8*>(X + ((PRB * b + pr) * HO + px) * COUT + 8 * cg) = mx;
     }
     __syncthreads();
+    FDR_STAMP(a, kst + 2 * b + 1);  // band b pool done
   }
 }
 
@@ -352,7 +373,7 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
   FDR_STAMP(a, 2);
 
   // ---- stage 1 ----
-  stage_entry_h<3, 16, 64, kBR1>(R, R + kS1, R + kX1, af3, pk + L.conv_b[0], wave, ln);
+  stage_entry_h<3, 16, 64, kBR1>(R, R + kS1, R + kX1, af3, pk + L.conv_b[0], wave, ln, a, 40);
   {
     h8 af[KSteps<16>::N][1];
     load_af<16, 1>(hp + L.conv_h[1], af, ln);
@@ -366,7 +387,7 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
     h8 af[KSteps<16>::N][2];
     load_af<16, 2>(hp + L.conv_h[5], af, ln);
     FDR_STAMP(a, 12);
-    stage_entry_h<16, 32, 32, kBR2>(R, R + kS2, R + kX2, af, pk + L.conv_b[5], wave, ln);
+    stage_entry_h<16, 32, 32, kBR2>(R, R + kS2, R + kX2, af, pk + L.conv_b[5], wave, ln, a, 48);
   }
   {
     h8 af[KSteps<32>::N][2];
@@ -381,7 +402,7 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
     h8 af[KSteps<32>::N][2];
     load_af<32, 2>(hp + L.conv_h[10], af, ln);
     FDR_STAMP(a, 22);
-    stage_entry_h<32, 32, 16, kBR3>(R, R + kS3, R + kX3, af, pk + L.conv_b[10], wave, ln);
+    stage_entry_h<32, 32, 16, kBR3>(R, R + kS3, R + kX3, af, pk + L.conv_b[10], wave, ln, a, 56);
   }
   {
     h8 af[KSteps<32>::N][2];

@@ -309,7 +309,8 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* desc, const float* t
 int fdr_impala_profile(int32_t enable);
 int fdr_impala_profile_read(double* ms);
 /* Diagnostics: subsequent fdr_impala_rollout launches write s_memtime clocks of conv workgroup 0 at
- * 33 phase boundaries into the DEVICE buffer buf (u64[33], overwritten each step); NULL = off. */
+ * its phase boundaries into the DEVICE buffer buf (u64[64]: 33 stage/block boundaries, then the
+ * fp16 entry-conv band boundaries at 40..63; overwritten each step); NULL = off. */
 int fdr_impala_debug_clock(uint64_t* buf);
 
 #ifdef __cplusplus

@@ -41,7 +41,7 @@ def main():
     idx = torch.randint(0, 4096, (args.lanes,), dtype=torch.int64).cuda()
     sign = torch.ones(args.lanes, dtype=torch.int8).cuda()
     lanes = engine.lanes_desc(theta, 0, table, idx, sign, 0.02)
-    dbg = torch.zeros(33, dtype=torch.int64).cuda()
+    dbg = torch.zeros(64, dtype=torch.int64).cuda()
     lib.fdr_impala_debug_clock(ctypes.c_void_p(dbg.data_ptr()))
     spec = engine.ImpalaSpec(A, args.envs, 2, entropy=False, fp16=args.fp16)
     engine.impala_rollout(spec, lanes, args.lanes, 1)
@@ -53,6 +53,17 @@ def main():
     print("conv workgroup 0: %d clocks total" % tot)
     for a, b in zip(order[:-1], order[1:]):
         print("%-28s %9d  %5.1f%%" % (NAMES[b], c[b] - c[a], 100.0 * (c[b] - c[a]) / tot))
+    if not args.fp16:  # f32 kernel: entry conv / pool clocks summed over the bands
+        for st, k0 in enumerate((40, 48, 56)):
+            print("  stage%d entry: conv %7d  pool %7d" % (st + 1, c[k0], c[k0 + 1]))
+    if args.fp16:  # entry-conv bands (fp16 kernel): conv + store, then pool, per band
+        for st, (k0, start, end, nb) in enumerate(((40, 2, 3, 2), (48, 12, 13, 2), (56, 22, 23, 1))):
+            prev = c[start]
+            for b in range(nb):
+                cv, pl = c[k0 + 2 * b], c[k0 + 2 * b + 1]
+                print("  stage%d band%d: conv %7d  pool %7d" % (st + 1, b, cv - prev, pl - cv))
+                prev = pl
+            print("  stage%d bn+relu to padded: %7d" % (st + 1, c[end] - prev))
 
 
 if __name__ == "__main__":
