@@ -185,10 +185,12 @@ template <int E, int MODE>
 __global__ __launch_bounds__(impala::kCoreThreads) void atari_core_kernel(Layout L, Args A) {
   const StepArgs& a = A.s;
   const Offsets& o = A.o;
+  // xs (the conv features) -> fc partials -> BN'd hidden + logits, phases separated by barriers
   __shared__ float xs[kFeat * E];
-  __shared__ float part[4 * kFc * E];
-  __shared__ float hs[kFc * E];
-  __shared__ float logit[E * impala::kMaxAct];
+  float* part = xs;
+  float* hs = xs + 4 * kFc * E;
+  float* logit = hs + kFc * E;
+  static_assert((5 * kFc + impala::kMaxAct) * E <= kFeat * E, "atari core LDS aliasing");
   const int lane = blockIdx.x, j = threadIdx.x;
   const float* pk = a.pack + (int64_t)lane * a.pack_stride;
   const int64_t e0 = (int64_t)lane * E;
@@ -207,7 +209,7 @@ __global__ __launch_bounds__(impala::kCoreThreads) void atari_core_kernel(Layout
   const float4* w4 = reinterpret_cast<const float4*>(pk + o.fcw) + c4;
 #pragma unroll 4
   for (int k = wq * (kFeat / 4); k < (wq + 1) * (kFeat / 4); ++k) {
-    const float4 w = w4[(int64_t)k * (kFc / 4)];
+    const float4 w = impala::ld_stream(w4 + (int64_t)k * (kFc / 4));
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const float x = xs[k * E + e];
@@ -217,6 +219,7 @@ __global__ __launch_bounds__(impala::kCoreThreads) void atari_core_kernel(Layout
       acc[3][e] = fmaf(w.w, x, acc[3][e]);
     }
   }
+  __syncthreads();  // every read of xs is done before the partials overwrite it
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll

@@ -85,6 +85,17 @@ constexpr int kCoreThreads = 256;
 constexpr int kBnTab = 15 * 32;
 
 __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
+
+// Streamed weights of the core kernels: each lane's W^T is read once per step and evicted before the
+// next step needs it (GBs per step), so the loads are non-temporal (measured: f32 core 0.75 -> 0.68 ms,
+// f16 0.41 -> 0.38 ms per step at 1024 lanes x 4 envs).
+template <class T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+  static_assert(sizeof(T) == 16, "16-byte streamed loads");
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+  return __builtin_bit_cast(T, v);
+}
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
 // Softmax, action (argmax / inverse CDF on the counter stream), synthetic reward and return, or the

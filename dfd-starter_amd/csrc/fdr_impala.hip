@@ -576,12 +576,15 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
 
 template <int E, int MODE>
 __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a) {
-  // xw: the BN'd features xs [2048][E] during the fc, then the fc partial sums [4][256][E], then the
-  // LSTM gate pre-activations [1024][E] -- each phase separated by a barrier.
+  // xw: the BN'd features xs [2048][E] during the fc, then the fc partial sums [4][256][E] (first
+  // half), then the LSTM gate pre-activations [1024][E] (first half) -- each phase separated by a
+  // barrier.  The core input, h and the logits live in xw's second half once the features are dead:
+  // 32 KiB per workgroup, so 5 lanes fit a CU and 1024 lanes run in one round (at 41 KiB only 3 did).
   __shared__ float xw[kFeat * E];
-  __shared__ float cis[kCoreIn * E]; // core input, [k][e]
-  __shared__ float hs[kHid * E];     // h (then BN(h')), [k][e]
-  __shared__ float logit[E * kMaxAct];
+  float* cis = xw + kFeat * E / 2;   // core input, [k][e]
+  float* hs = cis + kCoreIn * E;     // h (then BN(h')), [k][e]
+  float* logit = hs + kHid * E;      // [e][kMaxAct]
+  static_assert(kFeat * E / 2 + (kCoreIn + kHid) * E + E * kMaxAct <= kFeat * E, "core LDS aliasing");
   const int lane = blockIdx.x, j = threadIdx.x;
   const float* pk = a.pack + (int64_t)lane * a.pack_stride;
   const int64_t e0 = (int64_t)lane * E;
@@ -607,7 +610,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
     const float4* w4 = reinterpret_cast<const float4*>(pk + L.fc_wt) + c4;
 #pragma unroll 4
     for (int k = wq * (kFeat / 4); k < (wq + 1) * (kFeat / 4); ++k) {
-      const float4 w = w4[(int64_t)k * (kHid / 4)];
+      const float4 w = ld_stream(w4 + (int64_t)k * (kHid / 4));
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const float x = xw[k * E + e];
@@ -668,7 +671,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
     const float4* wl = reinterpret_cast<const float4*>(pk + L.lstm_wt) + j;
 #pragma unroll 4
     for (int k = 0; k < kCoreIn; ++k) {
-      const float4 w = wl[(int64_t)k * (kGates / 4)];
+      const float4 w = ld_stream(wl + (int64_t)k * (kGates / 4));
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const float x = cis[k * E + e];
@@ -680,7 +683,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
     }
 #pragma unroll 4
     for (int k = 0; k < kHid; ++k) {
-      const float4 w = wl[(int64_t)(kCoreIn + k) * (kGates / 4)];
+      const float4 w = ld_stream(wl + (int64_t)(kCoreIn + k) * (kGates / 4));
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const float x = hs[k * E + e];

@@ -417,11 +417,17 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
 
 // ---- core (fc + LSTM + head) with f16 weights ------------------------------------------------------
 template <int E, int MODE>
-__global__ __launch_bounds__(kCoreThreads) void core_kernel_h(Layout L, StepArgs a) {
-  __shared__ float xw[kFeat * E];  // xs [2048][E] -> fc partials [8][256][E] -> gates [x|h][1024][E]
-  __shared__ float cis[kCoreIn * E];
+__global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E <= 4 ? 4 : 1))) void core_kernel_h(
+    Layout L, StepArgs a) {  // E <= 4: <= 128 VGPRs -> 4 lanes per CU (the LDS allows 4)
+  // xw: xs [2048][E] -> fc partials [8][256][E] -> gates [x|h][1024][E], phases separated by
+  // barriers.  The core input lives in xw's second half between the fc and the gate writes, the
+  // logits at xw's start after the gates are consumed: 36 KiB per workgroup -> 4 lanes per CU, so
+  // 1024 lanes run in one round (at 41 KiB only 3 fit).
+  __shared__ float xw[kFeat * E];
   __shared__ float hs[kHid * E];
-  __shared__ float logit[E * kMaxAct];
+  float* cis = xw + kFeat * E / 2;
+  float* logit = xw;
+  static_assert(kCoreIn * E <= kFeat * E / 2 && E * kMaxAct <= kFeat * E, "core LDS aliasing");
   const int lane = blockIdx.x, j = threadIdx.x;
   const float* pk = a.pack + (int64_t)lane * a.pack_stride;
   const _Float16* hp = a.hpack + (int64_t)lane * a.hpack_stride;
@@ -448,7 +454,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_h(Layout L, StepArgs
     const h8* w8 = reinterpret_cast<const h8*>(hp + L.fc_wt_h) + c8;
 #pragma unroll 4
     for (int k = ks * 256; k < ks * 256 + 256; ++k) {
-      const h8 w = w8[(int64_t)k * (kHid / 8)];
+      const h8 w = ld_stream(w8 + (int64_t)k * (kHid / 8));
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const float x = xw[k * E + e];
@@ -463,13 +469,17 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_h(Layout L, StepArgs
       for (int e = 0; e < E; ++e) xw[(ks * kHid + 8 * c8 + c) * E + e] = acc[c][e];
     __syncthreads();
     const float bj = pk[L.fc_b + j];
+    float yv[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       float y = 0.f;
 #pragma unroll
       for (int q = 0; q < 8; ++q) y += xw[(q * kHid + j) * E + e];
-      cis[j * E + e] = relu(y + bj);
+      yv[e] = relu(y + bj);
     }
+    __syncthreads();  // every partial read before cis (inside xw) is written
+#pragma unroll
+    for (int e = 0; e < E; ++e) cis[j * E + e] = yv[e];
     if (j < E) {
       const float r = MODE == kForward ? (a.reward_in ? a.reward_in[e0 + j] : 0.f) : a.rprev[e0 + j];
       cis[kHid * E + j] = fminf(fmaxf(r, -1.f), 1.f);
@@ -509,7 +519,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_h(Layout L, StepArgs
     const h8* w8 = reinterpret_cast<const h8*>(hp + L.lstm_wt_h) + cg;
 #pragma unroll 4
     for (int k = 0; k < k_n; ++k) {
-      const h8 w = w8[(int64_t)(k_lo + k) * (kGates / 8)];
+      const h8 w = ld_stream(w8 + (int64_t)(k_lo + k) * (kGates / 8));
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         const float x = xin[k * E + e];
@@ -517,6 +527,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_h(Layout L, StepArgs
         for (int c = 0; c < 8; ++c) acc[c][e] = fmaf((float)w[c], x, acc[c][e]);
       }
     }
+    __syncthreads();  // every read of cis (inside xw) is done before the gates overwrite it
 #pragma unroll
     for (int c = 0; c < 8; ++c)
 #pragma unroll
