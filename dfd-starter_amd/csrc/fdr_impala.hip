@@ -345,27 +345,34 @@ __device__ __forceinline__ void to_padded(const float* X, float* T, const float*
   }
 }
 
-// Stage entry: X <- maxpool3s2p1(conv3x3(T) + b), in bands of BR conv rows ((BR-1) b - 1 .. (BR-1) b + BR - 2
-// -> pooled rows (BR-1)/2 * b ..) through the scratch S [COUT][BR][1 + H]: column 0 of S is -inf (the
-// pool's left pad) and conv row -1 of band 0 is stored as -inf, so the pool is branch-free and
-// separable -- one thread per (channel, pooled column): BR horizontal max3, then vertical max3.
-// The B fragments are loaded by the caller and reused by every band.
+// Stage entry: X <- maxpool3s2p1(conv3x3(T) + b) in bands of BR-1 new conv rows (8 b .. 8 b + 7 for
+// BR = 9) through the scratch S [COUT][BR][1 + H], a RING of conv rows: conv row g lives in slot
+// (g + 1) mod BR, so a band's pool window (rows 8 b - 1 .. 8 b + 7) is the previous band's last row
+// plus the new ones -- no row is computed twice and every band is (BR-1) H / 16 tiles (a multiple
+// of the 8 waves).  Column 0 of S is -inf (the pool's left pad) and conv row -1 (slot 0 before
+// band 0) is -inf, so the pool is branch-free and separable -- one thread per (channel, pooled
+// column): BR horizontal max3, then vertical max3.  The B fragments are loaded by the caller and
+// reused by every band.
 template <int CIN, int COUT, int H, int PLANE, int BR>
 __device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, const float (&bf)[(9 * CIN + 3) / 4],
                                             const float* __restrict__ bias, int wave, int lane, const StepArgs& a,
                                             int kst) {
-  constexpr int WP = H + 2, NT = COUT / 16, MT = BR * H / 16, PRB = (BR - 1) / 2;
+  constexpr int WP = H + 2, NT = COUT / 16, NR = BR - 1, MT = NR * H / 16, PRB = NR / 2;
   constexpr int TPW = (MT * NT + 7) / 8, HO = H / 2, SW = H + 1;
-  static_assert((BR * H) % 16 == 0 && H % (BR - 1) == 0, "band shape");
+  static_assert((NR * H) % 16 == 0 && H % NR == 0 && NR % 2 == 0, "band shape");
   const float bn_ = bias[(wave % NT) * 16 + (lane & 15)];
   uint64_t t_conv = 0, t_pool = 0, t0 = a.dbg ? clock64() : 0;  // diagnostics (fdr_impala_debug_clock)
-  for (int i = threadIdx.x; i < COUT * BR; i += kConvThreads) S[i * SW] = -FLT_MAX;
-  for (int b = 0; b < H / (BR - 1); ++b) {
+  for (int i = threadIdx.x; i < COUT * BR; i += kConvThreads) S[i * SW] = -FLT_MAX;  // pad column
+  for (int i = threadIdx.x; i < COUT * H; i += kConvThreads)                         // conv row -1
+    S[(i / H) * BR * SW + 1 + i % H] = -FLT_MAX;
+  for (int b = 0; b < H / NR; ++b) {
+    const int rot = (NR * b) % BR;  // slot of conv row NR b - 1
+    auto slot = [&](int r) { return rot + r >= BR ? rot + r - BR : rot + r; };  // conv row NR b - 1 + r
     f32x4 acc[TPW];
-    conv_mfma<CIN, NT, TPW, H, WP, PLANE, MT>(T + ((BR - 1) * b - 1) * WP, bf, acc, wave, lane);
+    conv_mfma<CIN, NT, TPW, H, WP, PLANE, MT>(T + NR * b * WP, bf, acc, wave, lane);
     conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) {
       const int r = m / H, x = m % H;
-      S[(n * BR + r) * SW + 1 + x] = (b == 0 && r == 0) ? -FLT_MAX : v + bn_;
+      S[(n * BR + slot(r + 1)) * SW + 1 + x] = v + bn_;
     });
     __syncthreads();
     if (a.dbg) {
@@ -378,7 +385,10 @@ __device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, 
       const float* sc = S + ch * BR * SW + 2 * px;  // columns 2px-1 .. 2px+1 (+1 for the pad column)
       float hm[BR];
 #pragma unroll
-      for (int r = 0; r < BR; ++r) hm[r] = fmaxf(fmaxf(sc[r * SW], sc[r * SW + 1]), sc[r * SW + 2]);
+      for (int r = 0; r < BR; ++r) {  // conv row NR b - 1 + r
+        const int sl = slot(r);
+        hm[r] = fmaxf(fmaxf(sc[sl * SW], sc[sl * SW + 1]), sc[sl * SW + 2]);
+      }
 #pragma unroll
       for (int pr = 0; pr < PRB; ++pr)
         X[(ch * HO + PRB * b + pr) * HO + px] = fmaxf(fmaxf(hm[2 * pr], hm[2 * pr + 1]), hm[2 * pr + 2]);
