@@ -8,10 +8,9 @@
 //   * theta'_l is built on the fly from theta + sign_l * fl32(sigma * table[idx_l + p])
 //     (bit-exact with worker/worker.py:28) while loading those registers; the same pass
 //     accumulates ||lambda_l||^2 for the learner (learner/finite_differences.py:107).
-//   * Activations cross lanes in registers: a 3-instruction permlane all-gather replicates the
-//     64-vector in every 16-lane row, then every FMA reads its input element through DPP
-//     row_newbcast (fdr_wave.h) -> one VALU op per MAC, no LDS traffic in the T-step loop except
-//     the env matrix rows.
+//   * Activations cross lanes through a 1 KiB per-wave LDS scratch (one ds_write_b32 per lane,
+//     broadcast ds_read_b128 back) feeding packed f32 FMAs, or through DPP row_newbcast where the
+//     input already sits in the caller's 16-lane row (the head, K a).
 //   * The env (synthetic linear-tanh system or the trap gridworld) runs inside the same loop.
 //   * 4 lanes (waves) per 256-thread workgroup, <= 128 VGPRs -> 16 waves/CU: 4096 lanes fill
 //     all 256 CUs in one wave of workgroups.
@@ -92,8 +91,9 @@ __device__ __forceinline__ void bn_fold(float w, float b, float rm, float rv, fl
 //
 //   L1 (NIN -> 64)  broadcast input (LDS), lane j: row j of W1 (VGPR pairs, or the per-wave LDS
 //                   tile when NIN > 8; bias folded into the padding column); output j in lane j.
-//   env (M s + K a) the state row-gathered by two permlane swaps, DPP row_newbcast FMAs against
-//                   this lane's row of [M | K] (LDS): no broadcast copy, few VGPRs.
+//   env (M s + K a) M s in the same pass as L1 over the broadcast input chunks (lane j < NIN: row j
+//                   of M from the block's LDS copy); K a by DPP row_newbcast FMAs once the action
+//                   (lanes 0 .. NA-1 of every row) is known.
 //   L2 (64 -> 64)   8 x 8 lane blocks: lane (r = j/8, c = j%8) holds W2[8r + pi_c(i)][8c + k]
 //                   (i, k < 8; 64 VGPRs), reads x[8c .. 8c + 7] (two b128), accumulates 8
 //                   partial outputs in 4 packed pairs, then a 3-level reduce-scatter over the 8
@@ -101,8 +101,9 @@ __device__ __forceinline__ void bn_fold(float w, float b, float rm, float rv, fl
 //                   leaves output 8r + c = j in lane j.  pi_c(i) = c ^ sigma(i),
 //                   sigma = (0 1 2 3 7 6 5 4), is the register order that makes every level send
 //                   the partner exactly the outputs it keeps.
-//   head (64 -> NOUT <= 16)  lane (q = j/16, o = j%16): W3[o][16q .. 16q + 15] against the
-//                   broadcast h[16q ..], then the 4-row all-reduce (two permlane swaps).
+//   head (64 -> NOUT <= 16)  lane (q = j/16, o = j%16): W3[o][16q .. 16q + 15] against h2[16q + i],
+//                   which sits in lane i of the lane's own row q (DPP row_newbcast FMAs, no LDS round
+//                   trip), then the 4-row all-reduce (two permlane swaps).
 // ---------------------------------------------------------------------------------------------
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -110,15 +111,11 @@ __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elemen
 
 __host__ __device__ constexpr int l2_sigma(int i) { return i < 4 ? i : 11 - i; }
 
-// per-wave LDS scratch for the cross-lane hand-offs of one step (16-B aligned slots)
-// (LDS ops of one wave complete in order, so the step's input x can share h2's slot: it is read
-// before h2 is written, and h2 is read before the next step's x is written)
+// per-wave LDS scratch for the cross-lane hand-offs of one step (16-B aligned slots).  LDS ops of
+// one wave complete in order: a slot is rewritten only after the reads of its previous contents.
 struct alignas(16) WaveScratch {
-  float h1[kHidden];
-  union {
-    float x[kWave];  // policy input (+ the 1 of the folded bias column), written by every lane
-    float h2[kHidden];
-  };
+  float h1[kHidden];  // layer-1 output (L2 input); the env state when it differs from the policy input
+  float x[kWave];     // policy input (+ the 1 of the folded bias column), written by every lane
 };
 
 template <int N>
@@ -242,35 +239,6 @@ struct MlpLane {
     }
   }
 
-  // First hidden layer of unit j from the row all-gather X of the input (fdr_wave.h): every MAC a
-  // DPP row_newbcast FMA against the lane's W1 row -- no broadcast copy of the input.
-  static constexpr int NQI = (NIN + 15) / 16;
-  __device__ __forceinline__ float layer1_dpp(const float (&X)[NQI]) const {
-    float w[NX];
-    if constexpr (kW1Lds) {
-#pragma unroll
-      for (int q = 0; q < NX / 4; ++q) {
-        const float4 t = tile[q * kWave];
-        w[4 * q] = t.x;
-        w[4 * q + 1] = t.y;
-        w[4 * q + 2] = t.z;
-        w[4 * q + 3] = t.w;
-      }
-    } else {
-#pragma unroll
-      for (int p = 0; p < NX / 2; ++p) {
-        w[2 * p] = w1[p].x;
-        w[2 * p + 1] = w1[p].y;
-      }
-    }
-    const float z = dot_gathered<NIN>(X, w, kBiasCol ? w[NIN] : b1);
-    if constexpr (DISC) {
-      return fmaf(fmaxf(z, 0.f), a1, c1);
-    } else {
-      return tanh_fast(z);
-    }
-  }
-
   // First hidden layer of unit j against the broadcast input xs (xs[NIN] == 1 picks up the folded
   // bias).
   __device__ __forceinline__ float layer1(const float (&xs)[NX]) const {
@@ -294,11 +262,48 @@ struct MlpLane {
     }
   }
 
+  // First hidden layer and the env's M s in one pass over the broadcast input chunks (LDS):
+  // returns unit j's activation, sets env = M[j] . x.  Chunks are consumed as they arrive so at most
+  // two are live (VGPR budget: W2 holds 64 of the 128).
+  // ss: the env state's broadcast copy when it differs from the policy input (nullptr: same)
+  template <bool kSameInput>
+  __device__ __forceinline__ float layer1_env_pk(const float* xs, const float* ss, const float* mrow,
+                                                 float& env) const {
+    const float4* x4 = reinterpret_cast<const float4*>(xs);
+    const float4* s4 = reinterpret_cast<const float4*>(ss);
+    const float4* m4 = reinterpret_cast<const float4*>(mrow);
+    // four independent chains: back-to-back dependent packed FMAs cost an s_nop each
+    f2 acc0 = {b1, 0.f}, acc1 = {0.f, 0.f}, accm0 = {0.f, 0.f}, accm1 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NX / 4; ++q) {
+      const float4 xv = x4[q], mv = m4[q];
+      const float4 sv = kSameInput ? xv : s4[q];
+      float4 w;
+      if constexpr (kW1Lds) {
+        w = tile[q * kWave];
+      } else {
+        w = float4{w1[2 * q].x, w1[2 * q].y, w1[2 * q + 1].x, w1[2 * q + 1].y};
+      }
+      acc0 = pk_fma(f2{w.x, w.y}, f2{xv.x, xv.y}, acc0);
+      accm0 = pk_fma(f2{mv.x, mv.y}, f2{sv.x, sv.y}, accm0);
+      acc1 = pk_fma(f2{w.z, w.w}, f2{xv.z, xv.w}, acc1);
+      accm1 = pk_fma(f2{mv.z, mv.w}, f2{sv.z, sv.w}, accm1);
+    }
+    const f2 am = accm0 + accm1, ah = acc0 + acc1;
+    env = am.x + am.y;
+    const float z = ah.x + ah.y;
+    if constexpr (DISC) {
+      return fmaf(fmaxf(z, 0.f), a1, c1);
+    } else {
+      return tanh_fast(z);
+    }
+  }
+
   // second hidden layer and the head: h = layer-1 output of unit j; returns the head
   // pre-activation for output o = j & 15 (identical in the 4 rows).
   template <class Mark>
   __device__ __forceinline__ float layers23(float h, Scratch* sc, int j, Mark&& mark) const {
-    const int c = j & 7, q = j >> 4;
+    const int c = j & 7;
     sc->h1[j] = h;
     wave_lds_sync();
     float x[8];
@@ -323,17 +328,17 @@ struct MlpLane {
       h2 = tanh_fast(z);
     }
     mark(1, h2);
-    sc->h2[j] = h2;
-    wave_lds_sync();
-    const float4* hv = reinterpret_cast<const float4*>(sc->h2 + 16 * q);
-    f2 a3 = {0.f, 0.f}, a4 = {0.f, 0.f};
+    // h2[16q + i] sits in lane i of row q: DPP row_newbcast FMAs, no LDS round trip
+    float w3[16];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      const float4 u = hv[m], w = tile[(kW1Chunks + m) * kWave];
-      a3 = pk_fma(f2{w.x, w.y}, f2{u.x, u.y}, a3);
-      a4 = pk_fma(f2{w.z, w.w}, f2{u.z, u.w}, a4);
+      const float4 w = tile[(kW1Chunks + m) * kWave];
+      w3[4 * m] = w.x;
+      w3[4 * m + 1] = w.y;
+      w3[4 * m + 2] = w.z;
+      w3[4 * m + 3] = w.w;
     }
-    const float out = row_allreduce_sum((a3.x + a3.y) + (a4.x + a4.y)) + b3;
+    const float out = row_allreduce_sum(dot_row16(h2, w3, 0.f)) + b3;
     mark(2, out);
     return out;
   }
@@ -394,7 +399,6 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
   using Lane = MlpLane<NIN, NA, DISC>;
   constexpr int NX = Lane::NX;
   // env rows [M[i] (NX) | K[i] (one column per action)], stride MKS (b128 rows)
-  constexpr int NQI = Lane::NQI;  // row-gathered registers of the input / state
   constexpr int NMK = NX + round4(NA);
   constexpr int MKS = NMK % 8 == 0 ? NMK + 4 : NMK;
   __shared__ float4 env4[(ENV == FDR_ENV_SYNTH) ? NIN * MKS / 4 : 1];
@@ -417,7 +421,10 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
   const bool det = a.lanes.deterministic ? a.lanes.deterministic[lane] != 0 : false;
   Lane pl;
   pl.load(src, j, a.bn_mean, a.bn_var, wtile + wv * Lane::kTileF4);
-  const double n2 = wave_sum(src.n2);
+  {  // written now: a double live across the T-step loop would be spilled
+    const double n2 = wave_sum(src.n2);
+    if (j == 0 && a.norm2) a.norm2[lane] = n2;
+  }
 
   const int ji = j < NIN ? j : NIN - 1;
   constexpr bool norm_obs = (FEAT & 4) != 0;
@@ -472,8 +479,11 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
     const uint64_t h = hash_ctr(key, ulane, (uint64_t)(t + ds), (uint64_t)dk);
     rbuf = DISC ? uniform24(h) : normal_bm(h);
   };
+  const int zbase = 4 * (o < NA ? o : 0);  // ds_bpermute byte address of dim o in step 0 of a batch
   auto fetch_z = [&](int t) {
-    return DISC ? 0.f : __shfl(rbuf, (t % kStepsPerBatch) * NA + (o < NA ? o : 0), kWave);
+    if constexpr (DISC) return 0.f;
+    const int addr = zbase + 4 * NA * (t % kStepsPerBatch);
+    return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, rbuf)));
   };
   for (int t = 0; t < T; ++t) {
     // The W1 / M / K rows are loop-invariant LDS data; hoisting their loads out of the loop would
@@ -504,27 +514,24 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
         os_m2 += (delta * delta_n) * (float)cc;
       }
     }
-    // policy input row-gathered into NQI registers (two permlane swaps)
     auto* sc = &scratch[wv];
     constexpr bool kSame = !DISC && !norm_obs;  // mujoco: policy input == env state
-    float X[NQI];
-    row_allgather<NQI>(policy_input(s), X);
-    const float h1 = pl.layer1_dpp(X);
-    // env dynamics M s: independent of the action, issued beside the first layer
     const float* mrow = envMK + ji * MKS;
     float pre = 0.f;
+    // policy input (and env state) broadcast through the wave's LDS scratch, then packed FMAs
+    // against the lane's W1 row and M row (two MACs per instruction instead of one DPP FMA)
+    sc->x[j] = j < NIN ? policy_input(s) : (j == NIN ? 1.f : 0.f);
+    if constexpr (ENV == FDR_ENV_SYNTH && !kSame) sc->h1[j] = j < NIN ? s : 0.f;
+    wave_lds_sync();
+    float h1;
     if constexpr (ENV == FDR_ENV_SYNTH) {
-      float S[NQI];
-      if constexpr (kSame) {
-#pragma unroll
-        for (int q = 0; q < NQI; ++q) S[q] = X[q];
-      } else {
-        row_allgather<NQI>(s, S);
-      }
-      float mr[NIN];
-#pragma unroll
-      for (int k = 0; k < NIN; ++k) mr[k] = mrow[k];
-      pre = dot_gathered<NIN>(S, mr, 0.f);
+      // one pass over the input chunks: W1 row j against x, M row j against s (M's padding
+      // columns are 0, so the bias column's 1 drops out of M s)
+      h1 = pl.template layer1_env_pk<kSame>(sc->x, sc->h1, mrow, pre);
+    } else {
+      float xb[NX];
+      lds_bcast<NX>(sc->x, xb);
+      h1 = pl.layer1(xb);
     }
     mark(0, h1);
     const float y = pl.layers23(h1, sc, j, mark);
@@ -564,7 +571,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
     } else {
       const float th = tanh_fast(y);
       const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
-      eacc += (j < NA) ? __builtin_amdgcn_logf(sd) * 0.693147180559945309f : 0.f;  // v_log_f32: sd in [0.1, 1]
+      eacc += __builtin_amdgcn_logf(sd);  // log2; lanes >= NA and the ln 2 scale: epilogue
       act_c = det ? th : gauss_action(th, sd, zt);
     }
 
@@ -600,6 +607,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
 #endif
 
   // ---- epilogue ----
+  if constexpr (!DISC) eacc *= 0.693147180559945309f;
   const double esum = wave_sum((j < NA) ? (double)eacc : 0.0);
   if (j == 0) {
     double r = racc;
@@ -609,7 +617,6 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
     if constexpr (!DISC) e += (double)NA * 1.4189385332046727;  // 0.5 + 0.5*ln(2*pi) per dim
     a.ent[lane] = e;
     a.steps[lane] = T;
-    if (a.norm2) a.norm2[lane] = n2;
   }
   if constexpr (FEAT & 2) {
     if (j < NIN) {
