@@ -42,7 +42,13 @@ constexpr int kS3 = kT2;                          // S3 [17][16][32] after T2
 constexpr int kX3 = kS3 + kBR3 * 16 * 32;         // X3 [8][8][32]
 constexpr int kRegion = kX1 + 32 * 32 * 16;       // max extent
 static_assert(kT1 <= kX1 && kX2 + 16 * 16 * 32 <= kRegion && kX3 + 8 * 8 * 32 <= kX2, "fp16 LDS plan");
-constexpr int kHLdsBytes = (kHGuard + kRegion) * 2 + 2 * kBnTab * 4;
+// conv weight staging buffer WB (halves): the A fragments of the widest conv (32 -> 32, 9 k-steps x 2
+// channel tiles).  Every wave of the workgroup needs the same fragments; fetched from the pack by
+// all 8 waves they cost 8 x 18 KB of vector-memory traffic per conv (~2,000 clocks of TA issue the
+// waves stall on).  Instead the workgroup copies each conv's block ONCE into WB (16 B per thread per
+// chunk) and the waves read their fragments from LDS.
+constexpr int kWB = 9 * 2 * 64 * 8;
+constexpr int kHLdsBytes = (kHGuard + kRegion) * 2 + 2 * kBnTab * 4 + kWB * 2;
 static_assert(kHLdsBytes <= 160 * 1024, "fp16 conv LDS");
 
 // ---- conv on f16 MFMA ---------------------------------------------------------------------------
@@ -59,6 +65,45 @@ __device__ __forceinline__ void load_af(const _Float16* __restrict__ wf, h8 (&af
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) af[s][nt] = *reinterpret_cast<const h8*>(wf + (((s * NT + nt) * 64) + lane) * 8);
 }
+
+// The same fragments from the workgroup's LDS copy of the block (layout identical to the pack's).
+template <int CIN, int NT>
+__device__ __forceinline__ void load_af_lds(const _Float16* wb, h8 (&af)[KSteps<CIN>::N][NT], int lane) {
+#pragma unroll
+  for (int s = 0; s < KSteps<CIN>::N; ++s)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) af[s][nt] = *reinterpret_cast<const h8*>(wb + (((s * NT + nt) * 64) + lane) * 8);
+}
+template <int CIN, int NT>
+constexpr int kBlockHalves = KSteps<CIN>::N * NT * 64 * 8;
+
+// Workgroup copy of one conv's weight block into WB, split so the HBM/L2 latency hides behind other
+// work: issue() starts the loads (16-B chunks, chunk c by thread c mod 512), commit() stores them to
+// WB.  WB protocol (every phase ends in a barrier): read WB -> af in phase k, commit the next block
+// in phase k+1 or later, read it in a phase after the commit.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+struct WStage {
+  u32x4 r[(kWB / 8 + kHThreads - 1) / kHThreads];
+  template <int NH>
+  __device__ __forceinline__ void issue(const _Float16* __restrict__ src) {
+    constexpr int NC = NH / 8, PER = (NC + kHThreads - 1) / kHThreads;
+    static_assert(NH % 8 == 0 && NH <= kWB, "weight block");
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int c = threadIdx.x + k * kHThreads;  // past the block: reload its last chunk (not stored)
+      r[k] = reinterpret_cast<const u32x4*>(src)[NC % kHThreads == 0 || c < NC ? c : NC - 1];
+    }
+  }
+  template <int NH>
+  __device__ __forceinline__ void commit(_Float16* wb) const {
+    constexpr int NC = NH / 8, PER = (NC + kHThreads - 1) / kHThreads;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int c = threadIdx.x + k * kHThreads;
+      if (NC % kHThreads == 0 || c < NC) reinterpret_cast<u32x4*>(wb)[c] = r[k];
+    }
+  }
+};
 
 // offset (halves) of this lane's 8 K-elements of k-step s inside the receptive field of a pixel
 template <int CIN, int CS, int WP>
@@ -175,11 +220,12 @@ __device__ __forceinline__ void to_padded_h(const _Float16* X, _Float16* T, cons
 
 // Stage entry: X <- maxpool3s2p1(conv3x3(T) + b) in bands of BR conv rows through S [BR][H][COUT]
 // (conv row -1 of band 0 stored as -inf); pool: one thread per (pooled pixel, 8-channel group).
-template <int CIN, int COUT, int H, int BR>
+// WB: the next conv's block (issued by the caller into st) is committed in band 0's pool phase.
+template <int CIN, int COUT, int H, int BR, int NH>
 __device__ __forceinline__ void stage_entry_h(const _Float16* T, _Float16* S, _Float16* X,
                                               const h8 (&af)[KSteps<CIN>::N][COUT / 16],
                                               const float* __restrict__ bias, int wave, int lane,
-                                              const StepArgs& a, int kst) {
+                                              const StepArgs& a, int kst, WStage& st, _Float16* wb) {
   constexpr int CS = Pix<CIN>::CS, WP = H + 2, NT = COUT / 16, MT = BR * H / 16;
   constexpr int TPW = (MT + 7) / 8, HO = H / 2, PRB = (BR - 1) / 2, G = COUT / 8;
   float bz[NT][4];
@@ -200,6 +246,7 @@ __device__ __forceinline__ void stage_entry_h(const _Float16* T, _Float16* S, _F
     });
     __syncthreads();
     FDR_STAMP(a, kst + 2 * b);  // diagnostics: band b conv + store done
+    if (b == 0) st.commit<NH>(wb);
     // 3x3 / stride-2 max pool, branch-free (the left tap of column 0 is clamped onto column 0,
     // which the window holds anyway) and fully unrolled so every load of a thread is in flight
     constexpr int NI = PRB * HO * G, IT = (NI + kHThreads - 1) / kHThreads;
@@ -229,14 +276,18 @@ __device__ __forceinline__ void stage_entry_h(const _Float16* T, _Float16* S, _F
 }
 
 // Two residual blocks; same fusion as the f32 path (fdr_impala.hip res_blocks).  af holds block 0's
-// first conv on entry; T holds relu(bn0(X)) with a zero border.
-template <int C, int H, int LAST>
+// first conv on entry, st the issued copy of its second conv; T holds relu(bn0(X)) with a zero border.
+// Weight pipeline (convs A B C D = i0, i1 of blocks 0 and 1, E = the next stage's entry conv):
+//   conv phase: MFMAs (af), commit the issued block to WB  |  epilogue phase: af <- WB, issue the next.
+// On exit WB holds E (NEXTH halves; NEXTH == 0: last stage, nothing staged).
+template <int C, int H, int LAST, int NEXTH>
 __device__ __forceinline__ void res_blocks_h(_Float16* T, _Float16* X, h8 (&af)[KSteps<C>::N][C / 16],
                                              const _Float16* __restrict__ hp, const float* __restrict__ pk,
                                              const Layout& L, int stage, const float* bsc, const float* bsh, int wave,
-                                             int lane, const StepArgs& a, int k0, float* __restrict__ out) {
+                                             int lane, const StepArgs& a, int k0, float* __restrict__ out,
+                                             WStage& st, _Float16* wb, const _Float16* __restrict__ next_w) {
   constexpr int CS = Pix<C>::CS, WP = H + 2, NT = C / 16, MT = H * H / 16;
-  constexpr int TPW = (MT + 7) / 8;
+  constexpr int TPW = (MT + 7) / 8, WH = kBlockHalves<C, C / 16>;
   auto tpos = [&](int m) { return ((m / H + 1) * WP + (m % H) + 1) * CS; };
   const int cl = 4 * (lane >> 4);  // this lane's 4 channels within an output-channel tile
 #pragma unroll
@@ -260,9 +311,15 @@ __device__ __forceinline__ void res_blocks_h(_Float16* T, _Float16* X, h8 (&af)[
     FDR_STAMP(a, k0 + 4 * r);
     f32x4 acc[TPW][NT];
     conv_h<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
-    load_af<C, NT>(hp + L.conv_h[i1], af, lane);
+    st.commit<WH>(wb);  // conv i1
     __syncthreads();  // every wave is done reading T
     FDR_STAMP(a, k0 + 4 * r + 1);
+    load_af_lds<C, NT>(wb, af, lane);
+    if (r == 0) {
+      st.issue<WH>(hp + L.conv_h[i1 + 1]);  // block 1 conv0
+    } else if constexpr (NEXTH > 0) {
+      st.issue<NEXTH>(next_w);
+    }
     conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
       const int nt = ch0 >> 4;
       float o[4];
@@ -273,8 +330,17 @@ __device__ __forceinline__ void res_blocks_h(_Float16* T, _Float16* X, h8 (&af)[
     __syncthreads();
     FDR_STAMP(a, k0 + 4 * r + 2);
     conv_h<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
+    if (r == 0) {
+      st.commit<WH>(wb);
+    } else if constexpr (NEXTH > 0) {
+      st.commit<NEXTH>(wb);
+    }
     __syncthreads();  // every wave is done reading T
     FDR_STAMP(a, k0 + 4 * r + 3);
+    if (r == 0) {
+      load_af_lds<C, NT>(wb, af, lane);  // block 1 conv0
+      st.issue<WH>(hp + L.conv_h[i1 + 2]);  // block 1 conv1
+    }
     conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
       const int nt = ch0 >> 4;
       const h4 xo = *reinterpret_cast<const h4*>(X + m * C + ch0);
@@ -297,7 +363,6 @@ __device__ __forceinline__ void res_blocks_h(_Float16* T, _Float16* X, h8 (&af)[
         for (int k = 0; k < 4; ++k) out[(ch0 + k) * H * H + m] = relu(xn[k]);  // flatten (C,H,W)
       }
     });
-    if (r == 0) load_af<C, NT>(hp + L.conv_h[i1 + 1], af, lane);
     __syncthreads();
   }
 }
@@ -315,8 +380,11 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
   float* bsh = bsc + kBnTab;
   _Float16* R = reinterpret_cast<_Float16*>(smem + 2 * kBnTab * 4) + kHGuard;
 
+  _Float16* wb = reinterpret_cast<_Float16*>(smem + kHLdsBytes - kWB * 2);
   h8 af3[KSteps<3>::N][1];
   load_af<3, 1>(hp + L.conv_h[0], af3, ln);
+  WStage st;
+  st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);  // committed in the stage-1 entry
   FDR_STAMP(a, 0);
   for (int i = threadIdx.x; i < kBnTab; i += kHThreads) {
     const int idx = i >> 5, ch = i & 31;
@@ -373,44 +441,55 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
   FDR_STAMP(a, 2);
 
   // ---- stage 1 ----
-  stage_entry_h<3, 16, 64, kBR1>(R, R + kS1, R + kX1, af3, pk + L.conv_b[0], wave, ln, a, 40);
+  stage_entry_h<3, 16, 64, kBR1, kBlockHalves<16, 1>>(R, R + kS1, R + kX1, af3, pk + L.conv_b[0], wave, ln, a, 40,
+                                                     st, wb);
   {
     h8 af[KSteps<16>::N][1];
-    load_af<16, 1>(hp + L.conv_h[1], af, ln);
+    load_af_lds<16, 1>(wb, af, ln);
+    st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[2]);
     to_padded_h<16, 32, true, true>(R + kX1, R, bsc + 1 * 32, bsh + 1 * 32);
     __syncthreads();
     FDR_STAMP(a, 3);
-    res_blocks_h<16, 32, 0>(R, R + kX1, af, hp, pk, L, 0, bsc, bsh, wave, ln, a, 4, nullptr);
+    res_blocks_h<16, 32, 0, kBlockHalves<16, 2>>(R, R + kX1, af, hp, pk, L, 0, bsc, bsh, wave, ln, a, 4, nullptr, st,
+                                                 wb, hp + L.conv_h[5]);
   }
   // ---- stage 2 ----
   {
     h8 af[KSteps<16>::N][2];
-    load_af<16, 2>(hp + L.conv_h[5], af, ln);
+    load_af_lds<16, 2>(wb, af, ln);
+    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
     FDR_STAMP(a, 12);
-    stage_entry_h<16, 32, 32, kBR2>(R, R + kS2, R + kX2, af, pk + L.conv_b[5], wave, ln, a, 48);
+    stage_entry_h<16, 32, 32, kBR2, kBlockHalves<32, 2>>(R, R + kS2, R + kX2, af, pk + L.conv_b[5], wave, ln, a, 48,
+                                                         st, wb);
   }
   {
     h8 af[KSteps<32>::N][2];
-    load_af<32, 2>(hp + L.conv_h[6], af, ln);
+    load_af_lds<32, 2>(wb, af, ln);
+    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[7]);
     to_padded_h<32, 16, true, true>(R + kX2, R, bsc + 6 * 32, bsh + 6 * 32);
     __syncthreads();
     FDR_STAMP(a, 13);
-    res_blocks_h<32, 16, 0>(R, R + kX2, af, hp, pk, L, 1, bsc, bsh, wave, ln, a, 14, nullptr);
+    res_blocks_h<32, 16, 0, kBlockHalves<32, 2>>(R, R + kX2, af, hp, pk, L, 1, bsc, bsh, wave, ln, a, 14, nullptr, st,
+                                                 wb, hp + L.conv_h[10]);
   }
   // ---- stage 3 ----
   {
     h8 af[KSteps<32>::N][2];
-    load_af<32, 2>(hp + L.conv_h[10], af, ln);
+    load_af_lds<32, 2>(wb, af, ln);
+    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
     FDR_STAMP(a, 22);
-    stage_entry_h<32, 32, 16, kBR3>(R, R + kS3, R + kX3, af, pk + L.conv_b[10], wave, ln, a, 56);
+    stage_entry_h<32, 32, 16, kBR3, kBlockHalves<32, 2>>(R, R + kS3, R + kX3, af, pk + L.conv_b[10], wave, ln, a, 56,
+                                                         st, wb);
   }
   {
     h8 af[KSteps<32>::N][2];
-    load_af<32, 2>(hp + L.conv_h[11], af, ln);
+    load_af_lds<32, 2>(wb, af, ln);
+    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[12]);
     to_padded_h<32, 8, true, true>(R + kX3, R, bsc + 11 * 32, bsh + 11 * 32);
     __syncthreads();
     FDR_STAMP(a, 23);
-    res_blocks_h<32, 8, 1>(R, R + kX3, af, hp, pk, L, 2, bsc, bsh, wave, ln, a, 24, a.feat + env * kFeat);
+    res_blocks_h<32, 8, 1, 0>(R, R + kX3, af, hp, pk, L, 2, bsc, bsh, wave, ln, a, 24, a.feat + env * kFeat, st, wb,
+                              nullptr);
   }
   FDR_STAMP(a, 32);
 }
