@@ -18,6 +18,9 @@
 
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <utility>
 
 #include "fdr_common.h"
 #include "fdr_internal.h"
@@ -628,6 +631,381 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
 }
 
 // ---------------------------------------------------------------------------------------------
+// Two lanes per wave: rollout_pair_kernel (synthetic env)
+//
+// The wave's halves (threads 0-31 / 32-63, two DPP rows each) run one lane each; thread t of a
+// half owns hidden units 2t, 2t+1 of layer 1 and units 16r + c, 16r + 8 + c (r = t/8, c = t%8) of
+// layer 2.  Per lane the MAC instructions are those of the one-lane-per-wave kernel, but the
+// per-lane scalar work (action, sampling, env tail, reward, loop control) is shared by the two
+// lanes of a wave, and each wave carries two independent dependency chains:
+//   L1 + M s   broadcast input of the half (LDS); W1 rows 2t, 2t+1 (per-wave tile) and M row t.
+//   L2         thread (r, c) holds W2[16r + 8e + (c ^ sigma(p))][8c + k] (p < 8, e < 2, k < 8:
+//              128 VGPRs) against h1[8c .. 8c + 7] (two b128), 16 partial outputs, then the
+//              3-level reduce-scatter of the one-lane kernel over 16 slots (8 + 4 + 2 DPP adds).
+//   head       thread (rho = t/16, o = t%16) sums W3[o][.] over the 32 units its own DPP row
+//              holds (32 row_newbcast FMAs), then the two rows of the half (one permlane16 swap).
+// ---------------------------------------------------------------------------------------------
+constexpr int kPairWaves = 2;  // waves per workgroup (4 lanes): 4 workgroups, 8 waves per CU
+
+template <int NIN, int NA, bool DISC>
+struct MlpPair {
+  using L = Layout<NIN, NA, DISC>;
+  static constexpr int NOUT = L::NOUT;
+  static constexpr int NX = round4(NIN);
+  static_assert(NX <= 32, "pair kernel: policy input wider than 32");
+  static constexpr bool kBiasCol = NIN < NX;
+  static constexpr bool kW1Lds = NIN > 8;
+  static constexpr int kW1Chunks = kW1Lds ? NX / 4 : 0;     // per W1 row
+  static constexpr int kTileF4 = (2 * kW1Chunks + 8) * kWave;  // float4 per wave: W1 rows, W3 slice
+  f2 w1a[kW1Lds ? 1 : NX / 2], w1b[kW1Lds ? 1 : NX / 2];
+  float b1a, b1b;
+  const float4* tile;  // this thread's column of the wave tile (chunk m at tile[m * kWave])
+  f2 w2[64];           // w2[p * 8 + k] = (W2[16r + (c ^ sigma(p))][8c + k], W2[16r + 8 + (c ^ sigma(p))][8c + k])
+  float b2a, b2b, b3;
+  float a0, c0, a1a, c1a, a1b, c1b, a2a, c2a, a2b, c2b;  // discrete: folded BN
+
+  // unit of layer 2 that row-thread k's value e (0: z.x, 1: z.y) holds, within the row's 32 units
+  __host__ __device__ static constexpr int head_unit(int rho, int k, int e) {
+    return 32 * rho + 16 * (k >> 3) + 8 * e + (k & 7);
+  }
+
+  __device__ __forceinline__ void load(ParamSrc& src, int t, int tid, const float* bn_mean, const float* bn_var,
+                                       float4* wave_tile) {
+    const int r = t >> 3, c = t & 7, rho = t >> 4, o = t & 15;
+    const int ua = 2 * t, ub = 2 * t + 1;
+    float4* my = wave_tile + tid;
+    tile = my;
+    auto w1v = [&](int u, int k) {
+      return k < NIN ? src.get(L::L1W + (int64_t)u * NIN + k) : (k == NIN ? src.get(L::L1B + u) : 0.f);
+    };
+    if constexpr (kW1Lds) {
+#pragma unroll
+      for (int m = 0; m < kW1Chunks; ++m) {
+        const float e0 = w1v(ua, 4 * m), e1 = w1v(ua, 4 * m + 1), e2 = w1v(ua, 4 * m + 2), e3 = w1v(ua, 4 * m + 3);
+        my[m * kWave] = float4{e0, e1, e2, e3};
+        const float f0 = w1v(ub, 4 * m), f1 = w1v(ub, 4 * m + 1), f2_ = w1v(ub, 4 * m + 2), f3 = w1v(ub, 4 * m + 3);
+        my[(kW1Chunks + m) * kWave] = float4{f0, f1, f2_, f3};
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < NX / 2; ++p) {
+        const float e0 = w1v(ua, 2 * p), e1 = w1v(ua, 2 * p + 1);
+        w1a[p] = f2{e0, e1};
+        const float f0 = w1v(ub, 2 * p), f1 = w1v(ub, 2 * p + 1);
+        w1b[p] = f2{f0, f1};
+      }
+    }
+    b1a = kBiasCol ? 0.f : src.get(L::L1B + ua);
+    b1b = kBiasCol ? 0.f : src.get(L::L1B + ub);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int row0 = 16 * r + (c ^ l2_sigma(p)), row1 = row0 + 8;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float e0 = src.get(L::L2W + (int64_t)row0 * kHidden + 8 * c + k);
+        const float e1 = src.get(L::L2W + (int64_t)row1 * kHidden + 8 * c + k);
+        w2[p * 8 + k] = f2{e0, e1};
+      }
+    }
+    b2a = src.get(L::L2B + 16 * r + c);
+    b2b = src.get(L::L2B + 16 * r + 8 + c);
+    if (o < NOUT) {
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        float e[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int w = 4 * m + i;  // w < 16: value z.x of row-thread w; else z.y of row-thread w - 16
+          e[i] = src.get(L::L3W + (int64_t)o * kHidden + head_unit(rho, w & 15, w >> 4));
+        }
+        my[(2 * kW1Chunks + m) * kWave] = float4{e[0], e[1], e[2], e[3]};
+      }
+      b3 = rho == 0 ? src.get(L::L3B + o) : src.get_nocount(L::L3B + o);
+    } else {
+#pragma unroll
+      for (int m = 0; m < 8; ++m) my[(2 * kW1Chunks + m) * kWave] = float4{0.f, 0.f, 0.f, 0.f};
+      b3 = 0.f;
+    }
+    wave_lds_sync();
+    a0 = c0 = a1a = c1a = a1b = c1b = a2a = c2a = a2b = c2b = 0.f;
+    if constexpr (DISC) {
+      if (t < NIN) {
+        const float w = src.get(L::BN0W + t), b = src.get(L::BN0B + t);
+        bn_fold(w, b, bn_mean ? bn_mean[t] : 0.f, bn_var ? bn_var[t] : 1.f, a0, c0);
+      }
+      auto fold = [&](int64_t wofs, int64_t bofs, int stat, int u, float& av, float& cv) {
+        const float w = src.get(wofs + u), b = src.get(bofs + u);
+        bn_fold(w, b, bn_mean ? bn_mean[stat + u] : 0.f, bn_var ? bn_var[stat + u] : 1.f, av, cv);
+      };
+      fold(L::BN1W, L::BN1B, NIN, ua, a1a, c1a);
+      fold(L::BN1W, L::BN1B, NIN, ub, a1b, c1b);
+      fold(L::BN2W, L::BN2B, NIN + kHidden, 16 * r + c, a2a, c2a);
+      fold(L::BN2W, L::BN2B, NIN + kHidden, 16 * r + 8 + c, a2b, c2b);
+    }
+  }
+
+  __device__ __forceinline__ float input_transform(float x) const {
+    if constexpr (DISC) {
+      return fmaf(x, a0, c0);
+    } else {
+      return x;
+    }
+  }
+
+  __device__ __forceinline__ float act1(float z, float av, float cv) const {
+    if constexpr (DISC) {
+      return fmaf(fmaxf(z, 0.f), av, cv);
+    } else {
+      return tanh_fast(z);
+    }
+  }
+
+  // Layer 1 (units 2t, 2t+1) and the env's M[t] . s in one pass over the broadcast input chunks.
+  template <bool kSameInput>
+  __device__ __forceinline__ f2 layer1_env(const float* xs, const float* ss, const float* mrow, float& env) const {
+    const float4* x4 = reinterpret_cast<const float4*>(xs);
+    const float4* s4 = reinterpret_cast<const float4*>(ss);
+    const float4* m4 = reinterpret_cast<const float4*>(mrow);
+    f2 aa0 = {b1a, 0.f}, aa1 = {0.f, 0.f}, ab0 = {b1b, 0.f}, ab1 = {0.f, 0.f};
+    f2 am0 = {0.f, 0.f}, am1 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NX / 4; ++q) {
+      const float4 xv = x4[q], mv = m4[q];
+      const float4 sv = kSameInput ? xv : s4[q];
+      float4 wa, wb;
+      if constexpr (kW1Lds) {
+        wa = tile[q * kWave];
+        wb = tile[(kW1Chunks + q) * kWave];
+      } else {
+        wa = float4{w1a[2 * q].x, w1a[2 * q].y, w1a[2 * q + 1].x, w1a[2 * q + 1].y};
+        wb = float4{w1b[2 * q].x, w1b[2 * q].y, w1b[2 * q + 1].x, w1b[2 * q + 1].y};
+      }
+      aa0 = pk_fma(f2{wa.x, wa.y}, f2{xv.x, xv.y}, aa0);
+      ab0 = pk_fma(f2{wb.x, wb.y}, f2{xv.x, xv.y}, ab0);
+      am0 = pk_fma(f2{mv.x, mv.y}, f2{sv.x, sv.y}, am0);
+      aa1 = pk_fma(f2{wa.z, wa.w}, f2{xv.z, xv.w}, aa1);
+      ab1 = pk_fma(f2{wb.z, wb.w}, f2{xv.z, xv.w}, ab1);
+      am1 = pk_fma(f2{mv.z, mv.w}, f2{sv.z, sv.w}, am1);
+    }
+    const f2 am = am0 + am1, ha = aa0 + aa1, hb = ab0 + ab1;
+    env = am.x + am.y;
+    return f2{act1(ha.x + ha.y, a1a, c1a), act1(hb.x + hb.y, a1b, c1b)};
+  }
+
+  // Layer 2 and the head: h1 = this thread's layer-1 units (2t, 2t+1); h1s = the half's scratch.
+  // Returns the head pre-activation for output o = t & 15 (identical in both rows of the half).
+  __device__ __forceinline__ float layers23(f2 h1, float* h1s, int t) const {
+    const int c = t & 7;
+    reinterpret_cast<f2*>(h1s)[t] = h1;
+    wave_lds_sync();
+    float x[8];
+    lds_bcast<8>(h1s + 8 * c, x);
+    f2 acc[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) acc[p] = f2{0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int p = 0; p < 8; ++p) acc[p] = pk_fma(w2[p * 8 + k], f2{x[k], x[k]}, acc[p]);
+    // reduce-scatter over the 8 threads of the half-row: slot i = acc[i / 2][i % 2], output of
+    // slot i = 16r + 8 (i % 2) + (c ^ sigma(i / 2)); partners c ^ 7, c ^ 2, c ^ 1
+    f2 q[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      q[p] = f2{acc[p].x + dpp_mov<kDppHalfMirror>(acc[p + 4].x), acc[p].y + dpp_mov<kDppHalfMirror>(acc[p + 4].y)};
+    f2 rr[2];
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      rr[p] = f2{q[p].x + dpp_mov<kDppQuadXor2>(q[p + 2].x), q[p].y + dpp_mov<kDppQuadXor2>(q[p + 2].y)};
+    const float za = (rr[0].x + dpp_mov<kDppQuadXor1>(rr[1].x)) + b2a;  // unit 16r + c
+    const float zb = (rr[0].y + dpp_mov<kDppQuadXor1>(rr[1].y)) + b2b;  // unit 16r + 8 + c
+    float h2a, h2b;
+    if constexpr (DISC) {
+      h2a = fmaf(fmaxf(za, 0.f), a2a, c2a);
+      h2b = fmaf(fmaxf(zb, 0.f), a2b, c2b);
+    } else {
+      h2a = tanh_fast(za);
+      h2b = tanh_fast(zb);
+    }
+    float w3[32];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const float4 w = tile[(2 * kW1Chunks + m) * kWave];
+      w3[4 * m] = w.x;
+      w3[4 * m + 1] = w.y;
+      w3[4 * m + 2] = w.z;
+      w3[4 * m + 3] = w.w;
+    }
+    float s0 = 0.f, s1 = 0.f;
+    dpp_fma_32x2(s0, s1, h2a, h2b, w3);
+    float u = s0 + s1, v = u;
+    permlane16_swap(u, v);  // u = row 2h's partial, v = row 2h+1's, in both rows of half h
+    return (u + v) + b3;
+  }
+
+  __device__ __forceinline__ float softmax(float logit, int t) const {
+    const bool valid = (t & 15) < NOUT;
+    const float v = valid ? logit : -FLT_MAX;
+    const float mx = row16_max(v);
+    const float e = valid ? expf(v - mx) : 0.f;
+    return e / row16_sum(e);
+  }
+};
+
+struct alignas(16) PairScratch {
+  float h1[2][kHidden];  // per half: layer-1 output; the env state when it differs from the input
+  float x[2][32];        // per half: policy input (+ the 1 of the folded bias column)
+};
+
+template <int K>
+__device__ __forceinline__ float row_bcast(float v) {  // lane K of the caller's 16-lane row
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x150 + K, 0xF, 0xF, false));
+}
+
+template <int N, int... I>
+__device__ __forceinline__ void row_bcast_all(float v, float (&out)[N], std::integer_sequence<int, I...>) {
+  ((out[I] = row_bcast<I>(v)), ...);
+}
+
+// FEAT bit 0: record visited observations; bit 2: observation normalisation (bit 1, the Welford
+// statistics, runs on rollout_kernel)
+template <int NIN, int NA, bool DISC, int FEAT>
+__global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(RolloutArgs a) {
+  using Lane = MlpPair<NIN, NA, DISC>;
+  constexpr int NX = Lane::NX;
+  constexpr int NMK = NX + round4(NA);
+  constexpr int MKS = NMK % 8 == 0 ? NMK + 4 : NMK;
+  __shared__ float4 env4[NIN * MKS / 4];
+  __shared__ float4 wtile[kPairWaves * Lane::kTileF4];
+  __shared__ PairScratch scratch[kPairWaves];
+  float* envMK = reinterpret_cast<float*>(env4);
+  for (int e = threadIdx.x; e < NIN * MKS; e += blockDim.x) {
+    const int i = e / MKS, k = e % MKS;
+    envMK[e] = k < NIN ? a.M[i * NIN + k] : (k >= NX && k < NX + NA ? a.K[i * NA + k - NX] : 0.f);
+  }
+  __syncthreads();
+
+  const int tid = threadIdx.x & 63, wv = threadIdx.x >> 6, hh = tid >> 5, t = tid & 31;
+  const int lane0 = (blockIdx.x * kPairWaves + wv) * 2;
+  if (lane0 >= a.n_lanes) return;  // whole wave idle
+  const bool active = lane0 + hh < a.n_lanes;
+  const int lane = active ? lane0 + hh : lane0;  // an idle half shadows its partner, writes nothing
+
+  ParamSrc src = a.lanes.src(lane);
+  const bool det = a.lanes.deterministic ? a.lanes.deterministic[lane] != 0 : false;
+  Lane pl;
+  pl.load(src, t, tid, a.bn_mean, a.bn_var, wtile + wv * Lane::kTileF4);
+  {
+    double n2 = src.n2;
+#pragma unroll
+    for (int m = 16; m >= 1; m >>= 1) n2 += __shfl_xor(n2, m, kWave);
+    if (t == 0 && active && a.norm2) a.norm2[lane] = n2;
+  }
+
+  const int ji = t < NIN ? t : NIN - 1;
+  constexpr bool norm_obs = (FEAT & 4) != 0;
+  const float om = norm_obs ? a.obs_mean[ji] : 0.f;
+  const float osd = norm_obs ? a.obs_std[ji] : 1.f;
+  auto policy_input = [&](float s) {
+    float x = s;
+    if (norm_obs) x = fminf(fmaxf((s - om) / osd, -10.f), 10.f);  // agent.py:40-41
+    return pl.input_transform(x);
+  };
+  float s = a.s0[ji];
+  const int T = a.T;
+  const uint64_t key = a.key;
+  const uint64_t ulane = (uint64_t)(a.lanes.lane_offset + lane);
+  double racc = 0.0;
+  float eacc = 0.f;
+  const int o = t & 15;
+  constexpr int kDrawsPerStep = DISC ? 1 : NA;
+  constexpr int kStepsPerBatch = 32 / kDrawsPerStep;
+  float rbuf = 0.f;
+  const int zbase = 4 * (32 * hh + (DISC ? 0 : (o < NA ? o : 0)));
+  auto* sc = &scratch[wv];
+  float* xs = sc->x[hh];
+  float* h1s = sc->h1[hh];
+  const float* mrow = envMK + ji * MKS;
+  constexpr bool kSame = !DISC && !norm_obs;
+  int tb = 0;
+  for (int st = 0; st < T; ++st) {
+    asm volatile("" ::: "memory");
+    if (!det && tb == 0) {  // draw batch: thread t holds the draw (step st + t / k, dim t % k)
+      const int ds = t / kDrawsPerStep, dk = t % kDrawsPerStep;
+      const uint64_t hsh = hash_ctr(key, ulane, (uint64_t)(st + ds), (uint64_t)dk);
+      rbuf = DISC ? uniform24(hsh) : normal_bm(hsh);
+    }
+    // this step's draw: the uniform (discrete) or the normal of action dim o (continuous)
+    const float zt = __builtin_bit_cast(
+        float, __builtin_amdgcn_ds_bpermute(zbase + 4 * kDrawsPerStep * tb, __builtin_bit_cast(int, rbuf)));
+    if constexpr (FEAT & 1) {
+      if (t < NIN && active) a.states[((int64_t)lane * T + st) * NIN + t] = s;
+    }
+    float pre = 0.f;
+    xs[t] = t < NIN ? policy_input(s) : (t == NIN ? 1.f : 0.f);
+    if constexpr (!kSame) h1s[t] = t < NIN ? s : 0.f;
+    wave_lds_sync();
+    const f2 h1 = pl.template layer1_env<kSame>(xs, h1s, mrow, pre);
+    const float y = pl.layers23(h1, h1s, t);
+    if constexpr (DISC) {
+      const float p = pl.softmax(y, t);
+      float pv[NA];
+      row_bcast_all(p, pv, std::make_integer_sequence<int, NA>{});  // pv[i] = p of output i
+      float tot = 0.f;
+#pragma unroll
+      for (int i = 0; i < NA; ++i) tot += pv[i];
+      int act_d = 0;
+      if (det) {
+        float best = pv[0];
+#pragma unroll
+        for (int i = 1; i < NA; ++i) {
+          act_d = pv[i] > best ? i : act_d;
+          best = fmaxf(best, pv[i]);
+        }
+      } else {
+        const float target = zt * tot;
+        float cs = 0.f;
+#pragma unroll
+        for (int i = 0; i < NA - 1; ++i) {
+          cs += pv[i];
+          act_d += cs <= target ? 1 : 0;
+        }
+      }
+      const float pn = p / tot;
+      const float lg = pn > 0.f ? logf(pn) : -FLT_MAX;
+      eacc -= (o < NA) ? pn * lg : 0.f;
+      pre += mrow[NX + act_d];
+    } else {
+      const float th = tanh_fast(y);
+      const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
+      eacc += __builtin_amdgcn_logf(sd);
+      const float act_c = det ? th : gauss_action(th, sd, zt);
+      float kr[NA];
+#pragma unroll
+      for (int m = 0; m < NA; ++m) kr[m] = mrow[NX + m];
+      dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in thread m of both rows of the half
+    }
+    s = tanh_fast(pre);
+    racc += (double)s;  // thread 0 of the half holds the reward s'[0]
+    tb = tb + 1 == kStepsPerBatch ? 0 : tb + 1;
+  }
+
+  if constexpr (!DISC) eacc *= 0.693147180559945309f;
+  double esum = (t < NA) ? (double)eacc : 0.0;  // row 0 of the half: one copy of each output
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) esum += __shfl_xor(esum, m, kWave);
+  if (t == 0 && active) {
+    double r = racc;
+    if (a.jiggle) r += (hash_ctr(key, ulane, kJiggleT, 15) & 1ull) ? 1e-12 : -1e-12;
+    a.ret[lane] = r;
+    double e = esum / (double)T;
+    if constexpr (!DISC) e += (double)NA * 1.4189385332046727;
+    a.ent[lane] = e;
+    a.steps[lane] = T;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Dispatch tables (compiled shapes)
 // ---------------------------------------------------------------------------------------------
 #define FDR_SHAPES(X) \
@@ -667,6 +1045,28 @@ static void launch_feat(const RolloutArgs& args, dim3 grid, dim3 block, hipStrea
 #undef FDR_FEAT_CASE
 }
 
+template <int NIN, int NA, bool DISC>
+static void launch_pair(const RolloutArgs& args, hipStream_t stream) {
+  const dim3 grid((args.n_lanes + 2 * kPairWaves - 1) / (2 * kPairWaves)), block(64 * kPairWaves);
+  const int feat = (args.states ? 1 : 0) | (args.obs_mean ? 4 : 0);
+  switch (feat) {
+    case 0: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 0>), grid, block, 0, stream, args); break;
+    case 1: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 1>), grid, block, 0, stream, args); break;
+    case 4: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 4>), grid, block, 0, stream, args); break;
+    default: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 5>), grid, block, 0, stream, args); break;
+  }
+}
+
+// Synthetic-env rollouts run two lanes per wave (rollout_pair_kernel) unless FDR_ROLLOUT=single
+// (one lane per wave, rollout_kernel); the Welford obs statistics and the trap env always use the latter.
+static bool use_pair_kernel() {
+  static const int v = [] {
+    const char* e = getenv("FDR_ROLLOUT");
+    return (e && strcmp(e, "single") == 0) ? 0 : 1;
+  }();
+  return v != 0;
+}
+
 int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream) {
   const dim3 grid((args.n_lanes + kLanesPerBlock - 1) / kLanesPerBlock), block(64 * kLanesPerBlock);
 #define FDR_ROLL(NIN, NA, DISC)                                                                 \
@@ -674,6 +1074,10 @@ int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hi
     if (Layout<NIN, NA, DISC>::P != k.n_params)                                                 \
       return set_error(FDR_ERR_INVALID, "n_params does not match the policy layout");           \
     if (env_kind == FDR_ENV_SYNTH) {                                                            \
+      if (use_pair_kernel() && !args.os_mean) {                                                 \
+        launch_pair<NIN, NA, DISC>(args, stream);                                               \
+        return check_launch("rollout_pair_kernel<synth>");                                      \
+      }                                                                                         \
       launch_feat<NIN, NA, DISC, FDR_ENV_SYNTH>(args, grid, block, stream);                     \
       return check_launch("rollout_kernel<synth>");                                             \
     }                                                                                           \

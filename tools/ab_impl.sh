@@ -1,0 +1,21 @@
+#!/bin/bash
+# A/B of the rollout implementations (FDR_ROLLOUT=single|pair) on the GPU box, then the GPU parity
+# tests on the default build.  Stops at the first fault / timeout.
+set -u
+mkdir -p gpurun_out
+FAULT='HSA_STATUS_ERROR|illegal memory access|Memory access fault|hipErrorIllegalAddress'
+export FDR_LIB=$PWD/dfd-starter_amd/fdr/libfdr.so
+for impl in ${IMPLS:-single pair single pair}; do
+  for c in ${CONFIGS:-halfcheetah cartpole}; do
+    FDR_ROLLOUT=$impl timeout -k 10 120 python tools/rollout_phases.py --config $c --iters 15 \
+      > gpurun_out/ab_${impl}_${c}.log 2>&1; rc=$?
+    if [ $rc -ne 0 ] || grep -qE "$FAULT" gpurun_out/ab_${impl}_${c}.log; then
+      echo "$impl $c FAIL rc=$rc"; tail -5 gpurun_out/ab_${impl}_${c}.log; exit 3; fi
+    echo "$impl $c: $(grep evaluate gpurun_out/ab_${impl}_${c}.log)"
+  done
+done
+if [ -z "${NO_PARITY:-}" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    > gpurun_out/ab_parity.log 2>&1; rc=$?
+  echo "parity rc=$rc"; tail -8 gpurun_out/ab_parity.log
+fi
