@@ -99,6 +99,7 @@ extern "C" {
 
 const char* fdr_version(void) { return "fdr 0.1 gfx950"; }
 const char* fdr_last_error(void) { return g_err.c_str(); }
+int fdr_rollout_set_impl(int32_t impl) { return fdr::set_rollout_impl(impl); }
 
 int fdr_ctx_create(int device, fdr_ctx** out) {
   if (!out) return set_error(FDR_ERR_INVALID, "out is NULL");

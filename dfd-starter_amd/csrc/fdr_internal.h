@@ -85,6 +85,7 @@ int launch_policy_forward(const PolicyKey& k, const LanesArgs& lanes, int n_lane
                           const float* bn_mean, const float* bn_var, const float* x, float* out0,
                           float* out1, hipStream_t stream);
 int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream);
+int set_rollout_impl(int impl);
 
 // Delayed-return perturbation rows (fdr_fd_lambda_norms / fdr_fd_grad_lambda), by value to kernels.
 int64_t bn_refresh_workspace_bytes(int n);

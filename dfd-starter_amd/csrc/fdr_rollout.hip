@@ -647,6 +647,39 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
 // ---------------------------------------------------------------------------------------------
 constexpr int kPairWaves = 2;  // waves per workgroup (4 lanes): 4 workgroups, 8 waves per CU
 
+// 16-slot reduce-scatter over the 8 threads of a half-row: v[i] += partner(c ^ 7).v[i + 8] (i < 8),
+// v[i] += partner(c ^ 2).v[i + 4] (i < 4), v[i] += partner(c ^ 1).v[i + 2] (i < 2).  s_nop: a DPP read
+// of a VGPR needs 2 wait states after its VALU write.
+__device__ __forceinline__ void reduce_scatter16(float (&v)[16]) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %8, %0 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %9, %1 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %2, %10, %2 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %3, %11, %3 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %4, %12, %4 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %5, %13, %5 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %6, %14, %6 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %7, %15, %7 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %4, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %5, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %2, %6, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %3, %7, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %2, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %3, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+      : "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
+}
+
+// tanh_fast on a register pair: packed mul / add / fma around the two exp and two rcp
+__device__ __forceinline__ f2 tanh2_fast(f2 x) {
+  const f2 t = x * f2{2.88539008177792681f, 2.88539008177792681f};
+  const f2 d = f2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + f2{1.f, 1.f};
+  return pk_fma(f2{-2.f, -2.f}, f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)}, f2{1.f, 1.f});
+}
+
 template <int NIN, int NA, bool DISC>
 struct MlpPair {
   using L = Layout<NIN, NA, DISC>;
@@ -660,6 +693,9 @@ struct MlpPair {
   f2 w1a[kW1Lds ? 1 : NX / 2], w1b[kW1Lds ? 1 : NX / 2];
   float b1a, b1b;
   const float4* tile;  // this thread's column of the wave tile (chunk m at tile[m * kWave])
+#ifdef FDR_PAIR_W3_VGPR
+  float w3[32];
+#endif
   f2 w2[64];           // w2[p * 8 + k] = (W2[16r + (c ^ sigma(p))][8c + k], W2[16r + 8 + (c ^ sigma(p))][8c + k])
   float b2a, b2b, b3;
   float a0, c0, a1a, c1a, a1b, c1b, a2a, c2a, a2b, c2b;  // discrete: folded BN
@@ -727,6 +763,16 @@ struct MlpPair {
       b3 = 0.f;
     }
     wave_lds_sync();
+#ifdef FDR_PAIR_W3_VGPR
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const float4 w = my[(2 * kW1Chunks + m) * kWave];
+      w3[4 * m] = w.x;
+      w3[4 * m + 1] = w.y;
+      w3[4 * m + 2] = w.z;
+      w3[4 * m + 3] = w.w;
+    }
+#endif
     a0 = c0 = a1a = c1a = a1b = c1b = a2a = c2a = a2b = c2b = 0.f;
     if constexpr (DISC) {
       if (t < NIN) {
@@ -789,12 +835,17 @@ struct MlpPair {
     }
     const f2 am = am0 + am1, ha = aa0 + aa1, hb = ab0 + ab1;
     env = am.x + am.y;
-    return f2{act1(ha.x + ha.y, a1a, c1a), act1(hb.x + hb.y, a1b, c1b)};
+    if constexpr (DISC) {
+      return f2{act1(ha.x + ha.y, a1a, c1a), act1(hb.x + hb.y, a1b, c1b)};
+    } else {
+      return tanh2_fast(f2{ha.x + ha.y, hb.x + hb.y});
+    }
   }
 
   // Layer 2 and the head: h1 = this thread's layer-1 units (2t, 2t+1); h1s = the half's scratch.
   // Returns the head pre-activation for output o = t & 15 (identical in both rows of the half).
-  __device__ __forceinline__ float layers23(f2 h1, float* h1s, int t) const {
+  template <class Mark>
+  __device__ __forceinline__ float layers23(f2 h1, float* h1s, int t, Mark&& mark) const {
     const int c = t & 7;
     reinterpret_cast<f2*>(h1s)[t] = h1;
     wave_lds_sync();
@@ -809,24 +860,23 @@ struct MlpPair {
       for (int p = 0; p < 8; ++p) acc[p] = pk_fma(w2[p * 8 + k], f2{x[k], x[k]}, acc[p]);
     // reduce-scatter over the 8 threads of the half-row: slot i = acc[i / 2][i % 2], output of
     // slot i = 16r + 8 (i % 2) + (c ^ sigma(i / 2)); partners c ^ 7, c ^ 2, c ^ 1
-    f2 q[4];
+    float sl[16];
 #pragma unroll
-    for (int p = 0; p < 4; ++p)
-      q[p] = f2{acc[p].x + dpp_mov<kDppHalfMirror>(acc[p + 4].x), acc[p].y + dpp_mov<kDppHalfMirror>(acc[p + 4].y)};
-    f2 rr[2];
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-      rr[p] = f2{q[p].x + dpp_mov<kDppQuadXor2>(q[p + 2].x), q[p].y + dpp_mov<kDppQuadXor2>(q[p + 2].y)};
-    const float za = (rr[0].x + dpp_mov<kDppQuadXor1>(rr[1].x)) + b2a;  // unit 16r + c
-    const float zb = (rr[0].y + dpp_mov<kDppQuadXor1>(rr[1].y)) + b2b;  // unit 16r + 8 + c
+    for (int i = 0; i < 16; ++i) sl[i] = (i & 1) ? acc[i >> 1].y : acc[i >> 1].x;
+    reduce_scatter16(sl);  // one asm block: the SLP vectoriser would split the DPP adds into movs
+    const float za = sl[0] + b2a;  // unit 16r + c
+    const float zb = sl[1] + b2b;  // unit 16r + 8 + c
+    mark(1, za);
     float h2a, h2b;
     if constexpr (DISC) {
       h2a = fmaf(fmaxf(za, 0.f), a2a, c2a);
       h2b = fmaf(fmaxf(zb, 0.f), a2b, c2b);
     } else {
-      h2a = tanh_fast(za);
-      h2b = tanh_fast(zb);
+      const f2 h2 = tanh2_fast(f2{za, zb});
+      h2a = h2.x;
+      h2b = h2.y;
     }
+#ifndef FDR_PAIR_W3_VGPR
     float w3[32];
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
@@ -836,11 +886,20 @@ struct MlpPair {
       w3[4 * m + 2] = w.z;
       w3[4 * m + 3] = w.w;
     }
+#endif
+#ifdef FDR_PAIR_HEAD2
     float s0 = 0.f, s1 = 0.f;
     dpp_fma_32x2(s0, s1, h2a, h2b, w3);
     float u = s0 + s1, v = u;
+#else
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // four independent chains of 8
+    dpp_fma_32x4(s0, s1, s2, s3, h2a, h2b, w3);
+    float u = (s0 + s2) + (s1 + s3), v = u;
+#endif
     permlane16_swap(u, v);  // u = row 2h's partial, v = row 2h+1's, in both rows of half h
-    return (u + v) + b3;
+    const float out = (u + v) + b3;
+    mark(2, out);
+    return out;
   }
 
   __device__ __forceinline__ float softmax(float logit, int t) const {
@@ -927,9 +986,27 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
   float* h1s = sc->h1[hh];
   const float* mrow = envMK + ji * MKS;
   constexpr bool kSame = !DISC && !norm_obs;
+#ifndef FDR_PAIR_KR_LDS
+  float kr[DISC ? 1 : NA];  // K row t: loop-invariant, kept in VGPRs
+#pragma unroll
+  for (int m = 0; m < (DISC ? 1 : NA); ++m) kr[m] = mrow[NX + m];
+#endif
   int tb = 0;
+#ifdef FDR_PHASE_STAMPS
+  uint64_t ph_acc[5] = {0, 0, 0, 0, 0};
+  uint64_t ph_last = 0;
+  auto mark = [&](int k, float dep) {
+    uint64_t now;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(now) : "v"(dep));
+    if (k >= 0) ph_acc[k] += now - ph_last;
+    ph_last = now;
+  };
+#else
+  auto mark = [](int, float) {};
+#endif
   for (int st = 0; st < T; ++st) {
     asm volatile("" ::: "memory");
+    mark(-1, s);
     if (!det && tb == 0) {  // draw batch: thread t holds the draw (step st + t / k, dim t % k)
       const int ds = t / kDrawsPerStep, dk = t % kDrawsPerStep;
       const uint64_t hsh = hash_ctr(key, ulane, (uint64_t)(st + ds), (uint64_t)dk);
@@ -946,7 +1023,8 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     if constexpr (!kSame) h1s[t] = t < NIN ? s : 0.f;
     wave_lds_sync();
     const f2 h1 = pl.template layer1_env<kSame>(xs, h1s, mrow, pre);
-    const float y = pl.layers23(h1, h1s, t);
+    mark(0, h1.x);
+    const float y = pl.layers23(h1, h1s, t, mark);
     if constexpr (DISC) {
       const float p = pl.softmax(y, t);
       float pv[NA];
@@ -980,16 +1058,24 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
       const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
       eacc += __builtin_amdgcn_logf(sd);
       const float act_c = det ? th : gauss_action(th, sd, zt);
+#ifdef FDR_PAIR_KR_LDS
       float kr[NA];
 #pragma unroll
       for (int m = 0; m < NA; ++m) kr[m] = mrow[NX + m];
+#endif
+      mark(3, act_c);
       dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in thread m of both rows of the half
     }
     s = tanh_fast(pre);
     racc += (double)s;  // thread 0 of the half holds the reward s'[0]
+    mark(4, s);
     tb = tb + 1 == kStepsPerBatch ? 0 : tb + 1;
   }
 
+#ifdef FDR_PHASE_STAMPS
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    for (int k = 0; k < 5; ++k) g_phase_stamps[k] = ph_acc[k];
+#endif
   if constexpr (!DISC) eacc *= 0.693147180559945309f;
   double esum = (t < NA) ? (double)eacc : 0.0;  // row 0 of the half: one copy of each output
 #pragma unroll
@@ -1057,14 +1143,22 @@ static void launch_pair(const RolloutArgs& args, hipStream_t stream) {
   }
 }
 
-// Synthetic-env rollouts run two lanes per wave (rollout_pair_kernel) unless FDR_ROLLOUT=single
-// (one lane per wave, rollout_kernel); the Welford obs statistics and the trap env always use the latter.
+// Synthetic-env rollouts run two lanes per wave (rollout_pair_kernel) unless FDR_ROLLOUT=single or
+// fdr_rollout_set_impl(FDR_ROLLOUT_SINGLE) (one lane per wave, rollout_kernel); the Welford obs
+// statistics and the trap env always use the latter.
+static int g_rollout_impl = -1;
 static bool use_pair_kernel() {
-  static const int v = [] {
+  if (g_rollout_impl < 0) {
     const char* e = getenv("FDR_ROLLOUT");
-    return (e && strcmp(e, "single") == 0) ? 0 : 1;
-  }();
-  return v != 0;
+    g_rollout_impl = (e && strcmp(e, "single") == 0) ? FDR_ROLLOUT_SINGLE : FDR_ROLLOUT_PAIR;
+  }
+  return g_rollout_impl == FDR_ROLLOUT_PAIR;
+}
+
+int set_rollout_impl(int impl) {
+  if (impl != FDR_ROLLOUT_PAIR && impl != FDR_ROLLOUT_SINGLE) return set_error(FDR_ERR_INVALID, "unknown rollout impl");
+  g_rollout_impl = impl;
+  return FDR_OK;
 }
 
 int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream) {

@@ -13,6 +13,7 @@ FDR_OK, FDR_ERR_INVALID, FDR_ERR_UNSUPPORTED, FDR_ERR_HIP, FDR_ERR_WORKSPACE = 0
 FDR_POLICY_DISCRETE, FDR_POLICY_MUJOCO = 0, 1
 FDR_ENV_SYNTH, FDR_ENV_TRAP = 0, 1
 FDR_DIST_L2, FDR_DIST_TVD, FDR_DIST_W2 = 0, 1, 2
+FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE = 0, 1
 
 EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy", "fdr_ctx_device",
            "fdr_perturb", "fdr_policy_forward", "fdr_rollout", "fdr_fd_weights",
@@ -23,7 +24,7 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_strategy_distances", "fdr_rollout_states", "fdr_rollout_ex", "fdr_obs_stats_merge",
            "fdr_fd_lambda_norms", "fdr_fd_grad_lambda", "fdr_bn_refresh_workspace_bytes", "fdr_bn_refresh",
            "fdr_atari_num_params", "fdr_atari_workspace_bytes", "fdr_atari_rollout",
-           "fdr_atari_forward_workspace_bytes", "fdr_atari_forward")
+           "fdr_atari_forward_workspace_bytes", "fdr_atari_forward", "fdr_rollout_set_impl")
 
 
 class FDRError(RuntimeError):
@@ -100,6 +101,7 @@ def _load():
                                              P, P, P, P, P, P, P, I64, P]),
         "fdr_atari_forward_workspace_bytes": (I64, [I32, I32]),
         "fdr_atari_forward": (ctypes.c_int, [P, ctypes.POINTER(AtariDesc), P, I32, P, P, P, P, I64, P]),
+        "fdr_rollout_set_impl": (ctypes.c_int, [I32]),
         "fdr_fd_weights": (ctypes.c_int, [P, P, I32, F64, I32, I32, P, P, I32, F32, P, P]),
         "fdr_fd_grad_workspace_bytes": (I64, [I32, I64]),
         "fdr_fd_grad": (ctypes.c_int, [P, P, I64, P, P, I32, I64, P, P, I64, P]),

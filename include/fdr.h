@@ -118,6 +118,16 @@ int fdr_rollout(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc*
                 const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
                 const float* obs_mean, const float* obs_std, double* ret, double* ent,
                 int32_t* steps, double* norm2, fdr_stream stream);
+/* Rollout kernel selection for the synthetic env (process-wide; default from the FDR_ROLLOUT
+ * environment variable, "single" = FDR_ROLLOUT_SINGLE, else FDR_ROLLOUT_PAIR):
+ *   FDR_ROLLOUT_PAIR    two lanes per wave (rollout_pair_kernel)
+ *   FDR_ROLLOUT_SINGLE  one lane per wave (rollout_kernel); always used for the trap env and for
+ *                       the Welford observation statistics of fdr_rollout_ex.
+ * Both compute the same episodes; sums are ordered differently (parity tolerances hold for both). */
+#define FDR_ROLLOUT_PAIR 0
+#define FDR_ROLLOUT_SINGLE 1
+int fdr_rollout_set_impl(int32_t impl);
+
 /* Same as fdr_rollout, and also writes every visited raw observation (before normalisation) to
  * states [n_lanes, T, n_in] f32 -- Agent.collect_return(save_states=True), worker/agent.py:36,58-59,
  * the eval states run_sequential.py:143 feeds into the novelty probe set zeta. */

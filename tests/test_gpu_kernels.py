@@ -111,18 +111,21 @@ def test_policy_forward_perturbed_lanes(eng, name):
         np.testing.assert_allclose(out[1].cpu().numpy(), ref[1], atol=1e-5)
 
 
-def _rollout_case(eng, name, L, T, det, seed=7, antithetic=True):
+def _rollout_case(eng, name, L, T, det, seed=7, antithetic=True, idx_seed=None):
     kind, n_in, n_act = SHAPES[name]
     torch.manual_seed(124)
     pol = opol.TorchPolicy(kind, n_in, n_act, seed=124)
     theta = pol.get_flat()
     P = theta.size
     t, tab = table(P)
+    # idx_seed: a private index stream (the same lanes on every call), else the table's own stream
+    draw = t.sample_indices if idx_seed is None else \
+        (lambda n: np.random.RandomState(idx_seed).randint(0, t.max_idx, size=n).astype(np.int64))
     if antithetic:
-        idx = np.repeat(t.sample_indices(L // 2), 2)
+        idx = np.repeat(draw(L // 2), 2)
         sign = np.tile(np.array([1, -1], np.int8), L // 2)
     else:
-        idx = t.sample_indices(L)
+        idx = draw(L)
         sign = np.ones(L, np.int8)
     sign[-2:] = 0                              # two eval lanes
     dflag = np.full(L, 1 if det else 0, np.int8)
@@ -147,6 +150,30 @@ def test_rollout_vs_oracle(eng, name, det):
     np.testing.assert_allclose(res.entropy.cpu().numpy(), r_ent, rtol=1e-5, atol=1e-5)
     assert np.array_equal(res.timesteps.cpu().numpy(), r_steps)
     np.testing.assert_allclose(res.norm2.cpu().numpy(), r_n2, rtol=1e-9, atol=0)
+
+
+@pytest.mark.parametrize("name,L,det", [("cheetah", 13, False), ("cheetah", 7, True), ("cartpole", 13, False),
+                                        ("cartpole", 9, True), ("cheetah", 64, False)])
+def test_rollout_pair_and_single_kernels_agree(eng, name, L, det):
+    """rollout_pair_kernel (two lanes per wave) and rollout_kernel (one lane per wave) against the
+    oracle and each other, incl. odd lane counts (a wave whose second half is idle)."""
+    from fdr._lib import FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, check, lib
+    out = {}
+    try:
+        for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
+            check(lib.fdr_rollout_set_impl(impl), "fdr_rollout_set_impl")
+            out[impl] = _rollout_case(eng, name, L, 120, det, antithetic=L % 2 == 0, idx_seed=L)
+    finally:
+        check(lib.fdr_rollout_set_impl(FDR_ROLLOUT_PAIR), "fdr_rollout_set_impl")
+    for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
+        res, (ref_ret, ref_ent, ref_steps, ref_n2) = out[impl]
+        assert res.reward.numel() == L
+        np.testing.assert_allclose(res.reward.cpu().numpy(), ref_ret, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(res.entropy.cpu().numpy(), ref_ent, rtol=1e-5, atol=1e-5)
+        assert np.array_equal(res.timesteps.cpu().numpy(), ref_steps)
+        np.testing.assert_allclose(res.norm2.cpu().numpy(), ref_n2, rtol=1e-9, atol=0)
+    a, b = out[FDR_ROLLOUT_SINGLE][0], out[FDR_ROLLOUT_PAIR][0]
+    np.testing.assert_allclose(a.reward.cpu().numpy(), b.reward.cpu().numpy(), rtol=1e-5, atol=1e-5)
 
 
 def test_rollout_reproducible_and_antithetic_norms(eng):

@@ -4,14 +4,16 @@
 set -u
 mkdir -p gpurun_out
 FAULT='HSA_STATUS_ERROR|illegal memory access|Memory access fault|hipErrorIllegalAddress'
-export FDR_LIB=$PWD/dfd-starter_amd/fdr/libfdr.so
-for impl in ${IMPLS:-single pair single pair}; do
+# RUNS: space-separated <lib>:<impl> pairs (lib = file stem under dfd-starter_amd/fdr/)
+for run in ${RUNS:-libfdr:single libfdr:pair libfdr:single libfdr:pair}; do
+  lib=${run%%:*}; impl=${run##*:}
   for c in ${CONFIGS:-halfcheetah cartpole}; do
-    FDR_ROLLOUT=$impl timeout -k 10 120 python tools/rollout_phases.py --config $c --iters 15 \
-      > gpurun_out/ab_${impl}_${c}.log 2>&1; rc=$?
-    if [ $rc -ne 0 ] || grep -qE "$FAULT" gpurun_out/ab_${impl}_${c}.log; then
-      echo "$impl $c FAIL rc=$rc"; tail -5 gpurun_out/ab_${impl}_${c}.log; exit 3; fi
-    echo "$impl $c: $(grep evaluate gpurun_out/ab_${impl}_${c}.log)"
+    log=gpurun_out/ab_${lib}_${impl}_${c}.log
+    FDR_LIB=$PWD/dfd-starter_amd/fdr/$lib.so FDR_ROLLOUT=$impl timeout -k 10 120 \
+      python tools/rollout_phases.py --config $c --iters 15 > $log 2>&1; rc=$?
+    if [ $rc -ne 0 ] || grep -qE "$FAULT" $log; then
+      echo "$lib $impl $c FAIL rc=$rc"; tail -5 $log; exit 3; fi
+    echo "$lib $impl $c: $(grep evaluate $log)"
   done
 done
 if [ -z "${NO_PARITY:-}" ]; then
