@@ -271,7 +271,10 @@ def main():
         achieved_tf = flops / (rollout_ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                    "kernel": "rollout_kernel<17,6,mujoco,synth>", "rollout_ms": round(rollout_ms, 4),
+                    "kernel": ("rollout_kernel<17,6,mujoco,synth> (one lane per wave)"
+                               if os.environ.get("FDR_ROLLOUT") == "single" else
+                               "rollout_pair_kernel<17,6,mujoco> (two lanes per wave)"),
+                    "rollout_ms": round(rollout_ms, 4),
                     "flop_per_lane_step": lane_step_flops(kind, n_in, n_act),
                     "note": "fp32 VALU/matrix peak; theta' is VGPR-resident for the whole episode, so the "
                             "kernel is compute-bound (DESIGN.md 'Roofline')",
