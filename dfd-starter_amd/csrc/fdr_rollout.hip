@@ -806,22 +806,38 @@ struct MlpPair {
     }
   }
 
+  // Loop-invariant LDS rows of layer 1 (W1 rows 2t, 2t+1 when kW1Lds) and the env's M row t, loaded
+  // a phase ahead of their use (after the head of the previous step), off the step's dependency chain.
+  struct L1Rows {
+    float4 wa[kW1Lds ? NX / 4 : 1], wb[kW1Lds ? NX / 4 : 1], m[NX / 4];
+  };
+  __device__ __forceinline__ void l1_prefetch(L1Rows& r, const float* mrow) const {
+    const float4* m4 = reinterpret_cast<const float4*>(mrow);
+#pragma unroll
+    for (int q = 0; q < NX / 4; ++q) {
+      if constexpr (kW1Lds) {
+        r.wa[q] = tile[q * kWave];
+        r.wb[q] = tile[(kW1Chunks + q) * kWave];
+      }
+      r.m[q] = m4[q];
+    }
+  }
+
   // Layer 1 (units 2t, 2t+1) and the env's M[t] . s in one pass over the broadcast input chunks.
   template <bool kSameInput>
-  __device__ __forceinline__ f2 layer1_env(const float* xs, const float* ss, const float* mrow, float& env) const {
+  __device__ __forceinline__ f2 layer1_env(const float* xs, const float* ss, const L1Rows& rows, float& env) const {
     const float4* x4 = reinterpret_cast<const float4*>(xs);
     const float4* s4 = reinterpret_cast<const float4*>(ss);
-    const float4* m4 = reinterpret_cast<const float4*>(mrow);
     f2 aa0 = {b1a, 0.f}, aa1 = {0.f, 0.f}, ab0 = {b1b, 0.f}, ab1 = {0.f, 0.f};
     f2 am0 = {0.f, 0.f}, am1 = {0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < NX / 4; ++q) {
-      const float4 xv = x4[q], mv = m4[q];
+      const float4 xv = x4[q], mv = rows.m[q];
       const float4 sv = kSameInput ? xv : s4[q];
       float4 wa, wb;
       if constexpr (kW1Lds) {
-        wa = tile[q * kWave];
-        wb = tile[(kW1Chunks + q) * kWave];
+        wa = rows.wa[q];
+        wb = rows.wb[q];
       } else {
         wa = float4{w1a[2 * q].x, w1a[2 * q].y, w1a[2 * q + 1].x, w1a[2 * q + 1].y};
         wb = float4{w1b[2 * q].x, w1b[2 * q].y, w1b[2 * q + 1].x, w1b[2 * q + 1].y};
@@ -986,6 +1002,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
   float* h1s = sc->h1[hh];
   const float* mrow = envMK + ji * MKS;
   constexpr bool kSame = !DISC && !norm_obs;
+  typename Lane::L1Rows l1rows;
+#ifndef FDR_PAIR_NO_PREFETCH
+  pl.l1_prefetch(l1rows, mrow);
+#endif
 #ifndef FDR_PAIR_KR_LDS
   float kr[DISC ? 1 : NA];  // K row t: loop-invariant, kept in VGPRs
 #pragma unroll
@@ -1022,9 +1042,15 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     xs[t] = t < NIN ? policy_input(s) : (t == NIN ? 1.f : 0.f);
     if constexpr (!kSame) h1s[t] = t < NIN ? s : 0.f;
     wave_lds_sync();
-    const f2 h1 = pl.template layer1_env<kSame>(xs, h1s, mrow, pre);
+#ifdef FDR_PAIR_NO_PREFETCH
+    pl.l1_prefetch(l1rows, mrow);
+#endif
+    const f2 h1 = pl.template layer1_env<kSame>(xs, h1s, l1rows, pre);
     mark(0, h1.x);
     const float y = pl.layers23(h1, h1s, t, mark);
+#ifndef FDR_PAIR_NO_PREFETCH
+    pl.l1_prefetch(l1rows, mrow);  // next step's rows, in flight during the action and env phases
+#endif
     if constexpr (DISC) {
       const float p = pl.softmax(y, t);
       float pv[NA];
