@@ -97,11 +97,9 @@ class FiniteDifferences(object):
         return self._out
 
     def _build_distance_map(self):
-        # finite_differences.py:66-73 (device copies of the recent parameter vectors)
-        flat = self.policy.flat.detach()
-        self.dist_map = {self.epoch: None}
-        for params, ep in self.policy_history:
-            self.dist_map[ep] = params - flat
+        # finite_differences.py:66-73: dist_map[ep] = theta_ep - theta_now for the recent epochs.  The
+        # differences are formed on first use (only stale returns read them), not eagerly every step.
+        self.dist_map = _LazyDistMap(self.epoch, self.policy_history, self.policy.flat.detach())
 
     def _update_policy_history(self):
         self.policy_history.append((self.policy.flat.detach().clone(), self.epoch))
@@ -160,3 +158,35 @@ class FiniteDifferences(object):
             n2 = engine.fd_lambda_norms(table, idx_d, sign_d, None, self.noise_std, None, P)
         b = FDBatch(rewards, None, None, n2, idx_d, sign_d, idx, sign, self.epoch)
         return self._step_batch(b, policy_reward)
+
+
+class _LazyDistMap(object):
+    """The learner's epoch -> drift map (finite_differences.py:66-73) with the same keys and values as the
+    reference's eager dict: None for the current epoch, theta_ep - theta_now (device f32) for the epochs
+    in the policy history.  A difference is computed on first access and cached; theta_now is the
+    learner's parameter tensor, which only changes in the next step, when the map is rebuilt."""
+
+    def __init__(self, epoch, history, flat):
+        self._cur = epoch
+        self._hist = {ep: params for params, ep in history}
+        self._flat = flat
+        self._cache = {}
+
+    def __contains__(self, ep):
+        return ep == self._cur or ep in self._hist
+
+    def __getitem__(self, ep):
+        if ep in self._hist:
+            if ep not in self._cache:
+                self._cache[ep] = self._hist[ep] - self._flat
+            return self._cache[ep]
+        if ep == self._cur:
+            return None
+        raise KeyError(ep)
+
+    def keys(self):
+        return [self._cur] + [ep for ep in self._hist if ep != self._cur]
+
+    def __len__(self):
+        return len(self.keys())
+

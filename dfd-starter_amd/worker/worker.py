@@ -60,13 +60,21 @@ class Worker(object):
         ring["events"][slot] = ev
         return out
 
+    def _lanes_to_device(self, idx, sign, det):
+        """The three per-lane descriptor arrays in ONE host-to-device copy: [idx i64 | sign i8 | det i8]."""
+        n = len(idx)
+        packed = np.empty(10 * n, np.uint8)
+        packed[:8 * n] = np.asarray(idx, np.int64).view(np.uint8)
+        packed[8 * n:9 * n] = np.asarray(sign, np.int8).view(np.uint8)
+        packed[9 * n:] = np.asarray(det, np.int8).view(np.uint8)
+        d = self._to_device(packed, torch.uint8)
+        return d[:8 * n].view(torch.int64), d[8 * n:9 * n].view(torch.int8), d[9 * n:].view(torch.int8)
+
     def launch(self, idx, sign, det, seed=None, out=None, jiggle=True, lane_offset=0):
         """Run one rollout over explicit lanes (host arrays) -> FDBatch (asynchronous)."""
         p = self.policy
         n = len(idx)
-        idx_d = self._to_device(np.asarray(idx, np.int64), torch.int64)
-        sign_d = self._to_device(np.asarray(sign, np.int8), torch.int8)
-        det_d = self._to_device(np.asarray(det, np.int8), torch.int8)
+        idx_d, sign_d, det_d = self._lanes_to_device(idx, sign, det)
         table = self.noise_source.device_table(p.flat.device)
         lanes = engine.lanes_desc(p.flat, 0, table, idx_d, sign_d, self.sigma, det_d, lane_offset)
         bm, bv = p.bn_stats()
