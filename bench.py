@@ -40,6 +40,7 @@ CONFIGS = {
     # BASELINE config 5 per GPU: as config 4 with A = 4 and fp16 rollouts
     "impala_fp16": ("impala", (64, 64, 3), 4, "frames", 1000),
 }
+DEFAULT_LANES = {"halfcheetah": 4096, "cartpole": 1024}   # BASELINE configs 3 and 2
 IMPALA_ENVS = 4
 IMPALA_LANES = 1024
 # ImpalaCNN conv stack, algorithmic FLOPs per env step: sum over the 15 convs of 2*Cin*9*Cout*Ho*Wo
@@ -47,6 +48,16 @@ IMPALA_CONV_FLOP = 2 * 9 * (3 * 16 * 64 * 64 + 4 * 16 * 16 * 32 * 32 + 16 * 32 *
                             + 32 * 32 * 16 * 16 + 4 * 32 * 32 * 8 * 8)
 # fc + LSTM + head weights streamed per (lane, step) by the core kernel (f32)
 IMPALA_CORE_BYTES = 4 * (2048 * 256 + 257 * 1024 + 256 * 1024)
+
+
+def rollout_kernel_name(kind, n_in, n_act, lanes, dev):
+    """Which synthetic-env rollout kernel fdr_rollout picks (FDR_ROLLOUT / auto rule, include/fdr.h)."""
+    import torch
+    mode = os.environ.get("FDR_ROLLOUT", "auto")
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    pair = mode == "pair" or (mode != "single" and lanes >= 16 * cus)
+    return ("rollout_pair_kernel<%d,%d,%s> (two lanes per wave)" if pair else
+            "rollout_kernel<%d,%d,%s,synth> (one lane per wave)") % (n_in, n_act, kind)
 
 
 def lane_step_flops(kind, n_in, n_act):
@@ -127,7 +138,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="halfcheetah", choices=list(CONFIGS))
-    ap.add_argument("--perturbations", type=int, default=4096, help="antithetic lanes per GPU")
+    ap.add_argument("--perturbations", type=int, default=None,
+                    help="antithetic lanes per GPU (default: the BASELINE config's -- 4096 halfcheetah, "
+                         "1024 cartpole, 1024 x 4 envs impala)")
     ap.add_argument("--episode-len", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -186,7 +199,7 @@ def main():
     omega = AdaptiveOmega()
     learner = FiniteDifferences(policy, DSGD(policy.parameters(), lr=0.01), omega, table, noise_std=0.02)
 
-    L = args.perturbations if not impala or args.perturbations != 4096 else IMPALA_LANES
+    L = args.perturbations or (IMPALA_LANES if impala else DEFAULT_LANES.get(args.config, 4096))
     E = IMPALA_ENVS if impala else 1
     n_dirs_global = (L // 2) * world
     from fdr import dist as fdist
@@ -271,9 +284,7 @@ def main():
         achieved_tf = flops / (rollout_ms * 1e-3) / 1e12
         roofline = {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                    "kernel": ("rollout_kernel<17,6,mujoco,synth> (one lane per wave)"
-                               if os.environ.get("FDR_ROLLOUT") == "single" else
-                               "rollout_pair_kernel<17,6,mujoco> (two lanes per wave)"),
+                    "kernel": rollout_kernel_name(kind, n_in, n_act, L, dev),
                     "rollout_ms": round(rollout_ms, 4),
                     "flop_per_lane_step": lane_step_flops(kind, n_in, n_act),
                     "note": "fp32 VALU/matrix peak; theta' is VGPR-resident for the whole episode, so the "

@@ -1169,20 +1169,33 @@ static void launch_pair(const RolloutArgs& args, hipStream_t stream) {
   }
 }
 
-// Synthetic-env rollouts run two lanes per wave (rollout_pair_kernel) unless FDR_ROLLOUT=single or
-// fdr_rollout_set_impl(FDR_ROLLOUT_SINGLE) (one lane per wave, rollout_kernel); the Welford obs
-// statistics and the trap env always use the latter.
+// Synthetic-env rollouts: rollout_pair_kernel (two lanes per wave) or rollout_kernel (one lane per
+// wave).  FDR_ROLLOUT_AUTO (default) takes the pair kernel once it puts >= 2 waves on every SIMD
+// (n_lanes >= 4 x SIMDs; measured DESIGN.md 3.0: below that the one-lane kernel's extra waves win);
+// FDR_ROLLOUT=pair|single|auto or fdr_rollout_set_impl overrides.  The Welford obs statistics and the
+// trap env always use rollout_kernel.
 static int g_rollout_impl = -1;
-static bool use_pair_kernel() {
+static int rollout_impl() {
   if (g_rollout_impl < 0) {
     const char* e = getenv("FDR_ROLLOUT");
-    g_rollout_impl = (e && strcmp(e, "single") == 0) ? FDR_ROLLOUT_SINGLE : FDR_ROLLOUT_PAIR;
+    g_rollout_impl = !e ? FDR_ROLLOUT_AUTO
+                        : strcmp(e, "single") == 0 ? FDR_ROLLOUT_SINGLE
+                                                   : strcmp(e, "pair") == 0 ? FDR_ROLLOUT_PAIR : FDR_ROLLOUT_AUTO;
   }
-  return g_rollout_impl == FDR_ROLLOUT_PAIR;
+  return g_rollout_impl;
+}
+static bool use_pair_kernel(int n_lanes) {
+  const int impl = rollout_impl();
+  if (impl != FDR_ROLLOUT_AUTO) return impl == FDR_ROLLOUT_PAIR;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  return n_lanes >= 4 * 4 * cus;  // 4 SIMDs per CU, 2 lanes x 2 waves per SIMD
 }
 
 int set_rollout_impl(int impl) {
-  if (impl != FDR_ROLLOUT_PAIR && impl != FDR_ROLLOUT_SINGLE) return set_error(FDR_ERR_INVALID, "unknown rollout impl");
+  if (impl != FDR_ROLLOUT_PAIR && impl != FDR_ROLLOUT_SINGLE && impl != FDR_ROLLOUT_AUTO)
+    return set_error(FDR_ERR_INVALID, "unknown rollout impl");
   g_rollout_impl = impl;
   return FDR_OK;
 }
@@ -1194,7 +1207,7 @@ int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hi
     if (Layout<NIN, NA, DISC>::P != k.n_params)                                                 \
       return set_error(FDR_ERR_INVALID, "n_params does not match the policy layout");           \
     if (env_kind == FDR_ENV_SYNTH) {                                                            \
-      if (use_pair_kernel() && !args.os_mean) {                                                 \
+      if (use_pair_kernel(args.n_lanes) && !args.os_mean) {                                                 \
         launch_pair<NIN, NA, DISC>(args, stream);                                               \
         return check_launch("rollout_pair_kernel<synth>");                                      \
       }                                                                                         \

@@ -119,13 +119,15 @@ int fdr_rollout(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc*
                 const float* obs_mean, const float* obs_std, double* ret, double* ent,
                 int32_t* steps, double* norm2, fdr_stream stream);
 /* Rollout kernel selection for the synthetic env (process-wide; default from the FDR_ROLLOUT
- * environment variable, "single" = FDR_ROLLOUT_SINGLE, else FDR_ROLLOUT_PAIR):
- *   FDR_ROLLOUT_PAIR    two lanes per wave (rollout_pair_kernel, DESIGN.md 3.1)
+ * environment variable: "pair", "single", else FDR_ROLLOUT_AUTO):
+ *   FDR_ROLLOUT_PAIR    two lanes per wave (rollout_pair_kernel, DESIGN.md 3.0)
  *   FDR_ROLLOUT_SINGLE  one lane per wave (rollout_kernel); always used for the trap env and for
- *                       the Welford observation statistics of fdr_rollout_ex.
+ *                       the Welford observation statistics of fdr_rollout_ex
+ *   FDR_ROLLOUT_AUTO    the pair kernel when n_lanes >= 16 x CUs (two pair waves per SIMD), else single
  * Both compute the same episodes; sums are ordered differently (parity tolerances hold for both). */
 #define FDR_ROLLOUT_PAIR 0
 #define FDR_ROLLOUT_SINGLE 1
+#define FDR_ROLLOUT_AUTO 2
 int fdr_rollout_set_impl(int32_t impl);
 
 /* Same as fdr_rollout, and also writes every visited raw observation (before normalisation) to

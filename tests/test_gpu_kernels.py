@@ -157,14 +157,14 @@ def test_rollout_vs_oracle(eng, name, det):
 def test_rollout_pair_and_single_kernels_agree(eng, name, L, det):
     """rollout_pair_kernel (two lanes per wave) and rollout_kernel (one lane per wave) against the
     oracle and each other, incl. odd lane counts (a wave whose second half is idle)."""
-    from fdr._lib import FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, check, lib
+    from fdr._lib import FDR_ROLLOUT_AUTO, FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, check, lib
     out = {}
     try:
         for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
             check(lib.fdr_rollout_set_impl(impl), "fdr_rollout_set_impl")
             out[impl] = _rollout_case(eng, name, L, 120, det, antithetic=L % 2 == 0, idx_seed=L)
     finally:
-        check(lib.fdr_rollout_set_impl(FDR_ROLLOUT_PAIR), "fdr_rollout_set_impl")
+        check(lib.fdr_rollout_set_impl(FDR_ROLLOUT_AUTO), "fdr_rollout_set_impl")
     for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
         res, (ref_ret, ref_ent, ref_steps, ref_n2) = out[impl]
         assert res.reward.numel() == L

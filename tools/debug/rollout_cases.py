@@ -20,4 +20,4 @@ for name in ("cheetah", "cartpole"):
                 d = np.abs(res.reward.cpu().numpy() - ref[0])
                 row.append("%s max %.2e bad %d" % ("single" if impl else "pair", d.max(), int((d > 1e-3).sum())))
             print(name, "L=%d anti=%d det=%d:" % (L, anti, det), " | ".join(row), flush=True)
-lib.fdr_rollout_set_impl(0)
+lib.fdr_rollout_set_impl(2)
