@@ -693,9 +693,6 @@ struct MlpPair {
   f2 w1a[kW1Lds ? 1 : NX / 2], w1b[kW1Lds ? 1 : NX / 2];
   float b1a, b1b;
   const float4* tile;  // this thread's column of the wave tile (chunk m at tile[m * kWave])
-#ifdef FDR_PAIR_W3_VGPR
-  float w3[32];
-#endif
   f2 w2[64];           // w2[p * 8 + k] = (W2[16r + (c ^ sigma(p))][8c + k], W2[16r + 8 + (c ^ sigma(p))][8c + k])
   float b2a, b2b, b3;
   float a0, c0, a1a, c1a, a1b, c1b, a2a, c2a, a2b, c2b;  // discrete: folded BN
@@ -751,7 +748,8 @@ struct MlpPair {
         float e[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int w = 4 * m + i;  // w < 16: value z.x of row-thread w; else z.y of row-thread w - 16
+          const int w = 4 * m + i;
+          // w < 16: value z.x of row-thread w; else z.y of row-thread w - 16
           e[i] = src.get(L::L3W + (int64_t)o * kHidden + head_unit(rho, w & 15, w >> 4));
         }
         my[(2 * kW1Chunks + m) * kWave] = float4{e[0], e[1], e[2], e[3]};
@@ -763,16 +761,6 @@ struct MlpPair {
       b3 = 0.f;
     }
     wave_lds_sync();
-#ifdef FDR_PAIR_W3_VGPR
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const float4 w = my[(2 * kW1Chunks + m) * kWave];
-      w3[4 * m] = w.x;
-      w3[4 * m + 1] = w.y;
-      w3[4 * m + 2] = w.z;
-      w3[4 * m + 3] = w.w;
-    }
-#endif
     a0 = c0 = a1a = c1a = a1b = c1b = a2a = c2a = a2b = c2b = 0.f;
     if constexpr (DISC) {
       if (t < NIN) {
@@ -892,7 +880,6 @@ struct MlpPair {
       h2a = h2.x;
       h2b = h2.y;
     }
-#ifndef FDR_PAIR_W3_VGPR
     float w3[32];
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
@@ -902,16 +889,9 @@ struct MlpPair {
       w3[4 * m + 2] = w.z;
       w3[4 * m + 3] = w.w;
     }
-#endif
-#ifdef FDR_PAIR_HEAD2
-    float s0 = 0.f, s1 = 0.f;
-    dpp_fma_32x2(s0, s1, h2a, h2b, w3);
-    float u = s0 + s1, v = u;
-#else
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // four independent chains of 8
     dpp_fma_32x4(s0, s1, s2, s3, h2a, h2b, w3);
     float u = (s0 + s2) + (s1 + s3), v = u;
-#endif
     permlane16_swap(u, v);  // u = row 2h's partial, v = row 2h+1's, in both rows of half h
     const float out = (u + v) + b3;
     mark(2, out);
