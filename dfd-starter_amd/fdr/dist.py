@@ -32,21 +32,34 @@ def lane_range(n_dirs, lanes_per_dir, world, rank):
     return d_lo * lanes_per_dir, d_hi * lanes_per_dir
 
 
-def gather_rewards(local, group=None):
-    """All-gather variable-length per-lane rewards -> (all rewards in rank order, this rank's offset)."""
+def gather_rewards(local, group=None, sizes=None):
+    """All-gather per-lane rewards -> (all rewards in rank order, this rank's offset).
+
+    sizes: every rank's lane count, when the caller knows the split (Worker.evaluate's standard
+    lane_range split sets FDBatch.rank_lanes): then the exchange is ONE all-gather issued on the
+    stream with no host synchronisation.  Without it the counts are exchanged first (a host sync)."""
     ws, rank = world_rank(group)
     if ws == 1:
         return local, 0
-    n = torch.tensor([local.numel()], dtype=torch.int64, device=local.device)
-    sizes = [torch.zeros_like(n) for _ in range(ws)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s.item()) for s in sizes]
+    if sizes is None:
+        n = torch.tensor([local.numel()], dtype=torch.int64, device=local.device)
+        counts = torch.empty(ws, dtype=torch.int64, device=local.device)
+        dist.all_gather_into_tensor(counts, n, group=group)
+        sizes = counts.tolist()
+    sizes = [int(s) for s in sizes]
+    if len(sizes) != ws or sizes[rank] != local.numel():
+        raise ValueError("gather_rewards: sizes %s do not match this rank's %d lanes" % (sizes, local.numel()))
     m = max(sizes)
-    buf = torch.zeros(m, dtype=local.dtype, device=local.device)
-    buf[:local.numel()] = local
-    outs = [torch.empty_like(buf) for _ in range(ws)]
-    dist.all_gather(outs, buf, group=group)
-    return torch.cat([o[:s] for o, s in zip(outs, sizes)]), sum(sizes[:rank])
+    if local.numel() == m:
+        buf = local.contiguous()
+    else:
+        buf = torch.zeros(m, dtype=local.dtype, device=local.device)
+        buf[:local.numel()] = local
+    out = torch.empty(ws * m, dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    if all(s == m for s in sizes):
+        return out, rank * m
+    return torch.cat([out[k * m:k * m + s] for k, s in enumerate(sizes)]), sum(sizes[:rank])
 
 
 def allreduce_grad(g, group=None):

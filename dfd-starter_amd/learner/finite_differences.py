@@ -72,7 +72,7 @@ class FiniteDifferences(object):
         if not bool(train.all()):
             raise ValueError("FDBatch for the learner must not contain eval lanes (sign 0)")
         P = self.policy.num_params
-        rewards_all, lane_lo = fdist.gather_rewards(b.reward, self.process_group)
+        rewards_all, lane_lo = fdist.gather_rewards(b.reward, self.process_group, getattr(b, "rank_lanes", None))
         coef = engine.fd_weights(rewards_all, policy_reward, lane_lo, b.sign, b.norm2, b.lanes_per_dir,
                                  self.noise_std)
         g = engine.fd_grad(table, b.dir_idx(), coef, P, self.gradient_memory)

@@ -107,9 +107,15 @@ class Worker(object):
         lpd = 2 if antithetic else 1
         lidx = np.repeat(idx, lpd)
         sign = np.tile(np.array([1, -1], np.int8), n_dirs) if antithetic else np.ones(n_dirs, np.int8)
-        if lane_range == "auto":
+        rank_lanes = None
+        if lane_range is not None:
             from fdr import dist as fdist
-            lane_range = fdist.lane_range(n_dirs, lpd, *fdist.world_rank())
+            world, rank = fdist.world_rank()
+            std = fdist.lane_range(n_dirs, lpd, world, rank)
+            if lane_range == "auto":
+                lane_range = std
+            if tuple(lane_range) == std:  # the standard split: every rank's lane count is known
+                rank_lanes = [hi - lo for lo, hi in (fdist.lane_range(n_dirs, lpd, world, k) for k in range(world))]
         if lane_range is not None:
             lo, hi = lane_range
             if lo % lpd or hi % lpd:
@@ -126,6 +132,7 @@ class Worker(object):
         b = FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, lidx, sign, self.epoch,
                     lanes_per_dir=lpd * E, novelty=nov)
         b.obs_stats = obs_partials(res)
+        b.rank_lanes = None if rank_lanes is None else [k * E for k in rank_lanes]
         return b
 
     # ---- reference API ----------------------------------------------------------------------

@@ -51,6 +51,13 @@ def _rank_main(rank, world, port, out_dir):
     local = torch.as_tensor(rewards[lo:hi])
     r_all, lane_lo = fdist.gather_rewards(local)
     assert lane_lo == lo and np.array_equal(r_all.numpy(), rewards)
+    # known split (Worker.evaluate's FDBatch.rank_lanes): one all-gather, no count exchange
+    sizes = [b - a for a, b in (fdist.lane_range(D, 2, world, k) for k in range(world))]
+    r_all2, lane_lo2 = fdist.gather_rewards(local, sizes=sizes)
+    assert lane_lo2 == lo and np.array_equal(r_all2.numpy(), rewards)
+    even = torch.as_tensor(rewards[:2 * world][2 * rank:2 * rank + 2])   # equal counts: no re-packing
+    r_even, lo_even = fdist.gather_rewards(even, sizes=[2] * world)
+    assert lo_even == 2 * rank and np.array_equal(r_even.numpy(), rewards[:2 * world])
     # coefficient of every local lane with the GLOBAL z-score, then the local partial gradient
     x = r_all.numpy() - 0.1
     m, s = x.mean(), x.std()
