@@ -176,6 +176,50 @@ def test_rollout_pair_and_single_kernels_agree(eng, name, L, det):
     np.testing.assert_allclose(a.reward.cpu().numpy(), b.reward.cpu().numpy(), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("name", ["cheetah", "cartpole"])
+def test_rollout_kernels_obs_norm_and_states_vs_oracle(eng, name):
+    """FEAT paths of both synthetic-env kernels (observation normalisation, visited states, both) against
+    the oracle, with the kernel forced (auto would pick the one-lane kernel at this lane count)."""
+    from envs import SyntheticEnv
+    from fdr._lib import FDR_ROLLOUT_AUTO, FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, check, lib
+    kind, n_in, n_act = SHAPES[name]
+    torch.manual_seed(124)
+    pol = opol.TorchPolicy(kind, n_in, n_act, seed=124)
+    theta = pol.get_flat()
+    t, tab = table(theta.size)
+    L, T, seed = 13, 80, 5
+    idx = np.random.RandomState(11).randint(0, t.max_idx, size=L).astype(np.int64)
+    sign = np.ones(L, np.int8)
+    sign[-1] = 0
+    om = np.linspace(-0.2, 0.2, n_in).astype(np.float32)
+    osd = np.linspace(0.5, 1.5, n_in).astype(np.float32)
+    spec = eng.PolicySpec(kind, n_in, n_act, theta.size)
+    lanes = eng.lanes_desc(dev(theta), 0, tab, dev(idx, torch.int64), dev(sign), 0.02)
+    env = SyntheticEnv(n_in, n_act, kind == "discrete", T, env_seed=0)
+    oenv = oenvs.BatchedSyntheticEnv(n_in, n_act, kind == "discrete", T, L, env_seed=0)
+    ref = oagent.evaluate_lanes(kind, n_in, n_act, theta, t.table, idx, sign, 0.02, oenv, seed, obs_mean=om,
+                                obs_std=osd, record_states=True)
+    ref_states = ref[-1]
+    try:
+        for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
+            check(lib.fdr_rollout_set_impl(impl), "fdr_rollout_set_impl")
+            for norm, rec in ((True, False), (False, True), (True, True)):
+                states = torch.empty((L, T, n_in), dtype=torch.float32, device=DEV) if rec else None
+                res = eng.rollout(spec, env, lanes, L, seed, obs_mean=dev(om) if norm else None,
+                                  obs_std=dev(osd) if norm else None, states=states)
+                torch.cuda.synchronize()
+                if norm:
+                    np.testing.assert_allclose(res.reward.cpu().numpy(), ref[0], rtol=1e-4, atol=1e-4)
+                    np.testing.assert_allclose(res.entropy.cpu().numpy(), ref[1], rtol=1e-5, atol=1e-5)
+                if rec and norm:
+                    np.testing.assert_allclose(states.cpu().numpy(), ref_states, atol=1e-4)
+                if rec and not norm:
+                    S = states.cpu().numpy()
+                    np.testing.assert_array_equal(S[:, 0], np.broadcast_to(ref_states[0, 0], S[:, 0].shape))
+    finally:
+        check(lib.fdr_rollout_set_impl(FDR_ROLLOUT_AUTO), "fdr_rollout_set_impl")
+
+
 def test_rollout_reproducible_and_antithetic_norms(eng):
     torch.manual_seed(124)
     pol = opol.TorchPolicy("mujoco", 17, 6, seed=124)
