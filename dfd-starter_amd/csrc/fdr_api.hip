@@ -393,6 +393,8 @@ int fdr_impala_debug_clock(uint64_t* buf) {
   return FDR_OK;
 }
 
+int fdr_impala_set_replay_gemm(int32_t on) { return impala::set_replay_gemm(on); }
+
 int fdr_strategy_distances(fdr_ctx* ctx, const float* strategies, int32_t n, const float* archive, int32_t n_archive,
                            int32_t n_states, int32_t dim, int32_t kind, double* dists, double* min_dist,
                            int32_t* argmin, fdr_stream stream) {

@@ -13,6 +13,7 @@ constexpr int kFeat = 2048;  // 32 x 8 x 8 (policies/impala.py:113)
 constexpr int kHid = 256;    // fc width == LSTM hidden
 constexpr int kGates = 1024;
 constexpr int kCoreIn = 257; // fc output + clipped reward (policies/impala.py:116, 163-164)
+constexpr int kReplayChunk = 64;  // entropy replay: steps per batched input-projection GEMM
 constexpr int kMaxAct = 32;
 constexpr int kMaxSections = 64;
 constexpr int kFramePix = 3 * 64 * 64;
@@ -62,6 +63,8 @@ struct StepArgs {
   float* c;
   float* rprev;
   float* ci;               // [t][lane*E+e][257] (entropy replay) or NULL
+  const float* gx;         // replay: x W_ih^T of steps [gx_t0, gx_t0 + kReplayChunk), [t - gx_t0][lane*E+e][1024], or NULL
+  int gx_t0;
   double* ret;
   double* ent;
   int32_t* actions;        // [lane*E+e][T] or NULL
@@ -91,9 +94,9 @@ __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
 // f16 0.41 -> 0.38 ms per step at 1024 lanes x 4 envs).
 template <class T>
 __device__ __forceinline__ T ld_stream(const T* p) {
-  static_assert(sizeof(T) == 16, "16-byte streamed loads");
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+  static_assert(sizeof(T) == 16 || sizeof(T) == 8, "8- or 16-byte streamed loads");
+  typedef float fv __attribute__((ext_vector_type(sizeof(T) / 4)));
+  const fv v = __builtin_nontemporal_load(reinterpret_cast<const fv*>(p));
   return __builtin_bit_cast(T, v);
 }
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
@@ -189,7 +192,7 @@ __global__ void core_kernel_h(Layout L, StepArgs a);
 constexpr int kHThreads = 512;
 
 struct Plan {  // workspace carve-up (byte offsets)
-  int64_t pack, hpack, feat, h, c, rprev, ci, n2, total;
+  int64_t pack, hpack, feat, h, c, rprev, ci, gx, n2, total;
   int nblk;    // prep blocks per lane
 };
 Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16 = false);
@@ -209,6 +212,7 @@ struct RolloutCall {
   float* probs;
 };
 int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t stream);
+int set_replay_gemm(int on);
 
 struct ForwardCall {
   const Layout* layout;

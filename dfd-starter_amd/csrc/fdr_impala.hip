@@ -132,6 +132,7 @@ Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16
   p.c = take(ne * kHid * 4);
   p.rprev = take(ne * 4);
   p.ci = take(entropy ? (int64_t)T * ne * kCoreIn * 4 : 0);
+  p.gx = take(entropy ? (int64_t)std::min(T, kReplayChunk) * ne * kGates * 4 : 0);
   p.n2 = take((int64_t)n_lanes * p.nblk * 8);
   p.total = o;
   return p;
@@ -654,7 +655,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
         dst[i] = cis[k * E + e];
       }
     }
-  } else {
+  } else if (!a.gx) {
     const float* src = a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn;
     for (int i = j; i < kCoreIn * E; i += kCoreThreads) {
       const int e = i / kCoreIn, k = i - e * kCoreIn;
@@ -679,16 +680,28 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
 #pragma unroll
       for (int e = 0; e < E; ++e) ax[c][e] = ah[c][e] = 0.f;
     const float4* wl = reinterpret_cast<const float4*>(pk + L.lstm_wt) + j;
-#pragma unroll 4
-    for (int k = 0; k < kCoreIn; ++k) {
-      const float4 w = ld_stream(wl + (int64_t)k * (kGates / 4));
+    if (MODE == kReplay && a.gx) {  // x W_ih^T precomputed by lstm_xproj_kernel (same fma chain)
+      const float4* g4 = reinterpret_cast<const float4*>(a.gx + ((int64_t)(a.t - a.gx_t0) * a.n_lanes * E + e0) * kGates);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const float x = cis[k * E + e];
-        ax[0][e] = fmaf(w.x, x, ax[0][e]);
-        ax[1][e] = fmaf(w.y, x, ax[1][e]);
-        ax[2][e] = fmaf(w.z, x, ax[2][e]);
-        ax[3][e] = fmaf(w.w, x, ax[3][e]);
+        const float4 g = ld_stream(g4 + (int64_t)e * (kGates / 4) + j);
+        ax[0][e] = g.x;
+        ax[1][e] = g.y;
+        ax[2][e] = g.z;
+        ax[3][e] = g.w;
+      }
+    } else {
+#pragma unroll 4
+      for (int k = 0; k < kCoreIn; ++k) {
+        const float4 w = ld_stream(wl + (int64_t)k * (kGates / 4));
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const float x = cis[k * E + e];
+          ax[0][e] = fmaf(w.x, x, ax[0][e]);
+          ax[1][e] = fmaf(w.y, x, ax[1][e]);
+          ax[2][e] = fmaf(w.z, x, ax[2][e]);
+          ax[3][e] = fmaf(w.w, x, ax[3][e]);
+        }
       }
     }
 #pragma unroll 4
@@ -830,6 +843,94 @@ int read_profile(double* out) {
   return FDR_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// Entropy replay, input projection.  The reference's get_entropy runs the stored core inputs through
+// the LSTM as ONE sequence (policies/impala.py:21-22, 166-182); the x W_ih^T half of every step's gates
+// does not depend on h, so -- as torch's LSTM does -- it is one GEMM per lane over a chunk of steps:
+// G[(t, e)][n] = sum_k x_(t,e)[k] W_ih^T[k][n] on v_mfma_f32_16x16x4_f32.  An f32 MFMA is a k-ordered
+// fma chain, so G is bit-identical to the k-loop the replay kernel ran, while W_ih is read once per
+// 64 rows instead of once per step (the replay then streams W_hh only).  fp16 mode reads the f16
+// W_ih^T (exact in f32), as its replay did.
+// Workgroup: 64 rows x 256 gate columns, 4 waves x (4 x 4) 16x16 tiles; K in LDS chunks of 32.
+// ------------------------------------------------------------------------------------------
+template <bool HALF>
+__global__ __launch_bounds__(256) void lstm_xproj_kernel(Layout L, StepArgs a, int t0, int tc, float* __restrict__ gx) {
+  constexpr int KC = 32, NKC = (kCoreIn + KC - 1) / KC, XP = 80, WP = 256 + 16;  // pads: conflict-free reads
+  __shared__ float xs[KC * XP];  // [k][row]
+  __shared__ float ws[KC * WP];  // [k][col]
+  const int lane = blockIdx.x, E = a.envs, rows = tc * E;
+  const int row0 = blockIdx.y * 64, n0 = blockIdx.z * 256;
+  const int tid = threadIdx.x, wave = tid >> 6, ln = tid & 63, g = ln >> 4, r = ln & 15;
+  const int64_t ne = (int64_t)a.n_lanes * E;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj) acc[ti][tj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; kc < NKC; ++kc) {
+    const int k0 = kc * KC;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {  // X tile: row-contiguous global reads (32 k of one row per half-wave)
+      const int i = tid + 256 * m, row = i >> 5, k = i & 31;
+      const int q = row0 + row;
+      float v = 0.f;
+      if (q < rows && k0 + k < kCoreIn) {
+        const int64_t t = t0 + q / E, e = q % E;
+        v = a.ci[((t * a.n_lanes + lane) * E + e) * kCoreIn + k0 + k];
+      }
+      xs[k * XP + row] = v;
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {  // W_ih^T tile [32 k][256 cols]
+      const int i = tid + 256 * m, k = i >> 6, c4 = i & 63;
+      float4 w = float4{0.f, 0.f, 0.f, 0.f};
+      if (k0 + k < kCoreIn) {
+        if constexpr (HALF) {
+          typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+          const h4v hv = *reinterpret_cast<const h4v*>(a.hpack + (int64_t)lane * a.hpack_stride + L.lstm_wt_h +
+                                                        (int64_t)(k0 + k) * kGates + n0 + 4 * c4);
+          w = float4{(float)hv[0], (float)hv[1], (float)hv[2], (float)hv[3]};
+        } else {
+          w = *reinterpret_cast<const float4*>(a.pack + (int64_t)lane * a.pack_stride + L.lstm_wt +
+                                               (int64_t)(k0 + k) * kGates + n0 + 4 * c4);
+        }
+      }
+      *reinterpret_cast<float4*>(ws + k * WP + 4 * c4) = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < KC / 4; ++s) {
+      const int k = 4 * s + g;
+      float av[4], bv[4];
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti) av[ti] = xs[k * XP + 16 * ti + r];
+#pragma unroll
+      for (int tj = 0; tj < 4; ++tj) bv[tj] = ws[k * WP + 64 * wave + 16 * tj + r];
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 4; ++tj) acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ti], bv[tj], acc[ti][tj], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int q = row0 + 16 * ti + 4 * g + v;
+      if (q >= rows) continue;
+      float* dst = gx + ((int64_t)(q / E) * ne + (int64_t)lane * E + q % E) * kGates + n0 + 64 * wave + r;
+#pragma unroll
+      for (int tj = 0; tj < 4; ++tj) dst[16 * tj] = acc[ti][tj][v];
+    }
+}
+
+static bool g_replay_gemm = true;  // fdr_impala_set_replay_gemm (diagnostics / A-B)
+int set_replay_gemm(int on) {
+  g_replay_gemm = on != 0;
+  return FDR_OK;
+}
+
 template <int E>
 static int launch_steps(const Layout& L, StepArgs a, int entropy, hipStream_t stream) {
   const int conv_grid = (a.n_lanes + 7) / 8 * 8 * a.envs;
@@ -851,14 +952,28 @@ static int launch_steps(const Layout& L, StepArgs a, int entropy, hipStream_t st
       hipLaunchKernelGGL((core_kernel<E, kRollout>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
     mark(stream);
   }
+  float* gx = const_cast<float*>(a.gx);
+  a.gx = nullptr;
   if (entropy)
-    for (int t = 0; t < a.T; ++t) {
-      a.t = t;
-      if (h)
-        hipLaunchKernelGGL((core_kernel_h<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
-      else
-        hipLaunchKernelGGL((core_kernel<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
-      mark(stream);
+    for (int t0 = 0; t0 < a.T; t0 += kReplayChunk) {
+      const int tc = std::min(kReplayChunk, a.T - t0);
+      if (g_replay_gemm && gx) {
+        const dim3 grid(a.n_lanes, (tc * E + 63) / 64, kGates / 256);
+        if (h)
+          hipLaunchKernelGGL(lstm_xproj_kernel<true>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);
+        else
+          hipLaunchKernelGGL(lstm_xproj_kernel<false>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);
+        a.gx = gx;
+        a.gx_t0 = t0;
+      }
+      for (int t = t0; t < t0 + tc; ++t) {
+        a.t = t;
+        if (h)
+          hipLaunchKernelGGL((core_kernel_h<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+        else
+          hipLaunchKernelGGL((core_kernel<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+        mark(stream);
+      }
     }
   return check_launch("impala step kernels");
 }
@@ -887,6 +1002,7 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
   a.c = reinterpret_cast<float*>(w + p.c);
   a.rprev = reinterpret_cast<float*>(w + p.rprev);
   a.ci = c.entropy ? reinterpret_cast<float*>(w + p.ci) : nullptr;
+  a.gx = c.entropy ? reinterpret_cast<float*>(w + p.gx) : nullptr;  // launch_steps hands it to the replay
   a.ret = c.ret;
   a.ent = c.ent;
   a.actions = c.actions;

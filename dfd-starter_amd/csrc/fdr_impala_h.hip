@@ -571,7 +571,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
         dst[i] = cis[k * E + e];
       }
     }
-  } else {
+  } else if (!a.gx) {
     const float* src = a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn;
     for (int i = j; i < kCoreIn * E; i += kCoreThreads) {
       const int e = i / kCoreIn, k = i - e * kCoreIn;
@@ -586,7 +586,41 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
     cj[e] = nd * a.c[(e0 + e) * kHid + j];
   }
   __syncthreads();
-  {  // gates: threads 0..127 stream W_ih^T (x part), 128..255 W_hh^T (h part), 8 columns each
+  if (MODE == kReplay && a.gx) {
+    // replay with x W_ih^T precomputed (lstm_xproj_kernel<true>): all 256 threads stream W_hh^T,
+    // 4 columns each (the same per-column fma chain as below, twice the waves in flight)
+    typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+    float acc[4][E];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[c][e] = 0.f;
+    const h4v* w4 = reinterpret_cast<const h4v*>(hp + L.lstm_wt_h) + j;
+#pragma unroll 4
+    for (int k = 0; k < kHid; ++k) {
+      const h4v w = ld_stream(w4 + (int64_t)(kCoreIn + k) * (kGates / 4));
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const float x = hs[k * E + e];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c][e] = fmaf((float)w[c], x, acc[c][e]);
+      }
+    }
+    const float4* g4 = reinterpret_cast<const float4*>(a.gx + ((int64_t)(a.t - a.gx_t0) * a.n_lanes * E + e0) * kGates);
+    float4 gv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) gv[e] = ld_stream(g4 + (int64_t)e * (kGates / 4) + j);
+    __syncthreads();  // every read of hs (inside xw) is done before the gates overwrite it
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float gx4[4] = {gv[e].x, gv[e].y, gv[e].z, gv[e].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        xw[(4 * j + c) * E + e] = gx4[c];
+        xw[(kGates + 4 * j + c) * E + e] = acc[c][e];
+      }
+    }
+  } else {  // gates: threads 0..127 stream W_ih^T (x part), 128..255 W_hh^T (h part), 8 columns each
     const int cg = j & 127, part = j >> 7;
     float acc[8][E];
 #pragma unroll

@@ -24,7 +24,8 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_strategy_distances", "fdr_rollout_states", "fdr_rollout_ex", "fdr_obs_stats_merge",
            "fdr_fd_lambda_norms", "fdr_fd_grad_lambda", "fdr_bn_refresh_workspace_bytes", "fdr_bn_refresh",
            "fdr_atari_num_params", "fdr_atari_workspace_bytes", "fdr_atari_rollout",
-           "fdr_atari_forward_workspace_bytes", "fdr_atari_forward", "fdr_rollout_set_impl")
+           "fdr_atari_forward_workspace_bytes", "fdr_atari_forward", "fdr_rollout_set_impl",
+           "fdr_impala_set_replay_gemm")
 
 
 class FDRError(RuntimeError):
@@ -102,6 +103,7 @@ def _load():
         "fdr_atari_forward_workspace_bytes": (I64, [I32, I32]),
         "fdr_atari_forward": (ctypes.c_int, [P, ctypes.POINTER(AtariDesc), P, I32, P, P, P, P, I64, P]),
         "fdr_rollout_set_impl": (ctypes.c_int, [I32]),
+        "fdr_impala_set_replay_gemm": (ctypes.c_int, [I32]),
         "fdr_fd_weights": (ctypes.c_int, [P, P, I32, F64, I32, I32, P, P, I32, F32, P, P]),
         "fdr_fd_grad_workspace_bytes": (I64, [I32, I64]),
         "fdr_fd_grad": (ctypes.c_int, [P, P, I64, P, P, I32, I64, P, P, I64, P]),

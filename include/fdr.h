@@ -324,6 +324,10 @@ int fdr_impala_profile_read(double* ms);
  * its phase boundaries into the DEVICE buffer buf (u64[64]: 33 stage/block boundaries, then the
  * fp16 entry-conv band boundaries at 40..63; overwritten each step); NULL = off. */
 int fdr_impala_debug_clock(uint64_t* buf);
+/* Entropy replay of fdr_impala_rollout (process-wide, default on): 1 = the x W_ih^T half of the
+ * replayed LSTM gates is one MFMA GEMM per lane over 64-step chunks (bit-identical gates; the replay
+ * streams W_hh only), 0 = every replay step streams [W_ih | W_hh] (the step kernel's form). */
+int fdr_impala_set_replay_gemm(int32_t on);
 
 #ifdef __cplusplus
 }

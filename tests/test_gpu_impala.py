@@ -256,3 +256,29 @@ def test_fp16_rollout_first_step_vs_oracle(engine, table):
     np.testing.assert_array_equal(out16.norm2.cpu().numpy(), out32.norm2.cpu().numpy())
     assert np.all(np.isfinite(out16.reward.cpu().numpy())) and np.all(np.isfinite(out16.entropy.cpu().numpy()))
     np.testing.assert_allclose(out16.entropy.cpu().numpy(), out32.entropy.cpu().numpy(), rtol=F16_RTOL)
+
+
+@pytest.mark.parametrize("fp16", [False, True])
+def test_replay_input_projection_gemm_bit_identical(engine, table, fp16):
+    """Entropy replay with the x W_ih^T half of the gates as one MFMA GEMM per 64-step chunk
+    (lstm_xproj_kernel) against the per-step streaming form: identical fma chains, so the entropies are
+    bit-identical; T = 70 spans two chunks (64 + 6) and E = 4 makes partial row blocks."""
+    from fdr._lib import check, lib
+    A, E, T, L = 6, 4, 70, 3
+    theta = _theta(A)
+    tt = torch.tensor(table, device="cuda")
+    lanes = engine.lanes_desc(torch.tensor(theta, device="cuda"), 0, tt,
+                              torch.tensor([10, 2000, 30000], dtype=torch.int64, device="cuda"),
+                              torch.tensor([1, -1, 1], dtype=torch.int8, device="cuda"), 0.02)
+    spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=fp16)
+    outs = []
+    try:
+        for on in (1, 0):
+            check(lib.fdr_impala_set_replay_gemm(on), "fdr_impala_set_replay_gemm")
+            out = engine.impala_rollout(spec, lanes, L, 11)
+            torch.cuda.synchronize()
+            outs.append(out.entropy.cpu().numpy().copy())
+    finally:
+        check(lib.fdr_impala_set_replay_gemm(1), "fdr_impala_set_replay_gemm")
+    assert np.all(np.isfinite(outs[0])) and np.any(outs[0] != 0)
+    np.testing.assert_array_equal(outs[0], outs[1])
