@@ -124,7 +124,7 @@ Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16
   const int64_t ne = (int64_t)n_lanes * envs;
   int64_t o = 0;
   auto take = [&](int64_t bytes) { const int64_t at = o; o += round_up(std::max<int64_t>(bytes, 0), 256); return at; };
-  p.nblk = (int)((L.pack + kPrepSpan - 1) / kPrepSpan);
+  p.nblk = prep_blocks(L);
   p.pack = take((int64_t)n_lanes * L.pack * 4);
   p.hpack = take(fp16 ? (int64_t)n_lanes * L.hpack * 2 : 0);
   p.feat = take(ne * kFeat * 4);
@@ -194,7 +194,7 @@ __device__ __forceinline__ int64_t section_src(const Section& s, int32_t u) {
 
 template <typename OUT>
 __global__ __launch_bounds__(kPrepThreads) void prep_kernel(Layout L, LanesArgs lanes, OUT* __restrict__ pack,
-                                                            double* __restrict__ n2_part, int half) {
+                                                            double* __restrict__ n2_part, int half, int n2_slots) {
   const int lane = blockIdx.y;
   ParamSrc src = lanes.src(lane);
   const int64_t j0 = (int64_t)blockIdx.x * kPrepSpan + threadIdx.x;
@@ -204,6 +204,18 @@ __global__ __launch_bounds__(kPrepThreads) void prep_kernel(Layout L, LanesArgs 
   OUT* out = pack + (int64_t)lane * len;
   const bool bad = src.n2 != src.n2;  // out-of-range table offset: NaN norm, unperturbed lane
   src.n2 = 0.0;
+  {  // a block entirely inside one transposed section has nothing to do (prep_transpose_kernel)
+    const int64_t b0 = (int64_t)blockIdx.x * kPrepSpan, b1 = b0 + kPrepSpan - 1;
+    int lo = 0, hi = nsec - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (sec[mid].dst <= b0) lo = mid; else hi = mid - 1;
+    }
+    if (sec[lo].kind == kTranspose && b0 >= sec[lo].dst && b1 < (int64_t)sec[lo].dst + sec[lo].len) {
+      if (!half && threadIdx.x == 0) n2_part[(int64_t)lane * n2_slots + blockIdx.x] = bad ? __builtin_nan("") : 0.0;
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < kPrepPer; ++i) {
     const int64_t j = j0 + (int64_t)i * kPrepThreads;
@@ -215,6 +227,7 @@ __global__ __launch_bounds__(kPrepThreads) void prep_kernel(Layout L, LanesArgs 
     }
     const Section& s = sec[lo];
     const int32_t u = (int32_t)(j - s.dst);
+    if (s.kind == kTranspose && j >= s.dst && u < s.len) continue;  // prep_transpose_kernel's part
     const int64_t p = (j >= s.dst && u < s.len) ? section_src(s, u) : -1;
     out[j] = (OUT)(p >= 0 ? (half ? src.get_nocount(p) : src.get(p)) : 0.f);
   }
@@ -228,8 +241,90 @@ __global__ __launch_bounds__(kPrepThreads) void prep_kernel(Layout L, LanesArgs 
   if (threadIdx.x == 0) {
     double t = 0.0;
     for (int w = 0; w < kPrepThreads / kWave; ++w) t += red[w];
-    n2_part[(int64_t)lane * gridDim.x + blockIdx.x] = bad ? __builtin_nan("") : t;
+    n2_part[(int64_t)lane * n2_slots + blockIdx.x] = bad ? __builtin_nan("") : t;
   }
+}
+
+// Transposed sections (fc W^T, [W_ih | W_hh]^T: 90 % of the pack) through a 64 x 64 LDS tile: theta and
+// the lane's noise-table slice are read along W's rows (coalesced) and W^T is written along its rows
+// (coalesced) -- the element-order gather of prep_kernel read them at a 4-8 KB stride (one 64-B
+// line per 4-byte element).  Same values (fl32(theta +- fl32(sigma eps))) and the same n2 terms.
+constexpr int kTT = 64;  // transpose tile edge
+__host__ __device__ inline int transpose_tiles(const Section& s) { return ((s.a + kTT - 1) / kTT) * ((s.b + kTT - 1) / kTT); }
+
+template <class OUT>
+__global__ __launch_bounds__(256) void prep_transpose_kernel(Layout L, LanesArgs lanes, OUT* __restrict__ pack,
+                                                             double* __restrict__ n2_part, int half, int n2_slot0,
+                                                             int n2_slots) {
+  __shared__ float tile[kTT][kTT + 1];
+  __shared__ double red[256 / kWave];
+  const int lane = blockIdx.y;
+  ParamSrc src = lanes.src(lane);
+  const bool bad = src.n2 != src.n2;
+  src.n2 = 0.0;
+  const Section* sec = half ? L.hsec : L.sec;
+  const int nsec = half ? L.n_hsections : L.n_sections;
+  int t = blockIdx.x, si = 0;
+  for (; si < nsec; ++si) {
+    if (sec[si].kind != kTranspose) continue;
+    const int n = transpose_tiles(sec[si]);
+    if (t < n) break;
+    t -= n;
+  }
+  const Section s = sec[si];
+  const int tr = (s.a + kTT - 1) / kTT;
+  const int r0 = (t % tr) * kTT, k0 = (t / tr) * kTT;
+  OUT* out = pack + (int64_t)lane * (half ? L.hpack : L.pack) + s.dst;
+#pragma unroll
+  for (int m = 0; m < kTT * kTT / 256; ++m) {  // W[r][k] along k
+    const int e = threadIdx.x + 256 * m, i = e / kTT, jj = e % kTT, r = r0 + i, k = k0 + jj;
+    float v = 0.f;
+    if (r < s.a && k < s.b) {
+      const int64_t p = (int64_t)s.src + (int64_t)r * s.b + k;
+      v = half ? src.get_nocount(p) : src.get(p);
+    }
+    tile[jj][i] = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < kTT * kTT / 256; ++m) {  // W^T[k][r] along r
+    const int e = threadIdx.x + 256 * m, jj = e / kTT, i = e % kTT, r = r0 + i, k = k0 + jj;
+    if (r < s.a && k < s.b) out[(int64_t)k * s.a + r] = (OUT)tile[jj][i];
+  }
+  if (half) return;
+  double n2 = wave_sum(src.n2);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n2;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = 0.0;
+    for (int w = 0; w < 256 / kWave; ++w) tot += red[w];
+    n2_part[(int64_t)lane * n2_slots + n2_slot0 + blockIdx.x] = bad ? __builtin_nan("") : tot;
+  }
+}
+
+static int generic_prep_blocks(const Layout& L, bool half) {
+  return (int)(((half ? L.hpack : L.pack) + kPrepSpan - 1) / kPrepSpan);
+}
+static int transpose_prep_tiles(const Layout& L, bool half) {
+  const Section* sec = half ? L.hsec : L.sec;
+  const int nsec = half ? L.n_hsections : L.n_sections;
+  int n = 0;
+  for (int i = 0; i < nsec; ++i)
+    if (sec[i].kind == kTranspose) n += transpose_tiles(sec[i]);
+  return n;
+}
+
+// theta' pack (half = 0, f32, with the per-lane n2 partials) or half pack (half = 1, f16)
+template <class OUT>
+static void launch_pack(const Layout& L, const LanesArgs& lanes, OUT* pack, double* n2, int n_lanes, int half,
+                        hipStream_t stream) {
+  const int g = generic_prep_blocks(L, half != 0), tt = transpose_prep_tiles(L, half != 0);
+  const int slots = prep_blocks(L);
+  hipLaunchKernelGGL(prep_kernel<OUT>, dim3(g, n_lanes), dim3(kPrepThreads), 0, stream, L, lanes, pack, n2, half,
+                     slots);
+  if (tt > 0)
+    hipLaunchKernelGGL(prep_transpose_kernel<OUT>, dim3(tt, n_lanes), dim3(256), 0, stream, L, lanes, pack, n2, half,
+                       generic_prep_blocks(L, false), slots);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -768,12 +863,12 @@ __global__ void init_kernel(int64_t n_env, float* h, float* c, float* rprev, dou
   }
 }
 
-int prep_blocks(const Layout& L) { return (int)((L.pack + kPrepSpan - 1) / kPrepSpan); }
+// n2 partial slots per lane: the generic prep blocks, then the transpose tiles
+int prep_blocks(const Layout& L) { return generic_prep_blocks(L, false) + transpose_prep_tiles(L, false); }
 
 int launch_prep(const Layout& L, const LanesArgs& lanes, float* pack, double* n2_part, int n_lanes,
                 hipStream_t stream) {
-  hipLaunchKernelGGL(prep_kernel<float>, dim3(prep_blocks(L), n_lanes), dim3(kPrepThreads), 0, stream, L, lanes,
-                     pack, n2_part, 0);
+  launch_pack<float>(L, lanes, pack, n2_part, n_lanes, 0, stream);
   return check_launch("prep_kernel");
 }
 
@@ -1011,13 +1106,11 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
   a.dbg = g_dbg;
   double* n2 = reinterpret_cast<double*>(w + p.n2);
 
-  hipLaunchKernelGGL(prep_kernel<float>, dim3(p.nblk, c.n_lanes), dim3(kPrepThreads), 0, stream, L, c.lanes,
-                     const_cast<float*>(a.pack), n2, 0);
+  launch_pack<float>(L, c.lanes, const_cast<float*>(a.pack), n2, c.n_lanes, 0, stream);
   if (c.fp16) {
     a.hpack = reinterpret_cast<_Float16*>(w + p.hpack);
     a.hpack_stride = L.hpack;
-    hipLaunchKernelGGL(prep_kernel<_Float16>, dim3((int)((L.hpack + kPrepSpan - 1) / kPrepSpan), c.n_lanes),
-                       dim3(kPrepThreads), 0, stream, L, c.lanes, a.hpack, n2, 1);
+    launch_pack<_Float16>(L, c.lanes, a.hpack, n2, c.n_lanes, 1, stream);
   }
   const int64_t ne = (int64_t)c.n_lanes * c.envs;
   hipLaunchKernelGGL(init_kernel, dim3((unsigned)((ne * kHid + 255) / 256)), dim3(256), 0, stream, ne, a.h, a.c,
@@ -1067,13 +1160,11 @@ int launch_forward(const ForwardCall& c, void* ws, int64_t ws_bytes, hipStream_t
   a.probs = c.probs;
   a.reward_in = c.reward;
   a.notdone = c.notdone;
-  hipLaunchKernelGGL(prep_kernel<float>, dim3(p.nblk, 1), dim3(kPrepThreads), 0, stream, L, lanes,
-                     const_cast<float*>(a.pack), reinterpret_cast<double*>(w + p.n2), 0);
+  launch_pack<float>(L, lanes, const_cast<float*>(a.pack), reinterpret_cast<double*>(w + p.n2), 1, 0, stream);
   if (c.fp16) {
     a.hpack = reinterpret_cast<_Float16*>(w + p.hpack);
     a.hpack_stride = 0;
-    hipLaunchKernelGGL(prep_kernel<_Float16>, dim3((int)((L.hpack + kPrepSpan - 1) / kPrepSpan), 1),
-                       dim3(kPrepThreads), 0, stream, L, lanes, a.hpack, reinterpret_cast<double*>(w + p.n2), 1);
+    launch_pack<_Float16>(L, lanes, a.hpack, reinterpret_cast<double*>(w + p.n2), 1, 1, stream);
   }
   if (c.fp16) {
     hipLaunchKernelGGL(conv_kernel_h, dim3((c.n_envs + 7) / 8 * 8), dim3(kHThreads), 0, stream, L, a);
