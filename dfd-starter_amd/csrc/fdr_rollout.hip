@@ -1004,14 +1004,13 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
 #else
   auto mark = [](int, float) {};
 #endif
-  for (int st = 0; st < T; ++st) {
-    asm volatile("" ::: "memory");
-    mark(-1, s);
-    if (!det && tb == 0) {  // draw batch: thread t holds the draw (step st + t / k, dim t % k)
-      const int ds = t / kDrawsPerStep, dk = t % kDrawsPerStep;
-      const uint64_t hsh = hash_ctr(key, ulane, (uint64_t)(st + ds), (uint64_t)dk);
-      rbuf = DISC ? uniform24(hsh) : normal_bm(hsh);
-    }
+  // draw batch starting at step st: thread t holds the draw of (step st + t / k, dim t % k)
+  auto draw = [&](int st) {
+    const int ds = t / kDrawsPerStep, dk = t % kDrawsPerStep;
+    const uint64_t hsh = hash_ctr(key, ulane, (uint64_t)(st + ds), (uint64_t)dk);
+    rbuf = DISC ? uniform24(hsh) : normal_bm(hsh);
+  };
+  auto step = [&](int st, int tb) {
     // this step's draw: the uniform (discrete) or the normal of action dim o (continuous)
     const float zt = __builtin_bit_cast(
         float, __builtin_amdgcn_ds_bpermute(zbase + 4 * kDrawsPerStep * tb, __builtin_bit_cast(int, rbuf)));
@@ -1075,7 +1074,44 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     s = tanh_fast(pre);
     racc += (double)s;  // thread 0 of the half holds the reward s'[0]
     mark(4, s);
-    tb = tb + 1 == kStepsPerBatch ? 0 : tb + 1;
+  };
+#ifndef FDR_PAIR_NO_UNROLL
+  if constexpr (!DISC) {
+    // continuous: the loop unrolled by the draw batch (5 steps for 6 dims); the draw is issued
+    // unconditionally at the top of the unrolled body (det lanes ignore it), so it schedules into the
+    // first step's waits instead of sitting behind a branch
+    int st = 0;
+    for (; st + kStepsPerBatch <= T; st += kStepsPerBatch) {
+      asm volatile("" ::: "memory");
+      mark(-1, s);
+      draw(st);
+#pragma unroll
+      for (int k = 0; k < kStepsPerBatch; ++k) {
+        if (k) {
+          asm volatile("" ::: "memory");
+          mark(-1, s);
+        }
+        step(st + k, k);
+      }
+    }
+    if (st < T) {
+      draw(st);
+      for (int k = 0; st + k < T; ++k) {
+        asm volatile("" ::: "memory");
+        mark(-1, s);
+        step(st + k, k);
+      }
+    }
+  } else
+#endif
+  {
+    for (int st = 0; st < T; ++st) {
+      asm volatile("" ::: "memory");
+      mark(-1, s);
+      if (!det && tb == 0) draw(st);
+      step(st, tb);
+      tb = tb + 1 == kStepsPerBatch ? 0 : tb + 1;
+    }
   }
 
 #ifdef FDR_PHASE_STAMPS
