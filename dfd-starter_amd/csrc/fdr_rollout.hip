@@ -889,8 +889,8 @@ struct MlpPair {
       w3[4 * m + 2] = w.z;
       w3[4 * m + 3] = w.w;
     }
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // four independent chains of 8
-    dpp_fma_32x4(s0, s1, s2, s3, h2a, h2b, w3);
+    float s0, s1, s2, s3;  // four independent chains of 8 (first product a v_mul: no zeroing)
+    dpp_dot_32x4(s0, s1, s2, s3, h2a, h2b, w3);
     float u = (s0 + s2) + (s1 + s3), v = u;
     permlane16_swap(u, v);  // u = row 2h's partial, v = row 2h+1's, in both rows of half h
     const float out = (u + v) + b3;
