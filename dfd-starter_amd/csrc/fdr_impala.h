@@ -13,6 +13,12 @@ constexpr int kFeat = 2048;  // 32 x 8 x 8 (policies/impala.py:113)
 constexpr int kHid = 256;    // fc width == LSTM hidden
 constexpr int kGates = 1024;
 constexpr int kCoreIn = 257; // fc output + clipped reward (policies/impala.py:116, 163-164)
+#ifndef FDR_CORE_UNROLL
+#define FDR_CORE_UNROLL 4  // weight-stream loop unroll of the core kernels (loads in flight per thread)
+#endif
+#ifndef FDR_CORE_UNROLL_H
+#define FDR_CORE_UNROLL_H 2  // fp16 step kernel's fc / gate streams (A/B: 0.377 -> 0.360 ms per step vs 4)
+#endif
 constexpr int kReplayChunk = 64;  // entropy replay: steps per batched input-projection GEMM
 constexpr int kMaxAct = 32;
 constexpr int kMaxSections = 64;

@@ -714,7 +714,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[c][e] = 0.f;
     const float4* w4 = reinterpret_cast<const float4*>(pk + L.fc_wt) + c4;
-#pragma unroll 4
+#pragma unroll FDR_CORE_UNROLL
     for (int k = wq * (kFeat / 4); k < (wq + 1) * (kFeat / 4); ++k) {
       const float4 w = ld_stream(w4 + (int64_t)k * (kHid / 4));
 #pragma unroll
@@ -786,7 +786,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
         ax[3][e] = g.w;
       }
     } else {
-#pragma unroll 4
+#pragma unroll FDR_CORE_UNROLL
       for (int k = 0; k < kCoreIn; ++k) {
         const float4 w = ld_stream(wl + (int64_t)k * (kGates / 4));
 #pragma unroll
@@ -799,7 +799,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
         }
       }
     }
-#pragma unroll 4
+#pragma unroll FDR_CORE_UNROLL
     for (int k = 0; k < kHid; ++k) {
       const float4 w = ld_stream(wl + (int64_t)(kCoreIn + k) * (kGates / 4));
 #pragma unroll

@@ -531,7 +531,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[c][e] = 0.f;
     const h8* w8 = reinterpret_cast<const h8*>(hp + L.fc_wt_h) + c8;
-#pragma unroll 4
+#pragma unroll FDR_CORE_UNROLL_H
     for (int k = ks * 256; k < ks * 256 + 256; ++k) {
       const h8 w = ld_stream(w8 + (int64_t)k * (kHid / 8));
 #pragma unroll
@@ -596,7 +596,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[c][e] = 0.f;
     const h4v* w4 = reinterpret_cast<const h4v*>(hp + L.lstm_wt_h) + j;
-#pragma unroll 4
+#pragma unroll FDR_CORE_UNROLL
     for (int k = 0; k < kHid; ++k) {
       const h4v w = ld_stream(w4 + (int64_t)(kCoreIn + k) * (kGates / 4));
 #pragma unroll
@@ -630,7 +630,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
     const int k_lo = part ? kCoreIn : 0, k_n = part ? kHid : kCoreIn;
     const float* xin = part ? hs : cis;
     const h8* w8 = reinterpret_cast<const h8*>(hp + L.lstm_wt_h) + cg;
-#pragma unroll 4
+#pragma unroll FDR_CORE_UNROLL_H
     for (int k = 0; k < k_n; ++k) {
       const h8 w = ld_stream(w8 + (int64_t)(k_lo + k) * (kGates / 8));
 #pragma unroll
