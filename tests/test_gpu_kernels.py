@@ -152,17 +152,20 @@ def test_rollout_vs_oracle(eng, name, det):
     np.testing.assert_allclose(res.norm2.cpu().numpy(), r_n2, rtol=1e-9, atol=0)
 
 
-@pytest.mark.parametrize("name,L,det", [("cheetah", 13, False), ("cheetah", 7, True), ("cartpole", 13, False),
-                                        ("cartpole", 9, True), ("cheetah", 64, False)])
-def test_rollout_pair_and_single_kernels_agree(eng, name, L, det):
+@pytest.mark.parametrize("name,L,det,T", [("cheetah", 13, False, 120), ("cheetah", 7, True, 120),
+                                          ("cartpole", 13, False, 120), ("cartpole", 9, True, 120),
+                                          ("cheetah", 64, False, 120), ("cheetah", 10, False, 123),
+                                          ("cheetah", 6, False, 3), ("cartpole", 6, False, 37)])
+def test_rollout_pair_and_single_kernels_agree(eng, name, L, det, T):
     """rollout_pair_kernel (two lanes per wave) and rollout_kernel (one lane per wave) against the
-    oracle and each other, incl. odd lane counts (a wave whose second half is idle)."""
+    oracle and each other, incl. odd lane counts (a wave whose second half is idle) and episode lengths
+    that are not a multiple of the pair kernel's 5-step unroll (remainder loop)."""
     from fdr._lib import FDR_ROLLOUT_AUTO, FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, check, lib
     out = {}
     try:
         for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
             check(lib.fdr_rollout_set_impl(impl), "fdr_rollout_set_impl")
-            out[impl] = _rollout_case(eng, name, L, 120, det, antithetic=L % 2 == 0, idx_seed=L)
+            out[impl] = _rollout_case(eng, name, L, T, det, antithetic=L % 2 == 0, idx_seed=L)
     finally:
         check(lib.fdr_rollout_set_impl(FDR_ROLLOUT_AUTO), "fdr_rollout_set_impl")
     for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
