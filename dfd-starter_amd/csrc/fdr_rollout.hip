@@ -983,14 +983,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
   const float* mrow = envMK + ji * MKS;
   constexpr bool kSame = !DISC && !norm_obs;
   typename Lane::L1Rows l1rows;
-#ifndef FDR_PAIR_NO_PREFETCH
   pl.l1_prefetch(l1rows, mrow);
-#endif
-#ifndef FDR_PAIR_KR_LDS
   float kr[DISC ? 1 : NA];  // K row t: loop-invariant, kept in VGPRs
 #pragma unroll
   for (int m = 0; m < (DISC ? 1 : NA); ++m) kr[m] = mrow[NX + m];
-#endif
   int tb = 0;
 #ifdef FDR_PHASE_STAMPS
   uint64_t ph_acc[5] = {0, 0, 0, 0, 0};
@@ -1021,15 +1017,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     xs[t] = t < NIN ? policy_input(s) : (t == NIN ? 1.f : 0.f);
     if constexpr (!kSame) h1s[t] = t < NIN ? s : 0.f;
     wave_lds_sync();
-#ifdef FDR_PAIR_NO_PREFETCH
-    pl.l1_prefetch(l1rows, mrow);
-#endif
     const f2 h1 = pl.template layer1_env<kSame>(xs, h1s, l1rows, pre);
     mark(0, h1.x);
     const float y = pl.layers23(h1, h1s, t, mark);
-#ifndef FDR_PAIR_NO_PREFETCH
     pl.l1_prefetch(l1rows, mrow);  // next step's rows, in flight during the action and env phases
-#endif
     if constexpr (DISC) {
       const float p = pl.softmax(y, t);
       float pv[NA];
@@ -1063,11 +1054,6 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
       const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
       eacc += __builtin_amdgcn_logf(sd);
       const float act_c = det ? th : gauss_action(th, sd, zt);
-#ifdef FDR_PAIR_KR_LDS
-      float kr[NA];
-#pragma unroll
-      for (int m = 0; m < NA; ++m) kr[m] = mrow[NX + m];
-#endif
       mark(3, act_c);
       dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in thread m of both rows of the half
     }
@@ -1075,7 +1061,6 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     racc += (double)s;  // thread 0 of the half holds the reward s'[0]
     mark(4, s);
   };
-#ifndef FDR_PAIR_NO_UNROLL
   if constexpr (!DISC) {
     // continuous: the loop unrolled by the draw batch (5 steps for 6 dims); the draw is issued
     // unconditionally at the top of the unrolled body (det lanes ignore it), so it schedules into the
@@ -1102,9 +1087,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
         step(st + k, k);
       }
     }
-  } else
-#endif
-  {
+  } else {
     for (int st = 0; st < T; ++st) {
       asm volatile("" ::: "memory");
       mark(-1, s);
