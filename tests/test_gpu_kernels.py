@@ -363,6 +363,17 @@ def test_full_size_properties(eng):
     # the counter stream is keyed by the lane id, so evaluate the picked lanes with their ids
     ref = _oracle_lanes_with_ids(kind, n_in, n_act, theta, t.table, idx[pick], sign[pick], oenv, 5, pick)
     np.testing.assert_allclose(ret[pick], ref, rtol=1e-4, atol=1e-4)
+    # every lane: the auto-selected two-lanes-per-wave kernel against the one-lane kernel
+    from fdr._lib import FDR_ROLLOUT_AUTO, FDR_ROLLOUT_SINGLE, check, lib
+    try:
+        check(lib.fdr_rollout_set_impl(FDR_ROLLOUT_SINGLE), "fdr_rollout_set_impl")
+        res1 = eng.rollout(spec, env, lanes, L, 5)
+        torch.cuda.synchronize()
+    finally:
+        check(lib.fdr_rollout_set_impl(FDR_ROLLOUT_AUTO), "fdr_rollout_set_impl")
+    np.testing.assert_allclose(ret, res1.reward.cpu().numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(res.entropy.cpu().numpy(), res1.entropy.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(n2, res1.norm2.cpu().numpy(), rtol=1e-12)
 
 
 def _oracle_lanes_with_ids(kind, n_in, n_act, theta, tab, idx, sign, env, seed, ids):
