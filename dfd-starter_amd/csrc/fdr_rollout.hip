@@ -350,9 +350,9 @@ struct MlpLane {
   __device__ __forceinline__ float softmax(float logit, int j) const {
     const bool valid = (j & 15) < NOUT;
     const float v = valid ? logit : -FLT_MAX;
-    const float mx = row16_max(v);
+    const float mx = row16_max_n<NOUT>(v);
     const float e = valid ? expf(v - mx) : 0.f;
-    return e / row16_sum(e);
+    return e / row16_sum_n<NOUT>(e);
   }
 };
 
@@ -901,9 +901,9 @@ struct MlpPair {
   __device__ __forceinline__ float softmax(float logit, int t) const {
     const bool valid = (t & 15) < NOUT;
     const float v = valid ? logit : -FLT_MAX;
-    const float mx = row16_max(v);
+    const float mx = row16_max_n<NOUT>(v);
     const float e = valid ? expf(v - mx) : 0.f;
-    return e / row16_sum(e);
+    return e / row16_sum_n<NOUT>(e);
   }
 };
 

@@ -10,7 +10,7 @@ for run in ${RUNS:-libfdr:single libfdr:pair libfdr:single libfdr:pair}; do
   for c in ${CONFIGS:-halfcheetah cartpole}; do
     log=gpurun_out/ab_${lib}_${impl}_${c}.log
     FDR_LIB=$PWD/dfd-starter_amd/fdr/$lib.so FDR_ROLLOUT=$impl timeout -k 10 120 \
-      python tools/rollout_phases.py --config $c --iters 15 > $log 2>&1; rc=$?
+      python tools/rollout_phases.py --config $c --iters 15 ${PHASE_ARGS:-} > $log 2>&1; rc=$?
     if [ $rc -ne 0 ] || grep -qE "$FAULT" $log; then
       echo "$lib $impl $c FAIL rc=$rc"; tail -5 $log; exit 3; fi
     echo "$lib $impl $c: $(grep evaluate $log)"
