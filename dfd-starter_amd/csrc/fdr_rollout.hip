@@ -341,7 +341,7 @@ struct MlpLane {
       w3[4 * m + 2] = w.z;
       w3[4 * m + 3] = w.w;
     }
-    const float out = row_allreduce_sum(dot_row16(h2, w3, 0.f)) + b3;
+    const float out = row_allreduce_sum(dot_row16(h2, w3)) + b3;
     mark(2, out);
     return out;
   }
