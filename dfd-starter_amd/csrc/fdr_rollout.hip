@@ -855,6 +855,16 @@ struct MlpPair {
     wave_lds_sync();
     float x[8];
     lds_bcast<8>(h1s + 8 * c, x);
+    // the head's W3 slice (loop-invariant LDS) requested here, in flight during the 64 packed FMAs
+    float w3[32];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const float4 w = tile[(2 * kW1Chunks + m) * kWave];
+      w3[4 * m] = w.x;
+      w3[4 * m + 1] = w.y;
+      w3[4 * m + 2] = w.z;
+      w3[4 * m + 3] = w.w;
+    }
     f2 acc[8];
 #pragma unroll
     for (int p = 0; p < 8; ++p) acc[p] = f2{0.f, 0.f};
@@ -879,15 +889,6 @@ struct MlpPair {
       const f2 h2 = tanh2_fast(f2{za, zb});
       h2a = h2.x;
       h2b = h2.y;
-    }
-    float w3[32];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const float4 w = tile[(2 * kW1Chunks + m) * kWave];
-      w3[4 * m] = w.x;
-      w3[4 * m + 1] = w.y;
-      w3[4 * m + 2] = w.z;
-      w3[4 * m + 3] = w.w;
     }
     float s0, s1, s2, s3;  // four independent chains of 8 (first product a v_mul: no zeroing)
     dpp_dot_32x4(s0, s1, s2, s3, h2a, h2b, w3);
