@@ -42,6 +42,7 @@ CONFIGS = {
 }
 DEFAULT_LANES = {"halfcheetah": 4096, "cartpole": 1024}   # BASELINE configs 3 and 2
 IMPALA_ENVS = 4
+ZETA_SIZE = 200           # run_sequential.py:30 default zeta_size
 IMPALA_LANES = 1024
 # ImpalaCNN conv stack, algorithmic FLOPs per env step: sum over the 15 convs of 2*Cin*9*Cout*Ho*Wo
 IMPALA_CONV_FLOP = 2 * 9 * (3 * 16 * 64 * 64 + 4 * 16 * 16 * 32 * 32 + 16 * 32 * 32 * 32 + 4 * 32 * 32 * 16 * 16
@@ -97,38 +98,46 @@ def _cpu_worker_impala(wid, seconds, T):
 
 def _cpu_worker(args):
     wid, seconds, cfg = args
-    import numpy as np
     import torch
-    torch.set_num_threads(1)
-    from oracle import agent, envs, noise, policies
+    torch.set_num_threads(1)                      # run_client.py:15
     kind, n_in, n_act, _, T = CONFIGS[cfg]
     if kind == "impala":
-        return _cpu_worker_impala(wid, seconds, T)
-    torch.manual_seed(124)
-    pol = policies.TorchPolicy(kind, n_in, n_act, seed=124)
-    theta = pol.get_flat()
-    tab = noise.NoiseTable(1 << 22, theta.size, 124 + wid)
-    env = envs.SyntheticEnv(n_in, n_act, kind == "discrete", T)
-    rng = np.random.RandomState(wid)
-    steps, t0, obs = 0, time.perf_counter(), env.reset()
-    while time.perf_counter() - t0 < seconds:
-        idx = int(tab.sample_indices(1)[0])
-        sg = 1 if steps % 2 == 0 else -1
-        pol.set_flat(noise.perturb(theta, tab.table, [idx], [sg], 0.02)[0])
-        nf = (lambda t: np.float32(rng.uniform())) if kind == "discrete" else \
-             (lambda t: rng.randn(n_act).astype(np.float32))
-        _, _, n, obs = agent.collect_return(pol, env, obs, False, nf, lambda: rng.choice((-1e-12, 1e-12)))
-        steps += n
-    return steps, time.perf_counter() - t0
+        steps, el = _cpu_worker_impala(wid, seconds, T)
+        return steps, 0, el
+    from oracle import agent
+    return agent.reference_collect_loop(kind, n_in, n_act, T, seconds, wid)
 
 
-def cpu_baseline(cfg, seconds, cores):
+def _cpu_learner(args):
+    P, n = args
+    import torch
+    torch.set_num_threads(1)
+    from oracle import agent
+    return agent.reference_learner_step_seconds(P, n)
+
+
+def cpu_cores():
+    """Host cores this process may use: the affinity set, capped by the harness's CPU share
+    (OMP_NUM_THREADS = 16 per GPU on the box; os.cpu_count() there reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(share))) if share and share.isdigit() else max(1, n)
+
+
+def cpu_baseline(cfg, seconds, cores, lanes, n_params, T):
+    """Oracle restatement of SequentialRunner.train's worker + learner (run_sequential.py:113-179) on `cores`
+    processes: env steps/s from whole reference-shaped episodes, and sec per FD step = lanes x T env steps at
+    that rate + the restated FiniteDifferences.step on `lanes` returns (one core)."""
     ctx = multiprocessing.get_context("fork")
     with ctx.Pool(cores) as pool:
         res = pool.map(_cpu_worker, [(i, seconds, cfg) for i in range(cores)])
+        n_learn = lanes if n_params * lanes <= 64e6 else 64
+        learn_s = pool.apply(_cpu_learner, ((n_params, n_learn),)) * lanes / n_learn
     steps = sum(r[0] for r in res)
-    wall = max(r[1] for r in res)
-    return steps / wall, steps
+    episodes = sum(r[1] for r in res)
+    wall = max(r[2] for r in res)
+    rate = steps / wall
+    return rate, steps, episodes, lanes * T / rate + learn_s, learn_s, n_learn
 
 
 # ------------------------------------------------------------------------------------------------
@@ -144,6 +153,7 @@ def main():
     ap.add_argument("--episode-len", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-variant", action="store_true", help="skip the 4096-pair variant line (config 3)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -153,15 +163,25 @@ def main():
     if args.episode_len:
         T = args.episode_len
 
+    L = args.perturbations or (IMPALA_LANES if kind == "impala" else DEFAULT_LANES.get(args.config, 4096))
+    E = IMPALA_ENVS if kind == "impala" else 1
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cores = max(1, min(16, os.cpu_count() or 1))
-        v, steps = cpu_baseline(args.config, args.cpu_seconds, cores)
+        from oracle import impala as oimp
+        from oracle import policies as opol
+        P = oimp.num_params(n_act) if kind == "impala" else opol.num_params(kind, n_in, n_act)
+        cores = cpu_cores()
+        v, steps, eps, fd_s, learn_s, n_learn = cpu_baseline(args.config, args.cpu_seconds, cores, L * E, P, T)
         cpu = {"value": round(v, 1), "unit": "env steps/s", "cores": cores, "kind": "port",
-               "sample": "%d processes x %.0f s of %s (T=%d, +/-eps perturbed %s policy, torch CPU "
-                         "forward per step, 1 thread each): %d env steps"
-                         % (cores, args.cpu_seconds, "whole episodes" if kind != "impala" else "episode steps",
-                            T, kind, steps)}
+               "sec_per_fd_step": round(fd_s, 3),
+               "sample": ("%d processes x %.0f s of the oracle's reference-shaped loop (worker/worker.py:20-57 + "
+                          "worker/agent.py:20-71: perturb, per-step batch-1 torch forward + torch %s sampling, "
+                          "env.step, end-of-episode entropy forward; 1 thread each as run_client.py:15; T=%d): "
+                          "%d env steps, %d whole episodes; sec_per_fd_step = %d lanes x T env steps at that rate "
+                          "+ FiniteDifferences.step restated on %d returns (%.3f s%s)"
+                          % (cores, args.cpu_seconds, "Categorical" if kind != "mujoco" else "Normal", T, steps,
+                             eps, L * E, n_learn, learn_s,
+                             ", scaled linearly from the sample" if n_learn != L * E else ""))}
 
     import numpy as np
     import torch
@@ -194,48 +214,77 @@ def main():
         env = SyntheticEnv.named(env_name, device=dev, episode_len=T)
     table = SharedNoiseTable(25_000_000, policy.num_params, random_seed=124)
     table.device_table(dev)
-    agent = Agent(policy, env, random_seed=124 + rank)
+    agent = Agent(policy, env, random_seed=124)   # rank-independent: lane streams are keyed by global lane id
     worker = Worker(policy, agent, table, None, sigma=0.02, random_seed=124)
     omega = AdaptiveOmega()
     learner = FiniteDifferences(policy, DSGD(policy.parameters(), lr=0.01), omega, table, noise_std=0.02)
 
-    L = args.perturbations or (IMPALA_LANES if impala else DEFAULT_LANES.get(args.config, 4096))
-    E = IMPALA_ENVS if impala else 1
+    novelty = args.config == "impala_fp16"     # config 5: strategy.sparse_history_manager + utils.adaptive_omega
+    if novelty:
+        from strategy import StrategyHandler
+        from utils import math_helpers
+        from run_sequential import SequentialRunner
+        handler = StrategyHandler(policy, math_helpers.categorical_tvd, max_history_size=200, fp16=True)
+        # zeta: ZETA_SIZE obs of random-action steps (run_sequential.py:198-213); archive: the policy + 3 nearby
+        zeta = SequentialRunner._random_action_obs(_ZetaSource(env, dev), ZETA_SIZE)
+        flat = policy.get_trainable_flat()
+        rs = np.random.RandomState(0)
+        handler.points = [flat] + [(flat + 0.02 * rs.randn(flat.size)).astype(np.float32) for _ in range(3)]
+        handler.set_zeta(zeta)
+        worker.strategy_handler = handler
+
     n_dirs_global = (L // 2) * world
     from fdr import dist as fdist
     lane_range = fdist.lane_range(n_dirs_global, 2, world, rank)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     roll_ms = []
     phase_ms = []
+    step_no = [0]
 
-    def fd_step(timed):
+    def fd_step(timed, n_dirs=n_dirs_global, rng=lane_range):
+        # the action stream is keyed by (step seed, global lane id): every rank evaluates the lanes of a
+        # 1-GPU run bit-identically, whatever the shard (include/fdr.h lane_offset)
+        seed = 1000 + step_no[0]
+        step_no[0] += 1
         if timed:
             ev0.record()
-        batch = worker.evaluate(n_dirs_global, antithetic=True, lane_range=lane_range)
+        batch = worker.evaluate(n_dirs, antithetic=True, lane_range=rng, seed=seed, novelty=novelty)
         if timed:
             ev1.record()
         out = learner.step_async(batch, 0.0, 0.0, 0.0)
+        if novelty:
+            # run_sequential.py:149-151 (the noisy mean reward; one host read per FD step) and :160
+            omega.step(float(batch.reward.mean().item()))
+            handler.add_policy(policy)
         if timed and impala:
             phase_ms.append(engine.impala_profile_read())
         return out, batch
 
+    def timed_loop(steps, **kw):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pairs = []
+        out = None
+        for _ in range(steps):
+            out, _ = fd_step(True, **kw)
+            pairs.append((ev0, ev1))
+            _new_events()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0, pairs, out
+
+    def _new_events():
+        nonlocal ev0, ev1
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
     for _ in range(args.warmup):
         out, _ = fd_step(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out, batch = fd_step(True)
-        # the rollout brackets are read after the loop; keep one pair per step
-        roll_ms.append((ev0, ev1))
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed, roll_ms, out = timed_loop(args.steps)
     rollout_ms = float(np.mean([a.elapsed_time(b) for a, b in roll_ms]))
     if world > 1:
         t = torch.tensor([elapsed, rollout_ms], dtype=torch.float64, device=dev)
@@ -243,16 +292,43 @@ def main():
         elapsed, rollout_ms = t.tolist()
     upd, gnorm = out.tolist()
     assert gnorm > 0 and np.isfinite(upd)
+    conv_phase = None
+    if impala:
+        conv_phase = [float(np.mean([p[i] for p in phase_ms])) for i in range(3)]
+        phase_ms.clear()
+
+    variants = {}
+    if not impala and args.config == "halfcheetah" and not args.no_variant:
+        # also report the 4096-pair variant (4096 directions x +-, 8192 lanes per GPU)
+        nv = 2 * n_dirs_global
+        rng2 = fdist.lane_range(nv, 2, world, rank)
+        fd_step(False, n_dirs=nv, rng=rng2)
+        k = max(1, min(args.steps, 10))
+        el2, pairs2, out2 = timed_loop(k, n_dirs=nv, rng=rng2)
+        r2 = float(np.mean([a.elapsed_time(b) for a, b in pairs2]))
+        if world > 1:
+            t = torch.tensor([el2, r2], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el2, r2 = t.tolist()
+        lanes2 = 2 * L
+        variants["4096_pairs"] = {
+            "value": round(lanes2 * T * world * k / el2, 1), "unit": "env steps/s", "steps": k,
+            "ms_per_step": round(el2 / k * 1e3, 4), "sec_per_fd_step": round(el2 / k, 6),
+            "perturbations_per_gpu": lanes2, "directions_per_gpu": lanes2 // 2, "rollout_ms": round(r2, 4),
+            "roofline_frac": round(lane_step_flops(kind, n_in, n_act) * lanes2 * T / (r2 * 1e-3) / 1e12
+                                   / FP32_PEAK_TFLOPS, 4),
+            "kernel": rollout_kernel_name(kind, n_in, n_act, lanes2, dev)}
 
     lane_steps = L * E * T * world * args.steps
     value = lane_steps / elapsed
-    traffic = None
+    prof = None
     pmc = os.path.join(REPO, "profiles", "pmc_rollout_%s.json" % args.config)
     if os.path.exists(pmc):
         with open(pmc) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            prof = json.load(f)
+    traffic = None if prof is None else prof.get("hbm_bytes_per_launch")
     if impala:
-        conv_ms, core_ms, replay_ms = (float(np.mean([p[i] for p in phase_ms])) for i in range(3))
+        conv_ms, core_ms, replay_ms = conv_phase
         if world > 1:
             t = torch.tensor([conv_ms, core_ms, replay_ms], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -262,45 +338,55 @@ def main():
         core_bytes = IMPALA_CORE_BYTES // (2 if fp16 else 1)
         core_gbs = core_bytes * L / (core_ms / T * 1e-3) / 1e9
         peak = FP16_PEAK_TFLOPS if fp16 else FP32_PEAK_TFLOPS
+        core_prof = None if prof is None else prof.get("core_kernel")
         roofline = {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(achieved_tf / peak, 4), "traffic": traffic,
                     "kernel": "impala conv_kernel_h (15 convs, v_mfma_f32_16x16x32_f16)" if fp16 else
                               "impala conv_kernel (15 convs, v_mfma_f32_16x16x4_f32)",
                     "conv_launch_ms": round(conv_launch_ms, 4), "flop_per_env_step": IMPALA_CONV_FLOP,
                     "envs_per_launch": L * E, "rollout_ms": round(rollout_ms, 3),
+                    "mfma_busy_pmc": None if prof is None else prof.get("mfma_busy"),
                     "core_kernel": {"bound": "hbm", "achieved": round(core_gbs, 1), "peak": HBM_PEAK_GBS,
                                     "unit": "GB/s", "frac": round(core_gbs / HBM_PEAK_GBS, 4),
-                                    "launch_ms": round(core_ms / T, 4), "bytes_per_lane_step": core_bytes},
+                                    "launch_ms": round(core_ms / T, 4), "bytes_per_lane_step": core_bytes,
+                                    "traffic": None if core_prof is None else core_prof.get("hbm_bytes_per_launch")},
                     "entropy_replay_ms": round(replay_ms, 3),
+                    "profile": None if prof is None else "profiles/%s_summary.md" % prof.get("tag"),
                     "note": ("dense f16 MFMA peak" if fp16 else "f32 MFMA peak (= f32 vector peak)") +
-                            "; conv time from HIP events between the step-loop launches (fdr_impala_profile)"}
+                            "; conv time from HIP events between the step-loop launches (fdr_impala_profile); "
+                            "traffic / mfma_busy_pmc: rocprofv3 PMC of the same command (profile)"}
         workload = ("BASELINE config %d per GPU: ImpalaPolicy(A=%d) P=%d, %d perturbations (%d directions x +/-) x "
                     "%d envs each, synthetic 3x64x64 frames, T=%d, %s, full FD step (rollout + entropy pass + "
-                    "weights + gradient + DSGD)" % (5 if fp16 else 4, n_act, policy.num_params, L, L // 2, E, T,
-                                                    "fp16 rollouts" if fp16 else "f32"))
+                    "weights + gradient + DSGD%s)" % (5 if fp16 else 4, n_act, policy.num_params, L, L // 2, E, T,
+                                                      "fp16 rollouts" if fp16 else "f32",
+                                                      " + lane novelty vs a TVD strategy archive over %d zeta obs + "
+                                                      "AdaptiveOmega step" % ZETA_SIZE if novelty else ""))
     else:
         flops = lane_step_flops(kind, n_in, n_act) * L * T
-        hbm_model_bytes = 4 * policy.num_params + 4 * n_in + 4 * n_act + 4
         achieved_tf = flops / (rollout_ms * 1e-3) / 1e12
-        roofline = {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
+        hbm = None
+        if traffic:
+            gbs = traffic / (rollout_ms * 1e-3) / 1e9
+            hbm = {"traffic_bytes_per_launch": traffic, "achieved": round(gbs, 1), "unit": "GB/s",
+                   "peak": HBM_PEAK_GBS, "frac": round(gbs / HBM_PEAK_GBS, 5)}
+        roofline = {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
                     "kernel": rollout_kernel_name(kind, n_in, n_act, L, dev),
                     "rollout_ms": round(rollout_ms, 4),
                     "flop_per_lane_step": lane_step_flops(kind, n_in, n_act),
-                    "note": "fp32 VALU/matrix peak; theta' is VGPR-resident for the whole episode, so the "
-                            "kernel is compute-bound (DESIGN.md 'Roofline')",
-                    "survey_hbm_model": {
-                        "bytes_per_lane_step": hbm_model_bytes,
-                        "achieved": round(hbm_model_bytes * L * T / (rollout_ms * 1e-3) / 1e9, 1),
-                        "unit": "GB/s", "peak": HBM_PEAK_GBS,
-                        "frac": round(hbm_model_bytes * L * T / (rollout_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
-                        "note": "SURVEY 8(d) model: theta' (4P B) + obs + action + reward streamed per lane-step; "
-                                "this design reads theta' once per episode, so the measured HBM bytes are "
-                                "'traffic' (the north star's >=40% HBM target is met on this model)"}}
+                    "hbm": hbm,
+                    "profile": None if prof is None else "profiles/%s_summary.md" % prof.get("tag"),
+                    "note": "f32 VALU peak (v_pk_fma_f32; = the f32 MFMA peak on gfx950): theta' is VGPR/LDS-resident "
+                            "for the whole episode, so the kernel is VALU-issue bound; its HBM traffic (PMC "
+                            "FETCH_SIZE x2 + WRITE_SIZE of the same kernel, 'profile') is the noise-table gather once "
+                            "per episode"}
         workload = ("BASELINE config 3: HalfCheetah-shaped synthetic env (obs 17, act 6), MujocoPolicy(17,6) P=%d, "
                     "%d antithetic perturbations per GPU (%d directions x +/-), T=%d fixed-length episodes, full FD "
                     "step (rollout + weights + gradient + DSGD)" % (policy.num_params, L, L // 2, T)
-                    if args.config == "halfcheetah" else args.config)
+                    if args.config == "halfcheetah" else
+                    "BASELINE config 2: CartPole-shaped synthetic env (obs 4, 2 actions), DiscretePolicy(4,2) P=%d, "
+                    "%d antithetic perturbations (%d directions x +/-), T=%d, full FD step" % (
+                        policy.num_params, L, L // 2, T) if args.config == "cartpole" else args.config)
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -320,12 +406,23 @@ def main():
                    "parallelism": "dp%d" % world},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "variants": variants or None,
         "update_norm": upd,
     }
+    if novelty:
+        line["config"]["novelty"] = {"archive": len(handler.points), "zeta": ZETA_SIZE, "omega": omega.omega}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+class _ZetaSource(object):
+    """The attributes SequentialRunner._random_action_obs reads (env, device, rng)."""
+
+    def __init__(self, env, dev):
+        import numpy as np
+        self.env, self.device, self.rng = env, dev, np.random.RandomState(124)
 
 
 if __name__ == "__main__":

@@ -378,6 +378,48 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* d, const float* thet
   return impala::launch_forward(f, ws, ws_bytes, (hipStream_t)stream);
 }
 
+int64_t fdr_impala_strategies_workspace_bytes(const fdr_impala_desc* d, int32_t n_lanes, int32_t n_states) {
+  impala::Layout L;
+  if (!d || n_lanes < 0 || n_states < 0 || !impala::make_layout(d->n_act, &L)) return -1;
+  return impala::strategies_workspace_bytes(L, n_lanes, n_states, d->fp16 != 0);
+}
+
+int fdr_impala_strategies(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lanes_desc* lanes, int32_t n_lanes,
+                          int32_t n_states, const float* frames, const float* reward, float* h, float* c,
+                          float* probs, void* ws, int64_t ws_bytes, fdr_stream stream) {
+  (void)ctx;
+  impala::Layout L;
+  int rc = impala_layout(d, &L);
+  if (rc) return rc;
+  impala::StrategiesCall sc{};
+  rc = lanes_args(lanes, n_lanes, L.P, &sc.lanes);
+  if (rc) return rc;
+  if (n_states < 0 || n_states > (1 << 20)) return set_error(FDR_ERR_INVALID, "n_states out of range");
+  if (n_states > 0 && (!frames || !probs)) return set_error(FDR_ERR_INVALID, "NULL frames / probs");
+  if ((h == nullptr) != (c == nullptr)) return set_error(FDR_ERR_INVALID, "h and c must both be given or both NULL");
+  sc.layout = &L;
+  sc.n_lanes = n_lanes;
+  sc.n_states = n_states;
+  sc.fp16 = d->fp16 != 0;
+  sc.frames = frames;
+  sc.reward = reward;
+  sc.h = h;
+  sc.c = c;
+  sc.probs = probs;
+  sc.bn_mean = d->bn_mean;
+  sc.bn_var = d->bn_var;
+  return impala::launch_strategies(sc, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int fdr_impala_env_frames(uint64_t env_seed, int32_t n_act, int64_t env_id, int32_t t0, int32_t n,
+                          const int32_t* actions, float* frames, float* reward, fdr_stream stream) {
+  if (n_act < 1 || n_act > impala::kMaxAct) return set_error(FDR_ERR_INVALID, "n_act must be in 1..32");
+  if (n < 0 || t0 < 0 || t0 + (int64_t)n >= (1 << 20) || env_id < 0) return set_error(FDR_ERR_INVALID, "bad range");
+  if (n > 0 && !frames) return set_error(FDR_ERR_INVALID, "NULL frames");
+  return impala::launch_env_frames(env_seed, n_act, (uint64_t)env_id, t0, n, actions, frames, reward,
+                                   (hipStream_t)stream);
+}
+
 int fdr_impala_profile(int32_t enable) {
   impala::set_profile(enable);
   return FDR_OK;

@@ -63,6 +63,7 @@ struct StepArgs {
   int64_t lane_offset;
   uint64_t fkey, rkey, akey;
   const float* frames;     // external frames [lane*E+e][3][64][64] (forward API) or NULL
+  int shared_frames;       // 1: every lane reads frames [e][3][64][64] (strategy probe set zeta)
   float* feat;             // [lane*E+e][2048]
   // core
   float* h;
@@ -89,7 +90,9 @@ struct StepArgs {
 
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
 constexpr float kBnEps = 1e-5f;
-enum CoreMode { kRollout = 0, kReplay = 1, kForward = 2 };
+// kStrategy: the replay's sequence form over a probe set (get_strategy), probabilities out
+enum CoreMode { kRollout = 0, kReplay = 1, kForward = 2, kStrategy = 3 };
+constexpr bool seq_mode(int m) { return m == kReplay || m == kStrategy; }
 constexpr int kCoreThreads = 256;
 constexpr int kBnTab = 15 * 32;
 
@@ -130,6 +133,8 @@ __device__ __forceinline__ void core_finish(const StepArgs& a, const float* logi
     if constexpr (MODE == kForward) {
       if (a.probs)
         for (int i = 0; i < A; ++i) a.probs[ge * A + i] = p[i];
+    } else if constexpr (MODE == kStrategy) {
+      for (int i = 0; i < A; ++i) a.probs[(ge * a.T + a.t) * A + i] = p[i];
     } else if constexpr (MODE == kReplay) {
       // torch Categorical(probs).entropy(): normalise, log clamped at float min
       float tot = 0.f;
@@ -236,6 +241,24 @@ struct ForwardCall {
   const float* bn_var;
 };
 int64_t forward_workspace_bytes(const Layout& L, int n_envs, bool fp16 = false);
+
+// get_strategy over a probe set (policies/impala.py:24-27): Z shared frames, one LSTM sequence per lane
+struct StrategiesCall {
+  const Layout* layout;
+  LanesArgs lanes;
+  int n_lanes, n_states, fp16;
+  const float* frames;   // [Z][3][64][64] f32 0..255
+  const float* reward;   // [Z] or NULL
+  float* h;              // [n_lanes][256] in/out initial state, or NULL (zero state)
+  float* c;
+  float* probs;          // [n_lanes][Z][A]
+  const float* bn_mean;
+  const float* bn_var;
+};
+int64_t strategies_workspace_bytes(const Layout& L, int n_lanes, int n_states, bool fp16);
+int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipStream_t stream);
+int launch_env_frames(uint64_t env_seed, int n_act, uint64_t env_id, int t0, int n, const int32_t* actions,
+                      float* frames, float* reward, hipStream_t stream);
 void set_profile(int on);
 void set_debug_clock(uint64_t* buf);
 int read_profile(double* out3);

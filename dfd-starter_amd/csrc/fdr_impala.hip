@@ -606,7 +606,7 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
 
   // ---- frame (policies/impala.py:147: frame / 255) -> BN2d(3) -> padded [3][66][66] ----
   if (a.frames) {
-    const float* fr = a.frames + env * kFramePix;
+    const float* fr = a.frames + (a.shared_frames ? (int64_t)e : env) * kFramePix;
     for (int p = threadIdx.x; p < kFramePix; p += kConvThreads) {
       const int ch = p >> 12, y = (p >> 6) & 63, x = p & 63;
       T[ch * FPLANE + (y + 1) * FW + x + 1] = fmaf(fr[p] / 255.0f, bsc[ch], bsh[ch]);
@@ -697,7 +697,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
   const int A = a.n_act;
   const int c4 = j & 63, wq = j >> 6;  // float4 column group, wave index
 
-  if constexpr (MODE != kReplay) {
+  if constexpr (!seq_mode(MODE)) {
     for (int k = j; k < kFeat; k += kCoreThreads) {
       const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + k] : 0.f;
       const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + k] : 1.f;
@@ -775,7 +775,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
 #pragma unroll
       for (int e = 0; e < E; ++e) ax[c][e] = ah[c][e] = 0.f;
     const float4* wl = reinterpret_cast<const float4*>(pk + L.lstm_wt) + j;
-    if (MODE == kReplay && a.gx) {  // x W_ih^T precomputed by lstm_xproj_kernel (same fma chain)
+    if (seq_mode(MODE) && a.gx) {  // x W_ih^T precomputed by lstm_xproj_kernel (same fma chain)
       const float4* g4 = reinterpret_cast<const float4*>(a.gx + ((int64_t)(a.t - a.gx_t0) * a.n_lanes * E + e0) * kGates);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
@@ -1174,6 +1174,225 @@ int launch_forward(const ForwardCall& c, void* ws, int64_t ws_bytes, hipStream_t
     hipLaunchKernelGGL((core_kernel<1, kForward>), dim3(c.n_envs), dim3(kCoreThreads), 0, stream, L, a);
   }
   return check_launch("impala forward");
+}
+
+
+// ------------------------------------------------------------------------------------------
+// get_strategy over a probe set zeta (policies/impala.py:24-27 -> ImpalaCNN.forward :136-186): the Z
+// stacked obs are ONE batch_first LSTM sequence per lane (B = 1, T = Z), so per lane the conv stack runs
+// on Z shared frames (conv kernel, shared_frames), the fc is one GEMM over the Z feature rows
+// (fc_rows_kernel below), the LSTM input projection one GEMM per 64-step chunk (lstm_xproj_kernel) and
+// the recurrence + head one core-kernel launch per step (kStrategy: probabilities out).
+// ------------------------------------------------------------------------------------------
+// ci[z][lane][0:256] = relu(BN1d(feat_(lane, z)) W_fc^T + b_fc), ci[z][lane][256] = clamp(reward_z, -1, 1)
+// (policies/impala.py:161-164) on v_mfma_f32_16x16x4_f32: 64 rows x 256 columns per workgroup, K = 2048
+// in LDS chunks of 32 with the eval-mode BN folded into the X-tile load.  fp16 mode reads the f16 W^T.
+template <bool HALF>
+__global__ __launch_bounds__(256) void fc_rows_kernel(Layout L, StepArgs a, int z0, int zc) {
+  constexpr int KC = 32, XP = 80, WP = 256 + 16;
+  __shared__ float xs[KC * XP];  // [k][row]
+  __shared__ float ws[KC * WP];  // [k][col]
+  const int lane = blockIdx.x, row0 = blockIdx.y * 64;
+  const int tid = threadIdx.x, wave = tid >> 6, ln = tid & 63, g = ln >> 4, r = ln & 15;
+  const float* pk = a.pack + (int64_t)lane * a.pack_stride;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < 4; ++tj) acc[ti][tj] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < kFeat; k0 += KC) {
+    const int kk = k0 + (tid & 31);  // every X element this thread loads has this k
+    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + kk] : 0.f;
+    const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + kk] : 1.f;
+    const float sc = pk[L.bn_w[15] + kk] * (1.f / sqrtf(rv + kBnEps));
+    const float sh = pk[L.bn_b[15] + kk] - rm * sc;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int i = tid + 256 * m, row = i >> 5, q = row0 + row;
+      xs[(i & 31) * XP + row] = q < zc ? fmaf(a.feat[((int64_t)lane * zc + q) * kFeat + kk], sc, sh) : 0.f;
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const int i = tid + 256 * m, k = i >> 6, c4 = i & 63;
+      float4 w;
+      if constexpr (HALF) {
+        typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+        const h4v hv = *reinterpret_cast<const h4v*>(a.hpack + (int64_t)lane * a.hpack_stride + L.fc_wt_h +
+                                                      (int64_t)(k0 + k) * kHid + 4 * c4);
+        w = float4{(float)hv[0], (float)hv[1], (float)hv[2], (float)hv[3]};
+      } else {
+        w = *reinterpret_cast<const float4*>(pk + L.fc_wt + (int64_t)(k0 + k) * kHid + 4 * c4);
+      }
+      *reinterpret_cast<float4*>(ws + k * WP + 4 * c4) = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < KC / 4; ++s) {
+      const int k = 4 * s + g;
+      float av[4], bv[4];
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti) av[ti] = xs[k * XP + 16 * ti + r];
+#pragma unroll
+      for (int tj = 0; tj < 4; ++tj) bv[tj] = ws[k * WP + 64 * wave + 16 * tj + r];
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+        for (int tj = 0; tj < 4; ++tj) acc[ti][tj] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ti], bv[tj], acc[ti][tj], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  float bias[4];
+#pragma unroll
+  for (int tj = 0; tj < 4; ++tj) bias[tj] = pk[L.fc_b + 64 * wave + 16 * tj + r];
+#pragma unroll
+  for (int ti = 0; ti < 4; ++ti)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int q = row0 + 16 * ti + 4 * g + v;
+      if (q >= zc) continue;
+      float* dst = a.ci + ((int64_t)(z0 + q) * a.n_lanes + lane) * kCoreIn + 64 * wave + r;
+#pragma unroll
+      for (int tj = 0; tj < 4; ++tj) dst[16 * tj] = relu(acc[ti][tj][v] + bias[tj]);
+    }
+  if (blockIdx.y == 0 && tid < zc) {
+    const float rw = a.reward_in ? a.reward_in[z0 + tid] : 0.f;
+    a.ci[((int64_t)(z0 + tid) * a.n_lanes + lane) * kCoreIn + kHid] = fminf(fmaxf(rw, -1.f), 1.f);
+  }
+}
+
+namespace {
+struct StratPlan {
+  int64_t pack, hpack, feat, ci, gx, h, c, n2, total;
+  int nblk;
+};
+StratPlan strat_plan(const Layout& L, int n_lanes, int Z, bool fp16) {
+  StratPlan p{};
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) { const int64_t at = o; o += round_up(std::max<int64_t>(bytes, 0), 256); return at; };
+  const int zc = std::min(Z, kReplayChunk);
+  p.nblk = prep_blocks(L);
+  p.pack = take((int64_t)n_lanes * L.pack * 4);
+  p.hpack = take(fp16 ? (int64_t)n_lanes * L.hpack * 2 : 0);
+  p.feat = take((int64_t)n_lanes * zc * kFeat * 4);
+  p.ci = take((int64_t)Z * n_lanes * kCoreIn * 4);
+  p.gx = take((int64_t)zc * n_lanes * kGates * 4);
+  p.h = take((int64_t)n_lanes * kHid * 4);
+  p.c = take((int64_t)n_lanes * kHid * 4);
+  p.n2 = take((int64_t)n_lanes * p.nblk * 8);
+  p.total = o;
+  return p;
+}
+}  // namespace
+
+int64_t strategies_workspace_bytes(const Layout& L, int n_lanes, int n_states, bool fp16) {
+  return strat_plan(L, n_lanes, n_states, fp16).total;
+}
+
+int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  const Layout& L = *c.layout;
+  const int Z = c.n_states;
+  const StratPlan p = strat_plan(L, c.n_lanes, Z, c.fp16 != 0);
+  if (!ws || ws_bytes < p.total) return set_error(FDR_ERR_WORKSPACE, "impala strategies workspace too small");
+  if (c.n_lanes == 0 || Z == 0) return FDR_OK;
+  char* w = static_cast<char*>(ws);
+  const bool half = c.fp16 != 0;
+  StepArgs a{};
+  a.pack = reinterpret_cast<float*>(w + p.pack);
+  a.pack_stride = L.pack;
+  a.bn_mean = c.bn_mean;
+  a.bn_var = c.bn_var;
+  a.n_lanes = c.n_lanes;
+  a.n_act = L.n_act;
+  a.T = Z;
+  a.shared_frames = 1;
+  a.reward_in = c.reward;
+  a.feat = reinterpret_cast<float*>(w + p.feat);
+  a.ci = reinterpret_cast<float*>(w + p.ci);
+  a.h = c.h ? c.h : reinterpret_cast<float*>(w + p.h);
+  a.c = c.c ? c.c : reinterpret_cast<float*>(w + p.c);
+  a.probs = c.probs;
+  double* n2 = reinterpret_cast<double*>(w + p.n2);
+  launch_pack<float>(L, c.lanes, const_cast<float*>(a.pack), n2, c.n_lanes, 0, stream);
+  if (half) {
+    a.hpack = reinterpret_cast<_Float16*>(w + p.hpack);
+    a.hpack_stride = L.hpack;
+    launch_pack<_Float16>(L, c.lanes, a.hpack, n2, c.n_lanes, 1, stream);
+  }
+  if (!c.h || !c.c) {  // the reset state (worker/agent.py:66 resets the policy before compute_novelty)
+    if (hipMemsetAsync(a.h, 0, (size_t)c.n_lanes * kHid * 4, stream) != hipSuccess ||
+        hipMemsetAsync(a.c, 0, (size_t)c.n_lanes * kHid * 4, stream) != hipSuccess)
+      return set_error(FDR_ERR_HIP, "memset of the initial LSTM state failed");
+  }
+  for (int z0 = 0; z0 < Z; z0 += kReplayChunk) {
+    const int zc = std::min(kReplayChunk, Z - z0);
+    a.envs = zc;
+    a.frames = c.frames + (int64_t)z0 * kFramePix;
+    const int conv_grid = (c.n_lanes + 7) / 8 * 8 * zc;
+    if (half)
+      hipLaunchKernelGGL(conv_kernel_h, dim3(conv_grid), dim3(kHThreads), 0, stream, L, a);
+    else
+      hipLaunchKernelGGL(conv_kernel, dim3(conv_grid), dim3(kConvThreads), 0, stream, L, a);
+    const dim3 grid(c.n_lanes, (zc + 63) / 64);
+    if (half)
+      hipLaunchKernelGGL(fc_rows_kernel<true>, grid, dim3(256), 0, stream, L, a, z0, zc);
+    else
+      hipLaunchKernelGGL(fc_rows_kernel<false>, grid, dim3(256), 0, stream, L, a, z0, zc);
+  }
+  a.envs = 1;
+  float* gx = reinterpret_cast<float*>(w + p.gx);
+  for (int t0 = 0; t0 < Z; t0 += kReplayChunk) {
+    const int tc = std::min(kReplayChunk, Z - t0);
+    const dim3 grid(c.n_lanes, (tc + 63) / 64, kGates / 256);
+    a.gx = nullptr;
+    if (half)
+      hipLaunchKernelGGL(lstm_xproj_kernel<true>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);
+    else
+      hipLaunchKernelGGL(lstm_xproj_kernel<false>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);
+    a.gx = gx;
+    a.gx_t0 = t0;
+    for (int t = t0; t < t0 + tc; ++t) {
+      a.t = t;
+      if (half)
+        hipLaunchKernelGGL((core_kernel_h<1, kStrategy>), dim3(c.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+      else
+        hipLaunchKernelGGL((core_kernel<1, kStrategy>), dim3(c.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
+    }
+  }
+  return check_launch("impala strategies");
+}
+
+// ------------------------------------------------------------------------------------------
+// The synthetic frame env's observations outside a rollout (eval states / the probe set zeta,
+// run_sequential.py:142-143, 198-213): frame_t of env `env_id` (the conv kernel's generator) and, given
+// the actions taken, the reward each step returns.  One workgroup per step.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void env_frames_kernel(uint64_t fkey, uint64_t rkey, int n_act, uint64_t env_id,
+                                                         int t0, const int32_t* actions, float* frames,
+                                                         float* reward) {
+  const int i = blockIdx.x, t = t0 + i;
+  float* fr = frames + (int64_t)i * kFramePix;
+  for (int w = threadIdx.x; w < kFramePix / 8; w += blockDim.x) {
+    const uint64_t hb = mix64(fkey + ((env_id << 32) | ((uint64_t)t << 11) | (uint64_t)w) * kGolden);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fr[8 * w + j] = (float)((uint32_t)(hb >> (8 * j)) & 255u);
+  }
+  if (threadIdx.x == 0 && reward) {
+    float r = 0.f;
+    if (actions) {
+      const int tgt = (int)((mix64(rkey + ((env_id << 32) | ((uint64_t)t << 11)) * kGolden) >> 40) % (uint64_t)n_act);
+      const int act = actions[i];
+      r = act == tgt ? 1.f : (act == (tgt + 1) % n_act ? -1.f : 0.f);
+    }
+    reward[i] = r;
+  }
+}
+
+int launch_env_frames(uint64_t env_seed, int n_act, uint64_t env_id, int t0, int n, const int32_t* actions,
+                      float* frames, float* reward, hipStream_t stream) {
+  if (n == 0) return FDR_OK;
+  hipLaunchKernelGGL(env_frames_kernel, dim3(n), dim3(256), 0, stream, mix64(env_seed ^ kFrameSalt),
+                     mix64(env_seed ^ kRewardSalt), n_act, env_id, t0, actions, frames, reward);
+  return check_launch("impala env frames");
 }
 
 }  // namespace impala

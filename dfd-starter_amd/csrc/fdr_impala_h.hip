@@ -413,7 +413,7 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
     const int y = w >> 3, x0 = (w & 7) * 8;
     float v[3][8];
     if (a.frames) {
-      const float* fr = a.frames + env * kFramePix;
+      const float* fr = a.frames + (a.shared_frames ? (int64_t)e : env) * kFramePix;
 #pragma unroll
       for (int c = 0; c < 3; ++c)
 #pragma unroll
@@ -513,7 +513,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
   const int64_t e0 = (int64_t)lane * E;
   const int A = a.n_act;
 
-  if constexpr (MODE != kReplay) {
+  if constexpr (!seq_mode(MODE)) {
     for (int k = j; k < kFeat; k += kCoreThreads) {
       const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + k] : 0.f;
       const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + k] : 1.f;
@@ -586,7 +586,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
     cj[e] = nd * a.c[(e0 + e) * kHid + j];
   }
   __syncthreads();
-  if (MODE == kReplay && a.gx) {
+  if (seq_mode(MODE) && a.gx) {
     // replay with x W_ih^T precomputed (lstm_xproj_kernel<true>): all 256 threads stream W_hh^T,
     // 4 columns each (the same per-column fma chain as below, twice the waves in flight)
     typedef _Float16 h4v __attribute__((ext_vector_type(4)));
@@ -685,6 +685,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
 template __global__ void core_kernel_h<1, kRollout>(Layout, StepArgs);
 template __global__ void core_kernel_h<1, kReplay>(Layout, StepArgs);
 template __global__ void core_kernel_h<1, kForward>(Layout, StepArgs);
+template __global__ void core_kernel_h<1, kStrategy>(Layout, StepArgs);
 template __global__ void core_kernel_h<2, kRollout>(Layout, StepArgs);
 template __global__ void core_kernel_h<2, kReplay>(Layout, StepArgs);
 template __global__ void core_kernel_h<4, kRollout>(Layout, StepArgs);

@@ -25,7 +25,8 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_fd_lambda_norms", "fdr_fd_grad_lambda", "fdr_bn_refresh_workspace_bytes", "fdr_bn_refresh",
            "fdr_atari_num_params", "fdr_atari_workspace_bytes", "fdr_atari_rollout",
            "fdr_atari_forward_workspace_bytes", "fdr_atari_forward", "fdr_rollout_set_impl",
-           "fdr_impala_set_replay_gemm")
+           "fdr_impala_set_replay_gemm", "fdr_impala_strategies_workspace_bytes", "fdr_impala_strategies",
+           "fdr_impala_env_frames")
 
 
 class FDRError(RuntimeError):
@@ -115,6 +116,10 @@ def _load():
         "fdr_impala_rollout": (ctypes.c_int, [P, ctypes.POINTER(ImpalaDesc), ctypes.POINTER(LanesDesc), I32, U64,
                                               I32, P, P, P, P, P, P, P, I64, P]),
         "fdr_impala_forward_workspace_bytes": (I64, [I32, I32, I32]),
+        "fdr_impala_env_frames": (ctypes.c_int, [U64, I32, I64, I32, I32, P, P, P, P]),
+        "fdr_impala_strategies_workspace_bytes": (I64, [ctypes.POINTER(ImpalaDesc), I32, I32]),
+        "fdr_impala_strategies": (ctypes.c_int, [P, ctypes.POINTER(ImpalaDesc), ctypes.POINTER(LanesDesc), I32, I32,
+                                                 P, P, P, P, P, P, I64, P]),
         "fdr_impala_profile": (ctypes.c_int, [I32]),
         "fdr_impala_profile_read": (ctypes.c_int, [P]),
         "fdr_impala_debug_clock": (ctypes.c_int, [P]),

@@ -263,6 +263,52 @@ def impala_forward(spec, theta, frames, h, c, reward=None, notdone=None, bn_mean
     return (probs, f) if feat else probs
 
 
+def impala_strategies(spec, lanes, n_lanes, frames, reward=None, h=None, c=None, bn_mean=None, bn_var=None):
+    """get_strategy of n_lanes ImpalaPolicy parameter vectors over the Z shared probe obs: the stacked obs
+    run as ONE LSTM sequence per lane (policies/impala.py:24-27) from (h, c) [n_lanes, 256] (updated in
+    place) or from the reset state (None).  frames [Z, 3, 64, 64] (0..255), reward [Z] -> probs
+    [n_lanes, Z, A] f32."""
+    dev = frames.device
+    _check_dev(frames, reward, h, c)
+    frames = frames.to(torch.float32).reshape(-1, 3 * 64 * 64).contiguous()
+    Z = frames.shape[0]
+    if reward is not None:
+        reward = reward.to(torch.float32).reshape(-1).contiguous()
+        if reward.numel() != Z:
+            raise ValueError("reward must have one entry per probe frame")
+    if (h is None) != (c is None):
+        raise ValueError("give both h and c, or neither")
+    for t in (h, c):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != n_lanes * 256):
+            raise ValueError("h / c must be contiguous float32 [n_lanes, 256]")
+    probs = torch.empty((n_lanes, Z, spec.n_act), dtype=torch.float32, device=dev)
+    d = spec.desc(bn_mean, bn_var)
+    nb = lib.fdr_impala_strategies_workspace_bytes(ctypes.byref(d), n_lanes, Z)
+    if nb < 0:
+        raise ValueError("bad impala spec")
+    ws = _workspace("impala_strat", nb, dev)
+    check(lib.fdr_impala_strategies(None, ctypes.byref(d), ctypes.byref(lanes), n_lanes, Z, _p(frames), _p(reward),
+                                    _p(h), _p(c), _p(probs), _p(ws), ws.numel(), _stream(dev)),
+          "fdr_impala_strategies")
+    return probs
+
+
+def impala_env_frames(env_seed, n_act, env_id, t0, n, actions=None, device=None):
+    """The frame env's observations frame_t (t0 <= t < t0 + n) of global env env_id -> (frames [n, 3, 64, 64]
+    f32, rewards [n] f32 returned by the steps given actions [n] (device i32; None -> 0))."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if actions is not None:
+        _check_dev(actions)
+        actions = actions.to(torch.int32).reshape(-1).contiguous()
+        if actions.numel() != n:
+            raise ValueError("actions must have n entries")
+    frames = torch.empty((n, 3, 64, 64), dtype=torch.float32, device=dev)
+    reward = torch.empty(n, dtype=torch.float32, device=dev)
+    check(lib.fdr_impala_env_frames(ctypes.c_uint64(int(env_seed) & ((1 << 64) - 1)), int(n_act), int(env_id), int(t0),
+                                    int(n), _p(actions), _p(frames), _p(reward), _stream(dev)), "fdr_impala_env_frames")
+    return frames, reward
+
+
 def impala_profile(enable):
     lib.fdr_impala_profile(1 if enable else 0)
 

@@ -121,19 +121,32 @@ class ImpalaPolicy(Policy):
         return int(Categorical(probs=probs.cpu()).sample().item())      # discrete.py:21-24
 
     @torch.no_grad()
+    def _sequence(self, x):
+        """The reference's stacked obs (impala.py:35-45: B = n, T = 1) through ImpalaCNN.forward: the
+        batch_first LSTM reads them as ONE sequence of length n (B = 1) from self.state, and only the first
+        obs' done flag masks the incoming state (the zip over notdone.unbind() yields one pair,
+        impala.py:165-176).  self.state becomes the end-of-sequence state (impala.py:184).  -> probs [n, A]."""
+        fr, rw, dn = self._stack(list(x) if not isinstance(x, dict) else x)
+        dev = self.flat.device
+        h, c = (s[:1].reshape(1, 256).clone().contiguous() for s in self.state)
+        if bool(dn[0]):
+            h.zero_()
+            c.zero_()
+        bm, bv = self.bn_stats()
+        probs = engine.impala_strategies(self.spec, engine.lanes_desc(self.flat, 0), 1, fr.to(dev), rw.to(dev),
+                                         h, c, bm, bv)
+        self.state = (h, c)
+        return probs[0]
+
+    @torch.no_grad()
     def get_entropy(self, x):
-        """impala.py:21-22: the stacked obs run as ONE LSTM sequence from the current state."""
-        fr, rw, dn = self._stack(list(x))
-        ents = []
-        for i in range(fr.shape[0]):
-            p = self._step(fr[i:i + 1], rw[i:i + 1], torch.zeros(1, dtype=torch.bool))
-            ents.append(Categorical(probs=p).entropy())
-        return torch.cat(ents).mean().item()
+        """impala.py:21-22 -> discrete.py:26-29: mean Categorical entropy of the stacked obs' sequence."""
+        return Categorical(probs=self._sequence(x)).entropy().mean().item()
 
     @torch.no_grad()
     def get_strategy(self, x):
-        fr, rw, dn = self._stack(list(x) if not isinstance(x, dict) else x)
-        return self._step(fr, rw, dn).cpu().numpy()                      # impala.py:24-27
+        """impala.py:24-27: the probabilities of the stacked obs' sequence, [n, A] (host)."""
+        return self._sequence(x).cpu().numpy()
 
     @torch.no_grad()
     def compute_vbn(self, buffer):

@@ -2,9 +2,13 @@
 (SURVEY 8f.2).
 
 A strategy is ``policy.get_strategy(zeta)`` over the probe states zeta (discrete: probs; mujoco:
-[mean | std]); the archive holds up to ``max_history_size`` strategies as ONE device tensor
-[H, Z, D].  Strategies come from the HIP policy forward over (policy, state) pairs
-(``engine.lane_strategies``), distances and novelty from ``fdr_strategy_distances`` (the reference's
+[mean | std]; ImpalaPolicy: probs of the zeta obs run as ONE LSTM sequence, policies/impala.py:24-27);
+the archive holds up to ``max_history_size`` strategies as ONE device tensor [H, Z, D].  MLP strategies
+come from the HIP policy forward over (policy, state) pairs (``engine.lane_strategies``), ImpalaPolicy
+strategies from ``fdr_impala_strategies`` (conv stack over the shared zeta frames, per-lane fc / LSTM
+sequence) started from the reset state -- the state Worker._build_ret scores novelty in
+(worker/agent.py:66 resets the policy before worker.py:53).  Distances and novelty come from
+``fdr_strategy_distances`` (the reference's
 ``l2_dist`` / ``categorical_tvd`` / ``gaussian_wasserstein_dist_from_strategies``, f64 accumulation).
 ``lane_novelty`` scores every perturbed lane of a batch in two launches -- the batched form of
 ``Worker._build_ret``'s per-return ``compute_novelty`` (worker/worker.py:53), which the reference
@@ -23,8 +27,9 @@ KIND_BY_NAME = {"l2_dist": "l2", "categorical_tvd": "tvd", "gaussian_wasserstein
 
 
 class StrategyHandler(object):
-    def __init__(self, policy, strategy_distance_fn=None, max_history_size=200):
+    def __init__(self, policy, strategy_distance_fn=None, max_history_size=200, fp16=False):
         self.policy = policy
+        self.fp16 = bool(fp16)        # ImpalaPolicy: strategies in the rollouts' fp16 mode (BASELINE config 5)
         self.strategy_distance_fn = strategy_distance_fn
         name = getattr(strategy_distance_fn, "__name__", "l2_dist") if strategy_distance_fn is not None \
             else "l2_dist"                     # compute_strategy_novelty's default (math_helpers.py:148-149)
@@ -36,28 +41,45 @@ class StrategyHandler(object):
         self.archive = None           # device f32 [H, Z, D]
         self.pair = None              # host f64 [H, H] known distances (inf on the diagonal)
         self.worst_point_idx = 0
-        self.zeta = None              # device f32 [Z, n_in]
+        self.zeta = None              # device f32 [Z, n_in]; ImpalaPolicy: (frames [Z, 3, 64, 64], reward [Z])
 
     # ---- strategies on the device ------------------------------------------------------------
     def _dev(self):
         return self.policy.flat.device
 
+    def _strategies(self, lanes_fn, n):
+        """get_strategy(zeta) of n parameter vectors; lanes_fn(Z) -> lanes descriptor (see engine.lane_strategies)."""
+        p = self.policy
+        bm, bv = p.bn_stats()
+        if p.KIND == "impala":
+            frames, reward = self.zeta
+            spec = engine.ImpalaSpec(p.output_shape, fp16=self.fp16)
+            return engine.impala_strategies(spec, lanes_fn(1), n, frames, reward, bn_mean=bm, bn_var=bv)
+        if p.KIND != "discrete" and p.KIND != "mujoco":
+            raise NotImplementedError("strategies of a %s policy are not built (novelty needs get_strategy over "
+                                      "zeta: policies/atari.py:31-32)" % p.KIND)
+        return engine.lane_strategies(p.spec, lanes_fn, n, self.zeta, bm, bv)
+
     def _strategies_of_flat(self, flat):
         """get_strategy(zeta) of one parameter vector -> [1, Z, D]."""
-        p = self.policy
         base = torch.as_tensor(np.asarray(flat, np.float32), device=self._dev()).contiguous()
-        bm, bv = p.bn_stats()
-        return engine.lane_strategies(p.spec, lambda Z: engine.lanes_desc(base, 0), 1, self.zeta, bm, bv)
+        return self._strategies(lambda Z: engine.lanes_desc(base, 0), 1)
+
+    def _strategies_of_flats(self, flats):
+        """Strategies of the archived vectors -> [H, Z, D] (ImpalaPolicy: one launch, lane l reads flats[l])."""
+        if self.policy.KIND == "impala":
+            base = torch.as_tensor(np.stack([np.asarray(f, np.float32) for f in flats]), device=self._dev())
+            base = base.contiguous()
+            return self._strategies(lambda Z: engine.lanes_desc(base, base.shape[1]), len(flats))
+        return torch.cat([self._strategies_of_flat(f) for f in flats])
 
     def lane_strategies(self, table, idx, sign, sigma):
         """Strategies of the perturbed lanes theta + sign * sigma * table[idx:] -> [n, Z, D]."""
         p = self.policy
-        n = idx.numel()
-        bm, bv = p.bn_stats()
 
         def lanes(Z):
             return engine.lanes_desc(p.flat, 0, table, idx.repeat_interleave(Z), sign.repeat_interleave(Z), sigma)
-        return engine.lane_strategies(p.spec, lanes, n, self.zeta, bm, bv)
+        return self._strategies(lanes, idx.numel())
 
     @property
     def strategy_tensor(self):
@@ -69,14 +91,19 @@ class StrategyHandler(object):
 
     # ---- reference API -----------------------------------------------------------------------
     def set_zeta(self, zeta):
-        """strategy_handler.py:19-24 -> evaluate_strategies + _construct_table (:33-71)."""
+        """strategy_handler.py:19-24 -> evaluate_strategies + _construct_table (:33-71).  ImpalaPolicy: zeta
+        is a list of obs dicts or one stacked dict {frame, reward, done} (impala.py:35-45)."""
         if zeta is None or len(zeta) == 0:
             return
-        z = torch.as_tensor(np.asarray(zeta, np.float32), device=self._dev())
-        self.zeta = z.reshape(z.shape[0], -1).contiguous()
+        if self.policy.KIND == "impala":
+            fr, rw, _ = self.policy._stack(zeta)
+            self.zeta = (fr.to(self._dev()).contiguous(), rw.to(self._dev()).contiguous())
+        else:
+            z = torch.as_tensor(np.asarray(zeta, np.float32), device=self._dev())
+            self.zeta = z.reshape(z.shape[0], -1).contiguous()
         if not self.points:
             return
-        self.archive = torch.cat([self._strategies_of_flat(f) for f in self.points]).contiguous()
+        self.archive = self._strategies_of_flats(self.points).contiguous()
         self._construct_table()
 
     def _construct_table(self):

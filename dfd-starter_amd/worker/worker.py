@@ -150,6 +150,8 @@ class Worker(object):
         if E > 1:
             idx, sign, is_eval = np.repeat(idx, E), np.repeat(sign, E), np.repeat(is_eval, E)
         eval_states = self.eval_states() if is_eval.any() else None
+        if isinstance(eval_states, dict):   # ImpalaPolicy: the stacked obs dict -> the reference's list of dicts
+            eval_states = [{k: v[i:i + 1] for k, v in eval_states.items()} for i in range(len(eval_states["frame"]))]
         b = FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, idx, sign, self.epoch,
                     is_eval=is_eval)
         b.novelty = None if nov is None else nov.cpu().numpy()
@@ -167,28 +169,47 @@ class Worker(object):
     # ---- novelty path -----------------------------------------------------------
     def lane_novelty(self, idx_d, sign_d):
         """compute_novelty of every lane's (perturbed) policy, worker.py:53, batched on the device
-        (f64 [n]); None without a strategy handler."""
+        (f64 [n]); None without a strategy handler.  With E envs per lane (ImpalaPolicy / AtariPolicy)
+        idx_d / sign_d repeat per env: one strategy per lane, its novelty repeated for the lane's envs."""
         h = self.strategy_handler
-        if h is None or self.policy.KIND in ("impala", "atari"):
+        if h is None:
             return None
-        return h.lane_novelty(self.noise_source.device_table(self.policy.flat.device), idx_d, sign_d, self.sigma)
+        E = getattr(self.agent.env, "envs_per_lane", 1)
+        if E > 1:
+            idx_d, sign_d = idx_d[::E].contiguous(), sign_d[::E].contiguous()
+        nov = h.lane_novelty(self.noise_source.device_table(self.policy.flat.device), idx_d, sign_d, self.sigma)
+        return nov.repeat_interleave(E) if E > 1 else nov
 
-    def eval_states(self):
-        """Visited raw observations of the deterministic unperturbed episode (agent.py:36,58-59 with
-        save_states=True) -> host f32 [T, n_in].  Every eval episode of an epoch starts from reset
-        with theta and deterministic actions, so one recorded lane serves all of them."""
+    def eval_states(self, max_states=None):
+        """Visited observations of the deterministic unperturbed episode (agent.py:36,58-59 with
+        save_states=True).  Every eval episode of an epoch starts from reset with theta and deterministic
+        actions, so one recorded lane serves all of them.
+          MLP policies: raw observations, host f32 [T, n_in] (fdr_rollout_states).
+          ImpalaPolicy: the obs dicts stacked (impala.py:35-45) -- {frame [n, 3, 64, 64], reward [n] (the
+          reward each obs carries: that of the previous step), done [n]} device tensors, n = min(T,
+          max_states) -- of env instance 0 (fdr_impala_env_frames over the recorded actions)."""
         p = self.policy
-        if p.KIND in ("impala", "atari"):
-            return None
         dev = p.flat.device
         T = self.agent.env.episode_len
-        states = torch.empty((1, T, p.input_shape), dtype=torch.float32, device=dev)
         det = torch.ones(1, dtype=torch.int8, device=dev)
-        om, osd = self.agent.obs_norm_tensors(self.fixed_obs_stats.mean, self.fixed_obs_stats.std)
         bm, bv = p.bn_stats()
+        if p.KIND == "impala":
+            env = self.agent.env
+            n = T if max_states is None else min(T, int(max_states))
+            spec = engine.ImpalaSpec(p.output_shape, 1, T, entropy=False, env_seed=env.env_seed, fp16=env.fp16)
+            res = engine.impala_rollout(spec, engine.lanes_desc(p.flat, 0, deterministic=det), 1, 0, jiggle=False,
+                                        bn_mean=bm, bn_var=bv, record=True, device=dev)
+            frames, r = engine.impala_env_frames(env.env_seed, p.output_shape, 0, 0, n, res.actions[0, :n], device=dev)
+            carried = torch.cat([torch.zeros(1, dtype=torch.float32, device=dev), r[:-1]])
+            return {"frame": frames, "reward": carried, "done": torch.zeros(n, dtype=torch.bool, device=dev)}
+        if p.KIND != "discrete" and p.KIND != "mujoco":
+            return None
+        states = torch.empty((1, T, p.input_shape), dtype=torch.float32, device=dev)
+        om, osd = self.agent.obs_norm_tensors(self.fixed_obs_stats.mean, self.fixed_obs_stats.std)
         engine.rollout(p.spec, self.agent.env, engine.lanes_desc(p.flat, 0, deterministic=det), 1, 0, jiggle=False,
                        obs_mean=om, obs_std=osd, bn_mean=bm, bn_var=bv, device=dev, states=states)
-        return states[0].cpu().numpy()
+        out = states[0].cpu().numpy()
+        return out if max_states is None else out[:int(max_states)]
 
     def update(self, state):
         # worker.py:40-43, with SURVEY finding 1 fixed: policy_params is the trainable flat vector

@@ -314,6 +314,26 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* desc, const float* t
                        float* c, float* probs, float* feat, void* workspace, int64_t workspace_bytes,
                        fdr_stream stream);
 
+/* ImpalaPolicy.get_strategy over a probe set (policies/impala.py:24-27, strategy/strategy_point.py:17-25,
+ * strategy/strategy_handler.py:25-31) for every lane's theta'_l: the Z stacked obs run through the network as
+ * ONE batch_first LSTM sequence (B = 1, T = Z, policies/impala.py:118, 161-176), exactly as the reference's
+ * _get_stacked_obs batch does.  frames [Z, 3, 64, 64] f32 (0..255) and reward [Z] (NULL = 0) are shared by
+ * all lanes; h / c [n_lanes, 256] = the state the sequence starts from, updated in place to its end state
+ * (NULL = the reset state, which is the state Worker._build_ret scores novelty in: worker/agent.py:66 resets
+ * the policy before compute_novelty).  probs [n_lanes, Z, A] f32 out.  Only n_act, n_params, fp16, bn_mean,
+ * bn_var of desc are read.  workspace: fdr_impala_strategies_workspace_bytes(desc, n_lanes, Z) bytes. */
+int64_t fdr_impala_strategies_workspace_bytes(const fdr_impala_desc* desc, int32_t n_lanes, int32_t n_states);
+int fdr_impala_strategies(fdr_ctx* ctx, const fdr_impala_desc* desc, const fdr_lanes_desc* lanes, int32_t n_lanes,
+                          int32_t n_states, const float* frames, const float* reward, float* h, float* c,
+                          float* probs, void* workspace, int64_t workspace_bytes, fdr_stream stream);
+
+/* Observations of the synthetic frame env outside a rollout (eval states and the probe set zeta,
+ * run_sequential.py:142-143, 198-213): frames [n, 3, 64, 64] f32 (0..255) of global env `env_id`
+ * (= lane_offset * E + lane * E + e of a rollout) at steps t0 .. t0+n-1, and -- given the actions [n] i32
+ * taken at those steps (NULL -> 0) -- reward [n] f32 (nullable) that each step returns. */
+int fdr_impala_env_frames(uint64_t env_seed, int32_t n_act, int64_t env_id, int32_t t0, int32_t n,
+                          const int32_t* actions, float* frames, float* reward, fdr_stream stream);
+
 /* Opt-in phase timing of fdr_impala_rollout (process-wide, not thread-safe): when enabled, HIP
  * events are recorded between the step-loop launches; fdr_impala_profile_read waits for the last
  * profiled rollout and returns HOST ms[3] = summed conv-stack / core (fc+LSTM+head) / entropy-replay

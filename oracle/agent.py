@@ -99,3 +99,69 @@ def evaluate_lanes(kind, n_in, n_act, theta, table, idx, sign, sigma, env, seed,
     if record_states:
         out = out + (states,)
     return out
+
+
+def reference_collect_loop(kind, n_in, n_act, T, seconds, wid, sigma=0.02):
+    """Worker.collect_returns + Agent.collect_return in the reference's own per-step form, for the on-box CPU
+    baseline (bench.py cpu_baseline): per episode perturb theta (worker/worker.py:26-32), then per step a
+    batch-1 torch forward and torch distribution sampling (policies/discrete.py:16-24, mujoco.py:15-22),
+    env.step, and the end-of-episode batched entropy forward (worker/agent.py:60-66).  Runs whole episodes
+    until `seconds` have passed; returns (env steps, episodes, elapsed s)."""
+    import time
+    import torch
+    from torch.distributions import Categorical, Normal
+    from .envs import SyntheticEnv
+    from .noise import NoiseTable
+    from .policies import TorchPolicy
+    torch.manual_seed(124 + wid)
+    pol = TorchPolicy(kind, n_in, n_act, seed=124)
+    theta = pol.get_flat()
+    tab = NoiseTable(1 << 22, theta.size, 124 + wid)
+    env = SyntheticEnv(n_in, n_act, kind == "discrete", T)
+    rng = np.random.RandomState(wid)
+    steps = episodes = 0
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        while time.perf_counter() - t0 < seconds:
+            idx = int(tab.sample_indices(1)[0])
+            pol.set_flat(theta + np.float32(sigma) * tab.decode(idx))
+            obs, states, reward = env.reset(), [], 0.0
+            for _ in range(T):
+                states.append(obs)
+                out = pol.forward(obs)
+                if kind == "discrete":
+                    a = int(Categorical(probs=out).sample().item())
+                else:
+                    a = Normal(out[0], out[1]).sample().numpy().reshape(-1)
+                obs, r, done, _ = env.step(a)
+                reward += r
+                steps += 1
+                if done:
+                    break
+            out = pol.forward(np.asarray(states))
+            ent = (Categorical(probs=out).entropy().mean() if kind == "discrete"
+                   else Normal(out[0], out[1]).entropy().sum(-1).mean()).item()
+            reward += rng.choice((-1e-12, 1e-12))
+            pol.set_flat(theta)
+            episodes += 1
+    return steps, episodes, time.perf_counter() - t0
+
+
+def reference_learner_step_seconds(P, n_returns, sigma=0.02, lr=0.01, repeats=2):
+    """FiniteDifferences.step (learner/finite_differences.py:24-64) restated on n_returns returns: decode +
+    lambda / ||lambda||^2 + z-score + the B x P dot + DSGD, on one core; median wall seconds."""
+    import time
+    from .learner import dsgd_step, fd_gradient
+    rs = np.random.RandomState(0)
+    table = rs.randn(1 << 23).astype(np.float32)
+    theta = (rs.randn(P) * 0.1).astype(np.float32)
+    idx = rs.randint(0, table.size - P, size=n_returns)
+    sign = np.ones(n_returns, np.int8)
+    rew = rs.randn(n_returns)
+    times = []
+    for _ in range(repeats):
+        t0 = time.perf_counter()
+        g, _ = fd_gradient(table, P, idx, sign, rew, 0.0, sigma)
+        dsgd_step(theta, g, lr)
+        times.append(time.perf_counter() - t0)
+    return float(np.median(times))

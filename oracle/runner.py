@@ -15,6 +15,11 @@ instead of the numpy-2-broken RNGNoiseSource).  RNG streams, in the reference's 
     captured its reset observation (run_sequential.py:92-103,198-213) -- reproduced.
 Novelty / strategy archive is computed by the reference but unused by the objective
 (learner/finite_differences.py:48), so it is not restated.
+
+``counter_seed`` switches to the GPU runner's semantics (dfd-starter_amd/run_sequential.py), so the product
+runner can be checked against this restatement: every episode starts from reset, the
+epoch's eval coins are flipped first and its training episodes take the counter stream of one batched
+launch (lane k = the k-th training return, key = Agent.next_seed(lanes of the epoch), eval lanes last).
 """
 import numpy as np
 import torch
@@ -53,8 +58,13 @@ class _AdaptiveOmega(object):
             self.omega = min(self.omega + self.increase, self.max_omega)
 
 
+def launch_seed(random_seed, episodes):
+    """Agent.next_seed (dfd-starter_amd/worker/agent.py): key of a launch after `episodes` earlier lanes."""
+    return (int(random_seed) * 1000003 + episodes) & ((1 << 63) - 1)
+
+
 def run_trap(n_epochs, batch_size=16, seed=124, noise_std=0.02, lr=0.01, eval_prob=0.05,
-             zeta_size=4, action_seed=777, table_size=2 ** 22):
+             zeta_size=4, action_seed=777, table_size=2 ** 22, counter_seed=False):
     torch.manual_seed(seed)
     np.random.seed(seed)
     omega = _AdaptiveOmega()
@@ -77,9 +87,38 @@ def run_trap(n_epochs, batch_size=16, seed=124, noise_std=0.02, lr=0.01, eval_pr
     def noise_fn(t):
         return np.float32(action_rng.uniform())
 
+    episodes = 0
     for _ in range(n_epochs):
         theta = learner.theta
         rets, any_eval = [], False
+        if counter_seed:
+            from . import rng as crng
+            coins = []
+            while sum(1 for c in coins if not c) < batch_size:
+                coins.append(worker_rng.uniform(0, 1) < eval_prob)
+            key = launch_seed(seed, episodes)
+            episodes += len(coins)
+            k_train = 0
+            for is_eval in coins:
+                if not is_eval:
+                    idx = int(table.sample_indices(1)[0])
+                    policy.set_flat(theta + np.float32(noise_std) * table.decode(idx))
+                    lane = k_train
+                    k_train += 1
+                else:
+                    idx = 0
+                    lane = -1
+                    policy.set_flat(theta)
+                r, e, steps, _ = collect_return(policy, env, env.reset(), is_eval,
+                                                lambda t, lane=lane: np.float32(crng.uniform(key, lane, t, 0)),
+                                                lambda: 0.0)
+                policy.set_flat(theta)
+                cum_steps += steps
+                if is_eval:
+                    any_eval = True
+                    policy_reward = policy_reward * 0.9 + r * 0.1
+                else:
+                    rets.append((learner.epoch, idx, r))
         while len(rets) < batch_size:
             is_eval = worker_rng.uniform(0, 1) < eval_prob
             if not is_eval:

@@ -553,9 +553,52 @@ def g11_atari():
          param_shapes=np.array([str(tuple(p.shape)) for p in pol.parameters()]))
 
 
+def g12_history():
+    """SparseHistoryManager replacement (strategy/sparse_history_manager.py:17-148 via StrategyHandler): a
+    DiscretePolicy (categorical_tvd) and a MujocoPolicy (gaussian_wasserstein_dist_from_strategies) archive of
+    6 points, filled, evaluated on zeta, then 14 more submit_policy calls that replace -- or not -- the less
+    novel member of the closest pair.  Records every submission's return value and worst_point_idx, the final
+    strategy tensor and the known-distance table."""
+    out = {}
+    rs = np.random.RandomState(12)
+    table = rs.randn(1 << 20).astype(np.float32)
+    for tag, Pol, n_in, n_act, dist in (("disc", DiscretePolicy, 4, 2, math_helpers.categorical_tvd),
+                                        ("mj", MujocoPolicy, 17, 6,
+                                         math_helpers.gaussian_wasserstein_dist_from_strategies)):
+        torch.manual_seed(124)
+        pol = Pol(n_in, n_act, seed=124)
+        theta = pol.get_trainable_flat().copy()
+        P = theta.size
+        H, N = 6, 20
+        scales = rs.choice([0.02, 0.05, 0.1, 0.2, 0.4], size=N).astype(np.float32)
+        offs = rs.randint(0, table.size - P, size=N)
+        flats = np.stack([(theta + scales[k] * table[offs[k]:offs[k] + P]).astype(np.float32) for k in range(N)])
+        zeta = rs.randn(10, n_in).astype(np.float32)
+        handler = StrategyHandler(pol, dist, max_history_size=H)
+        mgr = handler.strategy_history_manager
+        for k in range(H):
+            pol.set_trainable_flat(flats[k])
+            handler.add_policy(pol)
+        handler.set_zeta(zeta)
+        worst = [mgr.worst_point_idx]
+        rets = []
+        for k in range(H, N):
+            pol.set_trainable_flat(flats[k])
+            r = mgr.submit_policy(pol)
+            rets.append(-2 if r is None else int(r))
+            worst.append(mgr.worst_point_idx)
+        D = np.full((H, H), np.inf)
+        for (i, j), d in mgr.known_dists.items():
+            D[i, j] = D[j, i] = d
+        out.update({tag + "_flats": flats, tag + "_zeta": zeta, tag + "_returns": np.array(rets),
+                    tag + "_worst": np.array(worst), tag + "_strategies": np.asarray(mgr.strategy_tensor, np.float32),
+                    tag + "_dists": D, tag + "_H": np.array(H)})
+    save("g12_history.npz", **out)
+
+
 GENERATORS = {"g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
               "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g8": g8_impala,
-              "g9": g9_novelty, "g10": g10_welford, "g11": g11_atari}
+              "g9": g9_novelty, "g10": g10_welford, "g11": g11_atari, "g12": g12_history}
 
 if __name__ == "__main__":
     torch.set_num_threads(1)

@@ -215,3 +215,23 @@ def test_compute_vbn_on_device_vs_torch_train_mode():
     for g, w in zip(got, want):
         np.testing.assert_allclose(g.running_mean.cpu().numpy(), w.running_mean.numpy(), rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(g.running_var.cpu().numpy(), w.running_var.numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_sequential_runner_trap_vs_oracle_runner():
+    """The product SequentialRunner (batched GPU episodes, counter action stream) against the oracle's restated
+    runner driven by the same stream (oracle/runner.py counter_seed): index streams and eval schedule equal,
+    every epoch's (integer) trap returns equal up to the +-1e-12 jiggle, the final theta within 1e-6."""
+    from run_sequential import SequentialRunner
+    from oracle import runner as orunner
+    r = SequentialRunner(env_id="SimpleTrapEnv-v0", batch_size=16, random_seed=124, zeta_size=4, eval_prob=0.2,
+                         max_strategy_history_size=4, noise_table_size=2 ** 22, verbose=False)
+    r.train(2)
+    ref = orunner.run_trap(2, batch_size=16, seed=124, eval_prob=0.2, zeta_size=4, counter_seed=True)
+    assert len(r.history) == 2
+    for e in range(2):
+        np.testing.assert_array_equal(r.history[e]["idx"], ref["log"][e]["idx"])
+        np.testing.assert_allclose(r.history[e]["rewards"], ref["log"][e]["rewards"], rtol=0, atol=1e-9)
+        assert abs(r.history[e]["Update Magnitude"] - ref["log"][e]["update"]) < 1e-5
+    assert np.unique(np.round(np.concatenate([h["rewards"] for h in r.history]))).size > 1   # returns vary
+    np.testing.assert_allclose(r.policy.get_trainable_flat(), ref["theta"], rtol=0, atol=1e-6)
+    assert abs(r.policy_reward - ref["policy_reward"]) < 1e-9

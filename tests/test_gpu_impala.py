@@ -282,3 +282,74 @@ def test_replay_input_projection_gemm_bit_identical(engine, table, fp16):
         check(lib.fdr_impala_set_replay_gemm(1), "fdr_impala_set_replay_gemm")
     assert np.all(np.isfinite(outs[0])) and np.any(outs[0] != 0)
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_rollout_long_horizon_vs_oracle(engine, table):
+    """f32 rollout over T = 130 steps (three 64-step chunks of the entropy replay's input-projection GEMM,
+    the last partial) against the oracle: actions / integer returns exact, per-step probabilities and the
+    replayed entropy within 1e-5."""
+    A, E, T = 6, 2, 130
+    out, ref = _run(engine, table, A, E, T, [4321, 4321], [1, -1], [0, 0])
+    _compare(out, ref, 2, E, T, A)
+
+
+def test_fp16_multistep_drift_bound_vs_f32_oracle(engine, table):
+    """fp16 rollouts (config 5, A = 4, 4 envs) over 60 steps: the oracle (f32) is driven with the fp16 kernel's
+    own actions, so both see identical frames / rewards; every step's probabilities stay within the fp16
+    tolerance of f32 -- a bound on the drift of the fp16 LSTM state over the episode."""
+    A, E, T = 4, 4, 60
+    theta = _theta(A)
+    dev = "cuda"
+    lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
+                              torch.tensor([555], dtype=torch.int64, device=dev),
+                              torch.tensor([1], dtype=torch.int8, device=dev), 0.02)
+    out = engine.impala_rollout(engine.ImpalaSpec(A, E, T, entropy=False, env_seed=5, fp16=True), lanes, 1, 11,
+                                record=True)
+    torch.cuda.synchronize()
+    probs = out.probs.cpu().numpy().reshape(E, T, A)
+    acts = out.actions.cpu().numpy().reshape(E, T)
+    from oracle.noise import perturb
+    p = oi.unflatten(perturb(theta, table, [555], [1], 0.02)[0], A)
+    nb = oi.num_bn()
+    bn = oi.split_bn(np.zeros(nb, np.float32), np.ones(nb, np.float32))
+    envs = np.arange(E, dtype=np.uint64)
+    h, c, r_prev = torch.zeros(E, oi.HID), torch.zeros(E, oi.HID), np.zeros(E, np.float32)
+    worst = 0.0
+    for t in range(T):
+        pr, h, c, _, _ = oi.forward(p, bn, oi.frames(5, envs, t).astype(np.float32), r_prev, h, c)
+        worst = max(worst, float(np.abs(pr.numpy() - probs[:, t]).max()))
+        r_prev = oi.rewards(5, envs, t, acts[:, t], A)
+    assert worst <= F16_RTOL, worst
+    ret = sum(oi.rewards(5, envs, t, acts[:, t], A) for t in range(T)).astype(np.float64)
+    np.testing.assert_allclose(out.reward.cpu().numpy() - ret, 0.0, atol=2e-12)   # +- jiggle only
+
+
+@pytest.mark.parametrize("fp16", [False, True])
+def test_full_size_rollout_properties(engine, fp16):
+    """BASELINE configs 4/5 at full size (1024 lanes x 4 envs x T = 1000, A = 6 / 4): bitwise reproducible,
+    antithetic lanes have identical ||lambda||^2, returns integer (+- jiggle) within [-T, T], entropies finite
+    in (0, ln A]."""
+    A = 4 if fp16 else 6
+    L, E, T = 1024, 4, 1000
+    theta = _theta(A)
+    P = theta.size
+    dev = "cuda"
+    tab = torch.randn(25_000_000, generator=torch.Generator().manual_seed(124)).to(dev)
+    idx = torch.as_tensor(np.repeat(np.random.RandomState(4).randint(0, 25_000_000 - P, size=L // 2), 2), device=dev)
+    sign = torch.as_tensor(np.tile(np.array([1, -1], np.int8), L // 2), device=dev)
+    lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, tab, idx, sign, 0.02)
+    spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=fp16)
+    outs = []
+    for _ in range(2):
+        o = engine.impala_rollout(spec, lanes, L, 123)
+        torch.cuda.synchronize()
+        outs.append([t.cpu().numpy().copy() for t in (o.reward, o.entropy, o.timesteps, o.norm2)])
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+    ret, ent, steps, n2 = outs[0]
+    assert np.all(steps == T)
+    assert np.all(np.isfinite(ret)) and np.all(np.abs(ret) <= T + 1e-9)
+    np.testing.assert_allclose(ret, np.round(ret), rtol=0, atol=2e-12)
+    assert np.all(np.isfinite(ent)) and np.all(ent > 0) and np.all(ent <= np.log(A) + 1e-6)
+    np.testing.assert_array_equal(n2[0::2], n2[1::2])
+    assert np.all(n2 > 0)

@@ -410,3 +410,39 @@ def test_lambda_drift_norms_and_grad_vs_oracle(eng):
     g = eng.fd_grad_lambda(tab, dev(idx, torch.int64), dev(sign), dev(slot), dev(coef), 0.02, dev(drift), P)
     g_ref = coef @ lam.astype(np.float64)
     assert np.linalg.norm(g.cpu().numpy() - g_ref) <= 1e-12 * np.linalg.norm(g_ref)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_fd_weights_and_grad_sum_to_unsharded(eng, world):
+    """The multi-GPU learner's arithmetic on one GPU: a 512-direction antithetic batch split into the standard
+    rank slices (fdr.dist.lane_range); each slice runs fdr_fd_weights(lane_lo = its first lane) over the
+    all-gathered rewards and fdr_fd_grad over its directions.  The slices' gradients sum to the unsharded
+    gradient (the all-reduce) within f64 reordering, and to the oracle's."""
+    from fdr import dist as fdist
+    from oracle import learner as olearn
+    P, n_dirs, sigma = 6092, 512, 0.02
+    rs = np.random.RandomState(21)
+    table = rs.randn(1 << 22).astype(np.float32)
+    idx_dirs = rs.randint(0, table.size - P, size=n_dirs).astype(np.int64)
+    idx = np.repeat(idx_dirs, 2)
+    sign = np.tile(np.array([1, -1], np.int8), n_dirs)
+    rew = rs.randn(2 * n_dirs) * 3 + 1
+    s32 = np.float32(sigma)
+    n2 = np.array([float(np.dot((table[i:i + P] * s32).astype(np.float64), (table[i:i + P] * s32).astype(np.float64)))
+                   for i in idx])
+    tab = torch.as_tensor(table, device="cuda")
+    rew_d = torch.as_tensor(rew, device="cuda")
+    sign_d = torch.as_tensor(sign, device="cuda")
+    n2_d = torch.as_tensor(n2, device="cuda")
+    idx_d = torch.as_tensor(idx_dirs, device="cuda")
+    coef = eng.fd_weights(rew_d, 0.25, 0, sign_d, n2_d, 2, sigma)
+    g_full = eng.fd_grad(tab, idx_d, coef, P).cpu().numpy().copy()
+    g_sum = np.zeros(P)
+    for rank in range(world):
+        lo, hi = fdist.lane_range(n_dirs, 2, world, rank)
+        assert lo % 2 == 0 and hi % 2 == 0
+        c = eng.fd_weights(rew_d, 0.25, lo, sign_d[lo:hi].contiguous(), n2_d[lo:hi].contiguous(), 2, sigma)
+        g_sum += eng.fd_grad(tab, idx_d[lo // 2:hi // 2].contiguous(), c, P).cpu().numpy()
+    assert np.linalg.norm(g_sum - g_full) / np.linalg.norm(g_full) <= 1e-12
+    g_ref, _ = olearn.fd_gradient(table, P, idx, sign, rew, 0.25, sigma)
+    assert np.linalg.norm(g_full - g_ref) / np.linalg.norm(g_ref) <= 1e-5

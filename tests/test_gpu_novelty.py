@@ -112,3 +112,33 @@ def test_rollout_records_visited_states(engine):
     np.testing.assert_allclose(res.reward.cpu().numpy()[0], S[0, 1:, 0].sum() + np.tanh(S[0, -1] @ oenv.M.T
                                + op.lanes_forward("mujoco", 17, 6, theta[None], S[0, -1:])[0] @ oenv.K.T)[0, 0],
                                rtol=1e-4)
+
+
+@pytest.mark.parametrize("tag,kind,n_in,n_act,fn", [("disc", "discrete", 4, 2, "categorical_tvd"),
+                                                    ("mj", "mujoco", 17, 6, "gaussian_wasserstein_dist_from_strategies")])
+def test_archive_replacement_matches_reference(engine, golden, tag, kind, n_in, n_act, fn):
+    """StrategyHandler.add_policy on the device archive == the reference SparseHistoryManager (G12): every
+    submit's return (replaced index / -1), the worst_point_idx trace, the final archive and distance table."""
+    from policies import DiscretePolicy, MujocoPolicy
+    from strategy import StrategyHandler
+    from utils import math_helpers
+    z = golden("g12_history.npz")
+    H = int(z[tag + "_H"])
+    flats, zeta = z[tag + "_flats"], z[tag + "_zeta"]
+    torch.manual_seed(124)
+    pol = (DiscretePolicy if kind == "discrete" else MujocoPolicy)(n_in, n_act, seed=124, device="cuda")
+    h = StrategyHandler(pol, getattr(math_helpers, fn), max_history_size=H)
+    for k in range(H):
+        pol.set_trainable_flat(flats[k])
+        assert h.add_policy(pol) is None
+    h.set_zeta(zeta)
+    worst, rets = [h.worst_point_idx], []
+    for k in range(H, len(flats)):
+        pol.set_trainable_flat(flats[k])
+        r = h.add_policy(pol)
+        rets.append(-2 if r is None else r)
+        worst.append(h.worst_point_idx)
+    np.testing.assert_array_equal(rets, z[tag + "_returns"])
+    np.testing.assert_array_equal(worst, z[tag + "_worst"])
+    np.testing.assert_allclose(h.archive.cpu().numpy(), z[tag + "_strategies"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(h.pair, z[tag + "_dists"], rtol=1e-5)

@@ -188,3 +188,36 @@ def test_worker_synthetic_episodes(golden, name):
         assert steps == g[name + "_timesteps"][i]
         assert abs(r - g[name + "_reward"][i]) <= 1e-9 * max(1.0, abs(r))
         assert abs(e - g[name + "_entropy"][i]) < 1e-6
+
+
+def test_history_replacement_matches_reference(golden):
+    """oracle.history (SparseHistoryManager restated) reproduces the reference's submit_policy returns,
+    worst_point_idx trace, final strategies and distance table (G12), from strategies computed by the
+    oracle's policy forward."""
+    from oracle import history, policies
+    z = golden("g12_history.npz")
+    for tag, kind, n_in, n_act, dist in (("disc", "discrete", 4, 2, "tvd"), ("mj", "mujoco", 17, 6, "w2")):
+        pol = policies.TorchPolicy(kind, n_in, n_act, seed=124)
+        H = int(z[tag + "_H"])
+        flats, zeta = z[tag + "_flats"], z[tag + "_zeta"]
+
+        def strat(f):
+            pol.set_flat(f)
+            out = pol.forward(zeta)
+            return (torch.cat(out, -1) if isinstance(out, tuple) else out).detach().numpy()
+        hist = history.History(dist, H)
+        for k in range(H):
+            hist.submit(None, False)
+        hist.evaluate([strat(f) for f in flats[:H]])
+        worst, rets = [hist.worst_point_idx], []
+        for k in range(H, len(flats)):
+            r = hist.submit(strat(flats[k]), True)
+            rets.append(-2 if r is None else r)
+            worst.append(hist.worst_point_idx)
+        np.testing.assert_array_equal(rets, z[tag + "_returns"])
+        np.testing.assert_array_equal(worst, z[tag + "_worst"])
+        np.testing.assert_allclose(np.stack(hist.strategies), z[tag + "_strategies"], rtol=0, atol=1e-6)
+        D = np.full((H, H), np.inf)
+        for (i, j), d in hist.known.items():
+            D[i, j] = D[j, i] = d
+        np.testing.assert_allclose(D, z[tag + "_dists"], rtol=1e-6)

@@ -93,3 +93,19 @@ def test_abi_impala_layout_queries():
     rc = _lib.lib.fdr_impala_rollout(None, ctypes.byref(bad), ctypes.byref(ld), 1, 0, 0, 1, 1, 1, None, None,
                                      None, 1, 1 << 40, None)
     assert rc == _lib.FDR_ERR_UNSUPPORTED
+
+
+def test_strategy_sequence_matches_reference_entropy_pass(g8):
+    """oracle.strategy (get_strategy's one-sequence form) == the reference's stacked-obs pass (G8 ent_probs)."""
+    A, P = int(g8["A"]), int(g8["P"])
+    tab = np.random.RandomState(int(g8["table_seed"])).randn(2 ** 22).astype(np.float32)
+    off = int(g8["param_offset"])
+    p = oi.unflatten((tab[off:off + P] * np.float32(0.1)).astype(np.float32), A)
+    bn = oi.split_bn(g8["rm"], g8["rv"])
+    for q in range(g8["frames"].shape[0]):
+        h, c = torch.zeros(1, oi.HID), torch.zeros(1, oi.HID)
+        for t in range(g8["frames"].shape[1]):
+            _, h, c, _, _ = oi.forward(p, bn, g8["frames"][q, t:t + 1].astype(np.float32), g8["rewards"][q, t:t + 1],
+                                       h, c, notdone=[0.0 if g8["dones"][q, t] else 1.0])
+        pr, _, _ = oi.strategy(p, bn, g8["frames"][q].astype(np.float32), g8["rewards"][q], h, c)
+        np.testing.assert_allclose(pr, g8["ent_probs"][q], atol=1e-6)
