@@ -154,5 +154,6 @@ def test_sequential_runner_impala_fp16_config5(mods):
         assert rep["Update Magnitude"] > 0
         assert len(rep["rewards"]) == 4 * 2 * 4      # directions x antithetic x envs
     assert len(r.omega.reward_history) >= 1           # omega stepped on the eval epochs (run_sequential.py:149-151)
-    assert len(r.strategy_handler.points) == 5        # add_policy at start + once per epoch
+    # add_policy at start + once per epoch: the 5th submission meets a full archive (max 4) -> _replace_point
+    assert len(r.strategy_handler.points) == 4
     assert r.strategy_handler.archive is not None and r.strategy_handler.archive.shape[1:] == (16, 4)
