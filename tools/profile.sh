@@ -33,4 +33,4 @@ if [ -n "${EXTRA_PMC:-}" ]; then
     i=$((i + 1))
   done
 fi
-ls -R "$OUT" | head -50
+ls -R "$OUT" > "$OUT/ls.txt"

@@ -22,7 +22,18 @@ def per_kernel(path, counter=None):
     return out
 
 
-def main(d, tag, config="halfcheetah", dominant="rollout_kernel"):
+def mfma_pass(d):
+    """Per-kernel averages of the optional MFMA PMC pass (MFMA_PMC in tools/profile.sh)."""
+    path = os.path.join(d, "pmc_mfma", "run_counter_collection.csv")
+    if not os.path.exists(path):
+        return {}
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        acc[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in q.items()} for k, q in acc.items()}
+
+
+def main(d, tag, config="halfcheetah", dominant="rollout_kernel", secondary=None):
     stats = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
     fetch = per_kernel(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(d, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
@@ -60,6 +71,32 @@ def main(d, tag, config="halfcheetah", dominant="rollout_kernel"):
                       "VALU instructions per wave-step %.1f, LDS per wave-step %.1f." % (
                           dominant, avg_ns / 1e3, clk, q.get("SQ_INSTS_VALU", 0) / max(1, q.get("SQ_WAVES", 1)) / 1000,
                           q.get("SQ_INSTS_LDS", 0) / max(1, q.get("SQ_WAVES", 1)) / 1000)]
+        mf = mfma_pass(d)
+        if mf:
+            lines += ["", "MFMA pass (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8); MOPS x 512 = FLOP):", "",
+                      "| kernel | MFMA busy | MFMA FLOP executed (F32 + F16 MOPS x 512) | clock GHz |", "|---|---|---|---|"]
+            for k, q in mf.items():
+                cyc = q.get("GRBM_GUI_ACTIVE", 0) / 8
+                busy = q.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (1024 * cyc) if cyc else 0
+                flop = 512 * (q.get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0) + q.get("SQ_INSTS_VALU_MFMA_MOPS_F16", 0))
+                st = [x for x in stats if x["Name"] == k]
+                clk = cyc / (float(st[0]["AverageNs"]) * 1e-9) / 1e9 if st else 0
+                lines.append("| %s | %.3f | %.3e | %.2f |" % (k[:70], busy, flop, clk))
+                if dominant in k:
+                    rollout["mfma_busy"] = round(busy, 4)
+                    rollout["mfma_flop_per_launch"] = flop
+        if secondary:
+            for k in fetch:
+                if secondary in k:
+                    f = sum(float(r["Counter_Value"]) for r in fetch[k]) / len(fetch[k])
+                    w = sum(float(r["Counter_Value"]) for r in write.get(k, [])) / max(1, len(write.get(k, [])))
+                    st = [x for x in stats if x["Name"] == k]
+                    rollout["core_kernel"] = dict(kernel=k, fetch_size_kb=f, write_size_kb=w,
+                                                  hbm_bytes_per_launch=f * 1024 * 2 + w * 1024,
+                                                  avg_duration_us=float(st[0]["AverageNs"]) / 1e3 if st else None)
+                    lines += ["", "Secondary kernel %s: HBM bytes/launch %.0f (FETCH x2 + WRITE), avg %.1f us" % (
+                        k[:70], f * 1024 * 2 + w * 1024, rollout["core_kernel"]["avg_duration_us"] or 0)]
+                    break
         with open(os.path.join("profiles", "pmc_rollout_%s.json" % config), "w") as fh:
             json.dump(dict(rollout, source=d, tag=tag), fh, indent=1)
     with open(os.path.join("profiles", "%s_summary.md" % tag), "w") as fh:
