@@ -154,6 +154,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variant", action="store_true", help="skip the 4096-pair variant line (config 3)")
+    ap.add_argument("--no-novelty", action="store_true", help="config 5 without the novelty archive / omega "
+                    "(rocprof passes: the archive's conv launches would mix into the rollout conv's average)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -219,7 +221,7 @@ def main():
     omega = AdaptiveOmega()
     learner = FiniteDifferences(policy, DSGD(policy.parameters(), lr=0.01), omega, table, noise_std=0.02)
 
-    novelty = args.config == "impala_fp16"     # config 5: strategy.sparse_history_manager + utils.adaptive_omega
+    novelty = args.config == "impala_fp16" and not args.no_novelty     # config 5: strategy.sparse_history_manager + utils.adaptive_omega
     if novelty:
         from strategy import StrategyHandler
         from utils import math_helpers

@@ -13,5 +13,5 @@ run_cfg cartpole
 MFMA_PMC="SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" \
   run_cfg impala --steps 2 --warmup 1 --episode-len 40
 MFMA_PMC="SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE" \
-  run_cfg impala_fp16 --steps 2 --warmup 1 --episode-len 40
+  run_cfg impala_fp16 --steps 2 --warmup 1 --episode-len 40 --no-novelty
 echo profile_round done
