@@ -154,6 +154,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variant", action="store_true", help="skip the 4096-pair variant line (config 3)")
+    ap.add_argument("--event-every", type=int, default=1,
+                    help="bracket every k-th FD step's rollout with HIP events (1: every step)")
     ap.add_argument("--no-novelty", action="store_true", help="config 5 without the novelty archive / omega "
                     "(rocprof passes: the archive's conv launches would mix into the rollout conv's average)")
     args = ap.parse_args()
@@ -238,21 +240,30 @@ def main():
     n_dirs_global = (L // 2) * world
     from fdr import dist as fdist
     lane_range = fdist.lane_range(n_dirs_global, 2, world, rank)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     roll_ms = []
     phase_ms = []
     step_no = [0]
+    # HIP event pairs bracketing each rollout, created and first recorded before the timed region (a fresh
+    # event's first record allocates its signal: that is not work of the step)
+    ev_pool = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(max(args.steps, 10) + 1)]
+    for a_, b_ in ev_pool:
+        a_.record()
+        b_.record()
+    torch.cuda.synchronize()
+    cur = [None]
 
     def fd_step(timed, n_dirs=n_dirs_global, rng=lane_range):
+        timed = timed and cur[0] is not None
         # the action stream is keyed by (step seed, global lane id): every rank evaluates the lanes of a
         # 1-GPU run bit-identically, whatever the shard (include/fdr.h lane_offset)
         seed = 1000 + step_no[0]
         step_no[0] += 1
         if timed:
-            ev0.record()
-        batch = worker.evaluate(n_dirs, antithetic=True, lane_range=rng, seed=seed, novelty=novelty)
+            cur[0][0].record()
+        batch = worker.evaluate(n_dirs, antithetic=True, lane_range=rng, seed=seed, novelty=novelty, prefetch=True)
         if timed:
-            ev1.record()
+            cur[0][1].record()
         out = learner.step_async(batch, 0.0, 0.0, 0.0)
         if novelty:
             # run_sequential.py:149-151 (the noisy mean reward; one host read per FD step) and :160
@@ -270,24 +281,22 @@ def main():
         t0 = time.perf_counter()
         pairs = []
         out = None
-        for _ in range(steps):
+        for i in range(steps):
+            cur[0] = ev_pool[i % len(ev_pool)] if i % args.event_every == 0 else None
             out, _ = fd_step(True, **kw)
-            pairs.append((ev0, ev1))
-            _new_events()
+            if cur[0] is not None:
+                pairs.append(cur[0])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        return time.perf_counter() - t0, pairs, out
-
-    def _new_events():
-        nonlocal ev0, ev1
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        el = time.perf_counter() - t0
+        return el, [a_.elapsed_time(b_) for a_, b_ in pairs], out
 
     for _ in range(args.warmup):
         out, _ = fd_step(False)
     elapsed, roll_ms, out = timed_loop(args.steps)
-    rollout_ms = float(np.mean([a.elapsed_time(b) for a, b in roll_ms]))
+    rollout_ms = float(np.mean(roll_ms))
     if world > 1:
         t = torch.tensor([elapsed, rollout_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -306,8 +315,8 @@ def main():
         rng2 = fdist.lane_range(nv, 2, world, rank)
         fd_step(False, n_dirs=nv, rng=rng2)
         k = max(1, min(args.steps, 10))
-        el2, pairs2, out2 = timed_loop(k, n_dirs=nv, rng=rng2)
-        r2 = float(np.mean([a.elapsed_time(b) for a, b in pairs2]))
+        el2, ms2, out2 = timed_loop(k, n_dirs=nv, rng=rng2)
+        r2 = float(np.mean(ms2))
         if world > 1:
             t = torch.tensor([el2, r2], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

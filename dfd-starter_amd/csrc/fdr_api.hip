@@ -55,6 +55,15 @@ int launch_strategy_dist(const float* S, int n, const float* B, int H, int Z, in
                          double* min_d, int32_t* arg, hipStream_t stream);
 int launch_dsgd(float* theta, const double* g, int64_t P, double lr, double lr_scale, double* out,
                 void* ws, int64_t ws_bytes, hipStream_t stream);
+int launch_dsgd_ex(float* theta, const double* src, int mom, int64_t P, double lr, double lr_scale, double* g_out,
+                   double* out, void* ws, int64_t ws_bytes, hipStream_t stream);
+int64_t fused_workspace_bytes(int n_dirs, int n_local, int64_t P, int mode);
+int64_t fused_counter_bytes(int n_dirs, int64_t P);
+int launch_fd_grad_fused(const float* table, int64_t table_size, const int64_t* idx, int n_dirs, int64_t P,
+                         const double* r_all, int n_all, double pr, int lo, const int8_t* sign, const double* n2,
+                         int lpd, float sigma, int mode, double* out, float* theta, double lr, double lr_scale,
+                         float* hist, double* dsgd_out, void* ws, int64_t ws_bytes, hipStream_t stream);
+int launch_rank_weights(const double* r_all, int n_all, int lo, int n_local, double* w, hipStream_t stream);
 
 static int policy_key(const fdr_policy_desc* p, PolicyKey* k) {
   if (!p) return set_error(FDR_ERR_INVALID, "policy desc is NULL");
@@ -279,8 +288,80 @@ int fdr_dsgd_step(fdr_ctx* ctx, float* theta, const double* g, int64_t n_params,
                   fdr_stream stream) {
   (void)ctx;
   if (!theta || !g || !out || n_params <= 0) return set_error(FDR_ERR_INVALID, "bad arguments");
-  return launch_dsgd(theta, g, n_params, lr, lr_scale, out, workspace, workspace_bytes,
-                     (hipStream_t)stream);
+  return launch_dsgd_ex(theta, g, 0, n_params, lr, lr_scale, nullptr, out, workspace, workspace_bytes,
+                        (hipStream_t)stream);
+}
+
+int fdr_dsgd_step_ex(fdr_ctx* ctx, float* theta, const double* src, int32_t src_is_moments, int64_t n_params,
+                     double lr, double lr_scale, double* g_out, double* out, void* workspace, int64_t workspace_bytes,
+                     fdr_stream stream) {
+  (void)ctx;
+  if (!theta || !src || !out || n_params <= 0) return set_error(FDR_ERR_INVALID, "bad arguments");
+  return launch_dsgd_ex(theta, src, src_is_moments ? 1 : 0, n_params, lr, lr_scale, g_out, out, workspace,
+                        workspace_bytes, (hipStream_t)stream);
+}
+
+int64_t fdr_fd_grad_fused_workspace_bytes(int32_t n_dirs, int32_t lanes_per_dir, int64_t n_params, int32_t mode) {
+  if (lanes_per_dir < 1) return -1;
+  return fused_workspace_bytes(n_dirs, n_dirs * lanes_per_dir, n_params, mode);
+}
+
+int64_t fdr_fd_grad_fused_counter_bytes(int32_t n_dirs, int64_t n_params) {
+  return n_params > 0 ? fused_counter_bytes(n_dirs, n_params) : -1;
+}
+
+static int fd_grad_fused_impl(const float* table, int64_t table_size, const int64_t* idx_local, int32_t n_dirs,
+                              int64_t n_params, const double* rewards_all, int32_t n_all, double policy_reward,
+                              int32_t lane_lo, const int8_t* sign_local, const double* norm2_local, int32_t lanes_per_dir,
+                              float sigma, int32_t mode, double* out, float* theta, double lr, double lr_scale,
+                              float* hist, double* dsgd_out, void* workspace, int64_t workspace_bytes,
+                              fdr_stream stream) {
+  if (!table || !out || n_params <= 0 || table_size < n_params || n_dirs < 0)
+    return set_error(FDR_ERR_INVALID, "bad arguments");
+  if (mode != FDR_WEIGHT_ZSCORE && mode != FDR_WEIGHT_CENTERED_RANK && mode != FDR_WEIGHT_MOMENTS)
+    return set_error(FDR_ERR_INVALID, "unknown weighting mode");
+  if (lanes_per_dir < 1) return set_error(FDR_ERR_INVALID, "lanes_per_dir < 1");
+  if (n_dirs == 0) return set_error(FDR_ERR_INVALID, "no directions (DSGD would divide by ||g|| = 0)");
+  const int n_local = n_dirs * lanes_per_dir;
+  if (!idx_local || !rewards_all || !sign_local || !norm2_local) return set_error(FDR_ERR_INVALID, "NULL pointer");
+  if (n_all <= 0 || lane_lo < 0 || lane_lo + n_local > n_all) return set_error(FDR_ERR_INVALID, "bad lane range");
+  if (mode == FDR_WEIGHT_MOMENTS && (lane_lo != 0 || n_all != n_local))
+    return set_error(FDR_ERR_INVALID, "moments form takes the local rewards only (lane_lo = 0, n_all = n_local)");
+  return launch_fd_grad_fused(table, table_size, idx_local, n_dirs, n_params, rewards_all, n_all, policy_reward,
+                              lane_lo, sign_local, norm2_local, lanes_per_dir, sigma, mode, out, theta, lr, lr_scale,
+                              hist, dsgd_out, workspace, workspace_bytes, (hipStream_t)stream);
+}
+
+int fdr_fd_grad_fused(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx_local, int32_t n_dirs,
+                      int64_t n_params, const double* rewards_all, int32_t n_all, double policy_reward, int32_t lane_lo,
+                      const int8_t* sign_local, const double* norm2_local, int32_t lanes_per_dir, float sigma,
+                      int32_t mode, double* out, void* workspace, int64_t workspace_bytes, fdr_stream stream) {
+  (void)ctx;
+  return fd_grad_fused_impl(table, table_size, idx_local, n_dirs, n_params, rewards_all, n_all, policy_reward, lane_lo,
+                            sign_local, norm2_local, lanes_per_dir, sigma, mode, out, nullptr, 0.0, 0.0, nullptr,
+                            nullptr, workspace, workspace_bytes, stream);
+}
+
+int fdr_fd_step(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx_local, int32_t n_dirs,
+                int64_t n_params, const double* rewards_all, int32_t n_all, double policy_reward,
+                const int8_t* sign_local, const double* norm2_local, int32_t lanes_per_dir, float sigma, int32_t mode,
+                float* theta, double lr, double lr_scale, double* g, float* theta_hist, double* out, void* workspace,
+                int64_t workspace_bytes, fdr_stream stream) {
+  (void)ctx;
+  if (!theta || !g || !out) return set_error(FDR_ERR_INVALID, "NULL theta / g / out");
+  if (mode == FDR_WEIGHT_MOMENTS) return set_error(FDR_ERR_INVALID, "fdr_fd_step takes z-score or centred-rank weights");
+  if (n_all != n_dirs * lanes_per_dir) return set_error(FDR_ERR_INVALID, "fdr_fd_step is single-process: n_all = n_local");
+  return fd_grad_fused_impl(table, table_size, idx_local, n_dirs, n_params, rewards_all, n_all, policy_reward, 0,
+                            sign_local, norm2_local, lanes_per_dir, sigma, mode, g, theta, lr, lr_scale, theta_hist,
+                            out, workspace, workspace_bytes, stream);
+}
+
+int fdr_rank_weights(fdr_ctx* ctx, const double* rewards_all, int32_t n_all, int32_t lane_lo, int32_t n_local,
+                     double* w, fdr_stream stream) {
+  (void)ctx;
+  if (!rewards_all || !w || n_all <= 0 || lane_lo < 0 || n_local < 0 || lane_lo + n_local > n_all)
+    return set_error(FDR_ERR_INVALID, "bad arguments");
+  return launch_rank_weights(rewards_all, n_all, lane_lo, n_local, w, (hipStream_t)stream);
 }
 
 }  // extern "C"

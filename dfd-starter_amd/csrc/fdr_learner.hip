@@ -524,3 +524,545 @@ int launch_bn_refresh(int n_in, const float* theta, const float* x, int n, float
 }
 
 }  // namespace fdr
+
+namespace fdr {
+
+// ------------------------------------------------------------------------------------------
+// Fused learner step (fdr_fd_grad_fused / fdr_fd_step): the weighting, the noise-weighted gradient and
+// its chunk combine in ONE launch -- and, single-process with P <= 65536, DSGD in the same launch.
+//
+// fd_grad_fused_kernel, grid (column blocks of 256, row chunks), 256 threads:
+//   1. the chunk's first 64 table rows are requested up front (they do not depend on the weights);
+//   2. meanwhile the workgroup forms the weights of ITS directions: the z-score statistics over all
+//      rewards (f64, the same fixed-order tree in every workgroup, so all agree bit for bit), or
+//      precomputed centred-rank weights, or the raw moments form; coefficients in LDS (NaN for a row
+//      whose table offset is out of range: the gradient is poisoned, the table never over-read);
+//   3. f64 column sums over the chunk's rows;
+//   4. chunk partials are combined in the same launch: slab store -> agent-scope release -> ticket on
+//      the column block's counter; the last arriver acquires and sums the slabs in chunk order
+//      (deterministic and placement-independent: cdna_hip_programming.md Guideline 16, counter form)
+//      and resets the counter;
+//   5. (fdr_fd_step) each column block's owner publishes sum fl32(-g)^2 of its columns and takes a
+//      ticket on the DSGD counter; the last owner forms ||fl32(-g)|| in column-block order and applies
+//      the update to all of theta (dynamic_sgd.py:19-39), then ||d theta||.
+// Counters must be zero before the first launch on a workspace (the caller zeroes the leading counter
+// block once); every launch leaves them zero.
+// ------------------------------------------------------------------------------------------
+constexpr int kFusedRows = 64;       // table rows per pass: loads in flight per thread
+constexpr int kFusedMaxRows = 1024;  // directions per chunk (LDS coefficient arrays)
+
+struct FdArgs {
+  const float* table;
+  int64_t max_idx;
+  const int64_t* idx;    // per LOCAL lane [n_dirs * lpd]; direction d's row starts at idx[d * lpd]
+  int n_dirs;
+  int64_t P;
+  const double* r_all;   // [n_all]
+  int n_all;
+  double pr;
+  int lo;
+  const int8_t* sign;    // [n_dirs * lpd] (local lanes)
+  const double* n2;      // [n_dirs * lpd]
+  const double* w;       // centred-rank weights of the local lanes
+  int lpd;
+  float sigma;
+  int rows_per_chunk, n_chunks, col_blocks;
+  double* partial;       // [n_chunks][P] (x2 in MOMENTS mode)
+  unsigned* cnt;         // [col_blocks] chunk tickets, [col_blocks] the DSGD ticket
+  double* out;           // g [P]; MOMENTS: [A | B | sum r' | sum r'^2 | n]
+  double* gsq;           // [col_blocks] sum fl32(-g)^2 per column block (fdr_fd_step), or NULL
+};
+
+// handed-off payload is stored write-through (sc1: an agent-scope relaxed atomic store), so the ticket needs
+// no release fence (cdna_hip_programming.md Guideline 16 R1)
+__device__ __forceinline__ void store_wt(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void publish_and_ticket(unsigned* cnt, unsigned need, int* s_flag) {
+  // every storing wave drains its sc1 stores, the workgroup meets, ONE lane takes the ticket
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == need - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *s_flag = last;
+  }
+  __syncthreads();
+}
+
+// sum over k < n of base[k * stride] in k order, 16 loads in flight
+__device__ __forceinline__ double sum_slabs(const double* base, int64_t stride, int n) {
+  double s = 0.0;
+  int k = 0;
+  for (; k + 16 <= n; k += 16) {
+    double v[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = base[(int64_t)(k + e) * stride];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) s += v[e];
+  }
+  for (; k < n; ++k) s += base[(int64_t)k * stride];
+  return s;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void fd_grad_fused_kernel(FdArgs a) {
+  __shared__ double cA[kFusedMaxRows];
+  __shared__ double cB[MODE == FDR_WEIGHT_MOMENTS ? kFusedMaxRows : 1];
+  __shared__ double red[4];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x;
+  const int chunk = blockIdx.y, cb = blockIdx.x;
+  const int d0 = chunk * a.rows_per_chunk, d1 = min(a.n_dirs, d0 + a.rows_per_chunk);
+  const int64_t P = a.P;
+  const int64_t col = (int64_t)cb * 256 + tid;
+  const bool ok = col < P;
+  const int64_t cc = ok ? col : 0;
+  auto row_off = [&](int d) {
+    const int64_t off = a.idx[(int64_t)d * a.lpd];
+    return (off < 0 || off > a.max_idx) ? (int64_t)-1 : off;
+  };
+  float v[kFusedRows];
+  auto load_pass = [&](int r0) {
+#pragma unroll
+    for (int r = 0; r < kFusedRows; ++r) {
+      const int d = r0 + r;
+      float x = 0.f;
+      if (d < d1) {
+        const int64_t off = row_off(d);
+        x = a.table[(off < 0 ? 0 : off) + cc];
+      }
+      v[r] = x;
+    }
+  };
+  load_pass(d0);
+
+  // this thread's first direction's per-lane inputs, requested before the statistics need them
+  constexpr int kMaxLpd = 4;
+  const int dmine = d0 + tid;
+  double xin[kMaxLpd], vin[kMaxLpd];
+#pragma unroll
+  for (int k = 0; k < kMaxLpd; ++k) {
+    xin[k] = 0.0;
+    vin[k] = 0.0;
+    if (dmine < d1 && k < a.lpd) {
+      const int i = dmine * a.lpd + k;
+      const int sg = a.sign[i];
+      vin[k] = sg == 0 ? 0.0 : (double)sg * (double)a.sigma / a.n2[i];
+      if constexpr (MODE == FDR_WEIGHT_CENTERED_RANK) xin[k] = a.w[i];
+      else xin[k] = a.r_all[a.lo + i] - a.pr;
+    }
+  }
+  double mean = 0.0, sd = 0.0;
+  if constexpr (MODE == FDR_WEIGHT_ZSCORE) {
+    // one load pass, the values kept in registers for the second (same per-thread order as a reload)
+    constexpr int kR = 16;
+    double xr[kR];
+#pragma unroll
+    for (int k = 0; k < kR; ++k) {
+      const int i = tid + 256 * k;
+      xr[k] = i < a.n_all ? a.r_all[i] - a.pr : 0.0;
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kR; ++k)
+      if (tid + 256 * k < a.n_all) s += xr[k];
+    for (int i = tid + 256 * kR; i < a.n_all; i += 256) s += a.r_all[i] - a.pr;
+    mean = block_sum_256(s, red) / (double)a.n_all;
+    double q = 0.0;
+#pragma unroll
+    for (int k = 0; k < kR; ++k)
+      if (tid + 256 * k < a.n_all) {
+        const double d = xr[k] - mean;
+        q += d * d;
+      }
+    for (int i = tid + 256 * kR; i < a.n_all; i += 256) {
+      const double d = (a.r_all[i] - a.pr) - mean;
+      q += d * d;
+    }
+    sd = sqrt(block_sum_256(q, red) / (double)a.n_all);
+  }
+  auto weight = [&](double x) {
+    if constexpr (MODE == FDR_WEIGHT_ZSCORE) return sd == 0.0 ? x : (x - mean) / sd;  // math_helpers.py:127-134
+    else return x;
+  };
+  if (dmine < d1 && a.lpd <= kMaxLpd) {
+    double c = 0.0, b = 0.0;
+#pragma unroll
+    for (int k = 0; k < kMaxLpd; ++k)
+      if (k < a.lpd && vin[k] != 0.0) {
+        c += weight(xin[k]) * vin[k];
+        b += vin[k];
+      }
+    if (row_off(dmine) < 0) c = b = __builtin_nan("");
+    cA[dmine - d0] = c;
+    if constexpr (MODE == FDR_WEIGHT_MOMENTS) cB[dmine - d0] = b;
+  }
+  for (int d = d0 + tid + (a.lpd <= kMaxLpd ? 256 : 0); d < d1; d += 256) {  // further directions of this thread
+    double c = 0.0, b = 0.0;
+    for (int k = 0; k < a.lpd; ++k) {
+      const int i = d * a.lpd + k;
+      const int sg = a.sign[i];
+      if (sg == 0) continue;
+      const double vi = (double)sg * (double)a.sigma / a.n2[i];
+      double x;
+      if constexpr (MODE == FDR_WEIGHT_CENTERED_RANK) x = a.w[i];
+      else x = a.r_all[a.lo + i] - a.pr;
+      c += weight(x) * vi;
+      b += vi;
+    }
+    if (row_off(d) < 0) c = b = __builtin_nan("");
+    cA[d - d0] = c;
+    if constexpr (MODE == FDR_WEIGHT_MOMENTS) cB[d - d0] = b;
+  }
+  __syncthreads();
+
+  double acc0 = 0.0, acc1 = 0.0, bcc0 = 0.0, bcc1 = 0.0;
+  for (int r0 = d0; r0 < d1; r0 += kFusedRows) {
+    if (r0 != d0) load_pass(r0);
+#pragma unroll
+    for (int r = 0; r < kFusedRows; r += 2) {
+      if (r0 + r < d1) {
+        acc0 = fma(cA[r0 + r - d0], (double)v[r], acc0);
+        if constexpr (MODE == FDR_WEIGHT_MOMENTS) bcc0 = fma(cB[r0 + r - d0], (double)v[r], bcc0);
+      }
+      if (r0 + r + 1 < d1) {
+        acc1 = fma(cA[r0 + r + 1 - d0], (double)v[r + 1], acc1);
+        if constexpr (MODE == FDR_WEIGHT_MOMENTS) bcc1 = fma(cB[r0 + r + 1 - d0], (double)v[r + 1], bcc1);
+      }
+    }
+  }
+  const double ga = acc0 + acc1, gb = bcc0 + bcc1;
+
+  bool owner = true;  // this workgroup holds the final g of its column block
+  double gfin = ga;
+  if (a.n_chunks == 1) {
+    if (ok) {
+      store_wt(a.out + col, ga);
+      if constexpr (MODE == FDR_WEIGHT_MOMENTS) a.out[P + col] = gb;
+    }
+  } else {
+    if (ok) {
+      store_wt(a.partial + (int64_t)chunk * P + col, ga);
+      if constexpr (MODE == FDR_WEIGHT_MOMENTS) store_wt(a.partial + ((int64_t)a.n_chunks + chunk) * P + col, gb);
+    }
+    publish_and_ticket(a.cnt + cb, (unsigned)a.n_chunks, &s_flag);
+    owner = s_flag != 0;
+    if (owner) {
+      double sa = 0.0, sb = 0.0;
+      if (ok) {
+        sa = sum_slabs(a.partial + col, P, a.n_chunks);
+        store_wt(a.out + col, sa);  // read by the DSGD workgroup of fdr_fd_step
+        if constexpr (MODE == FDR_WEIGHT_MOMENTS) {
+          sb = sum_slabs(a.partial + (int64_t)a.n_chunks * P + col, P, a.n_chunks);
+          a.out[P + col] = sb;
+        }
+      }
+      gfin = sa;
+      if (tid == 0) __hip_atomic_store(a.cnt + cb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if constexpr (MODE == FDR_WEIGHT_MOMENTS) {
+    if (cb == 0 && chunk == 0) {  // the local reward moments [sum r' | sum r'^2 | n]
+      double s = 0.0, q = 0.0;
+      for (int i = tid; i < a.n_all; i += 256) {
+        const double x = a.r_all[a.lo + i] - a.pr;
+        s += x;
+        q += x * x;
+      }
+      s = block_sum_256(s, red);
+      q = block_sum_256(q, red);
+      if (tid == 0) {
+        a.out[2 * P] = s;
+        a.out[2 * P + 1] = q;
+        a.out[2 * P + 2] = (double)a.n_all;
+      }
+    }
+  } else {
+    if (a.gsq && owner) {  // fdr_fd_step: this column block's sum fl32(-g)^2 for the DSGD launch
+      const float gr = ok ? (float)(-gfin) : 0.f;  // set_grad_from_flat casts to f32 (policy.py:68)
+      const double part = block_sum_256((double)gr * (double)gr, red);
+      if (tid == 0) a.gsq[cb] = part;
+    }
+  }
+}
+
+// DSGD after fd_grad_fused (fdr_fd_step): one 256-column block per workgroup.  Every workgroup forms
+// ||fl32(-g)|| from the per-column-block partials in the same order, updates its columns
+// (dynamic_sgd.py:19-39), writes theta_new to the history slot (the learner's policy_history,
+// finite_differences.py:75-78) and its sum of squared updates; the last workgroup (ticket) forms ||d theta||.
+__global__ __launch_bounds__(256) void dsgd_apply_cb_kernel(float* __restrict__ theta, const double* __restrict__ g,
+                                                            int64_t P, const double* __restrict__ gsq, int col_blocks,
+                                                            double lr, double lr_scale, float* __restrict__ hist,
+                                                            double* __restrict__ upart, unsigned* __restrict__ cnt,
+                                                            double* __restrict__ out) {
+#pragma clang fp contract(off)
+  __shared__ double red[4];
+  __shared__ double gs[256];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x, cb = blockIdx.x;
+  const int64_t p = (int64_t)cb * 256 + tid;
+  const double gv = p < P ? g[p] : 0.0;
+  const float old = p < P ? theta[p] : 0.f;
+  double ss = 0.0;
+  for (int k0 = 0; k0 < col_blocks; k0 += 256) {
+    __syncthreads();
+    if (k0 + tid < col_blocks) gs[tid] = gsq[k0 + tid];
+    __syncthreads();
+    for (int k = 0; k < min(256, col_blocks - k0); ++k) ss += gs[k];
+  }
+  const float norm = (float)sqrt(ss);  // flat_grad.norm().item() (dynamic_sgd.py:27)
+  double u = 0.0;
+  float nw = old;
+  if (norm > 0.f) {
+    const double coef = lr * sqrt((double)P) * lr_scale / (double)norm;  // dynamic_sgd.py:30,51
+    const float c32 = (float)coef;
+    const float g32 = (float)(-gv);
+    nw = old - c32 * g32;  // p.sub_(coef * grad_slice) (dynamic_sgd.py:36)
+    const float dd = old - nw;
+    u = p < P ? (double)dd * (double)dd : 0.0;
+  }
+  if (p < P) {
+    theta[p] = nw;
+    if (hist) hist[p] = nw;
+  }
+  u = block_sum_256(u, red);
+  if (tid == 0) store_wt(upart + cb, u);
+  publish_and_ticket(cnt, (unsigned)col_blocks, &s_flag);
+  if (s_flag) {
+    double t = 0.0;
+    for (int k0 = 0; k0 < col_blocks; k0 += 256) {
+      __syncthreads();
+      if (k0 + tid < col_blocks) gs[tid] = upart[k0 + tid];
+      __syncthreads();
+      for (int k = 0; k < min(256, col_blocks - k0); ++k) t += gs[k];
+    }
+    if (tid == 0) {
+      out[0] = sqrt(t);
+      out[1] = (double)norm;
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+struct FusedPlan {
+  int col_blocks, rows_per_chunk, n_chunks;
+};
+static FusedPlan fused_plan(int n_dirs, int64_t P) {
+  FusedPlan f;
+  f.col_blocks = (int)((P + 255) / 256);
+  const int target_chunks = std::max(1, 1024 / std::max(1, f.col_blocks));
+  const int rows = std::max(kFusedRows, (n_dirs + target_chunks - 1) / target_chunks);
+  f.rows_per_chunk = std::min(kFusedMaxRows, (rows + kFusedRows - 1) / kFusedRows * kFusedRows);
+  f.n_chunks = std::max(1, (n_dirs + f.rows_per_chunk - 1) / f.rows_per_chunk);
+  return f;
+}
+
+// workspace: [counters: col_blocks + 1 u32, padded to 256 B][gsq][update partials][rank weights][partial slabs]
+static int64_t pad256(int64_t b) { return (b + 255) / 256 * 256; }
+int64_t fused_counter_bytes(int n_dirs, int64_t P) {
+  const FusedPlan f = fused_plan(std::max(1, n_dirs), P);
+  return pad256((int64_t)(f.col_blocks + 1) * 4);
+}
+int64_t fused_workspace_bytes(int n_dirs, int n_local, int64_t P, int mode) {
+  if (n_dirs < 0 || P <= 0) return -1;
+  const FusedPlan f = fused_plan(std::max(1, n_dirs), P);
+  const int64_t slabs = f.n_chunks > 1 ? (int64_t)f.n_chunks * P * 8 * (mode == FDR_WEIGHT_MOMENTS ? 2 : 1) : 0;
+  return fused_counter_bytes(n_dirs, P) + 2 * pad256((int64_t)f.col_blocks * 8) +
+         pad256((int64_t)std::max(0, n_local) * 8) + slabs;
+}
+
+// centred rank (build extension; the standard ES transform): rank of r_i among all n_all returns,
+// ties broken by lane index; w_i = rank_i / (n_all - 1) - 0.5.  Each thread counts over LDS tiles.
+__global__ __launch_bounds__(256) void rank_weights_kernel(const double* __restrict__ r_all, int n_all, int lo,
+                                                           int n_local, double* __restrict__ w) {
+  __shared__ double tile[2048];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int gi = lo + (i < n_local ? i : 0);
+  const double ri = r_all[gi];
+  int rank = 0;
+  for (int t0 = 0; t0 < n_all; t0 += 2048) {
+    const int tn = min(2048, n_all - t0);
+    __syncthreads();
+    for (int k = threadIdx.x; k < tn; k += 256) tile[k] = r_all[t0 + k];
+    __syncthreads();
+    for (int k = 0; k < tn; ++k) {
+      const double rk = tile[k];
+      rank += (rk < ri || (rk == ri && t0 + k < gi)) ? 1 : 0;
+    }
+  }
+  if (i < n_local) w[i] = n_all > 1 ? (double)rank / (double)(n_all - 1) - 0.5 : 0.0;
+}
+
+int launch_fd_grad_fused(const float* table, int64_t table_size, const int64_t* idx, int n_dirs, int64_t P,
+                         const double* r_all, int n_all, double pr, int lo, const int8_t* sign, const double* n2,
+                         int lpd, float sigma, int mode, double* out, float* theta, double lr, double lr_scale,
+                         float* hist, double* dsgd_out, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  const int n_local = n_dirs * lpd;
+  if (!ws || ws_bytes < fused_workspace_bytes(n_dirs, n_local, P, mode))
+    return set_error(FDR_ERR_WORKSPACE, "fd_grad_fused workspace too small");
+  const FusedPlan f = fused_plan(n_dirs, P);
+  char* w = static_cast<char*>(ws);
+  const int64_t cnt_b = fused_counter_bytes(n_dirs, P);
+  const int64_t cb_b = pad256((int64_t)f.col_blocks * 8);
+  const int64_t w_b = pad256((int64_t)n_local * 8);
+  FdArgs a{};
+  a.table = table;
+  a.max_idx = table_size - P;
+  a.idx = idx;
+  a.n_dirs = n_dirs;
+  a.P = P;
+  a.r_all = r_all;
+  a.n_all = n_all;
+  a.pr = pr;
+  a.lo = lo;
+  a.sign = sign;
+  a.n2 = n2;
+  a.lpd = lpd;
+  a.sigma = sigma;
+  a.rows_per_chunk = f.rows_per_chunk;
+  a.n_chunks = f.n_chunks;
+  a.col_blocks = f.col_blocks;
+  a.cnt = reinterpret_cast<unsigned*>(w);
+  double* gsq = reinterpret_cast<double*>(w + cnt_b);
+  double* upart = reinterpret_cast<double*>(w + cnt_b + cb_b);
+  a.gsq = theta ? gsq : nullptr;
+  a.w = reinterpret_cast<double*>(w + cnt_b + 2 * cb_b);
+  a.partial = reinterpret_cast<double*>(w + cnt_b + 2 * cb_b + w_b);
+  a.out = out;
+  const dim3 grid(f.col_blocks, f.n_chunks);
+  switch (mode) {
+    case FDR_WEIGHT_ZSCORE:
+      hipLaunchKernelGGL(fd_grad_fused_kernel<FDR_WEIGHT_ZSCORE>, grid, dim3(256), 0, stream, a);
+      break;
+    case FDR_WEIGHT_CENTERED_RANK:
+      hipLaunchKernelGGL(rank_weights_kernel, dim3((n_local + 255) / 256), dim3(256), 0, stream, r_all, n_all, lo,
+                         n_local, const_cast<double*>(a.w));
+      hipLaunchKernelGGL(fd_grad_fused_kernel<FDR_WEIGHT_CENTERED_RANK>, grid, dim3(256), 0, stream, a);
+      break;
+    case FDR_WEIGHT_MOMENTS:
+      if (theta) return set_error(FDR_ERR_INVALID, "the moments form is reduced across ranks before DSGD");
+      hipLaunchKernelGGL(fd_grad_fused_kernel<FDR_WEIGHT_MOMENTS>, grid, dim3(256), 0, stream, a);
+      break;
+    default:
+      return set_error(FDR_ERR_INVALID, "unknown weighting mode");
+  }
+  int rc = check_launch("fd_grad_fused_kernel");
+  if (rc || !theta) return rc;
+  hipLaunchKernelGGL(dsgd_apply_cb_kernel, dim3(f.col_blocks), dim3(256), 0, stream, theta, out, P, gsq, f.col_blocks,
+                     lr, lr_scale, hist, upart, a.cnt + f.col_blocks, dsgd_out);
+  return check_launch("dsgd_apply_cb_kernel");
+}
+
+int launch_rank_weights(const double* r_all, int n_all, int lo, int n_local, double* w, hipStream_t stream) {
+  if (n_local == 0) return FDR_OK;
+  hipLaunchKernelGGL(rank_weights_kernel, dim3((n_local + 255) / 256), dim3(256), 0, stream, r_all, n_all, lo, n_local,
+                     w);
+  return check_launch("rank_weights_kernel");
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused DSGD (P <= kDsgdFusedMaxP): ONE 1024-thread workgroup does the norm of fl32(-g), the update
+// and ||d theta|| (dynamic_sgd.py:19-39) with barriers only.  src = g, or (moments form) the summed
+// [A | B | sum r' | sum r'^2 | n] from which g = (A - m B) / sd (z-score identity), also
+// written to g_out.  Same per-element arithmetic and the same f32 norm as the 3-kernel path.
+// ------------------------------------------------------------------------------------------
+constexpr int64_t kDsgdFusedMaxP = 1 << 16;
+
+__device__ __forceinline__ double grad_elem(const double* src, int64_t P, int64_t p, bool mom, double m, double inv_sd,
+                                            bool unit) {
+  if (!mom) return src[p];
+  const double A = src[p], B = src[P + p];
+  return unit ? A : (A - m * B) * inv_sd;
+}
+
+__device__ __forceinline__ void moment_stats(const double* src, int64_t P, double& m, double& inv_sd, bool& unit) {
+  const double s = src[2 * P], q = src[2 * P + 1], n = src[2 * P + 2];
+  m = s / n;
+  const double var = fmax(q / n - m * m, 0.0);
+  unit = var == 0.0;  // standardize_arr returns the input unchanged when std == 0
+  inv_sd = unit ? 1.0 : 1.0 / sqrt(var);
+}
+
+__device__ double block_sum_1024x(double v, double* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, j = threadIdx.x & 63;
+  __syncthreads();
+  if (j == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int i = 0; i < 16; ++i) s += red[i];
+  return s;
+}
+
+__global__ __launch_bounds__(1024) void dsgd_fused_kernel(float* __restrict__ theta, const double* __restrict__ src,
+                                                          int64_t P, int mom, double lr, double lr_scale,
+                                                          double* __restrict__ g_out, double* __restrict__ out) {
+#pragma clang fp contract(off)
+  __shared__ double red[16];
+  double m = 0.0, inv_sd = 1.0;
+  bool unit = true;
+  if (mom) moment_stats(src, P, m, inv_sd, unit);
+  double s = 0.0;
+  for (int64_t p = threadIdx.x; p < P; p += 1024) {
+    const double g = grad_elem(src, P, p, mom, m, inv_sd, unit);
+    if (mom && g_out) g_out[p] = g;
+    const float gr = (float)(-g);
+    s += (double)gr * (double)gr;
+  }
+  const float norm = (float)sqrt(block_sum_1024x(s, red));
+  double u = 0.0;
+  if (norm > 0.f) {
+    const double coef = lr * sqrt((double)P) * lr_scale / (double)norm;
+    const float c32 = (float)coef;
+    for (int64_t p = threadIdx.x; p < P; p += 1024) {
+      const float gr = (float)(-grad_elem(src, P, p, mom, m, inv_sd, unit));
+      const float old = theta[p];
+      const float nw = old - c32 * gr;
+      theta[p] = nw;
+      const float dd = old - nw;
+      u += (double)dd * (double)dd;
+    }
+  }
+  u = block_sum_1024x(u, red);
+  if (threadIdx.x == 0) {
+    out[0] = sqrt(u);
+    out[1] = (double)norm;
+  }
+}
+
+// multi-block path for large P (ImpalaPolicy), moments-aware
+__global__ __launch_bounds__(256) void moments_to_grad_kernel(const double* __restrict__ src, int64_t P,
+                                                              double* __restrict__ g) {
+  double m, inv_sd;
+  bool unit;
+  moment_stats(src, P, m, inv_sd, unit);
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x)
+    g[p] = grad_elem(src, P, p, true, m, inv_sd, unit);
+}
+
+int launch_dsgd_ex(float* theta, const double* src, int mom, int64_t P, double lr, double lr_scale, double* g_out,
+                   double* out, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  if (P <= kDsgdFusedMaxP) {
+    hipLaunchKernelGGL(dsgd_fused_kernel, dim3(1), dim3(1024), 0, stream, theta, src, P, mom, lr, lr_scale, g_out, out);
+    return check_launch("dsgd_fused_kernel");
+  }
+  const double* g = src;
+  if (mom) {
+    if (!g_out) return set_error(FDR_ERR_INVALID, "moments form needs g_out for large P");
+    const int rb = (int)std::min<int64_t>((P + 255) / 256, 2048);
+    hipLaunchKernelGGL(moments_to_grad_kernel, dim3(rb), dim3(256), 0, stream, src, P, g_out);
+    int rc = check_launch("moments_to_grad_kernel");
+    if (rc) return rc;
+    g = g_out;
+  }
+  return launch_dsgd(theta, g, P, lr, lr_scale, out, ws, ws_bytes, stream);
+}
+
+}  // namespace fdr

@@ -14,6 +14,7 @@ FDR_POLICY_DISCRETE, FDR_POLICY_MUJOCO = 0, 1
 FDR_ENV_SYNTH, FDR_ENV_TRAP = 0, 1
 FDR_DIST_L2, FDR_DIST_TVD, FDR_DIST_W2 = 0, 1, 2
 FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_AUTO = 0, 1, 2
+FDR_WEIGHT_ZSCORE, FDR_WEIGHT_CENTERED_RANK, FDR_WEIGHT_MOMENTS = 0, 1, 2
 
 EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy", "fdr_ctx_device",
            "fdr_perturb", "fdr_policy_forward", "fdr_rollout", "fdr_fd_weights",
@@ -26,7 +27,8 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_atari_num_params", "fdr_atari_workspace_bytes", "fdr_atari_rollout",
            "fdr_atari_forward_workspace_bytes", "fdr_atari_forward", "fdr_rollout_set_impl",
            "fdr_impala_set_replay_gemm", "fdr_impala_strategies_workspace_bytes", "fdr_impala_strategies",
-           "fdr_impala_env_frames")
+           "fdr_impala_env_frames", "fdr_fd_grad_fused_workspace_bytes", "fdr_fd_grad_fused_counter_bytes",
+           "fdr_fd_grad_fused", "fdr_rank_weights", "fdr_dsgd_step_ex", "fdr_fd_step")
 
 
 class FDRError(RuntimeError):
@@ -109,6 +111,14 @@ def _load():
         "fdr_fd_grad_workspace_bytes": (I64, [I32, I64]),
         "fdr_fd_grad": (ctypes.c_int, [P, P, I64, P, P, I32, I64, P, P, I64, P]),
         "fdr_dsgd_workspace_bytes": (I64, [I64]),
+        "fdr_fd_grad_fused_workspace_bytes": (I64, [I32, I32, I64, I32]),
+        "fdr_fd_grad_fused_counter_bytes": (I64, [I32, I64]),
+        "fdr_fd_grad_fused": (ctypes.c_int, [P, P, I64, P, I32, I64, P, I32, F64, I32, P, P, I32, F32, I32, P, P, I64,
+                                             P]),
+        "fdr_rank_weights": (ctypes.c_int, [P, P, I32, I32, I32, P, P]),
+        "fdr_fd_step": (ctypes.c_int, [P, P, I64, P, I32, I64, P, I32, F64, P, P, I32, F32, I32, P, F64, F64, P, P, P,
+                                       P, I64, P]),
+        "fdr_dsgd_step_ex": (ctypes.c_int, [P, P, P, I32, I64, F64, F64, P, P, P, I64, P]),
         "fdr_dsgd_step": (ctypes.c_int, [P, P, P, I64, F64, F64, P, P, I64, P]),
         "fdr_impala_num_params": (I64, [I32]),
         "fdr_impala_num_bn_stats": (I64, []),

@@ -149,12 +149,86 @@ def fd_weights(rewards_all, policy_reward, lane_lo, sign_local, norm2_local, lan
 _WS = {}
 
 
-def _workspace(key, nbytes, device):
+def _workspace(key, nbytes, device, zeroed=False):
+    """Per-(purpose, device) scratch, grown on demand.  zeroed: allocated zero-filled (the in-launch
+    counters of fdr_fd_grad_fused must start at zero; every call leaves them zero)."""
     buf = _WS.get((key, device))
     if buf is None or buf.numel() < nbytes:
-        buf = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+        n = max(int(nbytes), 16)
+        buf = torch.zeros(n, dtype=torch.uint8, device=device) if zeroed else \
+            torch.empty(n, dtype=torch.uint8, device=device)
         _WS[(key, device)] = buf
     return buf
+
+
+WEIGHT_MODES = {"zscore": _lib.FDR_WEIGHT_ZSCORE, "centred_rank": _lib.FDR_WEIGHT_CENTERED_RANK,
+                "moments": _lib.FDR_WEIGHT_MOMENTS}
+
+
+def fd_grad_fused(table, idx_local, rewards_all, policy_reward, lane_lo, sign_local, norm2_local, lanes_per_dir, sigma,
+                  n_params, mode="zscore", out=None):
+    """Weights + noise-weighted gradient in one launch (fdr_fd_grad_fused).  idx_local / sign_local / norm2_local:
+    one entry per local lane.  mode "zscore" / "centred_rank" -> g f64 [P]; "moments" (local rewards only) ->
+    [A | B | sum r' | sum r'^2 | n] f64 [2P + 3]."""
+    _check_dev(table, idx_local, rewards_all, sign_local, norm2_local)
+    dev = table.device
+    n_dirs = idx_local.numel() // int(lanes_per_dir)
+    m = WEIGHT_MODES[mode]
+    n_out = 2 * n_params + 3 if mode == "moments" else n_params
+    if out is None:
+        out = torch.empty(n_out, dtype=torch.float64, device=dev)
+    nb = lib.fdr_fd_grad_fused_workspace_bytes(n_dirs, int(lanes_per_dir), n_params, m)
+    ws = _workspace("fused_%d" % m, nb, dev, zeroed=True)
+    check(lib.fdr_fd_grad_fused(None, _p(table), table.numel(), _p(idx_local), n_dirs, n_params, _p(rewards_all),
+                                rewards_all.numel(), float(policy_reward), int(lane_lo), _p(sign_local), _p(norm2_local),
+                                int(lanes_per_dir), float(sigma), m, _p(out), _p(ws), ws.numel(), _stream(dev)),
+          "fdr_fd_grad_fused")
+    return out
+
+
+def fd_step(table, idx_local, rewards, policy_reward, sign_local, norm2_local, lanes_per_dir, sigma, theta, lr,
+            lr_scale, mode="zscore", g=None, out=None, theta_hist=None):
+    """The single-process FD step (fdr_fd_step): weights + gradient (-> g) in one launch, DSGD on theta in place in
+    a second; theta_hist (f32 [P], optional) receives the updated theta.  Returns device f64[2] =
+    (||d theta||, ||grad||)."""
+    _check_dev(table, idx_local, rewards, sign_local, norm2_local, theta, g, theta_hist)
+    dev = table.device
+    P = theta.numel()
+    n_dirs = idx_local.numel() // int(lanes_per_dir)
+    m = WEIGHT_MODES[mode]
+    if g is None:
+        g = torch.empty(P, dtype=torch.float64, device=dev)
+    if out is None:
+        out = torch.empty(2, dtype=torch.float64, device=dev)
+    nb = lib.fdr_fd_grad_fused_workspace_bytes(n_dirs, int(lanes_per_dir), P, m)
+    ws = _workspace("fused_%d" % m, nb, dev, zeroed=True)
+    check(lib.fdr_fd_step(None, _p(table), table.numel(), _p(idx_local), n_dirs, P, _p(rewards), rewards.numel(),
+                          float(policy_reward), _p(sign_local), _p(norm2_local), int(lanes_per_dir), float(sigma), m,
+                          _p(theta), float(lr), float(lr_scale), _p(g), _p(theta_hist), _p(out), _p(ws), ws.numel(),
+                          _stream(dev)), "fdr_fd_step")
+    return out
+
+
+def rank_weights(rewards_all, lane_lo, n_local):
+    """Centred-rank weights of lanes [lane_lo, lane_lo + n_local) over rewards_all (f64 [n_local])."""
+    _check_dev(rewards_all)
+    w = torch.empty(n_local, dtype=torch.float64, device=rewards_all.device)
+    check(lib.fdr_rank_weights(None, _p(rewards_all), rewards_all.numel(), int(lane_lo), int(n_local), _p(w),
+                               _stream(rewards_all.device)), "fdr_rank_weights")
+    return w
+
+
+def dsgd_step_ex(theta, src, moments, lr, lr_scale, g_out=None, out=None):
+    """DSGD from g (moments=False) or from summed moments (g = (A - m B) / sd written to g_out)."""
+    _check_dev(theta, src, g_out)
+    dev = theta.device
+    if out is None:
+        out = torch.empty(2, dtype=torch.float64, device=dev)
+    nb = lib.fdr_dsgd_workspace_bytes(theta.numel())
+    ws = _workspace("dsgd", nb, dev)
+    check(lib.fdr_dsgd_step_ex(None, _p(theta), _p(src), 1 if moments else 0, theta.numel(), float(lr), float(lr_scale),
+                               _p(g_out), _p(out), _p(ws), ws.numel(), _stream(dev)), "fdr_dsgd_step_ex")
+    return out
 
 
 def fd_grad(table, idx_dirs, coef, n_params, g=None):

@@ -3,10 +3,16 @@
 ``step(batch, policy_reward, policy_novelty, policy_entropy)`` accepts either the reference's
 list of FDReturn or an FDBatch (device SoA from Worker.evaluate) and runs, all on the device:
 
-    fdr_fd_weights   z = standardize(r - r_pol) over the batch; coef_d = sum_i z_i s_i sigma / ||lambda_i||^2
-    fdr_fd_grad      g = sum_d coef_d * table[idx_d : idx_d + P]            (f64, fixed order)
-    [all_reduce(g)]  one RCCL all-reduce when the batch is sharded over ranks (DESIGN.md "Multi-GPU")
-    fdr_dsgd_step    theta <- theta - lr*sqrt(P)*lr_scale * fl32(-g) / ||fl32(-g)||
+    fdr_fd_grad_fused  ONE launch: z = standardize(r - r_pol) over the batch, coef_d = sum_i z_i s_i sigma /
+                       ||lambda_i||^2, g = sum_d coef_d * table[idx_d : idx_d + P] (f64, fixed order, chunk
+                       partials combined in-launch)
+    fdr_dsgd_step      ONE launch (P <= 65536): theta <- theta - lr*sqrt(P)*lr_scale * fl32(-g) / ||fl32(-g)||
+
+Sharded over ranks (DESIGN.md "Multi-GPU") the z-score step needs ONE collective: every rank reduces its lanes
+to the moments [A | B | sum r' | sum r'^2 | n] (A = sum r'_i v_i, B = sum v_i), one RCCL all-reduce sums them,
+and DSGD forms g = (A - m B) / sd on the fly (equal to the z-weighted sum in real arithmetic).
+``weighting="centred_rank"`` (build extension named by the north star; the reference's weighting is the
+z-score) ranks all returns, so it keeps the all-gather of the per-lane returns + the all-reduce of g.
 
 Returns carry a current epoch in the synchronous engine; returns from an older epoch (the
 reference's async server mode) add the parameter drift theta_epoch - theta_now to lambda
@@ -22,10 +28,16 @@ from utils import math_helpers
 
 from .fd_return import FDBatch
 
+FUSED_STEP_MAX_P = 1 << 16   # fdr_fd_step fuses DSGD into the gradient launch up to this many parameters
+
 
 class FiniteDifferences(object):
     def __init__(self, policy, gradient_optimizer, omega, noise_source, noise_std=0.1, batch_size=100,
-                 ent_coef=0.0, max_delayed_return=10, process_group=None):
+                 ent_coef=0.0, max_delayed_return=10, process_group=None, weighting="zscore", one_collective=True):
+        if weighting not in ("zscore", "centred_rank"):
+            raise ValueError("weighting must be 'zscore' (the reference) or 'centred_rank'")
+        self.weighting = weighting
+        self.one_collective = one_collective
         self.max_delayed_return = max_delayed_return
         self.ent_coef = ent_coef
         self.noise_std = noise_std
@@ -43,6 +55,10 @@ class FiniteDifferences(object):
         P = policy.num_params
         self.gradient_memory = torch.zeros(P, dtype=torch.float64, device=policy.flat.device)
         self._out = torch.zeros(2, dtype=torch.float64, device=policy.flat.device)
+        # policy_history entries written by the DSGD launch itself (no per-step copy): a ring one longer than
+        # the history, so a slot is rewritten only after its entry left the history
+        self._hist_ring = None
+        self._hist_next = 0
 
     # ------------------------------------------------------------------------------------------
     def _distributed(self):
@@ -66,43 +82,69 @@ class FiniteDifferences(object):
         return self._step_returns(list(batch), float(policy_reward))
 
     # ------------------------------------------------------------------------------------------
-    def _step_batch(self, b, policy_reward, extra_grad=None):
+    def _step_batch(self, b, policy_reward):
         table = self.noise_source.device_table(self.policy.flat.device)
         train = torch.as_tensor(b.sign_host != 0)
         if not bool(train.all()):
             raise ValueError("FDBatch for the learner must not contain eval lanes (sign 0)")
         P = self.policy.num_params
+        if not self._distributed():
+            if P <= FUSED_STEP_MAX_P:   # the whole step in one launch: weights + gradient + DSGD
+                lr, lr_scale = self._lr()
+                slot = self._hist_slot()
+                engine.fd_step(table, b.idx, b.reward, policy_reward, b.sign, b.norm2, b.lanes_per_dir, self.noise_std,
+                               self.policy.flat, lr, lr_scale, mode=self.weighting, g=self.gradient_memory, out=self._out,
+                               theta_hist=slot)
+                return self._after_update(slot)
+            g = engine.fd_grad_fused(table, b.idx, b.reward, policy_reward, 0, b.sign, b.norm2, b.lanes_per_dir,
+                                     self.noise_std, P, mode=self.weighting, out=self.gradient_memory)
+            return self._apply(g)
+        if self.weighting == "zscore" and self.one_collective:
+            mom = engine.fd_grad_fused(table, b.idx, b.reward, policy_reward, 0, b.sign, b.norm2, b.lanes_per_dir,
+                                       self.noise_std, P, mode="moments")
+            fdist.allreduce_grad(mom, self.process_group)            # the step's one collective
+            return self._apply(mom, moments=True)
         rewards_all, lane_lo = fdist.gather_rewards(b.reward, self.process_group, getattr(b, "rank_lanes", None))
-        coef = engine.fd_weights(rewards_all, policy_reward, lane_lo, b.sign, b.norm2, b.lanes_per_dir,
-                                 self.noise_std)
-        g = engine.fd_grad(table, b.dir_idx(), coef, P, self.gradient_memory)
-        if extra_grad is not None:
-            g.add_(extra_grad)
+        g = engine.fd_grad_fused(table, b.idx, rewards_all, policy_reward, lane_lo, b.sign, b.norm2,
+                                 b.lanes_per_dir, self.noise_std, P, mode=self.weighting, out=self.gradient_memory)
         fdist.allreduce_grad(g, self.process_group)
         return self._apply(g)
 
-    def _apply(self, g):
-        lr_scale = 1.0
+    def _lr(self):
         if self.using_dsgd:
             self.gradient_optimizer.adjust_lr(self.omega)
-            lr_scale = self.gradient_optimizer.lr_scale
-            lr = self.gradient_optimizer.lr
-        else:
-            lr = self.gradient_optimizer.param_groups[0]["lr"]
-        engine.dsgd_step(self.policy.flat, g, lr, lr_scale, self._out)
+            return self.gradient_optimizer.lr, self.gradient_optimizer.lr_scale
+        return self.gradient_optimizer.param_groups[0]["lr"], 1.0
+
+    def _hist_slot(self):
+        if self._hist_ring is None:
+            n = max(1, self.max_delayed_return) + 1
+            self._hist_ring = torch.empty((n, self.policy.num_params), dtype=torch.float32, device=self.policy.flat.device)
+        slot = self._hist_ring[self._hist_next]
+        self._hist_next = (self._hist_next + 1) % self._hist_ring.shape[0]
+        return slot
+
+    def _after_update(self, hist=None):
         self.gradient_optimizer.steps = getattr(self.gradient_optimizer, "steps", 0) + 1
         self.epoch += 1
         self._build_distance_map()
-        self._update_policy_history()
+        self._update_policy_history(hist)
         return self._out
+
+    def _apply(self, src, moments=False):
+        lr, lr_scale = self._lr()
+        engine.dsgd_step_ex(self.policy.flat, src, moments, lr, lr_scale, g_out=self.gradient_memory if moments else None,
+                            out=self._out)
+        return self._after_update()
 
     def _build_distance_map(self):
         # finite_differences.py:66-73: dist_map[ep] = theta_ep - theta_now for the recent epochs.  The
         # differences are formed on first use (only stale returns read them), not eagerly every step.
         self.dist_map = _LazyDistMap(self.epoch, self.policy_history, self.policy.flat.detach())
 
-    def _update_policy_history(self):
-        self.policy_history.append((self.policy.flat.detach().clone(), self.epoch))
+    def _update_policy_history(self, hist=None):
+        # finite_differences.py:75-78; hist: theta already copied by the DSGD launch (fdr_fd_step theta_hist)
+        self.policy_history.append((self.policy.flat.detach().clone() if hist is None else hist, self.epoch))
         while len(self.policy_history) > self.max_delayed_return:
             self.policy_history.pop(0)
 

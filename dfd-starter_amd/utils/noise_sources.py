@@ -6,7 +6,10 @@
     (noise_sources.py:45): sample() draws one, ``sample_batch(n)`` draws n at once -- numpy's
     vectorised randint yields the identical MT19937 stream (pinned in tests/test_oracle_golden.py);
   * the table is uploaded once per device and stays resident in HBM (100 MB at 25M entries);
-    the HIP kernels gather table[idx : idx + P] directly, theta' is never materialised.
+    the HIP kernels gather table[idx : idx + P] directly, theta' is never materialised;
+  * ``peek_batch(n)`` draws ahead without consuming: the next sample / sample_batch calls return those
+    indices first, so the stream is unchanged (a batch of n draws is n single draws) -- the worker uses it
+    to upload the next FD step's lane descriptors while the current rollout runs.
 """
 import numpy as np
 import torch
@@ -20,18 +23,34 @@ class SharedNoiseTable(object):
         self._n_params = n_params
         self._max_sample_idx = size - n_params
         self._device_tables = {}
+        self._ahead = np.empty(0, np.int64)     # drawn by peek_batch, not yet consumed
 
     @property
     def size(self):
         return self._table.size
 
     def sample(self):
-        idx = int(self._rng.randint(0, self._max_sample_idx))
+        idx = int(self.sample_batch(1)[0])
         return "{}".format(idx), self._table[idx:idx + self._n_params]
+
+    def _draw(self, n):
+        return self._rng.randint(0, self._max_sample_idx, size=int(n)).astype(np.int64)
+
+    def peek_batch(self, n):
+        """The next n indices, drawn ahead but not consumed."""
+        n = int(n)
+        if self._ahead.size < n:
+            self._ahead = np.concatenate([self._ahead, self._draw(n - self._ahead.size)])
+        return self._ahead[:n].copy()
 
     def sample_batch(self, n):
         """n indices in the order n sample() calls would draw them (int64 numpy array)."""
-        return self._rng.randint(0, self._max_sample_idx, size=int(n)).astype(np.int64)
+        n = int(n)
+        if self._ahead.size == 0:
+            return self._draw(n)
+        out = self.peek_batch(n)
+        self._ahead = self._ahead[n:]
+        return out
 
     def decode(self, noise_idx):
         noise_idx = int(noise_idx)

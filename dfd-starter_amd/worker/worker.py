@@ -36,10 +36,14 @@ class Worker(object):
         self.eval_prob = eval_prob
         self.fixed_obs_stats = WelfordRunningStat(policy.input_shape)
         self._pinned = {}
+        self._copy_stream = None
+        self._next = None      # (key, host lanes, device lanes) uploaded ahead by evaluate(prefetch=True)
 
     # ---- hot path ---------------------------------------------------------------------------
     def _to_device(self, arr, dtype):
-        """Async H2D through a small ring of pinned buffers; an event guards each buffer's reuse."""
+        """Async H2D through a small ring of pinned buffers on a side copy stream: the copy runs as soon as it
+        is enqueued (during the previous step's rollout, the host being ahead), and the compute stream only
+        waits on its event -- the upload is off the step's critical path.  An event guards each buffer's reuse."""
         dev = self.policy.flat.device
         key = (dtype, len(arr))
         ring = self._pinned.setdefault(key, {"bufs": [], "events": [], "next": 0})
@@ -54,9 +58,15 @@ class Worker(object):
                 ring["events"][slot].synchronize()
         buf = ring["bufs"][slot]
         buf.numpy()[:] = arr
-        out = buf.to(dev, non_blocking=True)
+        main = torch.cuda.current_stream(dev)
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(dev)
+        with torch.cuda.stream(self._copy_stream):
+            out = buf.to(dev, non_blocking=True)
         ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
+        ev.record(self._copy_stream)
+        main.wait_event(ev)
+        out.record_stream(main)
         ring["events"][slot] = ev
         return out
 
@@ -70,11 +80,12 @@ class Worker(object):
         d = self._to_device(packed, torch.uint8)
         return d[:8 * n].view(torch.int64), d[8 * n:9 * n].view(torch.int8), d[9 * n:].view(torch.int8)
 
-    def launch(self, idx, sign, det, seed=None, out=None, jiggle=True, lane_offset=0):
-        """Run one rollout over explicit lanes (host arrays) -> FDBatch (asynchronous)."""
+    def launch(self, idx, sign, det, seed=None, out=None, jiggle=True, lane_offset=0, lanes_dev=None):
+        """Run one rollout over explicit lanes (host arrays) -> FDBatch (asynchronous).  lanes_dev: the same lanes
+        already on the device (idx, sign, det), e.g. uploaded ahead by evaluate(prefetch=True)."""
         p = self.policy
         n = len(idx)
-        idx_d, sign_d, det_d = self._lanes_to_device(idx, sign, det)
+        idx_d, sign_d, det_d = lanes_dev if lanes_dev is not None else self._lanes_to_device(idx, sign, det)
         table = self.noise_source.device_table(p.flat.device)
         lanes = engine.lanes_desc(p.flat, 0, table, idx_d, sign_d, self.sigma, det_d, lane_offset)
         bm, bv = p.bn_stats()
@@ -97,13 +108,9 @@ class Worker(object):
                              bn_mean=bm, bn_var=bv, out=out, device=p.flat.device, obs_stats=chance)
         return res, idx_d, sign_d
 
-    def evaluate(self, n_dirs, antithetic=True, seed=None, lane_range=None, out=None, novelty=False):
-        """n_dirs perturbation directions (x2 lanes if antithetic) -> FDBatch on the device.
-        novelty=True also scores every lane against the strategy archive (FDBatch.novelty, device f64).
-
-        lane_range=(lo, hi) evaluates only that slice of the lanes (multi-GPU sharding: every rank
-        draws the full index list, in order, and keeps its contiguous share)."""
-        idx = self.noise_source.sample_batch(n_dirs)
+    def _lanes_of(self, idx, n_dirs, antithetic, lane_range):
+        """Host lane arrays of one evaluate() call from its direction indices: (lidx, sign, det, lane_range,
+        rank_lanes)."""
         lpd = 2 if antithetic else 1
         lidx = np.repeat(idx, lpd)
         sign = np.tile(np.array([1, -1], np.int8), n_dirs) if antithetic else np.ones(n_dirs, np.int8)
@@ -116,14 +123,35 @@ class Worker(object):
                 lane_range = std
             if tuple(lane_range) == std:  # the standard split: every rank's lane count is known
                 rank_lanes = [hi - lo for lo, hi in (fdist.lane_range(n_dirs, lpd, world, k) for k in range(world))]
-        if lane_range is not None:
             lo, hi = lane_range
             if lo % lpd or hi % lpd:
                 raise ValueError("lane_range must not split antithetic pairs")
             lidx, sign = lidx[lo:hi], sign[lo:hi]
-        det = np.zeros(len(lidx), np.int8)
+        return lidx, sign, np.zeros(len(lidx), np.int8), lane_range, rank_lanes
+
+    def evaluate(self, n_dirs, antithetic=True, seed=None, lane_range=None, out=None, novelty=False, prefetch=False):
+        """n_dirs perturbation directions (x2 lanes if antithetic) -> FDBatch on the device.
+        novelty=True also scores every lane against the strategy archive (FDBatch.novelty, device f64).
+
+        lane_range=(lo, hi) evaluates only that slice of the lanes (multi-GPU sharding: every rank
+        draws the full index list, in order, and keeps its contiguous share).
+        prefetch=True: after launching this rollout, the NEXT call's indices are drawn ahead
+        (SharedNoiseTable.peek_batch: the index stream is unchanged) and uploaded on the copy stream, so the
+        next rollout does not wait for its host-to-device copy; a next call with other arguments ignores it."""
+        key = (int(n_dirs), bool(antithetic), None if lane_range is None else tuple(lane_range))
+        pre, self._next = self._next, None
+        idx = self.noise_source.sample_batch(n_dirs)
+        lidx, sign, det, lane_range, rank_lanes = self._lanes_of(idx, n_dirs, antithetic, lane_range)
+        lanes_dev = None
+        if pre is not None and pre[0] == key and np.array_equal(pre[1], lidx):
+            lanes_dev = pre[2]
+        lpd = 2 if antithetic else 1
         lo = 0 if lane_range is None else lane_range[0]
-        res, idx_d, sign_d = self.launch(lidx, sign, det, seed=seed, out=out, lane_offset=lo)
+        res, idx_d, sign_d = self.launch(lidx, sign, det, seed=seed, out=out, lane_offset=lo, lanes_dev=lanes_dev)
+        if prefetch and hasattr(self.noise_source, "peek_batch"):
+            nidx = self.noise_source.peek_batch(n_dirs)
+            nl, ns, nd, _, _ = self._lanes_of(nidx, n_dirs, antithetic, key[2])
+            self._next = (key, nl, self._lanes_to_device(nl, ns, nd))
         E = getattr(self.agent.env, "envs_per_lane", 1)
         if E > 1:
             lidx, sign = np.repeat(lidx, E), np.repeat(sign, E)

@@ -182,6 +182,49 @@ int fdr_fd_grad(fdr_ctx* ctx, const float* table, int64_t table_size, const int6
                 const double* coef, int32_t n_dirs, int64_t n_params, double* g, void* workspace,
                 int64_t workspace_bytes, fdr_stream stream);
 
+/* ---- fused weighting + gradient (one launch; learner/finite_differences.py:40-49) -----------------
+ * out = sum over the n_dirs directions d of  coef_d * table[idx_local[d * lpd] : +P]  with the coefficients of
+ * fdr_fd_weights formed inside the launch from the weights w_i of the local lanes [lane_lo, +n_dirs*lpd)
+ * (idx_local, sign_local, norm2_local: one entry per local lane, lanes of a direction contiguous):
+ *   FDR_WEIGHT_ZSCORE         w = standardize(rewards_all - policy_reward) over all n_all lanes (the
+ *                             reference, utils/math_helpers.py:127-134); out = g [P] f64
+ *   FDR_WEIGHT_CENTERED_RANK  w_i = rank_i / (n_all - 1) - 0.5, rank over rewards_all with ties broken by
+ *                             lane index (build extension named by the north star; the standard ES
+ *                             centred rank); out = g [P]
+ *   FDR_WEIGHT_MOMENTS        the one-collective multi-GPU form of the z-score: with r' = r -
+ *                             policy_reward over the LOCAL lanes (rewards_all = the local rewards,
+ *                             n_all = n_local, lane_lo = 0), out = [A | B | sum r' | sum r'^2 | n]
+ *                             (2P + 3 f64): A = sum_i r'_i v_i, B = sum_i v_i, v_i = sign_i sigma eps_i /
+ *                             norm2_i.  Summed over ranks (one all-reduce) it gives g = (A - m B) / sd
+ *                             exactly in real arithmetic; fdr_dsgd_step_ex consumes it.
+ * Chunk partials are combined inside the launch (deterministic order).  workspace:
+ * fdr_fd_grad_fused_workspace_bytes(n_dirs, lanes_per_dir, P, mode) bytes whose first
+ * fdr_fd_grad_fused_counter_bytes(n_dirs, P) bytes must be zero before the first call on that workspace
+ * (every call leaves them zero). */
+#define FDR_WEIGHT_ZSCORE 0
+#define FDR_WEIGHT_CENTERED_RANK 1
+#define FDR_WEIGHT_MOMENTS 2
+int64_t fdr_fd_grad_fused_workspace_bytes(int32_t n_dirs, int32_t lanes_per_dir, int64_t n_params, int32_t mode);
+int64_t fdr_fd_grad_fused_counter_bytes(int32_t n_dirs, int64_t n_params);
+int fdr_fd_grad_fused(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx_local, int32_t n_dirs,
+                      int64_t n_params, const double* rewards_all, int32_t n_all, double policy_reward, int32_t lane_lo,
+                      const int8_t* sign_local, const double* norm2_local, int32_t lanes_per_dir, float sigma,
+                      int32_t mode, double* out, void* workspace, int64_t workspace_bytes, fdr_stream stream);
+/* The whole single-process FD step (FiniteDifferences.step, learner/finite_differences.py:24-64, with DSGD
+ * dynamic_sgd.py:19-39) in two launches: fdr_fd_grad_fused (mode ZSCORE or CENTERED_RANK over all n_all =
+ * n_dirs * lanes_per_dir lanes) writing g [P] and each column block's sum fl32(-g)^2, then the DSGD update of
+ * theta as fdr_dsgd_step (one workgroup per 256 parameters).  theta_hist [P] (nullable) receives the updated
+ * theta (the learner's policy_history entry, finite_differences.py:75-78) without a separate copy.
+ * out = [||d theta||, ||grad||].  workspace as fdr_fd_grad_fused. */
+int fdr_fd_step(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx_local, int32_t n_dirs,
+                int64_t n_params, const double* rewards_all, int32_t n_all, double policy_reward,
+                const int8_t* sign_local, const double* norm2_local, int32_t lanes_per_dir, float sigma, int32_t mode,
+                float* theta, double lr, double lr_scale, double* g, float* theta_hist, double* out, void* workspace,
+                int64_t workspace_bytes, fdr_stream stream);
+/* The centred-rank weights alone: w [n_local] f64 for lanes [lane_lo, lane_lo + n_local) of rewards_all. */
+int fdr_rank_weights(fdr_ctx* ctx, const double* rewards_all, int32_t n_all, int32_t lane_lo, int32_t n_local,
+                     double* w, fdr_stream stream);
+
 /* ---- delayed returns: lambda with policy drift (learner/finite_differences.py:66-73, 80-114) -----
  * Return i's perturbation lambda_i = fl32(sign_i * fl32(sigma * table[idx_i + p]) + D[slot_i][p]),
  * D = drift [n_slots, P] f32 (dist_map: theta of the return's epoch minus the current theta;
@@ -220,6 +263,13 @@ int64_t fdr_dsgd_workspace_bytes(int64_t n_params);
 int fdr_dsgd_step(fdr_ctx* ctx, float* theta, const double* g, int64_t n_params, double lr,
                   double lr_scale, double* out, void* workspace, int64_t workspace_bytes,
                   fdr_stream stream);
+
+/* DSGD from a gradient or from the summed moments of FDR_WEIGHT_MOMENTS (src_is_moments = 1: g = (A - m B) /
+ * sd with m, sd from [sum r' | sum r'^2 | n]; sd == 0 -> g = A, as standardize_arr; g is written to g_out).
+ * P <= 65536: one fused launch (norm + update + ||d theta||).  out, workspace as fdr_dsgd_step. */
+int fdr_dsgd_step_ex(fdr_ctx* ctx, float* theta, const double* src, int32_t src_is_moments, int64_t n_params,
+                     double lr, double lr_scale, double* g_out, double* out, void* workspace, int64_t workspace_bytes,
+                     fdr_stream stream);
 
 /* ---- strategy distances / novelty (utils/math_helpers.py:147-222, strategy/) -----------------
  * strategies [n, Z, D] f32 = get_strategy over the Z probe states for n policies (e.g. every

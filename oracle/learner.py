@@ -57,6 +57,39 @@ def fd_gradient(table, P, idx, sign, rewards, policy_reward, sigma, drift=None):
     return g, z
 
 
+def centred_ranks(x):
+    """Centred-rank weights (build extension; the standard ES transform -- the reference's weighting is the
+    z-score): rank of x_i among all returns, ties broken by index (stable sort), / (n - 1) - 0.5."""
+    x = np.asarray(x, dtype=np.float64)
+    n = x.size
+    r = np.empty(n, dtype=np.float64)
+    r[np.argsort(x, kind="stable")] = np.arange(n)
+    return r / (n - 1) - 0.5 if n > 1 else np.zeros(n)
+
+
+def fd_gradient_weights(table, P, idx, sign, weights, sigma):
+    """g = sum_i w_i v_i for given per-return weights (the centred-rank form of fd_gradient)."""
+    V, _ = perturbation_vectors(table, P, idx, sign, sigma)
+    return np.dot(np.asarray(weights, np.float64), V)
+
+
+def fd_moments(table, P, idx, sign, rewards, policy_reward, sigma):
+    """One rank's share of the one-collective z-score step: [A | B | sum r' | sum r'^2 | n] with
+    r' = r - policy_reward, A = sum r'_i v_i, B = sum v_i (f64)."""
+    V, _ = perturbation_vectors(table, P, idx, sign, sigma)
+    r = np.subtract(rewards, policy_reward).astype(np.float64)
+    return np.concatenate([np.dot(r, V), V.astype(np.float64).sum(0), [r.sum(), (r * r).sum(), float(r.size)]])
+
+
+def grad_from_moments(mom, P):
+    """g = (A - m B) / sd from summed moments (sd == 0: A, as standardize returns its input unchanged)."""
+    A, B = mom[:P], mom[P:2 * P]
+    s, q, n = mom[2 * P:2 * P + 3]
+    m = s / n
+    var = max(q / n - m * m, 0.0)
+    return A if var == 0 else (A - m * B) / np.sqrt(var)
+
+
 def dsgd_step(theta, g, lr, omega=0.0, omega_min=0.0, omega_max=1.0, min_scale=0.23, max_scale=1.0):
     theta = torch.as_tensor(np.asarray(theta, dtype=np.float32)).clone()
     P = theta.numel()

@@ -88,3 +88,44 @@ def test_two_rank_gradient_matches_single_process(tmp_path, world):
     # every rank holds the identical reduced gradient -> replicated DSGD stays in lock-step
     assert np.array_equal(np.load(os.path.join(str(tmp_path), "g0.npy")),
                           np.load(os.path.join(str(tmp_path), "g1.npy")))
+
+
+def _rank_main_moments(rank, world, port, out_dir):
+    """The one-collective z-score protocol (FiniteDifferences._step_batch, sharded): every rank reduces its lanes
+    to [A | B | sum r' | sum r'^2 | n], ONE all-reduce sums them, g = (A - m B) / sd."""
+    sys.path[:0] = [REPO, PKG]
+    import torch.distributed as dist
+    from fdr import dist as fdist
+    from oracle import learner as olearn
+    from oracle import noise as onoise
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    P, D, sigma = 1000, 37, 0.02
+    t = onoise.NoiseTable(1 << 16, P, 5)
+    idx = t.sample_indices(D)
+    lidx = np.repeat(idx, 2)
+    sign = np.tile(np.array([1, -1], np.int8), D)
+    rewards = np.random.RandomState(3).randn(2 * D) * 7 + 40      # a mean far from 0: cancellation check
+    lo, hi = fdist.lane_range(D, 2, world, rank)
+    mom = torch.as_tensor(olearn.fd_moments(t.table, P, lidx[lo:hi], sign[lo:hi], rewards[lo:hi], 0.5, sigma))
+    fdist.allreduce_grad(mom)                                      # the step's only collective
+    np.save(os.path.join(out_dir, "g%d.npy" % rank), olearn.grad_from_moments(mom.numpy(), P))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_one_collective_moments_gradient_matches_two_collective(tmp_path, world):
+    port = _free_port()
+    mp.spawn(_rank_main_moments, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    from oracle import learner as olearn
+    from oracle import noise as onoise
+    P, D = 1000, 37
+    t = onoise.NoiseTable(1 << 16, P, 5)
+    idx = t.sample_indices(D)
+    lidx = np.repeat(idx, 2)
+    sign = np.tile(np.array([1, -1], np.int8), D)
+    rewards = np.random.RandomState(3).randn(2 * D) * 7 + 40
+    g_ref, _ = olearn.fd_gradient(t.table, P, lidx, sign, rewards, 0.5, 0.02)   # all-gather + z-score form
+    for r in range(world):
+        g = np.load(os.path.join(str(tmp_path), "g%d.npy" % r))
+        assert np.linalg.norm(g - g_ref) / np.linalg.norm(g_ref) <= 1e-12
