@@ -100,36 +100,115 @@ static int lanes_args(const fdr_lanes_desc* l, int n_lanes, int64_t P, LanesArgs
 
 using namespace fdr;
 
+// fdr_ctx: one engine context per device (fdr::Context: rollout kernel selection, Impala phase profiling, replay
+// GEMM switch, debug clocks).  NULL = the process-wide default context.
 struct fdr_ctx {
-  int device;
+  fdr::Context c;
 };
+
+namespace fdr {
+Context& default_context() {
+  static Context* d = [] {
+    Context* c = new Context();
+    const char* e = getenv("FDR_ROLLOUT");
+    c->rollout_impl = !e ? FDR_ROLLOUT_AUTO
+                         : strcmp(e, "single") == 0 ? FDR_ROLLOUT_SINGLE
+                                                    : strcmp(e, "pair") == 0 ? FDR_ROLLOUT_PAIR : FDR_ROLLOUT_AUTO;
+    return c;
+  }();
+  return *d;
+}
+
+int context_cus(const Context& c) {
+  if (c.cus > 0) return c.cus;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus = 256;
+  return cus;
+}
+}  // namespace fdr
+
+// The context of a call: ctx, or the default one; a ctx is bound to its device (the caller's current device
+// must be that device -- its stream belongs to it).
+static int resolve(fdr_ctx* ctx, Context** out) {
+  if (!ctx) {
+    *out = &default_context();
+    return FDR_OK;
+  }
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess) return set_error(FDR_ERR_HIP, "hipGetDevice failed");
+  if (dev != ctx->c.device) {
+    char msg[96];
+    snprintf(msg, sizeof(msg), "fdr_ctx belongs to device %d, the current device is %d", ctx->c.device, dev);
+    return set_error(FDR_ERR_INVALID, msg);
+  }
+  *out = &ctx->c;
+  return FDR_OK;
+}
+
+#define FDR_CTX(ctx, C)          \
+  Context* C = nullptr;          \
+  {                              \
+    const int rc_ = resolve(ctx, &C); \
+    if (rc_) return rc_;         \
+  }                              \
+  (void)C
 
 extern "C" {
 
-const char* fdr_version(void) { return "fdr 0.1 gfx950"; }
+const char* fdr_version(void) { return "fdr 0.2 gfx950"; }
 const char* fdr_last_error(void) { return g_err.c_str(); }
-int fdr_rollout_set_impl(int32_t impl) { return fdr::set_rollout_impl(impl); }
+
+static int set_impl(Context& c, int32_t impl) {
+  if (impl != FDR_ROLLOUT_PAIR && impl != FDR_ROLLOUT_SINGLE && impl != FDR_ROLLOUT_AUTO)
+    return set_error(FDR_ERR_INVALID, "unknown rollout impl");
+  c.rollout_impl = impl;
+  return FDR_OK;
+}
+int fdr_rollout_set_impl(int32_t impl) { return set_impl(default_context(), impl); }
+int fdr_ctx_set_rollout_impl(fdr_ctx* ctx, int32_t impl) { return set_impl(ctx ? ctx->c : default_context(), impl); }
+int fdr_ctx_set_replay_gemm(fdr_ctx* ctx, int32_t on) {
+  (ctx ? ctx->c : default_context()).replay_gemm = on != 0;
+  return FDR_OK;
+}
+int fdr_ctx_impala_profile(fdr_ctx* ctx, int32_t enable) { return impala::set_profile(ctx ? ctx->c : default_context(), enable); }
+int fdr_ctx_impala_profile_read(fdr_ctx* ctx, double* ms) {
+  if (!ms) return set_error(FDR_ERR_INVALID, "NULL pointer");
+  return impala::read_profile(ctx ? ctx->c : default_context(), ms);
+}
+int fdr_ctx_impala_debug_clock(fdr_ctx* ctx, uint64_t* buf) {
+  (ctx ? ctx->c : default_context()).debug_clock = buf;
+  return FDR_OK;
+}
 
 int fdr_ctx_create(int device, fdr_ctx** out) {
   if (!out) return set_error(FDR_ERR_INVALID, "out is NULL");
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
     return set_error(FDR_ERR_HIP, "no such HIP device");
-  *out = new fdr_ctx{device};
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess)
+    return set_error(FDR_ERR_HIP, "hipDeviceGetAttribute failed");
+  fdr_ctx* c = new fdr_ctx();
+  c->c.device = device;
+  c->c.cus = cus;
+  c->c.rollout_impl = default_context().rollout_impl;  // FDR_ROLLOUT applies to new contexts too
+  *out = c;
   return FDR_OK;
 }
 
 int fdr_ctx_destroy(fdr_ctx* ctx) {
+  if (ctx) impala::destroy_profile(ctx->c.prof);
   delete ctx;
   return FDR_OK;
 }
 
-int fdr_ctx_device(const fdr_ctx* ctx) { return ctx ? ctx->device : -1; }
+int fdr_ctx_device(const fdr_ctx* ctx) { return ctx ? ctx->c.device : -1; }
 
 int fdr_perturb(fdr_ctx* ctx, const float* theta, int64_t n_params, const float* table,
                 int64_t table_size, const int64_t* idx, const int8_t* sign, int32_t n_lanes,
                 float sigma, float* out, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (!theta || !table || !idx || !out) return set_error(FDR_ERR_INVALID, "NULL pointer");
   if (n_params <= 0 || table_size < n_params || n_lanes < 0)
     return set_error(FDR_ERR_INVALID, "bad sizes");
@@ -141,7 +220,7 @@ int fdr_perturb(fdr_ctx* ctx, const float* theta, int64_t n_params, const float*
 int fdr_policy_forward(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_lanes_desc* lanes,
                        int32_t n_lanes, const float* x, float* out0, float* out1,
                        fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   PolicyKey k;
   int rc = policy_key(policy, &k);
   if (rc) return rc;
@@ -174,7 +253,7 @@ int fdr_rollout_states(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_en
 
 int fdr_obs_stats_merge(fdr_ctx* ctx, const float* mean, const float* m2, const int32_t* count, int32_t n, int32_t dim,
                         float* acc_mean, float* acc_m2, int64_t* acc_count, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (n < 0 || dim <= 0) return set_error(FDR_ERR_INVALID, "bad sizes");
   if ((n > 0 && (!mean || !m2 || !count)) || !acc_mean || !acc_m2 || !acc_count)
     return set_error(FDR_ERR_INVALID, "NULL pointer");
@@ -185,7 +264,7 @@ int fdr_rollout_ex(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_de
                    const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
                    const float* obs_mean, const float* obs_std, double* ret, double* ent, int32_t* steps,
                    double* norm2, const fdr_rollout_extras* extras, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   PolicyKey k;
   int rc = policy_key(policy, &k);
   if (rc) return rc;
@@ -244,14 +323,14 @@ int fdr_rollout_ex(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_de
       a.os_chance = extras->obs_chance;
     }
   }
-  return launch_rollout(k, env->kind, a, (hipStream_t)stream);
+  return launch_rollout(*C, k, env->kind, a, (hipStream_t)stream);
 }
 
 int fdr_fd_weights(fdr_ctx* ctx, const double* rewards_all, int32_t n_all, double policy_reward,
                    int32_t lane_lo, int32_t n_local, const int8_t* sign_local,
                    const double* norm2_local, int32_t lanes_per_dir, float sigma, double* coef,
                    fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (!rewards_all || !sign_local || !norm2_local || !coef)
     return set_error(FDR_ERR_INVALID, "NULL pointer");
   if (n_all <= 0 || lane_lo < 0 || n_local < 0 || lane_lo + n_local > n_all)
@@ -269,7 +348,7 @@ int64_t fdr_fd_grad_workspace_bytes(int32_t n_dirs, int64_t n_params) {
 int fdr_fd_grad(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx,
                 const double* coef, int32_t n_dirs, int64_t n_params, double* g, void* workspace,
                 int64_t workspace_bytes, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (!table || !g || n_params <= 0 || table_size < n_params || n_dirs < 0)
     return set_error(FDR_ERR_INVALID, "bad arguments");
   if (n_dirs == 0) {
@@ -286,7 +365,7 @@ int64_t fdr_dsgd_workspace_bytes(int64_t n_params) { return dsgd_workspace_bytes
 int fdr_dsgd_step(fdr_ctx* ctx, float* theta, const double* g, int64_t n_params, double lr,
                   double lr_scale, double* out, void* workspace, int64_t workspace_bytes,
                   fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (!theta || !g || !out || n_params <= 0) return set_error(FDR_ERR_INVALID, "bad arguments");
   return launch_dsgd_ex(theta, g, 0, n_params, lr, lr_scale, nullptr, out, workspace, workspace_bytes,
                         (hipStream_t)stream);
@@ -295,7 +374,7 @@ int fdr_dsgd_step(fdr_ctx* ctx, float* theta, const double* g, int64_t n_params,
 int fdr_dsgd_step_ex(fdr_ctx* ctx, float* theta, const double* src, int32_t src_is_moments, int64_t n_params,
                      double lr, double lr_scale, double* g_out, double* out, void* workspace, int64_t workspace_bytes,
                      fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (!theta || !src || !out || n_params <= 0) return set_error(FDR_ERR_INVALID, "bad arguments");
   return launch_dsgd_ex(theta, src, src_is_moments ? 1 : 0, n_params, lr, lr_scale, g_out, out, workspace,
                         workspace_bytes, (hipStream_t)stream);
@@ -336,7 +415,7 @@ int fdr_fd_grad_fused(fdr_ctx* ctx, const float* table, int64_t table_size, cons
                       int64_t n_params, const double* rewards_all, int32_t n_all, double policy_reward, int32_t lane_lo,
                       const int8_t* sign_local, const double* norm2_local, int32_t lanes_per_dir, float sigma,
                       int32_t mode, double* out, void* workspace, int64_t workspace_bytes, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   return fd_grad_fused_impl(table, table_size, idx_local, n_dirs, n_params, rewards_all, n_all, policy_reward, lane_lo,
                             sign_local, norm2_local, lanes_per_dir, sigma, mode, out, nullptr, 0.0, 0.0, nullptr,
                             nullptr, workspace, workspace_bytes, stream);
@@ -347,7 +426,7 @@ int fdr_fd_step(fdr_ctx* ctx, const float* table, int64_t table_size, const int6
                 const int8_t* sign_local, const double* norm2_local, int32_t lanes_per_dir, float sigma, int32_t mode,
                 float* theta, double lr, double lr_scale, double* g, float* theta_hist, double* out, void* workspace,
                 int64_t workspace_bytes, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (!theta || !g || !out) return set_error(FDR_ERR_INVALID, "NULL theta / g / out");
   if (mode == FDR_WEIGHT_MOMENTS) return set_error(FDR_ERR_INVALID, "fdr_fd_step takes z-score or centred-rank weights");
   if (n_all != n_dirs * lanes_per_dir) return set_error(FDR_ERR_INVALID, "fdr_fd_step is single-process: n_all = n_local");
@@ -358,7 +437,7 @@ int fdr_fd_step(fdr_ctx* ctx, const float* table, int64_t table_size, const int6
 
 int fdr_rank_weights(fdr_ctx* ctx, const double* rewards_all, int32_t n_all, int32_t lane_lo, int32_t n_local,
                      double* w, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (!rewards_all || !w || n_all <= 0 || lane_lo < 0 || n_local < 0 || lane_lo + n_local > n_all)
     return set_error(FDR_ERR_INVALID, "bad arguments");
   return launch_rank_weights(rewards_all, n_all, lane_lo, n_local, w, (hipStream_t)stream);
@@ -395,7 +474,7 @@ int fdr_impala_rollout(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lanes_d
                        int32_t n_lanes, uint64_t seed, int32_t jiggle, double* ret, double* ent,
                        int32_t* steps, double* norm2, int32_t* actions, float* probs, void* ws,
                        int64_t ws_bytes, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   impala::Layout L;
   int rc = impala_layout(d, &L);
   if (rc) return rc;
@@ -406,6 +485,7 @@ int fdr_impala_rollout(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lanes_d
   if (E != 1 && E != 2 && E != 4 && E != 8) return set_error(FDR_ERR_UNSUPPORTED, "envs_per_lane must be 1, 2, 4 or 8");
   if (d->episode_len <= 0 || d->episode_len >= (1 << 20)) return set_error(FDR_ERR_INVALID, "episode_len out of range");
   if (!ret || !ent || !steps) return set_error(FDR_ERR_INVALID, "NULL output");
+  c.ctx = C;
   c.layout = &L;
   c.n_lanes = n_lanes;
   c.envs = E;
@@ -436,7 +516,7 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* d, const float* thet
                        const float* frames, const float* reward, const float* notdone, float* h,
                        float* c, float* probs, float* feat, void* ws, int64_t ws_bytes,
                        fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   impala::Layout L;
   int rc = impala_layout(d, &L);
   if (rc) return rc;
@@ -468,7 +548,7 @@ int64_t fdr_impala_strategies_workspace_bytes(const fdr_impala_desc* d, int32_t 
 int fdr_impala_strategies(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lanes_desc* lanes, int32_t n_lanes,
                           int32_t n_states, const float* frames, const float* reward, float* h, float* c,
                           float* probs, void* ws, int64_t ws_bytes, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   impala::Layout L;
   int rc = impala_layout(d, &L);
   if (rc) return rc;
@@ -501,27 +581,15 @@ int fdr_impala_env_frames(uint64_t env_seed, int32_t n_act, int64_t env_id, int3
                                    (hipStream_t)stream);
 }
 
-int fdr_impala_profile(int32_t enable) {
-  impala::set_profile(enable);
-  return FDR_OK;
-}
-
-int fdr_impala_profile_read(double* ms) {
-  if (!ms) return set_error(FDR_ERR_INVALID, "NULL pointer");
-  return impala::read_profile(ms);
-}
-
-int fdr_impala_debug_clock(uint64_t* buf) {
-  impala::set_debug_clock(buf);
-  return FDR_OK;
-}
-
-int fdr_impala_set_replay_gemm(int32_t on) { return impala::set_replay_gemm(on); }
+int fdr_impala_profile(int32_t enable) { return fdr_ctx_impala_profile(nullptr, enable); }
+int fdr_impala_profile_read(double* ms) { return fdr_ctx_impala_profile_read(nullptr, ms); }
+int fdr_impala_debug_clock(uint64_t* buf) { return fdr_ctx_impala_debug_clock(nullptr, buf); }
+int fdr_impala_set_replay_gemm(int32_t on) { return fdr_ctx_set_replay_gemm(nullptr, on); }
 
 int fdr_strategy_distances(fdr_ctx* ctx, const float* strategies, int32_t n, const float* archive, int32_t n_archive,
                            int32_t n_states, int32_t dim, int32_t kind, double* dists, double* min_dist,
                            int32_t* argmin, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (n < 0 || n_archive <= 0 || n_states <= 0 || dim <= 0) return set_error(FDR_ERR_INVALID, "bad sizes");
   if (n > 0 && (!strategies || !archive)) return set_error(FDR_ERR_INVALID, "NULL pointer");
   if (kind != FDR_DIST_L2 && kind != FDR_DIST_TVD && kind != FDR_DIST_W2)
@@ -544,7 +612,7 @@ static int lambda_row(const float* table, int64_t table_size, const int64_t* idx
 int fdr_fd_lambda_norms(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx, const int8_t* sign,
                         const int32_t* slot, int32_t n, int64_t n_params, float sigma, const float* drift,
                         int32_t n_slots, double* norm2, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   LambdaRow R;
   int rc = lambda_row(table, table_size, idx, sign, slot, n, n_params, sigma, drift, n_slots, &R);
   if (rc) return rc;
@@ -556,7 +624,7 @@ int fdr_fd_grad_lambda(fdr_ctx* ctx, const float* table, int64_t table_size, con
                        const int32_t* slot, const double* coef, int32_t n, int64_t n_params, float sigma,
                        const float* drift, int32_t n_slots, double* g, void* ws, int64_t ws_bytes,
                        fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   LambdaRow R;
   int rc = lambda_row(table, table_size, idx, sign, slot, n, n_params, sigma, drift, n_slots, &R);
   if (rc) return rc;
@@ -569,7 +637,7 @@ int64_t fdr_bn_refresh_workspace_bytes(int32_t n) { return n < 0 ? -1 : bn_refre
 
 int fdr_bn_refresh(fdr_ctx* ctx, const fdr_policy_desc* policy, const float* theta, const float* x, int32_t n,
                    float momentum, float* bn_mean, float* bn_var, void* ws, int64_t ws_bytes, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (!policy || policy->kind != FDR_POLICY_DISCRETE || policy->hidden != kHidden)
     return set_error(FDR_ERR_UNSUPPORTED, "BN refresh is defined for the DiscretePolicy (hidden 64)");
   if (policy->n_in <= 0 || policy->n_in > 64) return set_error(FDR_ERR_UNSUPPORTED, "n_in must be in 1..64");
@@ -589,7 +657,7 @@ int64_t fdr_atari_workspace_bytes(const fdr_atari_desc* d, int32_t n_lanes) {
 int fdr_atari_rollout(fdr_ctx* ctx, const fdr_atari_desc* d, const fdr_lanes_desc* lanes, int32_t n_lanes,
                       uint64_t seed, int32_t jiggle, double* ret, double* ent, int32_t* steps, double* norm2,
                       int32_t* actions, float* probs, void* ws, int64_t ws_bytes, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (!d) return set_error(FDR_ERR_INVALID, "atari desc is NULL");
   const int64_t P = atari::num_params(d->n_act);
   if (P < 0) return set_error(FDR_ERR_UNSUPPORTED, "n_act must be in 1..32");
@@ -611,7 +679,7 @@ int64_t fdr_atari_forward_workspace_bytes(int32_t n_act, int32_t n) {
 
 int fdr_atari_forward(fdr_ctx* ctx, const fdr_atari_desc* d, const float* theta, int32_t n, const float* frames,
                       float* probs, float* feat, void* ws, int64_t ws_bytes, fdr_stream stream) {
-  (void)ctx;
+  FDR_CTX(ctx, C);
   if (!d) return set_error(FDR_ERR_INVALID, "atari desc is NULL");
   const int64_t P = atari::num_params(d->n_act);
   if (P < 0) return set_error(FDR_ERR_UNSUPPORTED, "n_act must be in 1..32");

@@ -209,6 +209,7 @@ struct Plan {  // workspace carve-up (byte offsets)
 Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16 = false);
 
 struct RolloutCall {
+  const Context* ctx;
   const Layout* layout;
   LanesArgs lanes;
   int n_lanes, envs, T, entropy, jiggle, fp16;
@@ -223,7 +224,6 @@ struct RolloutCall {
   float* probs;
 };
 int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t stream);
-int set_replay_gemm(int on);
 
 struct ForwardCall {
   const Layout* layout;
@@ -259,9 +259,9 @@ int64_t strategies_workspace_bytes(const Layout& L, int n_lanes, int n_states, b
 int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipStream_t stream);
 int launch_env_frames(uint64_t env_seed, int n_act, uint64_t env_id, int t0, int n, const int32_t* actions,
                       float* frames, float* reward, hipStream_t stream);
-void set_profile(int on);
-void set_debug_clock(uint64_t* buf);
-int read_profile(double* out3);
+int set_profile(Context& ctx, int on);
+int read_profile(Context& ctx, double* out3);
+void destroy_profile(Profile* p);
 int launch_forward(const ForwardCall& c, void* ws, int64_t ws_bytes, hipStream_t stream);
 
 }  // namespace impala

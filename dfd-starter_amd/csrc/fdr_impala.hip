@@ -889,9 +889,9 @@ __global__ void finish_kernel(int n_lanes, int envs, int T, int entropy, int jig
   }
 }
 
-// Opt-in phase timing (fdr_impala_profile): HIP events between the launches of the step loop, so
-// a caller (bench.py) can attribute the rollout's time to conv / core / replay kernels live.
-namespace {
+// Opt-in phase timing (fdr_ctx_impala_profile): HIP events between the launches of the step loop, so
+// a caller (bench.py) can attribute the rollout's time to conv / core / replay kernels live.  One
+// Profile per context.
 struct Profile {
   bool on = false;
   std::vector<hipEvent_t> ev;
@@ -905,36 +905,41 @@ struct Profile {
     return ev[used++];
   }
 };
-Profile g_prof;
-uint64_t* g_dbg = nullptr;
-}  // namespace
 
-void set_debug_clock(uint64_t* buf) { g_dbg = buf; }
+void destroy_profile(Profile* p) {
+  if (!p) return;
+  for (hipEvent_t e : p->ev) (void)hipEventDestroy(e);
+  delete p;
+}
 
-static void mark(hipStream_t s) {
-  if (g_prof.on) {
-    hipEvent_t e = g_prof.next();
+static void mark(Profile* p, hipStream_t s) {
+  if (p && p->on) {
+    hipEvent_t e = p->next();
     if (e) (void)hipEventRecord(e, s);
   }
 }
 
-void set_profile(int on) {
-  g_prof.on = on != 0;
-  g_prof.used = 0;
+int set_profile(Context& ctx, int on) {
+  if (!ctx.prof) ctx.prof = new Profile();
+  ctx.prof->on = on != 0;
+  ctx.prof->used = 0;
+  return FDR_OK;
 }
 
-int read_profile(double* out) {
+int read_profile(Context& ctx, double* out) {
   out[0] = out[1] = out[2] = 0.0;
-  const int need = 2 * g_prof.T + 1 + (g_prof.entropy ? g_prof.T : 0);
-  if (!g_prof.on || g_prof.used < need) return set_error(FDR_ERR_INVALID, "no profiled impala rollout");
-  if (hipEventSynchronize(g_prof.ev[need - 1]) != hipSuccess) return set_error(FDR_ERR_HIP, "event sync failed");
+  Profile* p = ctx.prof;
+  if (!p) return set_error(FDR_ERR_INVALID, "no profiled impala rollout");
+  const int need = 2 * p->T + 1 + (p->entropy ? p->T : 0);
+  if (!p->on || p->used < need) return set_error(FDR_ERR_INVALID, "no profiled impala rollout");
+  if (hipEventSynchronize(p->ev[need - 1]) != hipSuccess) return set_error(FDR_ERR_HIP, "event sync failed");
   auto ms = [](hipEvent_t a, hipEvent_t b) { float v = 0.f; (void)hipEventElapsedTime(&v, a, b); return (double)v; };
-  for (int t = 0; t < g_prof.T; ++t) {
-    out[0] += ms(g_prof.ev[2 * t], g_prof.ev[2 * t + 1]);
-    out[1] += ms(g_prof.ev[2 * t + 1], g_prof.ev[2 * t + 2]);
+  for (int t = 0; t < p->T; ++t) {
+    out[0] += ms(p->ev[2 * t], p->ev[2 * t + 1]);
+    out[1] += ms(p->ev[2 * t + 1], p->ev[2 * t + 2]);
   }
-  for (int t = 0; g_prof.entropy && t < g_prof.T; ++t)
-    out[2] += ms(g_prof.ev[2 * g_prof.T + t], g_prof.ev[2 * g_prof.T + t + 1]);
+  for (int t = 0; p->entropy && t < p->T; ++t)
+    out[2] += ms(p->ev[2 * p->T + t], p->ev[2 * p->T + t + 1]);
   return FDR_OK;
 }
 
@@ -1020,39 +1025,36 @@ __global__ __launch_bounds__(256) void lstm_xproj_kernel(Layout L, StepArgs a, i
     }
 }
 
-static bool g_replay_gemm = true;  // fdr_impala_set_replay_gemm (diagnostics / A-B)
-int set_replay_gemm(int on) {
-  g_replay_gemm = on != 0;
-  return FDR_OK;
-}
-
 template <int E>
-static int launch_steps(const Layout& L, StepArgs a, int entropy, hipStream_t stream) {
+static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int entropy, hipStream_t stream) {
   const int conv_grid = (a.n_lanes + 7) / 8 * 8 * a.envs;
   const bool h = a.hpack != nullptr;
-  g_prof.used = 0;
-  g_prof.T = a.T;
-  g_prof.entropy = entropy;
-  mark(stream);
+  Profile* prof = ctx.prof;
+  if (prof) {
+    prof->used = 0;
+    prof->T = a.T;
+    prof->entropy = entropy;
+  }
+  mark(prof, stream);
   for (int t = 0; t < a.T; ++t) {
     a.t = t;
     if (h)
       hipLaunchKernelGGL(conv_kernel_h, dim3(conv_grid), dim3(kHThreads), 0, stream, L, a);
     else
       hipLaunchKernelGGL(conv_kernel, dim3(conv_grid), dim3(kConvThreads), 0, stream, L, a);
-    mark(stream);
+    mark(prof, stream);
     if (h)
       hipLaunchKernelGGL((core_kernel_h<E, kRollout>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
     else
       hipLaunchKernelGGL((core_kernel<E, kRollout>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
-    mark(stream);
+    mark(prof, stream);
   }
   float* gx = const_cast<float*>(a.gx);
   a.gx = nullptr;
   if (entropy)
     for (int t0 = 0; t0 < a.T; t0 += kReplayChunk) {
       const int tc = std::min(kReplayChunk, a.T - t0);
-      if (g_replay_gemm && gx) {
+      if (ctx.replay_gemm && gx) {
         const dim3 grid(a.n_lanes, (tc * E + 63) / 64, kGates / 256);
         if (h)
           hipLaunchKernelGGL(lstm_xproj_kernel<true>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);
@@ -1067,7 +1069,7 @@ static int launch_steps(const Layout& L, StepArgs a, int entropy, hipStream_t st
           hipLaunchKernelGGL((core_kernel_h<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
         else
           hipLaunchKernelGGL((core_kernel<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
-        mark(stream);
+        mark(prof, stream);
       }
     }
   return check_launch("impala step kernels");
@@ -1103,7 +1105,7 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
   a.actions = c.actions;
   a.probs = c.probs;
   a.deterministic = c.lanes.deterministic;
-  a.dbg = g_dbg;
+  a.dbg = c.ctx->debug_clock;
   double* n2 = reinterpret_cast<double*>(w + p.n2);
 
   launch_pack<float>(L, c.lanes, const_cast<float*>(a.pack), n2, c.n_lanes, 0, stream);
@@ -1118,10 +1120,10 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
   int rc = check_launch("impala prep/init");
   if (rc) return rc;
   switch (c.envs) {
-    case 1: rc = launch_steps<1>(L, a, c.entropy, stream); break;
-    case 2: rc = launch_steps<2>(L, a, c.entropy, stream); break;
-    case 4: rc = launch_steps<4>(L, a, c.entropy, stream); break;
-    case 8: rc = launch_steps<8>(L, a, c.entropy, stream); break;
+    case 1: rc = launch_steps<1>(*c.ctx, L, a, c.entropy, stream); break;
+    case 2: rc = launch_steps<2>(*c.ctx, L, a, c.entropy, stream); break;
+    case 4: rc = launch_steps<4>(*c.ctx, L, a, c.entropy, stream); break;
+    case 8: rc = launch_steps<8>(*c.ctx, L, a, c.entropy, stream); break;
     default: return set_error(FDR_ERR_UNSUPPORTED, "envs_per_lane must be 1, 2, 4 or 8");
   }
   if (rc) return rc;

@@ -10,6 +10,23 @@ namespace fdr {
 int set_error(int code, const char* msg);
 int check_launch(const char* what);
 
+// Per-device engine state behind an fdr_ctx (include/fdr.h): the settings that were process-wide
+// globals before (rollout kernel selection, Impala phase profiling, replay GEMM switch, debug clocks).
+// A NULL ctx at the ABI means default_context(), the process-wide one (FDR_ROLLOUT read at first use).
+namespace impala {
+struct Profile;
+}
+struct Context {
+  int device = -1;      // -1: any (the default context follows the current device)
+  int cus = 0;          // compute units of `device` (0: query the current device)
+  int rollout_impl = 2; // FDR_ROLLOUT_AUTO
+  int replay_gemm = 1;
+  uint64_t* debug_clock = nullptr;
+  impala::Profile* prof = nullptr;  // owned, created on first enable
+};
+Context& default_context();
+int context_cus(const Context& c);
+
 struct PolicyKey {
   int n_in, n_act;
   bool discrete;
@@ -84,8 +101,7 @@ struct RolloutArgs {
 int launch_policy_forward(const PolicyKey& k, const LanesArgs& lanes, int n_lanes,
                           const float* bn_mean, const float* bn_var, const float* x, float* out0,
                           float* out1, hipStream_t stream);
-int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream);
-int set_rollout_impl(int impl);
+int launch_rollout(const Context& ctx, const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream);
 
 // Delayed-return perturbation rows (fdr_fd_lambda_norms / fdr_fd_grad_lambda), by value to kernels.
 int64_t bn_refresh_workspace_bytes(int n);

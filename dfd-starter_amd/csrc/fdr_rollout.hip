@@ -1170,44 +1170,22 @@ static void launch_pair(const RolloutArgs& args, hipStream_t stream) {
 }
 
 // Synthetic-env rollouts: rollout_pair_kernel (two lanes per wave) or rollout_kernel (one lane per
-// wave).  FDR_ROLLOUT_AUTO (default) takes the pair kernel once it puts >= 2 waves on every SIMD
-// (n_lanes >= 4 x SIMDs; measured DESIGN.md 3.0: below that the one-lane kernel's extra waves win);
-// FDR_ROLLOUT=pair|single|auto or fdr_rollout_set_impl overrides.  The Welford obs statistics and the
-// trap env always use rollout_kernel.
-static int g_rollout_impl = -1;
-static int rollout_impl() {
-  if (g_rollout_impl < 0) {
-    const char* e = getenv("FDR_ROLLOUT");
-    g_rollout_impl = !e ? FDR_ROLLOUT_AUTO
-                        : strcmp(e, "single") == 0 ? FDR_ROLLOUT_SINGLE
-                                                   : strcmp(e, "pair") == 0 ? FDR_ROLLOUT_PAIR : FDR_ROLLOUT_AUTO;
-  }
-  return g_rollout_impl;
-}
-static bool use_pair_kernel(int n_lanes) {
-  const int impl = rollout_impl();
-  if (impl != FDR_ROLLOUT_AUTO) return impl == FDR_ROLLOUT_PAIR;
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    cus = 256;
-  return n_lanes >= 4 * 4 * cus;  // 4 SIMDs per CU, 2 lanes x 2 waves per SIMD
+// wave), by the context's rollout_impl: FDR_ROLLOUT_AUTO (default) takes the pair kernel once it puts
+// >= 2 waves on every SIMD (n_lanes >= 4 x SIMDs; measured DESIGN.md 3.0: below that the one-lane kernel's
+// extra waves win).  The Welford obs statistics and the trap env always use rollout_kernel.
+static bool use_pair_kernel(const Context& ctx, int n_lanes) {
+  if (ctx.rollout_impl != FDR_ROLLOUT_AUTO) return ctx.rollout_impl == FDR_ROLLOUT_PAIR;
+  return n_lanes >= 4 * 4 * context_cus(ctx);  // 4 SIMDs per CU, 2 lanes x 2 waves per SIMD
 }
 
-int set_rollout_impl(int impl) {
-  if (impl != FDR_ROLLOUT_PAIR && impl != FDR_ROLLOUT_SINGLE && impl != FDR_ROLLOUT_AUTO)
-    return set_error(FDR_ERR_INVALID, "unknown rollout impl");
-  g_rollout_impl = impl;
-  return FDR_OK;
-}
-
-int launch_rollout(const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream) {
+int launch_rollout(const Context& ctx, const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream) {
   const dim3 grid((args.n_lanes + kLanesPerBlock - 1) / kLanesPerBlock), block(64 * kLanesPerBlock);
 #define FDR_ROLL(NIN, NA, DISC)                                                                 \
   if (k.n_in == NIN && k.n_act == NA && k.discrete == DISC) {                                   \
     if (Layout<NIN, NA, DISC>::P != k.n_params)                                                 \
       return set_error(FDR_ERR_INVALID, "n_params does not match the policy layout");           \
     if (env_kind == FDR_ENV_SYNTH) {                                                            \
-      if (use_pair_kernel(args.n_lanes) && !args.os_mean) {                                                 \
+      if (use_pair_kernel(ctx, args.n_lanes) && !args.os_mean) {                                            \
         launch_pair<NIN, NA, DISC>(args, stream);                                               \
         return check_launch("rollout_pair_kernel<synth>");                                      \
       }                                                                                         \

@@ -28,7 +28,9 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_atari_forward_workspace_bytes", "fdr_atari_forward", "fdr_rollout_set_impl",
            "fdr_impala_set_replay_gemm", "fdr_impala_strategies_workspace_bytes", "fdr_impala_strategies",
            "fdr_impala_env_frames", "fdr_fd_grad_fused_workspace_bytes", "fdr_fd_grad_fused_counter_bytes",
-           "fdr_fd_grad_fused", "fdr_rank_weights", "fdr_dsgd_step_ex", "fdr_fd_step")
+           "fdr_fd_grad_fused", "fdr_rank_weights", "fdr_dsgd_step_ex", "fdr_fd_step",
+           "fdr_ctx_set_rollout_impl", "fdr_ctx_set_replay_gemm", "fdr_ctx_impala_profile",
+           "fdr_ctx_impala_profile_read", "fdr_ctx_impala_debug_clock")
 
 
 class FDRError(RuntimeError):
@@ -106,6 +108,11 @@ def _load():
         "fdr_atari_forward_workspace_bytes": (I64, [I32, I32]),
         "fdr_atari_forward": (ctypes.c_int, [P, ctypes.POINTER(AtariDesc), P, I32, P, P, P, P, I64, P]),
         "fdr_rollout_set_impl": (ctypes.c_int, [I32]),
+        "fdr_ctx_set_rollout_impl": (ctypes.c_int, [P, I32]),
+        "fdr_ctx_set_replay_gemm": (ctypes.c_int, [P, I32]),
+        "fdr_ctx_impala_profile": (ctypes.c_int, [P, I32]),
+        "fdr_ctx_impala_profile_read": (ctypes.c_int, [P, P]),
+        "fdr_ctx_impala_debug_clock": (ctypes.c_int, [P, P]),
         "fdr_impala_set_replay_gemm": (ctypes.c_int, [I32]),
         "fdr_fd_weights": (ctypes.c_int, [P, P, I32, F64, I32, I32, P, P, I32, F32, P, P]),
         "fdr_fd_grad_workspace_bytes": (I64, [I32, I64]),

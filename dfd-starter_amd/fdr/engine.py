@@ -19,6 +19,66 @@ def _stream(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+class Context(object):
+    """One fdr_ctx (include/fdr.h): the engine state of one device -- rollout kernel selection, Impala phase
+    profiling, replay GEMM switch, debug clocks.  engine.context(device) holds the default one per device;
+    further contexts are independent (e.g. two rollout selections side by side in one process)."""
+
+    def __init__(self, device=None):
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        h = ctypes.c_void_p()
+        check(lib.fdr_ctx_create(int(dev.index), ctypes.byref(h)), "fdr_ctx_create")
+        self.handle = h
+
+    def set_rollout_impl(self, impl):
+        """"pair" | "single" | "auto" (FDR_ROLLOUT_*)."""
+        code = {"pair": _lib.FDR_ROLLOUT_PAIR, "single": _lib.FDR_ROLLOUT_SINGLE, "auto": _lib.FDR_ROLLOUT_AUTO}[impl]
+        check(lib.fdr_ctx_set_rollout_impl(self.handle, code), "fdr_ctx_set_rollout_impl")
+
+    def set_replay_gemm(self, on):
+        check(lib.fdr_ctx_set_replay_gemm(self.handle, 1 if on else 0), "fdr_ctx_set_replay_gemm")
+
+    def impala_profile(self, enable):
+        check(lib.fdr_ctx_impala_profile(self.handle, 1 if enable else 0), "fdr_ctx_impala_profile")
+
+    def impala_profile_read(self):
+        out = (ctypes.c_double * 3)()
+        check(lib.fdr_ctx_impala_profile_read(self.handle, ctypes.cast(out, ctypes.c_void_p)),
+              "fdr_ctx_impala_profile_read")
+        return tuple(out)
+
+    def impala_debug_clock(self, buf):
+        check(lib.fdr_ctx_impala_debug_clock(self.handle, None if buf is None else ctypes.c_void_p(buf.data_ptr())),
+              "fdr_ctx_impala_debug_clock")
+
+    def __del__(self):
+        try:
+            lib.fdr_ctx_destroy(self.handle)
+        except Exception:
+            pass
+
+
+_CTX = {}
+
+
+def context(device=None):
+    """The engine's context of `device` (created on first use)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    c = _CTX.get(dev)
+    if c is None:
+        c = _CTX[dev] = Context(dev)
+    return c
+
+
+def _c(device=None, ctx=None):
+    return (ctx if ctx is not None else context(device)).handle
+
+
 class PolicySpec(object):
     """Shape of a policy family (policies/discrete.py:34-48, policies/mujoco.py:32-41)."""
 
@@ -68,7 +128,7 @@ def perturb(theta, table, idx, sign, sigma):
     _check_dev(theta, table, idx, sign)
     n, P = idx.numel(), theta.numel()
     out = torch.empty((n, P), dtype=torch.float32, device=theta.device)
-    check(lib.fdr_perturb(None, _p(theta), P, _p(table), table.numel(), _p(idx), _p(sign), n,
+    check(lib.fdr_perturb(_c(theta.device), _p(theta), P, _p(table), table.numel(), _p(idx), _p(sign), n,
                           float(sigma), _p(out), _stream(theta.device)), "fdr_perturb")
     return out
 
@@ -81,7 +141,7 @@ def policy_forward(spec, lanes, n_lanes, x, bn_mean=None, bn_var=None):
     out0 = torch.empty((n_lanes, spec.n_act), dtype=torch.float32, device=dev)
     out1 = None if spec.kind == "discrete" else torch.empty_like(out0)
     pd = spec.desc(bn_mean, bn_var)
-    check(lib.fdr_policy_forward(None, ctypes.byref(pd), ctypes.byref(lanes), n_lanes, _p(x), _p(out0),
+    check(lib.fdr_policy_forward(_c(dev), ctypes.byref(pd), ctypes.byref(lanes), n_lanes, _p(x), _p(out0),
                                  _p(out1), _stream(dev)), "fdr_policy_forward")
     return out0 if out1 is None else (out0, out1)
 
@@ -94,7 +154,7 @@ class RolloutResult(object):
 
 
 def rollout(spec, env, lanes, n_lanes, seed, jiggle=True, obs_mean=None, obs_std=None,
-            bn_mean=None, bn_var=None, out=None, device=None, states=None, obs_stats=None):
+            bn_mean=None, bn_var=None, out=None, device=None, states=None, obs_stats=None, ctx=None):
     """fdr_rollout; fdr_rollout_ex when states (f32 [n_lanes, T, n_in] device tensor) is given or
     obs_stats = the per-step sampling chance (-> out.obs_mean / obs_m2 / obs_count per lane)."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -122,12 +182,12 @@ def rollout(spec, env, lanes, n_lanes, seed, jiggle=True, obs_mean=None, obs_std
             x.obs_mean, x.obs_m2, x.obs_count = out.obs_mean.data_ptr(), out.obs_m2.data_ptr(), \
                 out.obs_count.data_ptr()
             x.obs_chance = chance
-        check(lib.fdr_rollout_ex(None, ctypes.byref(pd), ctypes.byref(ed), ctypes.byref(lanes), n_lanes,
+        check(lib.fdr_rollout_ex(_c(dev, ctx), ctypes.byref(pd), ctypes.byref(ed), ctypes.byref(lanes), n_lanes,
                                  ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(obs_mean),
                                  _p(obs_std), _p(out.reward), _p(out.entropy), _p(out.timesteps),
                                  _p(out.norm2), ctypes.byref(x), _stream(dev)), "fdr_rollout_ex")
         return out
-    check(lib.fdr_rollout(None, ctypes.byref(pd), ctypes.byref(ed), ctypes.byref(lanes), n_lanes,
+    check(lib.fdr_rollout(_c(dev, ctx), ctypes.byref(pd), ctypes.byref(ed), ctypes.byref(lanes), n_lanes,
                           ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(obs_mean),
                           _p(obs_std), _p(out.reward), _p(out.entropy), _p(out.timesteps), _p(out.norm2),
                           _stream(dev)), "fdr_rollout")
@@ -140,7 +200,7 @@ def fd_weights(rewards_all, policy_reward, lane_lo, sign_local, norm2_local, lan
     n_dirs = n_local // lanes_per_dir
     if coef is None:
         coef = torch.empty(n_dirs, dtype=torch.float64, device=rewards_all.device)
-    check(lib.fdr_fd_weights(None, _p(rewards_all), rewards_all.numel(), float(policy_reward), int(lane_lo),
+    check(lib.fdr_fd_weights(_c(rewards_all.device), _p(rewards_all), rewards_all.numel(), float(policy_reward), int(lane_lo),
                              n_local, _p(sign_local), _p(norm2_local), int(lanes_per_dir), float(sigma),
                              _p(coef), _stream(rewards_all.device)), "fdr_fd_weights")
     return coef
@@ -179,7 +239,7 @@ def fd_grad_fused(table, idx_local, rewards_all, policy_reward, lane_lo, sign_lo
         out = torch.empty(n_out, dtype=torch.float64, device=dev)
     nb = lib.fdr_fd_grad_fused_workspace_bytes(n_dirs, int(lanes_per_dir), n_params, m)
     ws = _workspace("fused_%d" % m, nb, dev, zeroed=True)
-    check(lib.fdr_fd_grad_fused(None, _p(table), table.numel(), _p(idx_local), n_dirs, n_params, _p(rewards_all),
+    check(lib.fdr_fd_grad_fused(_c(dev), _p(table), table.numel(), _p(idx_local), n_dirs, n_params, _p(rewards_all),
                                 rewards_all.numel(), float(policy_reward), int(lane_lo), _p(sign_local), _p(norm2_local),
                                 int(lanes_per_dir), float(sigma), m, _p(out), _p(ws), ws.numel(), _stream(dev)),
           "fdr_fd_grad_fused")
@@ -202,7 +262,7 @@ def fd_step(table, idx_local, rewards, policy_reward, sign_local, norm2_local, l
         out = torch.empty(2, dtype=torch.float64, device=dev)
     nb = lib.fdr_fd_grad_fused_workspace_bytes(n_dirs, int(lanes_per_dir), P, m)
     ws = _workspace("fused_%d" % m, nb, dev, zeroed=True)
-    check(lib.fdr_fd_step(None, _p(table), table.numel(), _p(idx_local), n_dirs, P, _p(rewards), rewards.numel(),
+    check(lib.fdr_fd_step(_c(dev), _p(table), table.numel(), _p(idx_local), n_dirs, P, _p(rewards), rewards.numel(),
                           float(policy_reward), _p(sign_local), _p(norm2_local), int(lanes_per_dir), float(sigma), m,
                           _p(theta), float(lr), float(lr_scale), _p(g), _p(theta_hist), _p(out), _p(ws), ws.numel(),
                           _stream(dev)), "fdr_fd_step")
@@ -213,7 +273,7 @@ def rank_weights(rewards_all, lane_lo, n_local):
     """Centred-rank weights of lanes [lane_lo, lane_lo + n_local) over rewards_all (f64 [n_local])."""
     _check_dev(rewards_all)
     w = torch.empty(n_local, dtype=torch.float64, device=rewards_all.device)
-    check(lib.fdr_rank_weights(None, _p(rewards_all), rewards_all.numel(), int(lane_lo), int(n_local), _p(w),
+    check(lib.fdr_rank_weights(_c(rewards_all.device), _p(rewards_all), rewards_all.numel(), int(lane_lo), int(n_local), _p(w),
                                _stream(rewards_all.device)), "fdr_rank_weights")
     return w
 
@@ -226,7 +286,7 @@ def dsgd_step_ex(theta, src, moments, lr, lr_scale, g_out=None, out=None):
         out = torch.empty(2, dtype=torch.float64, device=dev)
     nb = lib.fdr_dsgd_workspace_bytes(theta.numel())
     ws = _workspace("dsgd", nb, dev)
-    check(lib.fdr_dsgd_step_ex(None, _p(theta), _p(src), 1 if moments else 0, theta.numel(), float(lr), float(lr_scale),
+    check(lib.fdr_dsgd_step_ex(_c(dev), _p(theta), _p(src), 1 if moments else 0, theta.numel(), float(lr), float(lr_scale),
                                _p(g_out), _p(out), _p(ws), ws.numel(), _stream(dev)), "fdr_dsgd_step_ex")
     return out
 
@@ -239,7 +299,7 @@ def fd_grad(table, idx_dirs, coef, n_params, g=None):
         g = torch.empty(n_params, dtype=torch.float64, device=dev)
     nb = lib.fdr_fd_grad_workspace_bytes(n_dirs, n_params)
     ws = _workspace("grad", nb, dev)
-    check(lib.fdr_fd_grad(None, _p(table), table.numel(), _p(idx_dirs), _p(coef), n_dirs, n_params, _p(g),
+    check(lib.fdr_fd_grad(_c(dev), _p(table), table.numel(), _p(idx_dirs), _p(coef), n_dirs, n_params, _p(g),
                           _p(ws), ws.numel(), _stream(dev)), "fdr_fd_grad")
     return g
 
@@ -252,7 +312,7 @@ def dsgd_step(theta, g, lr, lr_scale, out=None):
         out = torch.empty(2, dtype=torch.float64, device=dev)
     nb = lib.fdr_dsgd_workspace_bytes(theta.numel())
     ws = _workspace("dsgd", nb, dev)
-    check(lib.fdr_dsgd_step(None, _p(theta), _p(g), theta.numel(), float(lr), float(lr_scale), _p(out), _p(ws),
+    check(lib.fdr_dsgd_step(_c(dev), _p(theta), _p(g), theta.numel(), float(lr), float(lr_scale), _p(out), _p(ws),
                             ws.numel(), _stream(dev)), "fdr_dsgd_step")
     return out
 
@@ -288,7 +348,7 @@ class ImpalaSpec(object):
 
 
 def impala_rollout(spec, lanes, n_lanes, seed, jiggle=True, bn_mean=None, bn_var=None, record=False, out=None,
-                   device=None):
+                   device=None, ctx=None):
     """fdr_impala_rollout: returns RolloutResult with per-env [n_lanes*E] fields, norm2 per lane,
     plus .actions [n_lanes*E, T] / .probs [n_lanes*E, T, A] when record=True."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
@@ -306,7 +366,7 @@ def impala_rollout(spec, lanes, n_lanes, seed, jiggle=True, bn_mean=None, bn_var
     if nb < 0:
         raise ValueError("bad impala spec")
     ws = _workspace("impala", nb, dev)
-    check(lib.fdr_impala_rollout(None, ctypes.byref(d), ctypes.byref(lanes), n_lanes,
+    check(lib.fdr_impala_rollout(_c(dev, ctx), ctypes.byref(d), ctypes.byref(lanes), n_lanes,
                                  ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(out.reward),
                                  _p(out.entropy), _p(out.timesteps), _p(out.norm2), _p(out.actions), _p(out.probs),
                                  _p(ws), ws.numel(), _stream(dev)), "fdr_impala_rollout")
@@ -332,7 +392,7 @@ def impala_forward(spec, theta, frames, h, c, reward=None, notdone=None, bn_mean
     d = spec.desc(bn_mean, bn_var)
     nb = lib.fdr_impala_forward_workspace_bytes(spec.n_act, n, 1 if spec.fp16 else 0)
     ws = _workspace("impala_fwd", nb, dev)
-    check(lib.fdr_impala_forward(None, ctypes.byref(d), _p(theta), n, _p(frames), _p(reward), _p(notdone), _p(h),
+    check(lib.fdr_impala_forward(_c(dev), ctypes.byref(d), _p(theta), n, _p(frames), _p(reward), _p(notdone), _p(h),
                                  _p(c), _p(probs), _p(f), _p(ws), ws.numel(), _stream(dev)), "fdr_impala_forward")
     return (probs, f) if feat else probs
 
@@ -361,7 +421,7 @@ def impala_strategies(spec, lanes, n_lanes, frames, reward=None, h=None, c=None,
     if nb < 0:
         raise ValueError("bad impala spec")
     ws = _workspace("impala_strat", nb, dev)
-    check(lib.fdr_impala_strategies(None, ctypes.byref(d), ctypes.byref(lanes), n_lanes, Z, _p(frames), _p(reward),
+    check(lib.fdr_impala_strategies(_c(dev), ctypes.byref(d), ctypes.byref(lanes), n_lanes, Z, _p(frames), _p(reward),
                                     _p(h), _p(c), _p(probs), _p(ws), ws.numel(), _stream(dev)),
           "fdr_impala_strategies")
     return probs
@@ -383,15 +443,14 @@ def impala_env_frames(env_seed, n_act, env_id, t0, n, actions=None, device=None)
     return frames, reward
 
 
-def impala_profile(enable):
-    lib.fdr_impala_profile(1 if enable else 0)
+def impala_profile(enable, device=None):
+    """Phase timing of the device's Impala rollouts (its engine context)."""
+    context(device).impala_profile(enable)
 
 
-def impala_profile_read():
+def impala_profile_read(device=None):
     """(conv_ms, core_ms, replay_ms) summed over the last profiled fdr_impala_rollout (host sync)."""
-    out = (ctypes.c_double * 3)()
-    check(lib.fdr_impala_profile_read(ctypes.cast(out, ctypes.c_void_p)), "fdr_impala_profile_read")
-    return tuple(out)
+    return context(device).impala_profile_read()
 
 
 # ---- strategy distances / novelty (utils/math_helpers.py:147-222) ---------------------------------
@@ -411,7 +470,7 @@ def strategy_distances(strategies, archive, kind, full=False):
     mn = torch.empty(n, dtype=torch.float64, device=dev)
     am = torch.empty(n, dtype=torch.int32, device=dev)
     dd = torch.empty((n, H), dtype=torch.float64, device=dev) if full else None
-    check(lib.fdr_strategy_distances(None, _p(S), n, _p(B), H, Z, D, DIST_KINDS[kind], _p(dd), _p(mn), _p(am),
+    check(lib.fdr_strategy_distances(_c(dev), _p(S), n, _p(B), H, Z, D, DIST_KINDS[kind], _p(dd), _p(mn), _p(am),
                                      _stream(dev)), "fdr_strategy_distances")
     return (mn, am, dd) if full else (mn, am)
 
@@ -433,7 +492,7 @@ def obs_stats_merge(mean, m2, count, acc_mean, acc_m2, acc_count):
     """Fold per-lane Welford partials into the device accumulator (in place, lane order)."""
     _check_dev(mean, m2, count, acc_mean, acc_m2, acc_count)
     n, d = mean.shape
-    check(lib.fdr_obs_stats_merge(None, _p(mean), _p(m2), _p(count), n, d, _p(acc_mean), _p(acc_m2), _p(acc_count),
+    check(lib.fdr_obs_stats_merge(_c(mean.device), _p(mean), _p(m2), _p(count), n, d, _p(acc_mean), _p(acc_m2), _p(acc_count),
                                   _stream(mean.device)), "fdr_obs_stats_merge")
 
 
@@ -444,7 +503,7 @@ def fd_lambda_norms(table, idx, sign, slot, sigma, drift, n_params):
     n = idx.numel()
     n2 = torch.empty(n, dtype=torch.float64, device=table.device)
     ns = 0 if drift is None else drift.shape[0]
-    check(lib.fdr_fd_lambda_norms(None, _p(table), table.numel(), _p(idx), _p(sign), _p(slot), n, n_params,
+    check(lib.fdr_fd_lambda_norms(_c(table.device), _p(table), table.numel(), _p(idx), _p(sign), _p(slot), n, n_params,
                                   float(sigma), _p(drift), ns, _p(n2), _stream(table.device)), "fdr_fd_lambda_norms")
     return n2
 
@@ -459,7 +518,7 @@ def fd_grad_lambda(table, idx, sign, slot, coef, sigma, drift, n_params, g=None)
     ns = 0 if drift is None else drift.shape[0]
     nb = lib.fdr_fd_grad_workspace_bytes(n, n_params)
     ws = _workspace("grad", nb, dev)
-    check(lib.fdr_fd_grad_lambda(None, _p(table), table.numel(), _p(idx), _p(sign), _p(slot), _p(coef), n, n_params,
+    check(lib.fdr_fd_grad_lambda(_c(dev), _p(table), table.numel(), _p(idx), _p(sign), _p(slot), _p(coef), n, n_params,
                                  float(sigma), _p(drift), ns, _p(g), _p(ws), ws.numel(), _stream(dev)),
           "fdr_fd_grad_lambda")
     return g
@@ -472,7 +531,7 @@ def bn_refresh(spec, theta, x, bn_mean, bn_var, momentum=0.1):
     n = x.shape[0]
     pd = spec.desc(None, None)
     ws = _workspace("vbn", lib.fdr_bn_refresh_workspace_bytes(n), x.device)
-    check(lib.fdr_bn_refresh(None, ctypes.byref(pd), _p(theta), _p(x), n, float(momentum), _p(bn_mean), _p(bn_var),
+    check(lib.fdr_bn_refresh(_c(x.device), ctypes.byref(pd), _p(theta), _p(x), n, float(momentum), _p(bn_mean), _p(bn_var),
                              _p(ws), ws.numel(), _stream(x.device)), "fdr_bn_refresh")
 
 
@@ -512,7 +571,7 @@ def atari_rollout(spec, lanes, n_lanes, seed, jiggle=True, bn_mean=None, bn_var=
     d = spec.desc(bn_mean, bn_var)
     nb = lib.fdr_atari_workspace_bytes(ctypes.byref(d), n_lanes)
     ws = _workspace("atari", nb, dev)
-    check(lib.fdr_atari_rollout(None, ctypes.byref(d), ctypes.byref(lanes), n_lanes,
+    check(lib.fdr_atari_rollout(_c(dev), ctypes.byref(d), ctypes.byref(lanes), n_lanes,
                                 ctypes.c_uint64(seed & ((1 << 64) - 1)), 1 if jiggle else 0, _p(out.reward),
                                 _p(out.entropy), _p(out.timesteps), _p(out.norm2), _p(out.actions), _p(out.probs),
                                 _p(ws), ws.numel(), _stream(dev)), "fdr_atari_rollout")
@@ -528,6 +587,6 @@ def atari_forward(spec, theta, frames, bn_mean=None, bn_var=None, feat=False):
     f = torch.empty((n, 2592), dtype=torch.float32, device=dev) if feat else None
     d = spec.desc(bn_mean, bn_var)
     ws = _workspace("atari_fwd", lib.fdr_atari_forward_workspace_bytes(spec.n_act, n), dev)
-    check(lib.fdr_atari_forward(None, ctypes.byref(d), _p(theta), n, _p(frames), _p(probs), _p(f), _p(ws), ws.numel(),
+    check(lib.fdr_atari_forward(_c(dev), ctypes.byref(d), _p(theta), n, _p(frames), _p(probs), _p(f), _p(ws), ws.numel(),
                                 _stream(dev)), "fdr_atari_forward")
     return (probs, f) if feat else probs

@@ -84,13 +84,25 @@ typedef struct fdr_lanes_desc {
                            same numbers whichever GPU shard evaluates it */
 } fdr_lanes_desc;
 
-/* ---- context / errors ---------------------------------------------------------------- */
+/* ---- context / errors ----------------------------------------------------------------
+ * An fdr_ctx is the engine state of ONE device: the rollout kernel selection (fdr_ctx_set_rollout_impl),
+ * the Impala phase profiler, the entropy-replay GEMM switch and the debug clock buffer.  Every compute call
+ * takes a ctx; the caller's current HIP device must be the ctx's device (FDR_ERR_INVALID otherwise).  A ctx
+ * is not shared across threads without external locking; two contexts -- on one device or on two -- are
+ * independent.  ctx = NULL selects the process-wide default context (device-agnostic; FDR_ROLLOUT in the
+ * environment sets its initial rollout selection, and new contexts copy it). */
 const char* fdr_version(void);
 const char* fdr_last_error(void);
 typedef struct fdr_ctx fdr_ctx;
 int fdr_ctx_create(int device, fdr_ctx** out);
 int fdr_ctx_destroy(fdr_ctx* ctx);
 int fdr_ctx_device(const fdr_ctx* ctx);
+/* per-context settings (ctx = NULL: the default context) */
+int fdr_ctx_set_rollout_impl(fdr_ctx* ctx, int32_t impl);  /* FDR_ROLLOUT_* below */
+int fdr_ctx_set_replay_gemm(fdr_ctx* ctx, int32_t on);     /* see fdr_impala_set_replay_gemm */
+int fdr_ctx_impala_profile(fdr_ctx* ctx, int32_t enable);  /* see fdr_impala_profile */
+int fdr_ctx_impala_profile_read(fdr_ctx* ctx, double* ms);
+int fdr_ctx_impala_debug_clock(fdr_ctx* ctx, uint64_t* buf);
 
 /* ---- perturbation batch (worker/worker.py:26-30) ------------------------------------
  * out[l, p] = fl32(theta[p] + sign_l * fl32(fl32(sigma) * table[idx_l + p]))  (no FMA)   */
@@ -118,8 +130,9 @@ int fdr_rollout(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc*
                 const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,
                 const float* obs_mean, const float* obs_std, double* ret, double* ent,
                 int32_t* steps, double* norm2, fdr_stream stream);
-/* Rollout kernel selection for the synthetic env (process-wide; default from the FDR_ROLLOUT
- * environment variable: "pair", "single", else FDR_ROLLOUT_AUTO):
+/* Rollout kernel selection for the synthetic env (per context, fdr_ctx_set_rollout_impl; fdr_rollout_set_impl
+ * sets the default context's; default from the FDR_ROLLOUT environment variable: "pair", "single", else
+ * FDR_ROLLOUT_AUTO):
  *   FDR_ROLLOUT_PAIR    two lanes per wave (rollout_pair_kernel)
  *   FDR_ROLLOUT_SINGLE  one lane per wave (rollout_kernel); always used for the trap env and for
  *                       the Welford observation statistics of fdr_rollout_ex
@@ -384,7 +397,8 @@ int fdr_impala_strategies(fdr_ctx* ctx, const fdr_impala_desc* desc, const fdr_l
 int fdr_impala_env_frames(uint64_t env_seed, int32_t n_act, int64_t env_id, int32_t t0, int32_t n,
                           const int32_t* actions, float* frames, float* reward, fdr_stream stream);
 
-/* Opt-in phase timing of fdr_impala_rollout (process-wide, not thread-safe): when enabled, HIP
+/* Opt-in phase timing of fdr_impala_rollout (these four act on the default context; fdr_ctx_* above on one
+ * context; not thread-safe): when enabled, HIP
  * events are recorded between the step-loop launches; fdr_impala_profile_read waits for the last
  * profiled rollout and returns HOST ms[3] = summed conv-stack / core (fc+LSTM+head) / entropy-replay
  * kernel time.  Used by bench.py for the live roofline figure. */

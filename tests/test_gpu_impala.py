@@ -274,12 +274,12 @@ def test_replay_input_projection_gemm_bit_identical(engine, table, fp16):
     outs = []
     try:
         for on in (1, 0):
-            check(lib.fdr_impala_set_replay_gemm(on), "fdr_impala_set_replay_gemm")
+            engine.context().set_replay_gemm(on)
             out = engine.impala_rollout(spec, lanes, L, 11)
             torch.cuda.synchronize()
             outs.append(out.entropy.cpu().numpy().copy())
     finally:
-        check(lib.fdr_impala_set_replay_gemm(1), "fdr_impala_set_replay_gemm")
+        engine.context().set_replay_gemm(True)
     assert np.all(np.isfinite(outs[0])) and np.any(outs[0] != 0)
     np.testing.assert_array_equal(outs[0], outs[1])
 

@@ -18,6 +18,7 @@ from oracle import policies as opol
 
 pytestmark = pytest.mark.gpu
 
+IMPL_NAMES = {0: "pair", 1: "single", 2: "auto"}   # FDR_ROLLOUT_*
 SHAPES = {"trap": ("discrete", 2, 9), "cartpole": ("discrete", 4, 2), "cheetah": ("mujoco", 17, 6)}
 DEV = "cuda"
 
@@ -164,10 +165,10 @@ def test_rollout_pair_and_single_kernels_agree(eng, name, L, det, T):
     out = {}
     try:
         for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
-            check(lib.fdr_rollout_set_impl(impl), "fdr_rollout_set_impl")
+            eng.context().set_rollout_impl(IMPL_NAMES[impl])
             out[impl] = _rollout_case(eng, name, L, T, det, antithetic=L % 2 == 0, idx_seed=L)
     finally:
-        check(lib.fdr_rollout_set_impl(FDR_ROLLOUT_AUTO), "fdr_rollout_set_impl")
+        eng.context().set_rollout_impl("auto")
     for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
         res, (ref_ret, ref_ent, ref_steps, ref_n2) = out[impl]
         assert res.reward.numel() == L
@@ -205,7 +206,7 @@ def test_rollout_kernels_obs_norm_and_states_vs_oracle(eng, name):
     ref_states = ref[-1]
     try:
         for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
-            check(lib.fdr_rollout_set_impl(impl), "fdr_rollout_set_impl")
+            eng.context().set_rollout_impl(IMPL_NAMES[impl])
             for norm, rec in ((True, False), (False, True), (True, True)):
                 states = torch.empty((L, T, n_in), dtype=torch.float32, device=DEV) if rec else None
                 res = eng.rollout(spec, env, lanes, L, seed, obs_mean=dev(om) if norm else None,
@@ -220,7 +221,7 @@ def test_rollout_kernels_obs_norm_and_states_vs_oracle(eng, name):
                     S = states.cpu().numpy()
                     np.testing.assert_array_equal(S[:, 0], np.broadcast_to(ref_states[0, 0], S[:, 0].shape))
     finally:
-        check(lib.fdr_rollout_set_impl(FDR_ROLLOUT_AUTO), "fdr_rollout_set_impl")
+        eng.context().set_rollout_impl("auto")
 
 
 def test_rollout_reproducible_and_antithetic_norms(eng):
@@ -366,11 +367,11 @@ def test_full_size_properties(eng):
     # every lane: the auto-selected two-lanes-per-wave kernel against the one-lane kernel
     from fdr._lib import FDR_ROLLOUT_AUTO, FDR_ROLLOUT_SINGLE, check, lib
     try:
-        check(lib.fdr_rollout_set_impl(FDR_ROLLOUT_SINGLE), "fdr_rollout_set_impl")
+        eng.context().set_rollout_impl("single")
         res1 = eng.rollout(spec, env, lanes, L, 5)
         torch.cuda.synchronize()
     finally:
-        check(lib.fdr_rollout_set_impl(FDR_ROLLOUT_AUTO), "fdr_rollout_set_impl")
+        eng.context().set_rollout_impl("auto")
     np.testing.assert_allclose(ret, res1.reward.cpu().numpy(), rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(res.entropy.cpu().numpy(), res1.entropy.cpu().numpy(), rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(n2, res1.norm2.cpu().numpy(), rtol=1e-12)
@@ -446,3 +447,38 @@ def test_sharded_fd_weights_and_grad_sum_to_unsharded(eng, world):
     assert np.linalg.norm(g_sum - g_full) / np.linalg.norm(g_full) <= 1e-12
     g_ref, _ = olearn.fd_gradient(table, P, idx, sign, rew, 0.25, sigma)
     assert np.linalg.norm(g_full - g_ref) / np.linalg.norm(g_ref) <= 1e-5
+
+
+def test_two_contexts_hold_independent_rollout_selections(eng):
+    """fdr_ctx carries the rollout kernel selection: two contexts on one device, one set to the pair kernel and
+    one to the one-lane kernel, used alternately with no global state flipped, each reproduce (bitwise) the
+    kernel they select; the default context is untouched."""
+    from fdr import engine as E
+    name = "cheetah"
+    kind, n_in, n_act = SHAPES[name]
+    torch.manual_seed(124)
+    pol = opol.TorchPolicy(kind, n_in, n_act, seed=124)
+    theta = pol.get_flat()
+    P = theta.size
+    t, tab = table(P)
+    L = 64
+    idx = np.repeat(t.sample_indices(L // 2), 2)
+    sign = np.tile(np.array([1, -1], np.int8), L // 2)
+    from envs import SyntheticEnv
+    env = SyntheticEnv(n_in, n_act, False, 120, env_seed=0)
+    lanes = eng.lanes_desc(dev(theta), 0, tab, dev(idx, torch.int64), dev(sign, torch.int8), 0.02)
+    spec = eng.PolicySpec(kind, n_in, n_act, P)
+    ca, cb = E.Context(DEV), E.Context(DEV)
+    ca.set_rollout_impl("pair")
+    cb.set_rollout_impl("single")
+    outs = {}
+    for rep in range(2):
+        for name_, c in (("pair", ca), ("single", cb)):
+            r = eng.rollout(spec, env, lanes, L, 5, ctx=c)
+            outs.setdefault(name_, []).append(r.reward.cpu().numpy().copy())
+    for k in outs:
+        np.testing.assert_array_equal(outs[k][0], outs[k][1])
+    assert not np.array_equal(outs["pair"][0], outs["single"][0])     # different kernels: different sum order
+    np.testing.assert_allclose(outs["pair"][0], outs["single"][0], rtol=1e-4, atol=1e-4)
+    # the engine's own context of the device was never switched: auto (64 lanes -> one-lane kernel)
+    np.testing.assert_array_equal(eng.rollout(spec, env, lanes, L, 5).reward.cpu().numpy(), outs["single"][0])

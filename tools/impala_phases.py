@@ -42,11 +42,11 @@ def main():
     sign = torch.ones(args.lanes, dtype=torch.int8).cuda()
     lanes = engine.lanes_desc(theta, 0, table, idx, sign, 0.02)
     dbg = torch.zeros(64, dtype=torch.int64).cuda()
-    lib.fdr_impala_debug_clock(ctypes.c_void_p(dbg.data_ptr()))
+    engine.context().impala_debug_clock(dbg)
     spec = engine.ImpalaSpec(A, args.envs, 2, entropy=False, fp16=args.fp16)
     engine.impala_rollout(spec, lanes, args.lanes, 1)
     torch.cuda.synchronize()
-    lib.fdr_impala_debug_clock(None)
+    engine.context().impala_debug_clock(None)
     c = dbg.cpu().numpy().astype(np.int64)
     tot = c[32] - c[0]
     order = sorted(NAMES)
