@@ -113,6 +113,7 @@ Context& default_context() {
     const char* e = getenv("FDR_ROLLOUT");
     c->rollout_impl = !e ? FDR_ROLLOUT_AUTO
                          : strcmp(e, "single") == 0 ? FDR_ROLLOUT_SINGLE
+                         : strcmp(e, "wide") == 0   ? FDR_ROLLOUT_WIDE
                                                     : strcmp(e, "pair") == 0 ? FDR_ROLLOUT_PAIR : FDR_ROLLOUT_AUTO;
     return c;
   }();
@@ -160,7 +161,7 @@ const char* fdr_version(void) { return "fdr 0.2 gfx950"; }
 const char* fdr_last_error(void) { return g_err.c_str(); }
 
 static int set_impl(Context& c, int32_t impl) {
-  if (impl != FDR_ROLLOUT_PAIR && impl != FDR_ROLLOUT_SINGLE && impl != FDR_ROLLOUT_AUTO)
+  if (impl != FDR_ROLLOUT_PAIR && impl != FDR_ROLLOUT_SINGLE && impl != FDR_ROLLOUT_AUTO && impl != FDR_ROLLOUT_WIDE)
     return set_error(FDR_ERR_INVALID, "unknown rollout impl");
   c.rollout_impl = impl;
   return FDR_OK;

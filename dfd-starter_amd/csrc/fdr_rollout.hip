@@ -84,6 +84,14 @@ __device__ __forceinline__ void bn_fold(float w, float b, float rm, float rv, fl
   c = b - rm * a;
 }
 
+// Categorical entropy term p_n log2 p_n of a discrete action (p_n = p / tot, torch normalises probs;
+// the ln 2 scale is applied once in the epilogue).  Fast reciprocal and log2: the entropy is a reported
+// statistic (parity 1e-5), not an input to the trajectory; terms below 1e-30 contribute nothing.
+__device__ __forceinline__ float disc_entropy_term(float p, float tot) {
+  const float pn = p * __builtin_amdgcn_rcpf(tot);
+  return pn > 1e-30f ? pn * __builtin_amdgcn_logf(pn) : 0.f;
+}
+
 // ---------------------------------------------------------------------------------------------
 // One lane's policy, register resident.
 //
@@ -302,10 +310,79 @@ struct MlpLane {
     }
   }
 
+  // Layer 1 and the env's M s from register-resident operands (rollout_kernel<WIDE>): the broadcast
+  // input arrives through v_readlane (wave-uniform values), M row j is loop-invariant in VGPRs.
+  __device__ __forceinline__ float layer1_env_reg(const float (&xv)[NX], const float (&sv)[NX],
+                                                  const float (&mv)[NX], float& env) const {
+    static_assert(!kW1Lds, "register-input layer 1 needs W1 in VGPRs");
+    f2 acc0 = {b1, 0.f}, acc1 = {0.f, 0.f}, accm0 = {0.f, 0.f}, accm1 = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < NX / 4; ++q) {
+      acc0 = pk_fma(w1[2 * q], f2{xv[4 * q], xv[4 * q + 1]}, acc0);
+      accm0 = pk_fma(f2{mv[4 * q], mv[4 * q + 1]}, f2{sv[4 * q], sv[4 * q + 1]}, accm0);
+      acc1 = pk_fma(w1[2 * q + 1], f2{xv[4 * q + 2], xv[4 * q + 3]}, acc1);
+      accm1 = pk_fma(f2{mv[4 * q + 2], mv[4 * q + 3]}, f2{sv[4 * q + 2], sv[4 * q + 3]}, accm1);
+    }
+    const f2 am = accm0 + accm1, ah = acc0 + acc1;
+    env = am.x + am.y;
+    const float z = ah.x + ah.y;
+    if constexpr (DISC) {
+      return fmaf(fmaxf(z, 0.f), a1, c1);
+    } else {
+      return tanh_fast(z);
+    }
+  }
+
+  // this lane's W3 slice (the head's loop-invariant LDS tile chunks) into registers
+  __device__ __forceinline__ void head_weights(float (&w3)[16]) const {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const float4 w = tile[(kW1Chunks + m) * kWave];
+      w3[4 * m] = w.x;
+      w3[4 * m + 1] = w.y;
+      w3[4 * m + 2] = w.z;
+      w3[4 * m + 3] = w.w;
+    }
+  }
+
   // second hidden layer and the head: h = layer-1 output of unit j; returns the head
-  // pre-activation for output o = j & 15 (identical in the 4 rows).
+  // pre-activation for output o = j & 15 (identical in the 4 rows).  w3r: the head's W3 slice when the
+  // caller keeps it in registers (nullptr: read from the LDS tile each step).
   template <class Mark>
-  __device__ __forceinline__ float layers23(float h, Scratch* sc, int j, Mark&& mark) const {
+  __device__ __forceinline__ float layers23(float h, Scratch* sc, int j, Mark&& mark,
+                                            const float* w3r = nullptr) const {
+    const float h2 = layer2(h, sc, j);
+    mark(1, h2);
+    // h2[16q + i] sits in lane i of row q: DPP row_newbcast FMAs, no LDS round trip
+    float w3[16];
+    if (w3r) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) w3[i] = w3r[i];
+    } else {
+      head_weights(w3);
+    }
+    const float out = row_allreduce_sum(dot_row16(h2, w3)) + b3;
+    mark(2, out);
+    return out;
+  }
+
+  // Two-output head (discrete NA == 2, rollout_kernel<WIDE>): lane j multiplies its own unit h2[j] by
+  // w3c = (W3[0][j], W3[1][j]), keeps the product of output o = j & 1 and hands the other to its quad
+  // partner, then sums over the 32 lanes of its parity (row_ror 4, row_ror 8, quad xor 2, the 4-row
+  // permlane all-reduce): output o in every lane of parity o, 9 VALU instead of the 16-DPP-FMA dot.
+  __device__ __forceinline__ float head2(float h2, f2 w3c, float b3p, int j) const {
+    const f2 m = w3c * f2{h2, h2};
+    const bool odd = (j & 1) != 0;
+    const float keep = odd ? m.y : m.x, give = odd ? m.x : m.y;
+    float v = keep + dpp_mov<kDppQuadXor1>(give);
+    v += dpp_mov<kDppRowRor + 4>(v);
+    v += dpp_mov<kDppRowRor + 8>(v);
+    v += dpp_mov<kDppQuadXor2>(v);
+    return row_allreduce_sum(v) + b3p;
+  }
+
+  // second hidden layer: h = layer-1 output of unit j; returns unit j's activation
+  __device__ __forceinline__ float layer2(float h, Scratch* sc, int j) const {
     const int c = j & 7;
     sc->h1[j] = h;
     wave_lds_sync();
@@ -324,31 +401,18 @@ struct MlpLane {
     const float r0 = q0 + dpp_mov<kDppQuadXor2>(q2);
     const float r1 = q1 + dpp_mov<kDppQuadXor2>(q3);
     const float z = (r0 + dpp_mov<kDppQuadXor1>(r1)) + b2;
-    float h2;
     if constexpr (DISC) {
-      h2 = fmaf(fmaxf(z, 0.f), a2, c2);
+      return fmaf(fmaxf(z, 0.f), a2, c2);
     } else {
-      h2 = tanh_fast(z);
+      return tanh_fast(z);
     }
-    mark(1, h2);
-    // h2[16q + i] sits in lane i of row q: DPP row_newbcast FMAs, no LDS round trip
-    float w3[16];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const float4 w = tile[(kW1Chunks + m) * kWave];
-      w3[4 * m] = w.x;
-      w3[4 * m + 1] = w.y;
-      w3[4 * m + 2] = w.z;
-      w3[4 * m + 3] = w.w;
-    }
-    const float out = row_allreduce_sum(dot_row16(h2, w3)) + b3;
-    mark(2, out);
-    return out;
   }
 
-  // Discrete: softmax across the row (o = j & 15 < NA); returns p_o, 0 for o >= NA.
+  // Discrete: softmax across the row (o = j & 15 < NA); returns p_o, 0 for o >= NA.  kAll: every lane
+  // holds a logit (head2: output j & 1).
+  template <bool kAll = false>
   __device__ __forceinline__ float softmax(float logit, int j) const {
-    const bool valid = (j & 15) < NOUT;
+    const bool valid = kAll || (j & 15) < NOUT;
     const float v = valid ? logit : -FLT_MAX;
     const float mx = row16_max_n<NOUT>(v);
     const float e = valid ? expf(v - mx) : 0.f;
@@ -397,10 +461,18 @@ __global__ __launch_bounds__(64 * kLanesPerBlock) void policy_forward_kernel(
 // ---------------------------------------------------------------------------------------------
 // FEAT bit 0: record visited observations (fdr_rollout_states); bit 1: Welford obs statistics;
 // bit 2: observation normalisation (obs_mean / obs_std given)
-template <int NIN, int NA, bool DISC, int ENV, int FEAT>
-__global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(RolloutArgs a) {
+// WIDE (synthetic env, few lanes: <= 2 waves per SIMD): a 256-VGPR budget instead of 128, so the
+// step's loop invariants (M / K rows, the head's W3 slice) stay in registers; the policy input and env
+// state cross lanes by v_readlane instead of an LDS round trip (NIN <= 8); a discrete env's candidate
+// next states tanh(M s + K[:, a]) are formed for every action while the policy runs, so the action
+// only selects one.
+template <int NIN, int NA, bool DISC, int ENV, int FEAT, bool WIDE>
+__global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_kernel(RolloutArgs a) {
   using Lane = MlpLane<NIN, NA, DISC>;
   constexpr int NX = Lane::NX;
+  constexpr bool kRegIn = WIDE && ENV == FDR_ENV_SYNTH && !Lane::kW1Lds;
+  constexpr bool kCand = kRegIn && DISC && NA <= 4;
+  constexpr bool kHead2 = WIDE && DISC && NA == 2;
   // env rows [M[i] (NX) | K[i] (one column per action)], stride MKS (b128 rows)
   constexpr int NMK = NX + round4(NA);
   constexpr int MKS = NMK % 8 == 0 ? NMK + 4 : NMK;
@@ -409,7 +481,9 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
   __shared__ typename Lane::Scratch scratch[kLanesPerBlock];
   float* envMK = reinterpret_cast<float*>(env4);
 
-  const int j = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wv through readfirstlane: the compiler then treats the lane index (and det) as wave-uniform (SGPRs,
+  // scalar branches) instead of masking EXEC around the sampled / deterministic action paths
+  const int j = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = blockIdx.x * kLanesPerBlock + wv;
   if constexpr (ENV == FDR_ENV_SYNTH) {
     for (int e = threadIdx.x; e < NIN * MKS; e += blockDim.x) {  // padding columns zero (b128 row reads)
@@ -482,6 +556,29 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
     const uint64_t h = hash_ctr(key, ulane, (uint64_t)(t + ds), (uint64_t)dk);
     rbuf = DISC ? uniform24(h) : normal_bm(h);
   };
+  // WIDE: loop invariants in registers (M row ji, K row ji, the head's W3 slice)
+  float mreg[kRegIn ? NX : 1], kreg[WIDE ? NA : 1], w3reg[WIDE ? 16 : 1];
+  if constexpr (WIDE) {
+    if constexpr (ENV == FDR_ENV_SYNTH) {
+      const float* mr = envMK + ji * MKS;
+#pragma unroll
+      for (int k = 0; k < NA; ++k) kreg[k] = mr[NX + k];
+      if constexpr (kRegIn) {
+#pragma unroll
+        for (int k = 0; k < NX; ++k) mreg[k] = mr[k];
+      }
+    }
+    pl.head_weights(w3reg);
+  }
+  f2 w3c = {0.f, 0.f};  // head2: (W3[0][j], W3[1][j]) from lane (j >> 4, o) of the tile
+  float b3p = 0.f;
+  if constexpr (kHead2) {
+    const float* t0 = reinterpret_cast<const float*>(pl.tile - j + (Lane::kW1Chunks + ((j & 15) >> 2)) * kWave +
+                                                     (j >> 4) * 16);
+    w3c = f2{t0[j & 3], t0[4 + (j & 3)]};
+    const float b30 = readlane_f(pl.b3, 0), b31 = readlane_f(pl.b3, 1);
+    b3p = (j & 1) ? b31 : b30;
+  }
   const int zbase = 4 * (o < NA ? o : 0);  // ds_bpermute byte address of dim o in step 0 of a batch
   auto fetch_z = [&](int t) {
     if constexpr (DISC) return 0.f;
@@ -521,12 +618,28 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
     constexpr bool kSame = !DISC && !norm_obs;  // mujoco: policy input == env state
     const float* mrow = envMK + ji * MKS;
     float pre = 0.f;
+    float h1;
+    float cand[kCand ? NA : 1];  // discrete WIDE: next state for each action
+    if constexpr (kRegIn) {
+      // policy input and env state of lanes 0 .. NIN-1, wave-uniform through v_readlane
+      const float xin = j < NIN ? policy_input(s) : 0.f;
+      float xv[NX], sv[NX];
+#pragma unroll
+      for (int k = 0; k < NX; ++k) {
+        xv[k] = k < NIN ? readlane_f(xin, k) : (k == NIN ? 1.f : 0.f);
+        sv[k] = k < NIN ? (kSame ? xv[k] : readlane_f(s, k)) : 0.f;
+      }
+      h1 = pl.layer1_env_reg(xv, sv, mreg, pre);
+      if constexpr (kCand) {
+#pragma unroll
+        for (int i = 0; i < NA; ++i) cand[i] = tanh_fast(pre + kreg[i]);
+      }
+    } else {
     // policy input (and env state) broadcast through the wave's LDS scratch, then packed FMAs
     // against the lane's W1 row and M row (two MACs per instruction instead of one DPP FMA)
     sc->x[j] = j < NIN ? policy_input(s) : (j == NIN ? 1.f : 0.f);
     if constexpr (ENV == FDR_ENV_SYNTH && !kSame) sc->h1[j] = j < NIN ? s : 0.f;
     wave_lds_sync();
-    float h1;
     if constexpr (ENV == FDR_ENV_SYNTH) {
       // one pass over the input chunks: W1 row j against x, M row j against s (M's padding
       // columns are 0, so the bias column's 1 drops out of M s)
@@ -536,12 +649,21 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
       lds_bcast<NX>(sc->x, xb);
       h1 = pl.layer1(xb);
     }
+    }
     mark(0, h1);
-    const float y = pl.layers23(h1, sc, j, mark);
+    float y;
+    if constexpr (kHead2) {
+      const float h2 = pl.layer2(h1, sc, j);
+      mark(1, h2);
+      y = pl.head2(h2, w3c, b3p, j);
+      mark(2, y);
+    } else {
+      y = pl.layers23(h1, sc, j, mark, WIDE ? w3reg : nullptr);
+    }
     int act_d = 0;
     float act_c = 0.f;
     if constexpr (DISC) {
-      const float p = pl.softmax(y, j);
+      const float p = pl.template softmax<kHead2>(y, j);
       float pv[NA];
 #pragma unroll
       for (int i = 0; i < NA; ++i) pv[i] = readlane_f(p, i);
@@ -568,9 +690,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
         }
       }
       // Categorical(probs) entropy: probs normalised, log clamped (torch semantics)
-      const float pn = p / tot;
-      const float lg = pn > 0.f ? logf(pn) : -FLT_MAX;
-      eacc -= (j < NA) ? pn * lg : 0.f;
+      eacc -= (j < NA) ? disc_entropy_term(p, tot) : 0.f;
     } else {
       const float th = tanh_fast(y);
       const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
@@ -581,15 +701,21 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
     mark(3, DISC ? (float)act_d : act_c);
     // ---- env step ----
     if constexpr (ENV == FDR_ENV_SYNTH) {
-      if constexpr (DISC) {
-        pre += mrow[NX + act_d];
-      } else {
-        float kr[NA];
+      if constexpr (kCand) {
+        s = cand[0];
 #pragma unroll
-        for (int m = 0; m < NA; ++m) kr[m] = mrow[NX + m];
-        dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in lane m of every row
+        for (int i = 1; i < NA; ++i) s = act_d == i ? cand[i] : s;
+      } else {
+        if constexpr (DISC) {
+          pre += mrow[NX + act_d];
+        } else {
+          float kr[NA];
+#pragma unroll
+          for (int m = 0; m < NA; ++m) kr[m] = WIDE ? kreg[m] : mrow[NX + m];
+          dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in lane m of every row
+        }
+        s = tanh_fast(pre);
       }
-      s = tanh_fast(pre);
       racc += (double)s;  // lane 0 holds the reward s'[0]; other lanes' sums are discarded
     } else {
       // custom_envs/simple_trap_env: node.py:9-14, tile_map.py:11-23, environment.py:33-48
@@ -610,7 +736,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, 4) void rollout_kernel(Rollout
 #endif
 
   // ---- epilogue ----
-  if constexpr (!DISC) eacc *= 0.693147180559945309f;
+  eacc *= 0.693147180559945309f;  // log2 -> ln (both kinds)
   const double esum = wave_sum((j < NA) ? (double)eacc : 0.0);
   if (j == 0) {
     double r = racc;
@@ -1046,9 +1172,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
           act_d += cs <= target ? 1 : 0;
         }
       }
-      const float pn = p / tot;
-      const float lg = pn > 0.f ? logf(pn) : -FLT_MAX;
-      eacc -= (o < NA) ? pn * lg : 0.f;
+      eacc -= (o < NA) ? disc_entropy_term(p, tot) : 0.f;
       pre += mrow[NX + act_d];
     } else {
       const float th = tanh_fast(y);
@@ -1102,7 +1226,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
   if (blockIdx.x == 0 && threadIdx.x == 0)
     for (int k = 0; k < 5; ++k) g_phase_stamps[k] = ph_acc[k];
 #endif
-  if constexpr (!DISC) eacc *= 0.693147180559945309f;
+  eacc *= 0.693147180559945309f;  // log2 -> ln (both kinds)
   double esum = (t < NA) ? (double)eacc : 0.0;  // row 0 of the half: one copy of each output
 #pragma unroll
   for (int m = 16; m >= 1; m >>= 1) esum += __shfl_xor(esum, m, kWave);
@@ -1145,11 +1269,11 @@ int launch_policy_forward(const PolicyKey& k, const LanesArgs& lanes, int n_lane
   return set_error(FDR_ERR_UNSUPPORTED, "no compiled policy_forward for this (kind, n_in, n_act)");
 }
 
-template <int NIN, int NA, bool DISC, int ENV>
+template <int NIN, int NA, bool DISC, int ENV, bool WIDE = false>
 static void launch_feat(const RolloutArgs& args, dim3 grid, dim3 block, hipStream_t stream) {
   const int feat = (args.states ? 1 : 0) | (args.os_mean ? 2 : 0) | (args.obs_mean ? 4 : 0);
 #define FDR_FEAT_CASE(F) \
-  case F: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, F>), grid, block, 0, stream, args); break;
+  case F: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, F, WIDE>), grid, block, 0, stream, args); break;
   switch (feat) {
     FDR_FEAT_CASE(0) FDR_FEAT_CASE(1) FDR_FEAT_CASE(2) FDR_FEAT_CASE(3)
     FDR_FEAT_CASE(4) FDR_FEAT_CASE(5) FDR_FEAT_CASE(6) FDR_FEAT_CASE(7)
@@ -1178,6 +1302,14 @@ static bool use_pair_kernel(const Context& ctx, int n_lanes) {
   return n_lanes >= 4 * 4 * context_cus(ctx);  // 4 SIMDs per CU, 2 lanes x 2 waves per SIMD
 }
 
+// The register-rich one-lane kernel (rollout_kernel<WIDE>) when its 2-waves-per-SIMD occupancy holds
+// every lane in one pass (n_lanes <= 8 x CUs): below that the step is a latency chain, and VGPR room
+// buys a shorter one.
+static bool use_wide_kernel(const Context& ctx, int n_lanes) {
+  if (ctx.rollout_impl != FDR_ROLLOUT_AUTO) return ctx.rollout_impl == FDR_ROLLOUT_WIDE;
+  return n_lanes <= 2 * 4 * context_cus(ctx);
+}
+
 int launch_rollout(const Context& ctx, const PolicyKey& k, int env_kind, const RolloutArgs& args, hipStream_t stream) {
   const dim3 grid((args.n_lanes + kLanesPerBlock - 1) / kLanesPerBlock), block(64 * kLanesPerBlock);
 #define FDR_ROLL(NIN, NA, DISC)                                                                 \
@@ -1188,6 +1320,10 @@ int launch_rollout(const Context& ctx, const PolicyKey& k, int env_kind, const R
       if (use_pair_kernel(ctx, args.n_lanes) && !args.os_mean) {                                            \
         launch_pair<NIN, NA, DISC>(args, stream);                                               \
         return check_launch("rollout_pair_kernel<synth>");                                      \
+      }                                                                                         \
+      if (use_wide_kernel(ctx, args.n_lanes)) {                                                 \
+        launch_feat<NIN, NA, DISC, FDR_ENV_SYNTH, true>(args, grid, block, stream);             \
+        return check_launch("rollout_kernel<synth, wide>");                                     \
       }                                                                                         \
       launch_feat<NIN, NA, DISC, FDR_ENV_SYNTH>(args, grid, block, stream);                     \
       return check_launch("rollout_kernel<synth>");                                             \

@@ -13,7 +13,7 @@ FDR_OK, FDR_ERR_INVALID, FDR_ERR_UNSUPPORTED, FDR_ERR_HIP, FDR_ERR_WORKSPACE = 0
 FDR_POLICY_DISCRETE, FDR_POLICY_MUJOCO = 0, 1
 FDR_ENV_SYNTH, FDR_ENV_TRAP = 0, 1
 FDR_DIST_L2, FDR_DIST_TVD, FDR_DIST_W2 = 0, 1, 2
-FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_AUTO = 0, 1, 2
+FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_AUTO, FDR_ROLLOUT_WIDE = 0, 1, 2, 3
 FDR_WEIGHT_ZSCORE, FDR_WEIGHT_CENTERED_RANK, FDR_WEIGHT_MOMENTS = 0, 1, 2
 
 EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy", "fdr_ctx_device",

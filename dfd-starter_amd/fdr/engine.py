@@ -34,8 +34,9 @@ class Context(object):
         self.handle = h
 
     def set_rollout_impl(self, impl):
-        """"pair" | "single" | "auto" (FDR_ROLLOUT_*)."""
-        code = {"pair": _lib.FDR_ROLLOUT_PAIR, "single": _lib.FDR_ROLLOUT_SINGLE, "auto": _lib.FDR_ROLLOUT_AUTO}[impl]
+        """"pair" | "single" | "wide" | "auto" (FDR_ROLLOUT_*)."""
+        code = {"pair": _lib.FDR_ROLLOUT_PAIR, "single": _lib.FDR_ROLLOUT_SINGLE, "auto": _lib.FDR_ROLLOUT_AUTO,
+                "wide": _lib.FDR_ROLLOUT_WIDE}[impl]
         check(lib.fdr_ctx_set_rollout_impl(self.handle, code), "fdr_ctx_set_rollout_impl")
 
     def set_replay_gemm(self, on):

@@ -136,11 +136,16 @@ int fdr_rollout(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc*
  *   FDR_ROLLOUT_PAIR    two lanes per wave (rollout_pair_kernel)
  *   FDR_ROLLOUT_SINGLE  one lane per wave (rollout_kernel); always used for the trap env and for
  *                       the Welford observation statistics of fdr_rollout_ex
- *   FDR_ROLLOUT_AUTO    the pair kernel when n_lanes >= 16 x CUs (two pair waves per SIMD), else single
- * Both compute the same episodes; sums are ordered differently (parity tolerances hold for both). */
+ *   FDR_ROLLOUT_WIDE    one lane per wave with a 256-VGPR budget (rollout_kernel<WIDE>): loop invariants
+ *                       in registers, readlane input broadcast, per-action candidate next states
+ *   FDR_ROLLOUT_AUTO    the pair kernel when n_lanes >= 16 x CUs (two pair waves per SIMD), wide when
+ *                       n_lanes <= 8 x CUs (every lane in one pass at 2 waves per SIMD), else single
+ * All compute the same episodes; sums are ordered differently (parity tolerances hold for each).
+ * "pair" / "single" / "wide" are also the FDR_ROLLOUT environment variable's values. */
 #define FDR_ROLLOUT_PAIR 0
 #define FDR_ROLLOUT_SINGLE 1
 #define FDR_ROLLOUT_AUTO 2
+#define FDR_ROLLOUT_WIDE 3
 int fdr_rollout_set_impl(int32_t impl);
 
 /* Same as fdr_rollout, and also writes every visited raw observation (before normalisation) to

@@ -18,8 +18,10 @@ from oracle import policies as opol
 
 pytestmark = pytest.mark.gpu
 
-IMPL_NAMES = {0: "pair", 1: "single", 2: "auto"}   # FDR_ROLLOUT_*
+IMPL_NAMES = {0: "pair", 1: "single", 2: "auto", 3: "wide"}   # FDR_ROLLOUT_*
 SHAPES = {"trap": ("discrete", 2, 9), "cartpole": ("discrete", 4, 2), "cheetah": ("mujoco", 17, 6)}
+# the other compiled rollout shapes (no golden vectors: oracle parity only)
+ROLL_SHAPES = dict(SHAPES, lunar=("discrete", 8, 4), hopper=("mujoco", 11, 3))
 DEV = "cuda"
 
 
@@ -113,7 +115,7 @@ def test_policy_forward_perturbed_lanes(eng, name):
 
 
 def _rollout_case(eng, name, L, T, det, seed=7, antithetic=True, idx_seed=None):
-    kind, n_in, n_act = SHAPES[name]
+    kind, n_in, n_act = ROLL_SHAPES[name]
     torch.manual_seed(124)
     pol = opol.TorchPolicy(kind, n_in, n_act, seed=124)
     theta = pol.get_flat()
@@ -156,36 +158,39 @@ def test_rollout_vs_oracle(eng, name, det):
 @pytest.mark.parametrize("name,L,det,T", [("cheetah", 13, False, 120), ("cheetah", 7, True, 120),
                                           ("cartpole", 13, False, 120), ("cartpole", 9, True, 120),
                                           ("cheetah", 64, False, 120), ("cheetah", 10, False, 123),
-                                          ("cheetah", 6, False, 3), ("cartpole", 6, False, 37)])
+                                          ("cheetah", 6, False, 3), ("cartpole", 6, False, 37),
+                                          ("lunar", 13, False, 90), ("lunar", 8, True, 40), ("hopper", 11, False, 70)])
 def test_rollout_pair_and_single_kernels_agree(eng, name, L, det, T):
-    """rollout_pair_kernel (two lanes per wave) and rollout_kernel (one lane per wave) against the
-    oracle and each other, incl. odd lane counts (a wave whose second half is idle) and episode lengths
-    that are not a multiple of the pair kernel's 5-step unroll (remainder loop)."""
-    from fdr._lib import FDR_ROLLOUT_AUTO, FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, check, lib
+    """rollout_pair_kernel (two lanes per wave), rollout_kernel (one lane per wave) and its register-rich
+    WIDE variant against the oracle and each other, incl. odd lane counts (a wave whose second half is
+    idle) and episode lengths that are not a multiple of the pair kernel's 5-step unroll (remainder loop)."""
+    from fdr._lib import FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_WIDE
     out = {}
     try:
-        for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
+        for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR, FDR_ROLLOUT_WIDE):
             eng.context().set_rollout_impl(IMPL_NAMES[impl])
             out[impl] = _rollout_case(eng, name, L, T, det, antithetic=L % 2 == 0, idx_seed=L)
     finally:
         eng.context().set_rollout_impl("auto")
-    for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
+    for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR, FDR_ROLLOUT_WIDE):
         res, (ref_ret, ref_ent, ref_steps, ref_n2) = out[impl]
         assert res.reward.numel() == L
         np.testing.assert_allclose(res.reward.cpu().numpy(), ref_ret, rtol=1e-4, atol=1e-4)
         np.testing.assert_allclose(res.entropy.cpu().numpy(), ref_ent, rtol=1e-5, atol=1e-5)
         assert np.array_equal(res.timesteps.cpu().numpy(), ref_steps)
         np.testing.assert_allclose(res.norm2.cpu().numpy(), ref_n2, rtol=1e-9, atol=0)
-    a, b = out[FDR_ROLLOUT_SINGLE][0], out[FDR_ROLLOUT_PAIR][0]
+    a, b, w = out[FDR_ROLLOUT_SINGLE][0], out[FDR_ROLLOUT_PAIR][0], out[FDR_ROLLOUT_WIDE][0]
     np.testing.assert_allclose(a.reward.cpu().numpy(), b.reward.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(a.reward.cpu().numpy(), w.reward.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(a.norm2.cpu().numpy(), w.norm2.cpu().numpy())
 
 
 @pytest.mark.parametrize("name", ["cheetah", "cartpole"])
 def test_rollout_kernels_obs_norm_and_states_vs_oracle(eng, name):
     """FEAT paths of both synthetic-env kernels (observation normalisation, visited states, both) against
-    the oracle, with the kernel forced (auto would pick the one-lane kernel at this lane count)."""
+    the oracle, with the kernel forced (auto would pick the wide one-lane kernel at this lane count)."""
     from envs import SyntheticEnv
-    from fdr._lib import FDR_ROLLOUT_AUTO, FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, check, lib
+    from fdr._lib import FDR_ROLLOUT_PAIR, FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_WIDE
     kind, n_in, n_act = SHAPES[name]
     torch.manual_seed(124)
     pol = opol.TorchPolicy(kind, n_in, n_act, seed=124)
@@ -205,7 +210,7 @@ def test_rollout_kernels_obs_norm_and_states_vs_oracle(eng, name):
                                 obs_std=osd, record_states=True)
     ref_states = ref[-1]
     try:
-        for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR):
+        for impl in (FDR_ROLLOUT_SINGLE, FDR_ROLLOUT_PAIR, FDR_ROLLOUT_WIDE):
             eng.context().set_rollout_impl(IMPL_NAMES[impl])
             for norm, rec in ((True, False), (False, True), (True, True)):
                 states = torch.empty((L, T, n_in), dtype=torch.float32, device=DEV) if rec else None
