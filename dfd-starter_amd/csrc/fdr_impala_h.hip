@@ -55,7 +55,32 @@ static_assert(kHLdsBytes <= 160 * 1024, "fp16 conv LDS");
 template <int CIN>
 struct KSteps {
   static constexpr int N = CIN == 3 ? 2 : (9 * CIN + 31) / 32;
+  // The last K-step of the Cin = 3 and Cin = 16 convs is mostly padding (taps 8 + zeros: 27 -> 64,
+  // 144 -> 160): it runs as v_mfma_f32_16x16x16_f16, K = 16 (lane group g supplies k = 4g .. 4g+3 of
+  // tap 8), so the executed K is 48 and 144.
+  static constexpr bool kRem = CIN == 3 || CIN == 16;
+  static constexpr int NF = kRem ? N - 1 : N;  // full K = 32 steps
 };
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Cin = 16: the last fragment in the K = 16 layout (lane (o, g) holds tap 8 channels 4g .. 4g+3), read
+// straight from the K = 32 layout of the pack / WB (lane (o, g') holds k = 128 + 8g' .. +7, i.e. tap 8
+// channels 8g' .. 8g'+7 for g' < 2, zeros above): halves 4(g & 1) .. +3 of lane (o, g >> 1)'s chunk.
+// Cin = 3 needs no move: lane (o, 0) holds tap 8's four channel slots in halves 0..3 and every other lane
+// zeros there.
+template <int CIN, int NT>
+__device__ __forceinline__ void rem_fragment(const _Float16* w, h8 (&af)[KSteps<CIN>::N][NT], int lane) {
+  if constexpr (CIN == 16) {
+    constexpr int s = KSteps<CIN>::N - 1;
+    const int g = lane >> 4, src = (lane & 15) + 16 * (g >> 1);
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+      const h4 v = *reinterpret_cast<const h4*>(w + (((s * NT + nt) * 64) + src) * 8 + 4 * (g & 1));
+      af[s][nt] = h8{v[0], v[1], v[2], v[3], 0, 0, 0, 0};
+    }
+  }
+}
 
 // A fragments of one conv for ALL output-channel tiles: af[s][nt] (4 VGPRs each)
 template <int CIN, int NT>
@@ -64,6 +89,7 @@ __device__ __forceinline__ void load_af(const _Float16* __restrict__ wf, h8 (&af
   for (int s = 0; s < KSteps<CIN>::N; ++s)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) af[s][nt] = *reinterpret_cast<const h8*>(wf + (((s * NT + nt) * 64) + lane) * 8);
+  rem_fragment<CIN, NT>(wf, af, lane);
 }
 
 // The same fragments from the workgroup's LDS copy of the block (layout identical to the pack's).
@@ -73,6 +99,7 @@ __device__ __forceinline__ void load_af_lds(const _Float16* wb, h8 (&af)[KSteps<
   for (int s = 0; s < KSteps<CIN>::N; ++s)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) af[s][nt] = *reinterpret_cast<const h8*>(wb + (((s * NT + nt) * 64) + lane) * 8);
+  rem_fragment<CIN, NT>(wb, af, lane);
 }
 template <int CIN, int NT>
 constexpr int kBlockHalves = KSteps<CIN>::N * NT * 64 * 8;
@@ -81,7 +108,6 @@ constexpr int kBlockHalves = KSteps<CIN>::N * NT * 64 * 8;
 // work: issue() starts the loads (16-B chunks, chunk c by thread c mod 512), commit() stores them to
 // WB.  WB protocol (every phase ends in a barrier): read WB -> af in phase k, commit the next block
 // in phase k+1 or later, read it in a phase after the commit.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 struct WStage {
   u32x4 r[(kWB / 8 + kHThreads - 1) / kHThreads];
   template <int NH>
@@ -140,7 +166,7 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
     for (int nt = 0; nt < NT; ++nt) acc[i][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
+  for (int s = 0; s < KSteps<CIN>::NF; ++s) {
     if constexpr (CIN == 3) {
       const int o0 = k_offset<CIN, CS, WP>(s, g, 0), o1 = k_offset<CIN, CS, WP>(s, g, 1);
 #pragma unroll
@@ -158,6 +184,22 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
         const h8 b = *reinterpret_cast<const h8*>(Tin + base[i] + o);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b, acc[i][nt], 0, 0, 0);
+      }
+    }
+  }
+  // tap 8 on K = 16 (lane group g: channel slots 4g .. 4g+3).  Its products go to a fresh accumulator and
+  // are added by VALU: accumulating the K = 16 MFMA straight onto the K = 32 MFMAs' result (SrcC) gave
+  // wrong sums on gfx950 with this hipcc (a mixed-pass-count SrcC dependency; fp16 golden test, measured),
+  // the separate form is exact.
+  if constexpr (KSteps<CIN>::kRem) {
+    const int o = (2 * WP + 2) * CS + (CIN == 3 ? 0 : 4 * g);
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      const h4 b = *reinterpret_cast<const h4*>(Tin + base[i] + o);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const h8 w = af[KS - 1][nt];
+        acc[i][nt] += __builtin_amdgcn_mfma_f32_16x16x16f16(h4{w[0], w[1], w[2], w[3]}, b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
       }
     }
   }
