@@ -629,46 +629,69 @@ __global__ __launch_bounds__(256) void fd_grad_fused_kernel(FdArgs a) {
     return (off < 0 || off > a.max_idx) ? (int64_t)-1 : off;
   };
   float v[kFusedRows];
-  auto load_pass = [&](int r0) {
+  // Row offsets: lane l of every wave loads row r0 + l's offset (one vector load; clamped into the chunk,
+  // an invalid offset reads row 0 -- its coefficient is NaN) and the pass takes row r's through
+  // v_readlane, so the table address is scalar base + column.  (Per-row scalar loads were each followed
+  // by an lgkmcnt(0) wait: 64 dependent round trips before the last row was even requested.)
+  auto row_offsets = [&](int r0) {
+    int64_t off = a.idx[(int64_t)min(r0 + (tid & 63), d1 - 1) * a.lpd];
+    return (off < 0 || off > a.max_idx) ? (int64_t)0 : off;
+  };
+  auto load_pass = [&](int r0, int64_t offl) {
+    const unsigned lo = (unsigned)offl, hi = (unsigned)((uint64_t)offl >> 32);
 #pragma unroll
     for (int r = 0; r < kFusedRows; ++r) {
-      const int d = r0 + r;
-      float x = 0.f;
-      if (d < d1) {
-        const int64_t off = row_off(d);
-        x = a.table[(off < 0 ? 0 : off) + cc];
-      }
-      v[r] = x;
+      const int64_t o = (int64_t)(((uint64_t)(unsigned)__builtin_amdgcn_readlane((int)hi, r) << 32) |
+                                  (unsigned)__builtin_amdgcn_readlane((int)lo, r));
+      const float x = a.table[o + cc];  // unconditional (rows past the chunk repeat its last row): no branch
+      v[r] = r0 + r < d1 ? x : 0.f;
     }
   };
-  load_pass(d0);
-
-  // this thread's first direction's per-lane inputs, requested before the statistics need them
+  const int64_t off0 = row_offsets(d0);  // first in the vmcnt order: the table loads wait only for it
+  // Load order matters: vmcnt retires loads in issue order, so the statistics' inputs are requested
+  // BEFORE the chunk's 64 table rows -- consuming them then waits only for themselves, and the table
+  // rows stay in flight through the statistics (issued after the rows, they would wait for all 64).
+  // this thread's first direction's per-lane inputs
   constexpr int kMaxLpd = 4;
   const int dmine = d0 + tid;
+  // Branch-free (clamped indices, selects): a load under a condition ends its basic block with a full
+  // vmcnt(0) wait, which serialised these ~30 loads into as many L2 round trips (measured: the kernel's
+  // 24 us vs 10.5 us for the bare 50 MB stream, tools/learner_bench.py).
   double xin[kMaxLpd], vin[kMaxLpd];
+  {
+    const int nloc = max(1, (d1 - d0) * a.lpd);  // this chunk's local lanes: [d0 * lpd, d1 * lpd)
+    int sg[kMaxLpd];
+    double n2v[kMaxLpd], xv[kMaxLpd];
 #pragma unroll
-  for (int k = 0; k < kMaxLpd; ++k) {
-    xin[k] = 0.0;
-    vin[k] = 0.0;
-    if (dmine < d1 && k < a.lpd) {
-      const int i = dmine * a.lpd + k;
-      const int sg = a.sign[i];
-      vin[k] = sg == 0 ? 0.0 : (double)sg * (double)a.sigma / a.n2[i];
-      if constexpr (MODE == FDR_WEIGHT_CENTERED_RANK) xin[k] = a.w[i];
-      else xin[k] = a.r_all[a.lo + i] - a.pr;
+    for (int k = 0; k < kMaxLpd; ++k) {
+      const int i = d0 * a.lpd + min((dmine - d0) * a.lpd + k, nloc - 1);
+      sg[k] = a.sign[i];
+      n2v[k] = a.n2[i];
+      if constexpr (MODE == FDR_WEIGHT_CENTERED_RANK) xv[k] = a.w[i];
+      else xv[k] = a.r_all[a.lo + i];
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxLpd; ++k) {
+      // computed unconditionally (an unused lane's 0/0 is selected away): a division under the condition
+      // lets the compiler sink the n2 load into the branch, behind a vmcnt(0)
+      const double q = (double)sg[k] * (double)a.sigma / n2v[k];
+      const bool use = dmine < d1 && k < a.lpd && sg[k] != 0;
+      vin[k] = use ? q : 0.0;
+      xin[k] = use ? (MODE == FDR_WEIGHT_CENTERED_RANK ? xv[k] : xv[k] - a.pr) : 0.0;
     }
   }
   double mean = 0.0, sd = 0.0;
+  // one load pass, the values kept in registers for the second (same per-thread order as a reload)
+  constexpr int kR = MODE == FDR_WEIGHT_ZSCORE ? 16 : 1;
+  double xr[kR];
   if constexpr (MODE == FDR_WEIGHT_ZSCORE) {
-    // one load pass, the values kept in registers for the second (same per-thread order as a reload)
-    constexpr int kR = 16;
-    double xr[kR];
 #pragma unroll
-    for (int k = 0; k < kR; ++k) {
-      const int i = tid + 256 * k;
-      xr[k] = i < a.n_all ? a.r_all[i] - a.pr : 0.0;
-    }
+    for (int k = 0; k < kR; ++k) xr[k] = a.r_all[min(tid + 256 * k, a.n_all - 1)];  // clamped: no branches
+#pragma unroll
+    for (int k = 0; k < kR; ++k) xr[k] = tid + 256 * k < a.n_all ? xr[k] - a.pr : 0.0;
+  }
+  load_pass(d0, off0);  // the table rows: in flight from here through the statistics and the coefficients
+  if constexpr (MODE == FDR_WEIGHT_ZSCORE) {
     double s = 0.0;
 #pragma unroll
     for (int k = 0; k < kR; ++k)
@@ -725,7 +748,7 @@ __global__ __launch_bounds__(256) void fd_grad_fused_kernel(FdArgs a) {
 
   double acc0 = 0.0, acc1 = 0.0, bcc0 = 0.0, bcc1 = 0.0;
   for (int r0 = d0; r0 < d1; r0 += kFusedRows) {
-    if (r0 != d0) load_pass(r0);
+    if (r0 != d0) load_pass(r0, row_offsets(r0));
 #pragma unroll
     for (int r = 0; r < kFusedRows; r += 2) {
       if (r0 + r < d1) {

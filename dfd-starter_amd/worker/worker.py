@@ -40,10 +40,13 @@ class Worker(object):
         self._next = None      # (key, host lanes, device lanes) uploaded ahead by evaluate(prefetch=True)
 
     # ---- hot path ---------------------------------------------------------------------------
-    def _to_device(self, arr, dtype):
+    def _to_device(self, arr, dtype, defer_wait=False):
         """Async H2D through a small ring of pinned buffers on a side copy stream: the copy runs as soon as it
         is enqueued (during the previous step's rollout, the host being ahead), and the compute stream only
-        waits on its event -- the upload is off the step's critical path.  An event guards each buffer's reuse."""
+        waits on its event -- the upload is off the step's critical path.  An event guards each buffer's reuse.
+        defer_wait=True returns (tensor, event) and leaves the compute stream's wait to the consumer: a
+        cross-stream wait enqueued behind a running kernel costs ~10 us of barrier processing when that kernel
+        ends (measured, rocprofv3 kernel trace), so it is placed right before the rollout that needs the data."""
         dev = self.policy.flat.device
         key = (dtype, len(arr))
         ring = self._pinned.setdefault(key, {"bufs": [], "events": [], "next": 0})
@@ -65,20 +68,27 @@ class Worker(object):
             out = buf.to(dev, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(self._copy_stream)
-        main.wait_event(ev)
         out.record_stream(main)
         ring["events"][slot] = ev
+        if defer_wait:
+            return out, ev
+        main.wait_event(ev)
         return out
 
-    def _lanes_to_device(self, idx, sign, det):
-        """The three per-lane descriptor arrays in ONE host-to-device copy: [idx i64 | sign i8 | det i8]."""
+    def _lanes_to_device(self, idx, sign, det, defer_wait=False):
+        """The three per-lane descriptor arrays in ONE host-to-device copy: [idx i64 | sign i8 | det i8].
+        defer_wait: (arrays, copy event) -- the caller makes the compute stream wait on the event."""
         n = len(idx)
         packed = np.empty(10 * n, np.uint8)
         packed[:8 * n] = np.asarray(idx, np.int64).view(np.uint8)
         packed[8 * n:9 * n] = np.asarray(sign, np.int8).view(np.uint8)
         packed[9 * n:] = np.asarray(det, np.int8).view(np.uint8)
-        d = self._to_device(packed, torch.uint8)
-        return d[:8 * n].view(torch.int64), d[8 * n:9 * n].view(torch.int8), d[9 * n:].view(torch.int8)
+        d = self._to_device(packed, torch.uint8, defer_wait)
+        ev = None
+        if defer_wait:
+            d, ev = d
+        arrs = (d[:8 * n].view(torch.int64), d[8 * n:9 * n].view(torch.int8), d[9 * n:].view(torch.int8))
+        return (arrs, ev) if defer_wait else arrs
 
     def launch(self, idx, sign, det, seed=None, out=None, jiggle=True, lane_offset=0, lanes_dev=None):
         """Run one rollout over explicit lanes (host arrays) -> FDBatch (asynchronous).  lanes_dev: the same lanes
@@ -144,14 +154,15 @@ class Worker(object):
         lidx, sign, det, lane_range, rank_lanes = self._lanes_of(idx, n_dirs, antithetic, lane_range)
         lanes_dev = None
         if pre is not None and pre[0] == key and np.array_equal(pre[1], lidx):
-            lanes_dev = pre[2]
+            lanes_dev, ev = pre[2]
+            torch.cuda.current_stream(self.policy.flat.device).wait_event(ev)  # right before the rollout
         lpd = 2 if antithetic else 1
         lo = 0 if lane_range is None else lane_range[0]
         res, idx_d, sign_d = self.launch(lidx, sign, det, seed=seed, out=out, lane_offset=lo, lanes_dev=lanes_dev)
         if prefetch and hasattr(self.noise_source, "peek_batch"):
             nidx = self.noise_source.peek_batch(n_dirs)
             nl, ns, nd, _, _ = self._lanes_of(nidx, n_dirs, antithetic, key[2])
-            self._next = (key, nl, self._lanes_to_device(nl, ns, nd))
+            self._next = (key, nl, self._lanes_to_device(nl, ns, nd, defer_wait=True))
         E = getattr(self.agent.env, "envs_per_lane", 1)
         if E > 1:
             lidx, sign = np.repeat(lidx, E), np.repeat(sign, E)
