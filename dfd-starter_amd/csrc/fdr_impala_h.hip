@@ -155,6 +155,10 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
                                        f32x4 (&acc)[TPW][NT], int wave, int lane) {
   constexpr int KS = KSteps<CIN>::N;
   const int g = lane >> 4;
+  // tile i of this wave exists (wave-uniform): only the last i of a conv whose MT is not a multiple of 8
+  // can be past the end -- skipped, not recomputed (the clamped duplicate cost 21 % of the executed MFMA
+  // FLOP: stage-3 residual convs have 4 tiles for 8 waves, r05 PMC)
+  auto live = [&](int i) { return TPW * 8 == MT || i < TPW - 1 || wave + 8 * i < MT; };
   int base[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
@@ -171,6 +175,7 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
       const int o0 = k_offset<CIN, CS, WP>(s, g, 0), o1 = k_offset<CIN, CS, WP>(s, g, 1);
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
+        if (!live(i)) continue;
         const h4 lo = *reinterpret_cast<const h4*>(Tin + base[i] + o0);
         const h4 hi = *reinterpret_cast<const h4*>(Tin + base[i] + o1);
         const h8 b = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -181,6 +186,7 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
       const int o = k_offset<CIN, CS, WP>(s, g, 0);
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
+        if (!live(i)) continue;
         const h8 b = *reinterpret_cast<const h8*>(Tin + base[i] + o);
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b, acc[i][nt], 0, 0, 0);
@@ -195,6 +201,7 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
     const int o = (2 * WP + 2) * CS + (CIN == 3 ? 0 : 4 * g);
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
+      if (!live(i)) continue;
       const h4 b = *reinterpret_cast<const h4*>(Tin + base[i] + o);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {

@@ -2,8 +2,11 @@
 
 The per-step host loop of the reference is replaced by whole-episode rollouts inside the
 fdr_rollout kernel; ``collect_return`` keeps the single-episode API by launching one lane.
-Observation normalisation uses FIXED learner statistics (agent.py:37-41), passed to the kernel;
-the per-step Welford sampling of agent.py:38-39 is the obs-stats row (not built).
+Observation normalisation uses FIXED learner statistics (agent.py:37-41), passed to the kernel.
+The per-step Welford sampling of agent.py:37-39 is built: with ``normalize_obs`` every
+lane samples its raw observations inside the rollout (``fdr_rollout_ex`` per-lane partials, the same
+coin chance), and the learner folds them in lane order with ``fdr_obs_stats_merge``
+(``Worker.launch`` passes the chance; ``learner.fd_return.obs_partials`` carries the partials).
 """
 import numpy as np
 import torch

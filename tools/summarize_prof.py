@@ -1,7 +1,7 @@
 """Summarise a tools/profile.sh output directory into profiles/<tag>_summary.md + the PMC json
 bench.py reads (profiles/pmc_rollout_<config>.json).
 
-    python tools/summarize_prof.py gpurun_out/prof_r01 r01 [config [kernel-substring]]
+    python tools/summarize_prof.py gpurun_out/prof_r01 r01 [config [kernel-substring [secondary [T]]]]
 
 HBM bytes per launch = FETCH_SIZE*1024*2 + WRITE_SIZE*1024: MI355X_MICROARCH.md section HBM --
 on gfx950 FETCH_SIZE reports half of a wide coalesced read; that x2 correction is applied to the
@@ -33,7 +33,8 @@ def mfma_pass(d):
     return {k: {c: sum(v) / len(v) for c, v in q.items()} for k, q in acc.items()}
 
 
-def main(d, tag, config="halfcheetah", dominant="rollout_kernel", secondary=None):
+def main(d, tag, config="halfcheetah", dominant="rollout_kernel", secondary=None, steps="1000"):
+    steps = int(steps)  # env steps per launch of the dominant kernel (per-wave-step counts)
     stats = list(csv.DictReader(open(os.path.join(d, "trace", "run_kernel_stats.csv"))))
     fetch = per_kernel(os.path.join(d, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(d, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
@@ -69,8 +70,8 @@ def main(d, tag, config="halfcheetah", dominant="rollout_kernel", secondary=None
         rollout["effective_clock_ghz"] = clk
         lines += ["", "Dominant kernel (%s): avg %.1f us, effective clock %.2f GHz (GRBM_GUI_ACTIVE/8/duration), "
                       "VALU instructions per wave-step %.1f, LDS per wave-step %.1f." % (
-                          dominant, avg_ns / 1e3, clk, q.get("SQ_INSTS_VALU", 0) / max(1, q.get("SQ_WAVES", 1)) / 1000,
-                          q.get("SQ_INSTS_LDS", 0) / max(1, q.get("SQ_WAVES", 1)) / 1000)]
+                          dominant, avg_ns / 1e3, clk, q.get("SQ_INSTS_VALU", 0) / max(1, q.get("SQ_WAVES", 1)) / steps,
+                          q.get("SQ_INSTS_LDS", 0) / max(1, q.get("SQ_WAVES", 1)) / steps)]
         mf = mfma_pass(d)
         if mf:
             lines += ["", "MFMA pass (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8); MOPS x 512 = FLOP):", "",
@@ -85,6 +86,30 @@ def main(d, tag, config="halfcheetah", dominant="rollout_kernel", secondary=None
                 if dominant in k:
                     rollout["mfma_busy"] = round(busy, 4)
                     rollout["mfma_flop_per_launch"] = flop
+        ex = os.path.join(d, "pmc_extra0", "run_counter_collection.csv")
+        if os.path.exists(ex):  # issue / wait breakdown (tools/profile_round.sh ISSUE_PMC)
+            acc = collections.defaultdict(list)
+            for r in csv.DictReader(open(ex)):
+                if r["Kernel_Name"] == rollout["kernel"]:
+                    acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            q = {c: sum(v) / len(v) for c, v in acc.items()}
+            if q.get("SQ_WAVE_CYCLES") and q.get("GRBM_GUI_ACTIVE"):
+                cyc = q["GRBM_GUI_ACTIVE"] / 8
+                simds = 1024
+                issue = dict(counters=q,
+                             simd_valu_busy=q["SQ_ACTIVE_INST_VALU"] / (simds * cyc / 4),
+                             cycles_per_valu_inst=(q["SQ_ACTIVE_INST_VALU"] * 4 / rollout["sq"]["SQ_INSTS_VALU"]
+                                                   if rollout["sq"].get("SQ_INSTS_VALU") else None),
+                             wave_frac_active=q["SQ_ACTIVE_INST_ANY"] / q["SQ_WAVE_CYCLES"],
+                             wave_frac_wait_any=q["SQ_WAIT_ANY"] / q["SQ_WAVE_CYCLES"],
+                             wave_frac_wait_inst=q["SQ_WAIT_INST_ANY"] / q["SQ_WAVE_CYCLES"])
+                rollout["issue"] = issue
+                lines += ["", "Issue / wait PMC pass (quad-cycle SQ counters; SIMD VALU busy = SQ_ACTIVE_INST_VALU / "
+                              "(1024 SIMDs x GRBM_GUI_ACTIVE/8 / 4)): VALU busy %.3f, %.2f cycles per VALU instruction; "
+                              "wave cycles: %.1f %% issuing, %.1f %% waiting on counters, %.1f %% issue-stalled." % (
+                                  issue["simd_valu_busy"], issue["cycles_per_valu_inst"] or 0,
+                                  100 * issue["wave_frac_active"], 100 * issue["wave_frac_wait_any"],
+                                  100 * issue["wave_frac_wait_inst"])]
         if secondary:
             for k in fetch:
                 if secondary in k:
