@@ -154,8 +154,14 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-variant", action="store_true", help="skip the 4096-pair variant line (config 3)")
-    ap.add_argument("--event-every", type=int, default=1,
-                    help="bracket every k-th FD step's rollout with HIP events (1: every step)")
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="after the W warmup steps, further untimed FD steps until this much wall time has passed "
+                         "since the first warmup step: the GPU's clocks ramp over the first ~30 ms of sustained load "
+                         "(config 3 rollout 1.24 -> 1.06 ms over its first 25 launches, rocprofv3 trace, DESIGN.md 7); "
+                         "0 disables")
+    ap.add_argument("--timing-steps", type=int, default=10,
+                    help="FD steps of the rollout-timing pass that follows the timed region (HIP events around "
+                         "each rollout; Impala: the in-rollout conv/core phase events)")
     ap.add_argument("--no-novelty", action="store_true", help="config 5 without the novelty archive / omega "
                     "(rocprof passes: the archive's conv launches would mix into the rollout conv's average)")
     args = ap.parse_args()
@@ -211,7 +217,6 @@ def main():
         policy = ImpalaPolicy(n_in, n_act, seed=124, device=dev)
         fp16 = args.config == "impala_fp16"
         env = FrameEnv(n_act, episode_len=T, envs_per_lane=IMPALA_ENVS, env_seed=5, fp16=fp16)
-        engine.impala_profile(True)
     else:
         Pol = DiscretePolicy if kind == "discrete" else MujocoPolicy
         policy = Pol(n_in, n_act, seed=124, device=dev)
@@ -273,7 +278,10 @@ def main():
             phase_ms.append(engine.impala_profile_read())
         return out, batch
 
-    def timed_loop(steps, **kw):
+    def timed_loop(steps, events=False, **kw):
+        # events=False: the timed region carries no instrumentation (an event record on the stream costs
+        # ~5 us of barrier processing at each kernel boundary it sits on: rocprofv3 trace);
+        # the rollout's own time comes from a separate pass with events=True
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -282,7 +290,7 @@ def main():
         pairs = []
         out = None
         for i in range(steps):
-            cur[0] = ev_pool[i % len(ev_pool)] if i % args.event_every == 0 else None
+            cur[0] = ev_pool[i % len(ev_pool)] if events else None
             out, _ = fd_step(True, **kw)
             if cur[0] is not None:
                 pairs.append(cur[0])
@@ -293,9 +301,32 @@ def main():
         el = time.perf_counter() - t0
         return el, [a_.elapsed_time(b_) for a_, b_ in pairs], out
 
+    t_warm = time.perf_counter()
     for _ in range(args.warmup):
         out, _ = fd_step(False)
-    elapsed, roll_ms, out = timed_loop(args.steps)
+    # clock settle: untimed steps in chunks of 5 (one sync per chunk) until settle_ms of sustained load
+    # (N > 1: the ranks decide together, so every rank runs the same FD steps and collectives)
+    settle_steps = 0
+    while args.settle_ms > 0:
+        torch.cuda.synchronize()
+        go = (time.perf_counter() - t_warm) * 1e3 < args.settle_ms
+        if world > 1:
+            t = torch.tensor([1 if go else 0], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            go = bool(t.item())
+        if not go:
+            break
+        for _ in range(5):
+            out, _ = fd_step(False)
+        settle_steps += 5
+    elapsed, _, out = timed_loop(args.steps)
+    # rollout-timing pass (outside the timed region): HIP events bracketing each rollout on its stream,
+    # and for Impala the per-step-loop phase events of fdr_impala_profile
+    if impala:
+        engine.impala_profile(True)
+    _, roll_ms, _ = timed_loop(max(1, min(args.steps, args.timing_steps)), events=True)
+    if impala:
+        engine.impala_profile(False)
     rollout_ms = float(np.mean(roll_ms))
     if world > 1:
         t = torch.tensor([elapsed, rollout_ms], dtype=torch.float64, device=dev)
@@ -315,7 +346,8 @@ def main():
         rng2 = fdist.lane_range(nv, 2, world, rank)
         fd_step(False, n_dirs=nv, rng=rng2)
         k = max(1, min(args.steps, 10))
-        el2, ms2, out2 = timed_loop(k, n_dirs=nv, rng=rng2)
+        el2, _, out2 = timed_loop(k, n_dirs=nv, rng=rng2)
+        _, ms2, _ = timed_loop(k, events=True, n_dirs=nv, rng=rng2)
         r2 = float(np.mean(ms2))
         if world > 1:
             t = torch.tensor([el2, r2], dtype=torch.float64, device=dev)
@@ -404,7 +436,7 @@ def main():
         "unit": "env steps/s",
         "n_gpus": world,
         "steps": args.steps,
-        "warmup": args.warmup,
+        "warmup": args.warmup, "settle_steps": settle_steps,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "sec_per_fd_step": round(elapsed / args.steps, 6),
         "higher_is_better": True,

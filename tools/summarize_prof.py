@@ -68,10 +68,24 @@ def main(d, tag, config="halfcheetah", dominant="rollout_kernel", secondary=None
         clk = q.get("GRBM_GUI_ACTIVE", 0) / 8 / (avg_ns * 1e-9) / 1e9 if avg_ns else 0
         rollout["avg_duration_us"] = avg_ns / 1e3
         rollout["effective_clock_ghz"] = clk
+        # steady state: the last half of the dispatches (the clocks ramp over the first ~30 ms of load)
+        tr = os.path.join(d, "trace", "run_kernel_trace.csv")
+        if os.path.exists(tr):
+            durs = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                    for r in csv.DictReader(open(tr)) if r["Kernel_Name"] == st["Name"]]
+            durs = [x for _, x in sorted(durs)]
+            if durs:
+                tail = durs[len(durs) // 2:]
+                rollout["avg_duration_us_steady"] = sum(tail) / len(tail) / 1e3
+                rollout["dispatches"] = len(durs)
         lines += ["", "Dominant kernel (%s): avg %.1f us, effective clock %.2f GHz (GRBM_GUI_ACTIVE/8/duration), "
                       "VALU instructions per wave-step %.1f, LDS per wave-step %.1f." % (
                           dominant, avg_ns / 1e3, clk, q.get("SQ_INSTS_VALU", 0) / max(1, q.get("SQ_WAVES", 1)) / steps,
                           q.get("SQ_INSTS_LDS", 0) / max(1, q.get("SQ_WAVES", 1)) / steps)]
+        if "avg_duration_us_steady" in rollout:
+            lines += ["", "Steady state (last %d of %d dispatches, after the clock ramp): avg %.1f us." % (
+                rollout["dispatches"] - rollout["dispatches"] // 2, rollout["dispatches"],
+                rollout["avg_duration_us_steady"])]
         mf = mfma_pass(d)
         if mf:
             lines += ["", "MFMA pass (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8); MOPS x 512 = FLOP):", "",
