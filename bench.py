@@ -197,10 +197,17 @@ def main():
     import torch
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # FDR_BENCH_REHEARSE=1: rehearse the N-rank path on a one-GPU box (every rank on cuda:0, gloo) -- the
+    # exchange protocol, the collective settle and the max-over-ranks timing; not a scaling measurement
+    rehearse = os.environ.get("FDR_BENCH_REHEARSE") == "1"
+    dev_index = 0 if rehearse else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from dsgd import DSGD
     from envs import FrameEnv, SyntheticEnv
