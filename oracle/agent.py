@@ -48,9 +48,11 @@ def collect_return(policy, env, obs, deterministic, noise_fn, jiggle_fn, mean=No
 
 def evaluate_lanes(kind, n_in, n_act, theta, table, idx, sign, sigma, env, seed,
                    deterministic=False, bn_stats=None, obs_mean=None, obs_std=None, jiggle=True,
-                   obs_chance=None, record_states=False):
+                   obs_chance=None, record_states=False, lane_ids=None):
     """Batched numpy reference of fdr_rollout (synthetic env).  Returns ret, ent, steps, norm2
-    (+ the per-lane Welford statistics if obs_chance, + states [L, T, n_in] if record_states)."""
+    (+ the per-lane Welford statistics if obs_chance, + states [L, T, n_in] if record_states).
+    lane_ids: the global lane ids keying the counter stream (default 0 .. L-1), for sampled lanes of a
+    larger launch."""
     L = len(idx)
     thetas = perturb(theta, table, idx, sign, sigma)
     # squared norm of lambda = sign * fl32(sigma * eps) -- what the FD learner divides by
@@ -60,7 +62,7 @@ def evaluate_lanes(kind, n_in, n_act, theta, table, idx, sign, sigma, env, seed,
                                    (table[int(i):int(i) + P] * s32).astype(np.float64)))
                       if sg != 0 else 0.0 for i, sg in zip(idx, sign)])
     obs = env.reset()
-    lanes = np.arange(L, dtype=np.uint64)
+    lanes = np.arange(L, dtype=np.uint64) if lane_ids is None else np.asarray(lane_ids, dtype=np.uint64)
     ret = np.zeros(L, dtype=np.float64)
     ent = np.zeros(L, dtype=np.float64)
     det = np.broadcast_to(np.asarray(deterministic, dtype=bool), (L,))

@@ -382,6 +382,48 @@ def test_full_size_properties(eng):
     np.testing.assert_allclose(n2, res1.norm2.cpu().numpy(), rtol=1e-12)
 
 
+def test_full_size_properties_config2(eng):
+    """BASELINE config 2 size (1024 lanes x T=500, CartPole-shaped, discrete): the auto-selected WIDE one-lane
+    kernel is reproducible, antithetic norms are symmetric, sampled lanes match the oracle over the full
+    episode, and every lane matches the 128-VGPR one-lane kernel."""
+    name = "cartpole"
+    kind, n_in, n_act = SHAPES[name]
+    torch.manual_seed(124)
+    pol = opol.TorchPolicy(kind, n_in, n_act, seed=124)
+    theta = pol.get_flat()
+    P = theta.size
+    t, tab = table(P, size=25_000_000)
+    L, T = 1024, 500
+    idx = np.repeat(t.sample_indices(L // 2), 2)
+    sign = np.tile(np.array([1, -1], np.int8), L // 2)
+    from envs import SyntheticEnv
+    env = SyntheticEnv(n_in, n_act, True, T)
+    spec = eng.PolicySpec(kind, n_in, n_act, P)
+    lanes = eng.lanes_desc(dev(theta), 0, tab, dev(idx, torch.int64), dev(sign), 0.02)
+    res = eng.rollout(spec, env, lanes, L, 9)
+    res2 = eng.rollout(spec, env, lanes, L, 9)
+    ret = res.reward.cpu().numpy()
+    assert np.isfinite(ret).all() and torch.equal(res.reward, res2.reward)
+    assert (res.timesteps.cpu().numpy() == T).all()
+    n2 = res.norm2.cpu().numpy()
+    assert np.array_equal(n2[0::2], n2[1::2])
+    pick = np.array([0, 1, 333, 512, 1023])
+    oenv = oenvs.BatchedSyntheticEnv(n_in, n_act, True, T, len(pick), env_seed=0)
+    ref = oagent.evaluate_lanes(kind, n_in, n_act, theta, t.table, idx[pick], sign[pick], 0.02, oenv, 9,
+                                lane_ids=pick)
+    np.testing.assert_allclose(ret[pick], ref[0], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(res.entropy.cpu().numpy()[pick], ref[1], rtol=1e-5, atol=1e-5)
+    try:
+        eng.context().set_rollout_impl("single")
+        res1 = eng.rollout(spec, env, lanes, L, 9)
+        torch.cuda.synchronize()
+    finally:
+        eng.context().set_rollout_impl("auto")
+    np.testing.assert_allclose(ret, res1.reward.cpu().numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(res.entropy.cpu().numpy(), res1.entropy.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(n2, res1.norm2.cpu().numpy())
+
+
 def _oracle_lanes_with_ids(kind, n_in, n_act, theta, tab, idx, sign, env, seed, ids):
     from oracle import rng as crng
     thetas = onoise.perturb(theta, tab, idx, sign, 0.02)
