@@ -468,7 +468,7 @@ static int impala_layout(const fdr_impala_desc* d, impala::Layout* L) {
 int64_t fdr_impala_workspace_bytes(const fdr_impala_desc* d, int32_t n_lanes) {
   impala::Layout L;
   if (!d || n_lanes < 0 || !impala::make_layout(d->n_act, &L)) return -1;
-  return impala::plan(L, n_lanes, d->envs_per_lane, d->episode_len, d->entropy != 0, d->fp16 != 0).total;
+  return impala::plan(L, n_lanes, d->envs_per_lane, d->episode_len, d->entropy != 0, d->fp16 != 0, d->pairs != 0).total;
 }
 
 int fdr_impala_rollout(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lanes_desc* lanes,
@@ -494,6 +494,8 @@ int fdr_impala_rollout(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lanes_d
   c.entropy = d->entropy != 0;
   c.jiggle = jiggle;
   c.fp16 = d->fp16 != 0;
+  c.pairs = d->pairs != 0;
+  if (c.pairs && (n_lanes & 1)) return set_error(FDR_ERR_INVALID, "pairs: n_lanes must be even");
   c.seed = seed;
   c.env_seed = d->env_seed;
   c.bn_mean = d->bn_mean;

@@ -80,6 +80,12 @@ struct StepArgs {
   const float* reward_in;  // forward: reward carried by the obs
   const float* notdone;    // forward: done mask (policies/impala.py:170-176)
   uint64_t* dbg;           // diagnostics: phase clocks of conv workgroup 0 (fdr_impala_debug_clock) or NULL
+  // pair form of the fp16 rollout core step (fdr_impala_desc.pairs): theta's half pack, the pairs' sigma-eps
+  // half packs [n_lanes / 2][hpack], the lanes' signs
+  const _Float16* th;
+  const _Float16* ep;
+  int64_t ep_stride;
+  const int8_t* sign;
 };
 
 // phase clock of the first conv workgroup (s_memtime), for the phase breakdown in DESIGN.md
@@ -200,19 +206,23 @@ __global__ void finish_kernel(int n_lanes, int envs, int T, int entropy, int jig
 __global__ void conv_kernel_h(Layout L, StepArgs a);
 template <int E, int MODE>
 __global__ void core_kernel_h(Layout L, StepArgs a);
+template <int E>
+__global__ void core_kernel_hp(Layout L, StepArgs a);  // pair form (rollout mode), grid n_lanes / 2
 constexpr int kHThreads = 512;
 
 struct Plan {  // workspace carve-up (byte offsets)
-  int64_t pack, hpack, feat, h, c, rprev, ci, gx, n2, total;
+  int64_t pack, hpack, feat, h, c, rprev, ci, gx, n2, zeros, thpack, epack, idxe, total;
   int nblk;    // prep blocks per lane
 };
-Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16 = false);
+// pairs: the fp16 pair form (theta half pack, one sigma-eps half pack per pair, a zero base, pair offsets)
+Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16 = false, bool pairs = false);
+bool pair_core_supported(int envs);
 
 struct RolloutCall {
   const Context* ctx;
   const Layout* layout;
   LanesArgs lanes;
-  int n_lanes, envs, T, entropy, jiggle, fp16;
+  int n_lanes, envs, T, entropy, jiggle, fp16, pairs;
   uint64_t seed, env_seed;
   const float* bn_mean;
   const float* bn_var;

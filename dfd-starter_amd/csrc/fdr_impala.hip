@@ -119,7 +119,9 @@ constexpr int kPrepThreads = 256;
 constexpr int kPrepPer = 4;
 constexpr int kPrepSpan = kPrepThreads * kPrepPer;
 
-Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16) {
+bool pair_core_supported(int envs) { return envs == 1 || envs == 2 || envs == 4; }
+
+Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16, bool pairs) {
   Plan p{};
   const int64_t ne = (int64_t)n_lanes * envs;
   int64_t o = 0;
@@ -134,6 +136,11 @@ Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16
   p.ci = take(entropy ? (int64_t)T * ne * kCoreIn * 4 : 0);
   p.gx = take(entropy ? (int64_t)std::min(T, kReplayChunk) * ne * kGates * 4 : 0);
   p.n2 = take((int64_t)n_lanes * p.nblk * 8);
+  const bool pr = fp16 && pairs && pair_core_supported(envs);
+  p.zeros = take(pr ? L.P * 4 : 0);
+  p.thpack = take(pr ? L.hpack * 2 : 0);
+  p.epack = take(pr ? (int64_t)(n_lanes / 2) * L.hpack * 2 : 0);
+  p.idxe = take(pr ? (int64_t)(n_lanes / 2) * 8 : 0);
   p.total = o;
   return p;
 }
@@ -1025,6 +1032,12 @@ __global__ __launch_bounds__(256) void lstm_xproj_kernel(Layout L, StepArgs a, i
     }
 }
 
+// the pairs' table offsets idx[2p] (fdr_impala_desc.pairs: idx[2p] == idx[2p+1] by contract)
+__global__ void pair_offsets_kernel(const int64_t* __restrict__ idx, int n_pairs, int64_t* __restrict__ idxe) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_pairs) idxe[p] = idx[2 * p];
+}
+
 template <int E>
 static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int entropy, hipStream_t stream) {
   const int conv_grid = (a.n_lanes + 7) / 8 * 8 * a.envs;
@@ -1043,7 +1056,15 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
     else
       hipLaunchKernelGGL(conv_kernel, dim3(conv_grid), dim3(kConvThreads), 0, stream, L, a);
     mark(prof, stream);
-    if (h)
+    bool pair_done = false;
+    if constexpr (E <= 4) {
+      if (h && a.ep) {
+        hipLaunchKernelGGL((core_kernel_hp<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
+        pair_done = true;
+      }
+    }
+    if (pair_done) {
+    } else if (h)
       hipLaunchKernelGGL((core_kernel_h<E, kRollout>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
     else
       hipLaunchKernelGGL((core_kernel<E, kRollout>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
@@ -1077,7 +1098,7 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
 
 int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t stream) {
   const Layout& L = *c.layout;
-  const Plan p = plan(L, c.n_lanes, c.envs, c.T, c.entropy != 0, c.fp16 != 0);
+  const Plan p = plan(L, c.n_lanes, c.envs, c.T, c.entropy != 0, c.fp16 != 0, c.pairs != 0);
   if (!ws || ws_bytes < p.total) return set_error(FDR_ERR_WORKSPACE, "impala workspace too small");
   if (c.n_lanes == 0) return FDR_OK;
   char* w = static_cast<char*>(ws);
@@ -1113,6 +1134,30 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
     a.hpack = reinterpret_cast<_Float16*>(w + p.hpack);
     a.hpack_stride = L.hpack;
     launch_pack<_Float16>(L, c.lanes, a.hpack, n2, c.n_lanes, 1, stream);
+    if (c.pairs && pair_core_supported(c.envs) && c.lanes.table && c.lanes.base_stride == 0 && c.n_lanes >= 2) {
+      // the pair form's operands, built by the same pack kernels: theta's half pack (no table: theta' =
+      // theta) and per pair fl32(sigma eps) in f16 (a zero base, sign +1: fl32(0 + fl32(sigma eps)))
+      const int np = c.n_lanes / 2;
+      float* zeros = reinterpret_cast<float*>(w + p.zeros);
+      int64_t* idxe = reinterpret_cast<int64_t*>(w + p.idxe);
+      _Float16* th = reinterpret_cast<_Float16*>(w + p.thpack);
+      _Float16* ep = reinterpret_cast<_Float16*>(w + p.epack);
+      (void)hipMemsetAsync(zeros, 0, (size_t)L.P * 4, stream);
+      hipLaunchKernelGGL(pair_offsets_kernel, dim3((np + 255) / 256), dim3(256), 0, stream, c.lanes.idx, np, idxe);
+      LanesArgs lt = c.lanes;
+      lt.table = nullptr;
+      launch_pack<_Float16>(L, lt, th, n2, 1, 1, stream);
+      LanesArgs le = c.lanes;
+      le.base = zeros;
+      le.base_stride = 0;
+      le.idx = idxe;
+      le.sign = nullptr;
+      launch_pack<_Float16>(L, le, ep, n2, np, 1, stream);
+      a.th = th;
+      a.ep = ep;
+      a.ep_stride = L.hpack;
+      a.sign = c.lanes.sign;
+    }
   }
   const int64_t ne = (int64_t)c.n_lanes * c.envs;
   hipLaunchKernelGGL(init_kernel, dim3((unsigned)((ne * kHid + 255) / 256)), dim3(256), 0, stream, ne, a.h, a.c,

@@ -749,6 +749,176 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
   if (j < E) core_finish<E, MODE>(a, logit, lane, j);
 }
 
+// ---- pair form of the fp16 rollout core step (fdr_impala_desc.pairs) --------------------------------
+// Lanes 2p, 2p+1 of an antithetic pair share their table offset, so their fc / LSTM weights are
+// theta + s_l fl32(sigma eps).  One workgroup per pair streams the pair's sigma-eps half pack ONCE from HBM
+// (non-temporal) and theta's half pack (2.1 MB, read by every workgroup: L2-resident) and forms each lane's
+// weight w = f16(theta) + s_l f16(sigma eps) in registers -- half core_kernel_h's HBM bytes per lane.  The
+// pair's 2E envs are contiguous (envs 2pE .. 2pE + 2E - 1), so the state / feature / output indexing is
+// core_kernel_h's with E -> 2E; biases, BN and the head are each lane's own (its f32 pack).
+// Numerics: f16(theta) + s f16(sigma eps) in f32 vs f16(theta + s sigma eps): within the fp16 tolerance.
+template <int E>
+__global__ __launch_bounds__(kCoreThreads) void core_kernel_hp(Layout L, StepArgs a) {
+  constexpr int E2 = 2 * E;
+  __shared__ float xw[kFeat * E2];
+  __shared__ float hs[kHid * E2];
+  float* cis = xw + kFeat * E2 / 2;
+  float* logit = xw;
+  static_assert(kCoreIn * E2 <= kFeat * E2 / 2 && E2 * kMaxAct <= kFeat * E2, "core LDS aliasing");
+  const int pr = blockIdx.x, j = threadIdx.x;
+  const int l0 = 2 * pr;
+  const float* pk0 = a.pack + (int64_t)l0 * a.pack_stride;
+  const float* pk1 = pk0 + a.pack_stride;
+  const float sg0 = a.sign ? (float)a.sign[l0] : 1.f, sg1 = a.sign ? (float)a.sign[l0 + 1] : 1.f;
+  const _Float16* eh = a.ep + (int64_t)pr * a.ep_stride;
+  const int64_t e0 = (int64_t)l0 * E;
+  const int A = a.n_act;
+  auto pkof = [&](int e) { return e < E ? pk0 : pk1; };
+
+  for (int k = j; k < kFeat; k += kCoreThreads) {  // BN1d(2048), each lane's own parameters
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const float* pk = hf ? pk1 : pk0;
+      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + k] : 0.f;
+      const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + k] : 1.f;
+      const float sc = pk[L.bn_w[15] + k] * (1.f / sqrtf(rv + kBnEps));
+      const float sh = pk[L.bn_b[15] + k] - rm * sc;
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        xw[k * E2 + hf * E + e] = fmaf(a.feat[(e0 + hf * E + e) * kFeat + k], sc, sh);
+    }
+  }
+  __syncthreads();
+  // one streamed weight row (8 columns): w = theta + s_l E for each lane of the pair, 2E envs of FMAs
+  auto accum = [&](float (&acc)[8][E2], h8 wt, h8 we, const float* x) {
+    float wp[8], wm[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float t = (float)wt[c], d = (float)we[c];
+      wp[c] = fmaf(sg0, d, t);
+      wm[c] = fmaf(sg1, d, t);
+    }
+#pragma unroll
+    for (int e = 0; e < E2; ++e) {
+      const float xv = x[e];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[c][e] = fmaf(e < E ? wp[c] : wm[c], xv, acc[c][e]);
+    }
+  };
+  {  // fc: thread = (8 columns, one of 8 K-slices of 256 rows)
+    const int c8 = j & 31, ks = j >> 5;
+    float acc[8][E2];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int e = 0; e < E2; ++e) acc[c][e] = 0.f;
+    const h8* t8 = reinterpret_cast<const h8*>(a.th + L.fc_wt_h) + c8;
+    const h8* e8 = reinterpret_cast<const h8*>(eh + L.fc_wt_h) + c8;
+#pragma unroll FDR_CORE_UNROLL_H
+    for (int k = ks * 256; k < ks * 256 + 256; ++k)
+      accum(acc, t8[(int64_t)k * (kHid / 8)], ld_stream(e8 + (int64_t)k * (kHid / 8)), xw + k * E2);
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int e = 0; e < E2; ++e) xw[(ks * kHid + 8 * c8 + c) * E2 + e] = acc[c][e];
+  }
+  __syncthreads();
+  {
+    const float bj0 = pk0[L.fc_b + j], bj1 = pk1[L.fc_b + j];
+    float yv[E2];
+#pragma unroll
+    for (int e = 0; e < E2; ++e) {
+      float y = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) y += xw[(q * kHid + j) * E2 + e];
+      yv[e] = relu(y + (e < E ? bj0 : bj1));
+    }
+    __syncthreads();  // every partial read before cis (inside xw) is written
+#pragma unroll
+    for (int e = 0; e < E2; ++e) cis[j * E2 + e] = yv[e];
+  }
+  if (j < E2) cis[kHid * E2 + j] = fminf(fmaxf(a.rprev[e0 + j], -1.f), 1.f);
+  if (a.ci) {
+    __syncthreads();
+    float* dst = a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn;
+    for (int i = j; i < kCoreIn * E2; i += kCoreThreads) {
+      const int e = i / kCoreIn, k = i - e * kCoreIn;
+      dst[i] = cis[k * E2 + e];
+    }
+  }
+  float cj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    hs[j * E2 + e] = a.h[(e0 + e) * kHid + j];
+    cj[e] = a.c[(e0 + e) * kHid + j];
+  }
+  __syncthreads();
+  {  // gates: threads 0..127 stream W_ih^T (x part), 128..255 W_hh^T (h part), 8 columns each
+    const int cg = j & 127, part = j >> 7;
+    float acc[8][E2];
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int e = 0; e < E2; ++e) acc[c][e] = 0.f;
+    const int k_lo = part ? kCoreIn : 0, k_n = part ? kHid : kCoreIn;
+    const float* xin = part ? hs : cis;
+    const h8* t8 = reinterpret_cast<const h8*>(a.th + L.lstm_wt_h) + cg;
+    const h8* e8 = reinterpret_cast<const h8*>(eh + L.lstm_wt_h) + cg;
+#pragma unroll FDR_CORE_UNROLL_H
+    for (int k = 0; k < k_n; ++k)
+      accum(acc, t8[(int64_t)(k_lo + k) * (kGates / 8)], ld_stream(e8 + (int64_t)(k_lo + k) * (kGates / 8)),
+            xin + k * E2);
+    __syncthreads();  // every read of cis (inside xw) is done before the gates overwrite it
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int e = 0; e < E2; ++e) xw[(part * kGates + 8 * cg + c) * E2 + e] = acc[c][e];
+  }
+  __syncthreads();
+  float hj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    const float* pk = pkof(e);
+    float pre[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int col = g * kHid + j;
+      pre[g] = (xw[col * E2 + e] + pk[L.lstm_bih + col]) + (xw[(kGates + col) * E2 + e] + pk[L.lstm_bhh + col]);
+    }
+    const float gi = sigm(pre[0]), gf = sigm(pre[1]), gg = tanhf(pre[2]), go = sigm(pre[3]);
+    cj[e] = gf * cj[e] + gi * gg;
+    hj[e] = go * tanhf(cj[e]);
+    a.h[(e0 + e) * kHid + j] = hj[e];
+    a.c[(e0 + e) * kHid + j] = cj[e];
+  }
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const float* pk = hf ? pk1 : pk0;
+    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
+    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
+    const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
+    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+#pragma unroll
+    for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
+  }
+  __syncthreads();
+  if (j < A * E2) {  // head in f32 (A x 256, tiny), each lane's own
+    const int ai = j / E2, e = j - ai * E2;
+    const float* pk = pkof(e);
+    const float* w = pk + L.head_w + ai * kHid;
+    float s = 0.f;
+    for (int k = 0; k < kHid; ++k) s = fmaf(w[k], hs[k * E2 + e], s);
+    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
+  }
+  __syncthreads();
+  if (j < E2) core_finish<E, kRollout>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
+}
+
+template __global__ void core_kernel_hp<1>(Layout, StepArgs);
+template __global__ void core_kernel_hp<2>(Layout, StepArgs);
+template __global__ void core_kernel_hp<4>(Layout, StepArgs);
+
 template __global__ void core_kernel_h<1, kRollout>(Layout, StepArgs);
 template __global__ void core_kernel_h<1, kReplay>(Layout, StepArgs);
 template __global__ void core_kernel_h<1, kForward>(Layout, StepArgs);

@@ -70,7 +70,8 @@ class AtariDesc(ctypes.Structure):
 class ImpalaDesc(ctypes.Structure):
     _fields_ = [("n_act", ctypes.c_int32), ("envs_per_lane", ctypes.c_int32), ("episode_len", ctypes.c_int32),
                 ("entropy", ctypes.c_int32), ("env_seed", ctypes.c_uint64), ("n_params", ctypes.c_int64),
-                ("bn_mean", ctypes.c_void_p), ("bn_var", ctypes.c_void_p), ("fp16", ctypes.c_int32)]
+                ("bn_mean", ctypes.c_void_p), ("bn_var", ctypes.c_void_p), ("fp16", ctypes.c_int32),
+                ("pairs", ctypes.c_int32)]
 
 
 def _load():

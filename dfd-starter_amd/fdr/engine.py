@@ -330,9 +330,12 @@ def impala_num_bn_stats():
 class ImpalaSpec(object):
     """Shape of an ImpalaPolicy rollout: A actions, E envs per perturbation, T-step episodes."""
 
-    def __init__(self, n_act, envs_per_lane=1, episode_len=1, entropy=True, env_seed=0, fp16=False):
+    def __init__(self, n_act, envs_per_lane=1, episode_len=1, entropy=True, env_seed=0, fp16=False, pairs=False):
+        """pairs (fp16 mode): lanes 2p, 2p+1 are antithetic pairs -- the rollout's core step streams each pair's
+        sigma-eps once (fdr_impala_desc.pairs)."""
         self.n_act, self.envs_per_lane, self.episode_len = int(n_act), int(envs_per_lane), int(episode_len)
         self.entropy, self.env_seed, self.fp16 = bool(entropy), int(env_seed), bool(fp16)
+        self.pairs = bool(pairs)
         self.n_params = impala_num_params(n_act)
         if self.n_params < 0:
             raise ValueError("n_act out of range")
@@ -345,7 +348,8 @@ class ImpalaSpec(object):
         return _lib.ImpalaDesc(self.n_act, self.envs_per_lane, self.episode_len, 1 if self.entropy else 0,
                                self.env_seed & ((1 << 64) - 1), self.n_params,
                                None if bn_mean is None else bn_mean.data_ptr(),
-                               None if bn_var is None else bn_var.data_ptr(), 1 if self.fp16 else 0)
+                               None if bn_var is None else bn_var.data_ptr(), 1 if self.fp16 else 0,
+                               1 if self.pairs else 0)
 
 
 def impala_rollout(spec, lanes, n_lanes, seed, jiggle=True, bn_mean=None, bn_var=None, record=False, out=None,

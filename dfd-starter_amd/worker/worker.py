@@ -90,9 +90,11 @@ class Worker(object):
         arrs = (d[:8 * n].view(torch.int64), d[8 * n:9 * n].view(torch.int8), d[9 * n:].view(torch.int8))
         return (arrs, ev) if defer_wait else arrs
 
-    def launch(self, idx, sign, det, seed=None, out=None, jiggle=True, lane_offset=0, lanes_dev=None):
+    def launch(self, idx, sign, det, seed=None, out=None, jiggle=True, lane_offset=0, lanes_dev=None, pairs=False):
         """Run one rollout over explicit lanes (host arrays) -> FDBatch (asynchronous).  lanes_dev: the same lanes
-        already on the device (idx, sign, det), e.g. uploaded ahead by evaluate(prefetch=True)."""
+        already on the device (idx, sign, det), e.g. uploaded ahead by evaluate(prefetch=True).  pairs: lanes 2p,
+        2p+1 are antithetic pairs (checked here) -- an fp16 Impala rollout then streams each pair's sigma-eps once
+        (fdr_impala_desc.pairs)."""
         p = self.policy
         n = len(idx)
         idx_d, sign_d, det_d = lanes_dev if lanes_dev is not None else self._lanes_to_device(idx, sign, det)
@@ -105,8 +107,12 @@ class Worker(object):
             # E envs per lane: returns are per (lane, env), lane-major; idx / sign / norm2 repeat per env
             E = self.agent.env.envs_per_lane
             roll = engine.impala_rollout if p.KIND == "impala" else engine.atari_rollout
-            res = roll(self.agent.env.spec(), lanes, n, seed, jiggle=jiggle, bn_mean=bm, bn_var=bv,
-                       device=p.flat.device)
+            spec = self.agent.env.spec()
+            if pairs and p.KIND == "impala" and getattr(spec, "fp16", False):
+                ii, ss = np.asarray(idx), np.asarray(sign)
+                spec.pairs = bool(n % 2 == 0 and np.array_equal(ii[0::2], ii[1::2])
+                                  and np.all(ss[0::2].astype(np.int32) == -ss[1::2].astype(np.int32)))
+            res = roll(spec, lanes, n, seed, jiggle=jiggle, bn_mean=bm, bn_var=bv, device=p.flat.device)
             if E > 1:
                 res.norm2 = res.norm2.repeat_interleave(E)
                 idx_d, sign_d = idx_d.repeat_interleave(E), sign_d.repeat_interleave(E)
@@ -158,7 +164,8 @@ class Worker(object):
             torch.cuda.current_stream(self.policy.flat.device).wait_event(ev)  # right before the rollout
         lpd = 2 if antithetic else 1
         lo = 0 if lane_range is None else lane_range[0]
-        res, idx_d, sign_d = self.launch(lidx, sign, det, seed=seed, out=out, lane_offset=lo, lanes_dev=lanes_dev)
+        res, idx_d, sign_d = self.launch(lidx, sign, det, seed=seed, out=out, lane_offset=lo, lanes_dev=lanes_dev,
+                                         pairs=antithetic)
         if prefetch and hasattr(self.noise_source, "peek_batch"):
             nidx = self.noise_source.peek_batch(n_dirs)
             nl, ns, nd, _, _ = self._lanes_of(nidx, n_dirs, antithetic, key[2])

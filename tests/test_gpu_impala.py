@@ -324,8 +324,33 @@ def test_fp16_multistep_drift_bound_vs_f32_oracle(engine, table):
     np.testing.assert_allclose(out.reward.cpu().numpy() - ret, 0.0, atol=2e-12)   # +- jiggle only
 
 
-@pytest.mark.parametrize("fp16", [False, True])
-def test_full_size_rollout_properties(engine, fp16):
+def test_fp16_pair_core_matches_per_lane_core(engine, table):
+    """fdr_impala_desc.pairs (config 5's antithetic pairs): the core step forms w = f16(theta) + s f16(sigma eps)
+    from theta's shared half pack and the pair's sigma-eps half pack instead of streaming each lane's
+    f16(theta + s sigma eps).  Step 0 sees identical conv features in both forms: probabilities within the fp16
+    tolerance of the per-lane form and of the f32 path; norms identical; whole episodes finite."""
+    A, E, T = 4, 4, 5
+    theta = _theta(A)
+    idx = np.repeat(np.array([77, 2_000_000, 3_000_000, 4_500_000], np.int64), 2)
+    sign = np.tile(np.array([1, -1], np.int8), 4)
+    dev = "cuda"
+    lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
+                              torch.tensor(idx, device=dev), torch.tensor(sign, device=dev), 0.02)
+    outs = {}
+    for name, fp16, pairs in (("lane", True, False), ("pair", True, True), ("f32", False, False)):
+        outs[name] = engine.impala_rollout(engine.ImpalaSpec(A, E, T, env_seed=5, fp16=fp16, pairs=pairs), lanes,
+                                           len(idx), 11, record=True)
+    torch.cuda.synchronize()
+    p_pair = outs["pair"].probs.cpu().numpy()[:, 0]
+    np.testing.assert_allclose(p_pair, outs["lane"].probs.cpu().numpy()[:, 0], rtol=F16_RTOL / 4)
+    np.testing.assert_allclose(p_pair, outs["f32"].probs.cpu().numpy()[:, 0], rtol=F16_RTOL)
+    np.testing.assert_array_equal(outs["pair"].norm2.cpu().numpy(), outs["lane"].norm2.cpu().numpy())
+    for t in (outs["pair"].reward, outs["pair"].entropy):
+        assert np.all(np.isfinite(t.cpu().numpy()))
+
+
+@pytest.mark.parametrize("fp16,pairs", [(False, False), (True, False), (True, True)])
+def test_full_size_rollout_properties(engine, fp16, pairs):
     """BASELINE configs 4/5 at full size (1024 lanes x 4 envs x T = 1000, A = 6 / 4): bitwise reproducible,
     antithetic lanes have identical ||lambda||^2, returns integer (+- jiggle) within [-T, T], entropies finite
     in (0, ln A]."""
@@ -338,7 +363,7 @@ def test_full_size_rollout_properties(engine, fp16):
     idx = torch.as_tensor(np.repeat(np.random.RandomState(4).randint(0, 25_000_000 - P, size=L // 2), 2), device=dev)
     sign = torch.as_tensor(np.tile(np.array([1, -1], np.int8), L // 2), device=dev)
     lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, tab, idx, sign, 0.02)
-    spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=fp16)
+    spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=fp16, pairs=pairs)
     outs = []
     for _ in range(2):
         o = engine.impala_rollout(spec, lanes, L, 123)
