@@ -386,9 +386,9 @@ def main():
         conv_launch_ms = conv_ms / T
         achieved_tf = IMPALA_CONV_FLOP * L * E / (conv_launch_ms * 1e-3) / 1e12
         core_bytes = IMPALA_CORE_BYTES // (2 if fp16 else 1)
-        # fp16 antithetic pairs (fdr_impala_desc.pairs): one sigma-eps stream per pair from HBM + theta's shared
-        # half pack (L2-resident) -- the algorithmic HBM bytes are half the per-lane stream's
-        core_hbm = core_bytes * (L // 2 + 1) if fp16 else core_bytes * L
+        # antithetic pairs (fdr_impala_desc.pairs): one sigma-eps stream per pair from HBM + theta's shared pack
+        # (L2 / MALL-resident) -- the algorithmic HBM bytes are half the per-lane stream's
+        core_hbm = core_bytes * (L // 2 + 1)
         core_gbs = core_hbm / (core_ms / T * 1e-3) / 1e9
         peak = FP16_PEAK_TFLOPS if fp16 else FP32_PEAK_TFLOPS
         core_prof = None if prof is None else prof.get("core_kernel")
@@ -403,7 +403,7 @@ def main():
                                     "unit": "GB/s", "frac": round(core_gbs / HBM_PEAK_GBS, 4),
                                     "launch_ms": round(core_ms / T, 4), "bytes_per_lane_step": core_bytes,
                                     "hbm_bytes_per_launch_algorithmic": core_hbm,
-                                    "form": "pair (theta + s sigma-eps)" if fp16 else "per lane",
+                                    "form": "pair (theta + s sigma-eps)",
                                     "traffic": None if core_prof is None else core_prof.get("hbm_bytes_per_launch")},
                     "entropy_replay_ms": round(replay_ms, 3),
                     "profile": None if prof is None else "profiles/%s_summary.md" % prof.get("tag"),

@@ -80,10 +80,12 @@ struct StepArgs {
   const float* reward_in;  // forward: reward carried by the obs
   const float* notdone;    // forward: done mask (policies/impala.py:170-176)
   uint64_t* dbg;           // diagnostics: phase clocks of conv workgroup 0 (fdr_impala_debug_clock) or NULL
-  // pair form of the fp16 rollout core step (fdr_impala_desc.pairs): theta's half pack, the pairs' sigma-eps
-  // half packs [n_lanes / 2][hpack], the lanes' signs
+  // pair form of the rollout core step (fdr_impala_desc.pairs): theta's (half) pack, the pairs' sigma-eps
+  // (half) packs [n_lanes / 2][stride], the lanes' signs -- f16 operands in fp16 mode, f32 otherwise
   const _Float16* th;
   const _Float16* ep;
+  const float* th32;
+  const float* ep32;
   int64_t ep_stride;
   const int8_t* sign;
 };
@@ -208,10 +210,12 @@ template <int E, int MODE>
 __global__ void core_kernel_h(Layout L, StepArgs a);
 template <int E>
 __global__ void core_kernel_hp(Layout L, StepArgs a);  // pair form (rollout mode), grid n_lanes / 2
+template <int E>
+__global__ void core_kernel_p(Layout L, StepArgs a);   // f32 pair form (rollout mode, bit-exact), grid n_lanes / 2
 constexpr int kHThreads = 512;
 
 struct Plan {  // workspace carve-up (byte offsets)
-  int64_t pack, hpack, feat, h, c, rprev, ci, gx, n2, zeros, thpack, epack, idxe, total;
+  int64_t pack, hpack, feat, h, c, rprev, ci, gx, n2, zeros, thpack, epack, idxe, n2x, total;
   int nblk;    // prep blocks per lane
 };
 // pairs: the fp16 pair form (theta half pack, one sigma-eps half pack per pair, a zero base, pair offsets)

@@ -136,11 +136,13 @@ Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16
   p.ci = take(entropy ? (int64_t)T * ne * kCoreIn * 4 : 0);
   p.gx = take(entropy ? (int64_t)std::min(T, kReplayChunk) * ne * kGates * 4 : 0);
   p.n2 = take((int64_t)n_lanes * p.nblk * 8);
-  const bool pr = fp16 && pairs && pair_core_supported(envs);
+  const bool pr = pairs && pair_core_supported(envs);
+  const int64_t plen = fp16 ? L.hpack * 2 : L.pack * 4;  // one (half) pack in bytes
   p.zeros = take(pr ? L.P * 4 : 0);
-  p.thpack = take(pr ? L.hpack * 2 : 0);
-  p.epack = take(pr ? (int64_t)(n_lanes / 2) * L.hpack * 2 : 0);
+  p.thpack = take(pr ? plen : 0);
+  p.epack = take(pr ? (int64_t)(n_lanes / 2) * plen : 0);
   p.idxe = take(pr ? (int64_t)(n_lanes / 2) * 8 : 0);
+  p.n2x = take(pr && !fp16 ? (int64_t)(n_lanes / 2 + 1) * p.nblk * 8 : 0);  // the f32 pack kernels' n2 partials
   p.total = o;
   return p;
 }
@@ -860,6 +862,163 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
   if (j < E) core_finish<E, MODE>(a, logit, lane, j);
 }
 
+// ------------------------------------------------------------------------------------------
+// Pair form of the f32 rollout core step (fdr_impala_desc.pairs).  Lanes 2p, 2p+1 of an antithetic pair
+// share their table offset: their fc / LSTM weights are fl32(theta + s_l fl32(sigma eps)).  One workgroup
+// per pair streams the pair's fl32(sigma eps) pack once from HBM and theta's pack (read by every workgroup:
+// L2 / MALL) and forms w = fl32(theta + s_l E) in registers -- the per-lane pack's value bit for bit (an fma
+// with s = +-1 rounds theta +- E once), so every env sees core_kernel's exact fma chains; half its HBM bytes.
+// The pair's 2E envs are contiguous, biases / BN / head are each lane's own pack.
+// ------------------------------------------------------------------------------------------
+template <int E>
+__global__ __launch_bounds__(kCoreThreads) void core_kernel_p(Layout L, StepArgs a) {
+  constexpr int E2 = 2 * E;
+  __shared__ float xw[kFeat * E2];
+  float* cis = xw + kFeat * E2 / 2;
+  float* hs = cis + kCoreIn * E2;
+  float* logit = hs + kHid * E2;
+  static_assert(kFeat * E2 / 2 + (kCoreIn + kHid) * E2 + E2 * kMaxAct <= kFeat * E2, "core LDS aliasing");
+  const int pr = blockIdx.x, j = threadIdx.x;
+  const int l0 = 2 * pr;
+  const float* pk0 = a.pack + (int64_t)l0 * a.pack_stride;
+  const float* pk1 = pk0 + a.pack_stride;
+  const float sg0 = a.sign ? (float)a.sign[l0] : 1.f, sg1 = a.sign ? (float)a.sign[l0 + 1] : 1.f;
+  const float* ep = a.ep32 + (int64_t)pr * a.ep_stride;
+  const int64_t e0 = (int64_t)l0 * E;
+  const int A = a.n_act;
+  const int c4 = j & 63, wq = j >> 6;
+  auto pkof = [&](int e) { return e < E ? pk0 : pk1; };
+  // one streamed float4 row: w = fl32(theta + s_l E) per lane, then each env's fma chain of core_kernel
+  auto accum = [&](float (&acc)[4][E2], float4 t, float4 d, const float* x) {
+    const float tp[4] = {fmaf(sg0, d.x, t.x), fmaf(sg0, d.y, t.y), fmaf(sg0, d.z, t.z), fmaf(sg0, d.w, t.w)};
+    const float tm[4] = {fmaf(sg1, d.x, t.x), fmaf(sg1, d.y, t.y), fmaf(sg1, d.z, t.z), fmaf(sg1, d.w, t.w)};
+#pragma unroll
+    for (int e = 0; e < E2; ++e) {
+      const float xv = x[e];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c][e] = fmaf(e < E ? tp[c] : tm[c], xv, acc[c][e]);
+    }
+  };
+
+  for (int k = j; k < kFeat; k += kCoreThreads) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const float* pk = hf ? pk1 : pk0;
+      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + k] : 0.f;
+      const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + k] : 1.f;
+      const float sc = pk[L.bn_w[15] + k] * (1.f / sqrtf(rv + kBnEps));
+      const float sh = pk[L.bn_b[15] + k] - rm * sc;
+#pragma unroll
+      for (int e = 0; e < E; ++e) xw[k * E2 + hf * E + e] = fmaf(a.feat[(e0 + hf * E + e) * kFeat + k], sc, sh);
+    }
+  }
+  __syncthreads();
+  {
+    float acc[4][E2];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < E2; ++e) acc[c][e] = 0.f;
+    const float4* t4 = reinterpret_cast<const float4*>(a.th32 + L.fc_wt) + c4;
+    const float4* d4 = reinterpret_cast<const float4*>(ep + L.fc_wt) + c4;
+#pragma unroll FDR_CORE_UNROLL
+    for (int k = wq * (kFeat / 4); k < (wq + 1) * (kFeat / 4); ++k)
+      accum(acc, t4[(int64_t)k * (kHid / 4)], ld_stream(d4 + (int64_t)k * (kHid / 4)), xw + k * E2);
+    __syncthreads();  // xs is dead
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < E2; ++e) xw[(wq * kHid + 4 * c4 + c) * E2 + e] = acc[c][e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    const float y = ((xw[j * E2 + e] + xw[(kHid + j) * E2 + e]) + xw[(2 * kHid + j) * E2 + e]) +
+                    xw[(3 * kHid + j) * E2 + e];
+    cis[j * E2 + e] = relu(y + pkof(e)[L.fc_b + j]);
+  }
+  if (j < E2) cis[kHid * E2 + j] = fminf(fmaxf(a.rprev[e0 + j], -1.f), 1.f);
+  if (a.ci) {
+    __syncthreads();
+    float* dst = a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn;
+    for (int i = j; i < kCoreIn * E2; i += kCoreThreads) {
+      const int e = i / kCoreIn, k = i - e * kCoreIn;
+      dst[i] = cis[k * E2 + e];
+    }
+  }
+  float cj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    hs[j * E2 + e] = a.h[(e0 + e) * kHid + j];
+    cj[e] = a.c[(e0 + e) * kHid + j];
+  }
+  __syncthreads();
+  {
+    float ax[4][E2], ah[4][E2];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < E2; ++e) ax[c][e] = ah[c][e] = 0.f;
+    const float4* tl = reinterpret_cast<const float4*>(a.th32 + L.lstm_wt) + j;
+    const float4* dl = reinterpret_cast<const float4*>(ep + L.lstm_wt) + j;
+#pragma unroll FDR_CORE_UNROLL
+    for (int k = 0; k < kCoreIn; ++k)
+      accum(ax, tl[(int64_t)k * (kGates / 4)], ld_stream(dl + (int64_t)k * (kGates / 4)), cis + k * E2);
+#pragma unroll FDR_CORE_UNROLL
+    for (int k = 0; k < kHid; ++k)
+      accum(ah, tl[(int64_t)(kCoreIn + k) * (kGates / 4)], ld_stream(dl + (int64_t)(kCoreIn + k) * (kGates / 4)),
+            hs + k * E2);
+    const float4 bi0 = reinterpret_cast<const float4*>(pk0 + L.lstm_bih)[j];
+    const float4 bh0 = reinterpret_cast<const float4*>(pk0 + L.lstm_bhh)[j];
+    const float4 bi1 = reinterpret_cast<const float4*>(pk1 + L.lstm_bih)[j];
+    const float4 bh1 = reinterpret_cast<const float4*>(pk1 + L.lstm_bhh)[j];
+    const float bif0[4] = {bi0.x, bi0.y, bi0.z, bi0.w}, bhf0[4] = {bh0.x, bh0.y, bh0.z, bh0.w};
+    const float bif1[4] = {bi1.x, bi1.y, bi1.z, bi1.w}, bhf1[4] = {bh1.x, bh1.y, bh1.z, bh1.w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < E2; ++e)
+        xw[(4 * j + c) * E2 + e] = (ax[c][e] + (e < E ? bif0[c] : bif1[c])) + (ah[c][e] + (e < E ? bhf0[c] : bhf1[c]));
+  }
+  __syncthreads();
+  float hj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    const float gi = sigm(xw[j * E2 + e]);
+    const float gf = sigm(xw[(kHid + j) * E2 + e]);
+    const float gg = tanhf(xw[(2 * kHid + j) * E2 + e]);
+    const float go = sigm(xw[(3 * kHid + j) * E2 + e]);
+    cj[e] = gf * cj[e] + gi * gg;
+    hj[e] = go * tanhf(cj[e]);
+    a.h[(e0 + e) * kHid + j] = hj[e];
+    a.c[(e0 + e) * kHid + j] = cj[e];
+  }
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const float* pk = hf ? pk1 : pk0;
+    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
+    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
+    const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
+    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+#pragma unroll
+    for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
+  }
+  __syncthreads();
+  if (j < A * E2) {
+    const int ai = j / E2, e = j - ai * E2;
+    const float* pk = pkof(e);
+    const float* w = pk + L.head_w + ai * kHid;
+    float s = 0.f;
+    for (int k = 0; k < kHid; ++k) s = fmaf(w[k], hs[k * E2 + e], s);
+    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
+  }
+  __syncthreads();
+  if (j < E2) core_finish<E, kRollout>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
+}
+template __global__ void core_kernel_p<1>(Layout, StepArgs);
+template __global__ void core_kernel_p<2>(Layout, StepArgs);
+template __global__ void core_kernel_p<4>(Layout, StepArgs);
+
 __global__ void init_kernel(int64_t n_env, float* h, float* c, float* rprev, double* ret, double* ent) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (h && i < n_env * kHid) { h[i] = 0.f; c[i] = 0.f; }
@@ -1061,6 +1220,9 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
       if (h && a.ep) {
         hipLaunchKernelGGL((core_kernel_hp<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
         pair_done = true;
+      } else if (!h && a.ep32) {
+        hipLaunchKernelGGL((core_kernel_p<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
+        pair_done = true;
       }
     }
     if (pair_done) {
@@ -1134,30 +1296,41 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
     a.hpack = reinterpret_cast<_Float16*>(w + p.hpack);
     a.hpack_stride = L.hpack;
     launch_pack<_Float16>(L, c.lanes, a.hpack, n2, c.n_lanes, 1, stream);
-    if (c.pairs && pair_core_supported(c.envs) && c.lanes.table && c.lanes.base_stride == 0 && c.n_lanes >= 2) {
-      // the pair form's operands, built by the same pack kernels: theta's half pack (no table: theta' =
-      // theta) and per pair fl32(sigma eps) in f16 (a zero base, sign +1: fl32(0 + fl32(sigma eps)))
-      const int np = c.n_lanes / 2;
-      float* zeros = reinterpret_cast<float*>(w + p.zeros);
-      int64_t* idxe = reinterpret_cast<int64_t*>(w + p.idxe);
+  }
+  if (c.pairs && pair_core_supported(c.envs) && c.lanes.table && c.lanes.base_stride == 0 && c.n_lanes >= 2) {
+    // the pair form's operands, built by the same pack kernels: theta's pack (no table: theta' = theta) and
+    // per pair fl32(sigma eps) (a zero base, sign +1: fl32(0 + fl32(sigma eps))) -- f16 in fp16 mode
+    const int np = c.n_lanes / 2;
+    float* zeros = reinterpret_cast<float*>(w + p.zeros);
+    int64_t* idxe = reinterpret_cast<int64_t*>(w + p.idxe);
+    (void)hipMemsetAsync(zeros, 0, (size_t)L.P * 4, stream);
+    hipLaunchKernelGGL(pair_offsets_kernel, dim3((np + 255) / 256), dim3(256), 0, stream, c.lanes.idx, np, idxe);
+    LanesArgs lt = c.lanes;
+    lt.table = nullptr;
+    LanesArgs le = c.lanes;
+    le.base = zeros;
+    le.base_stride = 0;
+    le.idx = idxe;
+    le.sign = nullptr;
+    if (c.fp16) {
       _Float16* th = reinterpret_cast<_Float16*>(w + p.thpack);
       _Float16* ep = reinterpret_cast<_Float16*>(w + p.epack);
-      (void)hipMemsetAsync(zeros, 0, (size_t)L.P * 4, stream);
-      hipLaunchKernelGGL(pair_offsets_kernel, dim3((np + 255) / 256), dim3(256), 0, stream, c.lanes.idx, np, idxe);
-      LanesArgs lt = c.lanes;
-      lt.table = nullptr;
       launch_pack<_Float16>(L, lt, th, n2, 1, 1, stream);
-      LanesArgs le = c.lanes;
-      le.base = zeros;
-      le.base_stride = 0;
-      le.idx = idxe;
-      le.sign = nullptr;
       launch_pack<_Float16>(L, le, ep, n2, np, 1, stream);
       a.th = th;
       a.ep = ep;
       a.ep_stride = L.hpack;
-      a.sign = c.lanes.sign;
+    } else {  // f32: w = fl32(theta +- fl32(sigma eps)) in registers is the pack's value bit for bit
+      float* th = reinterpret_cast<float*>(w + p.thpack);
+      float* ep = reinterpret_cast<float*>(w + p.epack);
+      double* n2x = reinterpret_cast<double*>(w + p.n2x);  // these packs' norms are not the lanes'
+      launch_pack<float>(L, lt, th, n2x, 1, 0, stream);
+      launch_pack<float>(L, le, ep, n2x + p.nblk, np, 0, stream);
+      a.th32 = th;
+      a.ep32 = ep;
+      a.ep_stride = L.pack;
     }
+    a.sign = c.lanes.sign;
   }
   const int64_t ne = (int64_t)c.n_lanes * c.envs;
   hipLaunchKernelGGL(init_kernel, dim3((unsigned)((ne * kHid + 255) / 256)), dim3(256), 0, stream, ne, a.h, a.c,

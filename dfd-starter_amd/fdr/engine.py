@@ -331,8 +331,8 @@ class ImpalaSpec(object):
     """Shape of an ImpalaPolicy rollout: A actions, E envs per perturbation, T-step episodes."""
 
     def __init__(self, n_act, envs_per_lane=1, episode_len=1, entropy=True, env_seed=0, fp16=False, pairs=False):
-        """pairs (fp16 mode): lanes 2p, 2p+1 are antithetic pairs -- the rollout's core step streams each pair's
-        sigma-eps once (fdr_impala_desc.pairs)."""
+        """pairs: lanes 2p, 2p+1 are antithetic pairs -- the rollout's core step streams each pair's sigma-eps once
+        (fdr_impala_desc.pairs; f32: bit-identical to the per-lane form, fp16: within the fp16 tolerance)."""
         self.n_act, self.envs_per_lane, self.episode_len = int(n_act), int(envs_per_lane), int(episode_len)
         self.entropy, self.env_seed, self.fp16 = bool(entropy), int(env_seed), bool(fp16)
         self.pairs = bool(pairs)

@@ -93,7 +93,7 @@ class Worker(object):
     def launch(self, idx, sign, det, seed=None, out=None, jiggle=True, lane_offset=0, lanes_dev=None, pairs=False):
         """Run one rollout over explicit lanes (host arrays) -> FDBatch (asynchronous).  lanes_dev: the same lanes
         already on the device (idx, sign, det), e.g. uploaded ahead by evaluate(prefetch=True).  pairs: lanes 2p,
-        2p+1 are antithetic pairs (checked here) -- an fp16 Impala rollout then streams each pair's sigma-eps once
+        2p+1 are antithetic pairs (checked here) -- an Impala rollout then streams each pair's sigma-eps once
         (fdr_impala_desc.pairs)."""
         p = self.policy
         n = len(idx)
@@ -108,7 +108,7 @@ class Worker(object):
             E = self.agent.env.envs_per_lane
             roll = engine.impala_rollout if p.KIND == "impala" else engine.atari_rollout
             spec = self.agent.env.spec()
-            if pairs and p.KIND == "impala" and getattr(spec, "fp16", False):
+            if pairs and p.KIND == "impala":
                 ii, ss = np.asarray(idx), np.asarray(sign)
                 spec.pairs = bool(n % 2 == 0 and np.array_equal(ii[0::2], ii[1::2])
                                   and np.all(ss[0::2].astype(np.int32) == -ss[1::2].astype(np.int32)))

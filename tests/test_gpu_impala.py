@@ -349,7 +349,25 @@ def test_fp16_pair_core_matches_per_lane_core(engine, table):
         assert np.all(np.isfinite(t.cpu().numpy()))
 
 
-@pytest.mark.parametrize("fp16,pairs", [(False, False), (True, False), (True, True)])
+def test_f32_pair_core_bit_identical(engine, table):
+    """f32 pair form (fdr_impala_desc.pairs): w = fl32(theta + s fl32(sigma eps)) formed in registers is the
+    per-lane pack's value bit for bit, and every env keeps core_kernel's fma chains -- whole episodes with the
+    entropy replay are bitwise identical to the per-lane form (actions, probabilities, returns, entropies)."""
+    A, E, T = 6, 4, 40
+    theta = _theta(A)
+    idx = np.repeat(np.array([77, 2_000_000, 3_000_000], np.int64), 2)
+    sign = np.tile(np.array([1, -1], np.int8), 3)
+    dev = "cuda"
+    lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
+                              torch.tensor(idx, device=dev), torch.tensor(sign, device=dev), 0.02)
+    o = [engine.impala_rollout(engine.ImpalaSpec(A, E, T, env_seed=5, pairs=pr), lanes, len(idx), 11, record=True)
+         for pr in (False, True)]
+    torch.cuda.synchronize()
+    for f in ("actions", "probs", "reward", "entropy", "norm2"):
+        np.testing.assert_array_equal(getattr(o[0], f).cpu().numpy(), getattr(o[1], f).cpu().numpy())
+
+
+@pytest.mark.parametrize("fp16,pairs", [(False, False), (False, True), (True, False), (True, True)])
 def test_full_size_rollout_properties(engine, fp16, pairs):
     """BASELINE configs 4/5 at full size (1024 lanes x 4 envs x T = 1000, A = 6 / 4): bitwise reproducible,
     antithetic lanes have identical ||lambda||^2, returns integer (+- jiggle) within [-T, T], entropies finite
