@@ -185,29 +185,15 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
     }
   }
   if constexpr (CIN != 3) {
-    // B fragments one K-step ahead: step s+1's TPW reads are issued before step s's MFMAs, so every
-    // ds_read's latency hides behind MFMA work (load-then-use left two reads in flight per two MFMAs and the
-    // MFMA unit ~1/3 busy inside the conv phases: r05 ISA + PMC)
-    h8 bq[2][TPW];
-    auto load_b = [&](int s, h8 (&dst)[TPW]) {
-      const int o = k_offset<CIN, CS, WP>(s, g, 0);
-#pragma unroll
-      for (int i = 0; i < TPW; ++i)
-        if (live(i)) dst[i] = *reinterpret_cast<const h8*>(Tin + base[i] + o);
-    };
-    load_b(0, bq[0]);
 #pragma unroll
     for (int s = 0; s < KSteps<CIN>::NF; ++s) {
-      if (s + 1 < KSteps<CIN>::NF) load_b(s + 1, bq[(s + 1) & 1]);
-      // keep the prefetch ahead of this step's MFMAs: the machine scheduler otherwise sinks each read to just
-      // before its use (register-pressure heuristic), recreating the load-then-use chain
-      __builtin_amdgcn_sched_barrier(0);
+      const int o = k_offset<CIN, CS, WP>(s, g, 0);
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         if (!live(i)) continue;
+        const h8 b = *reinterpret_cast<const h8*>(Tin + base[i] + o);
 #pragma unroll
-        for (int nt = 0; nt < NT; ++nt)
-          acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], bq[s & 1][i], acc[i][nt], 0, 0, 0);
+        for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b, acc[i][nt], 0, 0, 0);
       }
     }
   }
