@@ -212,6 +212,10 @@ template <int E>
 __global__ void core_kernel_hp(Layout L, StepArgs a);  // pair form (rollout mode), grid n_lanes / 2
 template <int E>
 __global__ void core_kernel_p(Layout L, StepArgs a);   // f32 pair form (rollout mode, bit-exact), grid n_lanes / 2
+template <int E>
+__global__ void core_kernel_pr(Layout L, StepArgs a);  // f32 pair form of the replay (with a.gx)
+template <int E>
+__global__ void core_kernel_hpr(Layout L, StepArgs a); // fp16 pair form of the replay (with a.gx)
 constexpr int kHThreads = 512;
 
 struct Plan {  // workspace carve-up (byte offsets)

@@ -1015,6 +1015,107 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_p(Layout L, StepArgs
   __syncthreads();
   if (j < E2) core_finish<E, kRollout>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
 }
+// Replay (entropy pass) in the pair form: the x W_ih^T half of the gates comes precomputed per env
+// (lstm_xproj_kernel, a.gx), the W_hh h half streams theta + s_l fl32(sigma eps) for the pair -- the same
+// values and fma chains as core_kernel<E, kReplay> (bit-identical), half its W_hh bytes.
+template <int E>
+__global__ __launch_bounds__(kCoreThreads) void core_kernel_pr(Layout L, StepArgs a) {
+  constexpr int E2 = 2 * E;
+  __shared__ float xw[kGates * E2 + kHid * E2 + E2 * kMaxAct];
+  float* hs = xw + kGates * E2;
+  float* logit = hs + kHid * E2;
+  const int pr = blockIdx.x, j = threadIdx.x;
+  const int l0 = 2 * pr;
+  const float* pk0 = a.pack + (int64_t)l0 * a.pack_stride;
+  const float* pk1 = pk0 + a.pack_stride;
+  const float sg0 = a.sign ? (float)a.sign[l0] : 1.f, sg1 = a.sign ? (float)a.sign[l0 + 1] : 1.f;
+  const float* ep = a.ep32 + (int64_t)pr * a.ep_stride;
+  const int64_t e0 = (int64_t)l0 * E;
+  const int A = a.n_act;
+  float cj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    hs[j * E2 + e] = a.h[(e0 + e) * kHid + j];
+    cj[e] = a.c[(e0 + e) * kHid + j];
+  }
+  __syncthreads();
+  {
+    float ah[4][E2];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < E2; ++e) ah[c][e] = 0.f;
+    const float4* tl = reinterpret_cast<const float4*>(a.th32 + L.lstm_wt) + j;
+    const float4* dl = reinterpret_cast<const float4*>(ep + L.lstm_wt) + j;
+#pragma unroll FDR_CORE_UNROLL
+    for (int k = 0; k < kHid; ++k) {
+      const float4 t = tl[(int64_t)(kCoreIn + k) * (kGates / 4)];
+      const float4 d = ld_stream(dl + (int64_t)(kCoreIn + k) * (kGates / 4));
+      const float tp[4] = {fmaf(sg0, d.x, t.x), fmaf(sg0, d.y, t.y), fmaf(sg0, d.z, t.z), fmaf(sg0, d.w, t.w)};
+      const float tm[4] = {fmaf(sg1, d.x, t.x), fmaf(sg1, d.y, t.y), fmaf(sg1, d.z, t.z), fmaf(sg1, d.w, t.w)};
+#pragma unroll
+      for (int e = 0; e < E2; ++e) {
+        const float xv = hs[k * E2 + e];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) ah[c][e] = fmaf(e < E ? tp[c] : tm[c], xv, ah[c][e]);
+      }
+    }
+    const float4* g4 = reinterpret_cast<const float4*>(a.gx + ((int64_t)(a.t - a.gx_t0) * a.n_lanes * E + e0) * kGates);
+    const float4 bi0 = reinterpret_cast<const float4*>(pk0 + L.lstm_bih)[j];
+    const float4 bh0 = reinterpret_cast<const float4*>(pk0 + L.lstm_bhh)[j];
+    const float4 bi1 = reinterpret_cast<const float4*>(pk1 + L.lstm_bih)[j];
+    const float4 bh1 = reinterpret_cast<const float4*>(pk1 + L.lstm_bhh)[j];
+    const float bif0[4] = {bi0.x, bi0.y, bi0.z, bi0.w}, bhf0[4] = {bh0.x, bh0.y, bh0.z, bh0.w};
+    const float bif1[4] = {bi1.x, bi1.y, bi1.z, bi1.w}, bhf1[4] = {bh1.x, bh1.y, bh1.z, bh1.w};
+#pragma unroll
+    for (int e = 0; e < E2; ++e) {
+      const float4 g = ld_stream(g4 + (int64_t)e * (kGates / 4) + j);
+      const float gxv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        xw[(4 * j + c) * E2 + e] = (gxv[c] + (e < E ? bif0[c] : bif1[c])) + (ah[c][e] + (e < E ? bhf0[c] : bhf1[c]));
+    }
+  }
+  __syncthreads();
+  float hj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    const float gi = sigm(xw[j * E2 + e]);
+    const float gf = sigm(xw[(kHid + j) * E2 + e]);
+    const float gg = tanhf(xw[(2 * kHid + j) * E2 + e]);
+    const float go = sigm(xw[(3 * kHid + j) * E2 + e]);
+    cj[e] = gf * cj[e] + gi * gg;
+    hj[e] = go * tanhf(cj[e]);
+    a.h[(e0 + e) * kHid + j] = hj[e];
+    a.c[(e0 + e) * kHid + j] = cj[e];
+  }
+  __syncthreads();  // every read of hs is done before BN(h') overwrites it
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const float* pk = hf ? pk1 : pk0;
+    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
+    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
+    const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
+    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+#pragma unroll
+    for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
+  }
+  __syncthreads();
+  if (j < A * E2) {
+    const int ai = j / E2, e = j - ai * E2;
+    const float* pk = e < E ? pk0 : pk1;
+    const float* w = pk + L.head_w + ai * kHid;
+    float s = 0.f;
+    for (int k = 0; k < kHid; ++k) s = fmaf(w[k], hs[k * E2 + e], s);
+    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
+  }
+  __syncthreads();
+  if (j < E2) core_finish<E, kReplay>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
+}
+template __global__ void core_kernel_pr<1>(Layout, StepArgs);
+template __global__ void core_kernel_pr<2>(Layout, StepArgs);
+template __global__ void core_kernel_pr<4>(Layout, StepArgs);
+
 template __global__ void core_kernel_p<1>(Layout, StepArgs);
 template __global__ void core_kernel_p<2>(Layout, StepArgs);
 template __global__ void core_kernel_p<4>(Layout, StepArgs);
@@ -1248,7 +1349,18 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
       }
       for (int t = t0; t < t0 + tc; ++t) {
         a.t = t;
-        if (h)
+        bool pair_done = false;
+        if constexpr (E <= 4) {
+          if (a.gx && h && a.ep) {
+            hipLaunchKernelGGL((core_kernel_hpr<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
+            pair_done = true;
+          } else if (a.gx && !h && a.ep32) {
+            hipLaunchKernelGGL((core_kernel_pr<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
+            pair_done = true;
+          }
+        }
+        if (pair_done) {
+        } else if (h)
           hipLaunchKernelGGL((core_kernel_h<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
         else
           hipLaunchKernelGGL((core_kernel<E, kReplay>), dim3(a.n_lanes), dim3(kCoreThreads), 0, stream, L, a);

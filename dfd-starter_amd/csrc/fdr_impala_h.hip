@@ -901,6 +901,110 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_hp(Layout L, StepArg
   if (j < E2) core_finish<E, kRollout>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
 }
 
+// Replay (entropy pass) in the fp16 pair form: x W_ih^T precomputed per env (a.gx), W_hh^T streamed as
+// f16(theta) + s_l f16(sigma eps) for the pair (4 columns per thread, as core_kernel_h's replay).
+template <int E>
+__global__ __launch_bounds__(kCoreThreads) void core_kernel_hpr(Layout L, StepArgs a) {
+  constexpr int E2 = 2 * E;
+  typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+  __shared__ float xw[2 * kGates * E2];
+  __shared__ float hs[kHid * E2];
+  float* logit = xw;
+  const int pr = blockIdx.x, j = threadIdx.x;
+  const int l0 = 2 * pr;
+  const float* pk0 = a.pack + (int64_t)l0 * a.pack_stride;
+  const float* pk1 = pk0 + a.pack_stride;
+  const float sg0 = a.sign ? (float)a.sign[l0] : 1.f, sg1 = a.sign ? (float)a.sign[l0 + 1] : 1.f;
+  const _Float16* eh = a.ep + (int64_t)pr * a.ep_stride;
+  const int64_t e0 = (int64_t)l0 * E;
+  const int A = a.n_act;
+  float cj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    hs[j * E2 + e] = a.h[(e0 + e) * kHid + j];
+    cj[e] = a.c[(e0 + e) * kHid + j];
+  }
+  __syncthreads();
+  {
+    float acc[4][E2];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int e = 0; e < E2; ++e) acc[c][e] = 0.f;
+    const h4v* t4 = reinterpret_cast<const h4v*>(a.th + L.lstm_wt_h) + j;
+    const h4v* d4 = reinterpret_cast<const h4v*>(eh + L.lstm_wt_h) + j;
+#pragma unroll FDR_CORE_UNROLL
+    for (int k = 0; k < kHid; ++k) {
+      const h4v t = t4[(int64_t)(kCoreIn + k) * (kGates / 4)];
+      const h4v d = ld_stream(d4 + (int64_t)(kCoreIn + k) * (kGates / 4));
+      float wp[4], wm[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        wp[c] = fmaf(sg0, (float)d[c], (float)t[c]);
+        wm[c] = fmaf(sg1, (float)d[c], (float)t[c]);
+      }
+#pragma unroll
+      for (int e = 0; e < E2; ++e) {
+        const float xv = hs[k * E2 + e];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c][e] = fmaf(e < E ? wp[c] : wm[c], xv, acc[c][e]);
+      }
+    }
+    const float4* g4 = reinterpret_cast<const float4*>(a.gx + ((int64_t)(a.t - a.gx_t0) * a.n_lanes * E + e0) * kGates);
+#pragma unroll
+    for (int e = 0; e < E2; ++e) {
+      const float4 g = ld_stream(g4 + (int64_t)e * (kGates / 4) + j);
+      const float gx4[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        xw[(4 * j + c) * E2 + e] = gx4[c];
+        xw[(kGates + 4 * j + c) * E2 + e] = acc[c][e];
+      }
+    }
+  }
+  __syncthreads();
+  float hj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    const float* pk = e < E ? pk0 : pk1;
+    float pre[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int col = g * kHid + j;
+      pre[g] = (xw[col * E2 + e] + pk[L.lstm_bih + col]) + (xw[(kGates + col) * E2 + e] + pk[L.lstm_bhh + col]);
+    }
+    const float gi = sigm(pre[0]), gf = sigm(pre[1]), gg = tanhf(pre[2]), go = sigm(pre[3]);
+    cj[e] = gf * cj[e] + gi * gg;
+    hj[e] = go * tanhf(cj[e]);
+    a.h[(e0 + e) * kHid + j] = hj[e];
+    a.c[(e0 + e) * kHid + j] = cj[e];
+  }
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const float* pk = hf ? pk1 : pk0;
+    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
+    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
+    const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
+    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+#pragma unroll
+    for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
+  }
+  __syncthreads();  // gates read (xw) and BN(h') written before the logits reuse xw
+  if (j < A * E2) {
+    const int ai = j / E2, e = j - ai * E2;
+    const float* pk = e < E ? pk0 : pk1;
+    const float* w = pk + L.head_w + ai * kHid;
+    float s = 0.f;
+    for (int k = 0; k < kHid; ++k) s = fmaf(w[k], hs[k * E2 + e], s);
+    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
+  }
+  __syncthreads();
+  if (j < E2) core_finish<E, kReplay>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
+}
+template __global__ void core_kernel_hpr<1>(Layout, StepArgs);
+template __global__ void core_kernel_hpr<2>(Layout, StepArgs);
+template __global__ void core_kernel_hpr<4>(Layout, StepArgs);
+
 template __global__ void core_kernel_hp<1>(Layout, StepArgs);
 template __global__ void core_kernel_hp<2>(Layout, StepArgs);
 template __global__ void core_kernel_hp<4>(Layout, StepArgs);
