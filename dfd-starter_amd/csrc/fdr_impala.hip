@@ -358,7 +358,32 @@ struct Plane {  // padded [H+2][H+2] image, bank-staggered plane stride
   static constexpr int P = H == 64 ? RAW : RAW + ((16 - RAW % 64) % 64 + 64) % 64 + (H == 8 ? 2 : 0);
 };
 static_assert(Plane<32>::P == 1168 && Plane<16>::P == 336 && Plane<8>::P == 146, "plane strides");
-static_assert(16 * Plane<32>::P <= kTE && 3 * Plane<64>::P + 16 * kBand * 65 <= kTE, "LDS plan");
+
+// Channel skew of a padded plane (words), for the strides = 16 (mod 32) banks.  ds_write_b32 banks are
+// (a/4) mod 32 over 32-lane halves: an epilogue store of one M-tile (lanes: 16 channels x 2 pixel
+// quads) then hits 4 banks in 32 without the skew, an 8-way conflict (r05 PMC: SQ_LDS_BANK_CONFLICT
+// 15 % of the conv kernel's cycles).  With bits (c>>1)&1 -> 8 and (c>>2)&3 -> 0..3 the 32 lanes land on 32
+// banks.  An MFMA A-read takes channels 4q + g (g = lane >> 4): its skew (g>>1) 8 + (q & 3) is uniform
+// per 32-lane half, so the reads stay conflict-free.
+template <int PLANE>
+__device__ __forceinline__ constexpr int cskew(int c) {
+  return PLANE % 32 == 16 ? ((c >> 1) & 1) * 8 + ((c >> 2) & 3) : 0;
+}
+constexpr int kSkewPad = 16;  // room for the last plane's skew (<= 11) before the next region
+
+// X [C][H][H] with a per-channel XOR on bits 2-5 of the pixel index (HH >= 64): the residual read-modify-
+// write of an epilogue (lane: channel n, 4 pixels) goes from 16 channels on one 4-bank group to 16
+// distinct groups (ds_read_b128 / ds_write_b128 conflict-free); pool writes and the float4 reads of
+// to_padded stay contiguous.
+template <int HH>
+__device__ __forceinline__ int xpos(int c, int m) {
+  static_assert(HH >= 64, "swizzle spans 64 pixels");
+  return c * HH + (m ^ ((c & 15) << 2));
+}
+
+static_assert(16 * Plane<32>::P + kSkewPad <= kTE && 3 * Plane<64>::P + 16 * kBand * 65 <= kTE, "LDS plan");
+static_assert(16 * Plane<32>::P + kSkewPad + 32 * kBand * 33 + 32 * 16 * 16 <= kTE + kRX, "LDS plan, stage 2");
+static_assert(32 * Plane<16>::P + kSkewPad + 32 * 17 * 17 + 32 * 8 * 8 <= kTE + kRX, "LDS plan, stage 3");
 
 
 // B fragments of one conv for this wave's N-tile: bf[s] = B[k = 4s + (lane >> 4)][n], one VGPR each.
@@ -390,11 +415,11 @@ __device__ __forceinline__ void conv_mfma(const float* Tin, const float (&bf)[(9
   }
   if constexpr ((CIN & 3) == 0) {
 #pragma unroll
-    for (int i = 0; i < TPW; ++i) base[i] += g * PLANE;
+    for (int i = 0; i < TPW; ++i) base[i] += g * PLANE + cskew<PLANE>(g);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const int tap = s / (CIN / 4);
-      const int off = 4 * (s % (CIN / 4)) * PLANE + (tap / 3) * WP + (tap % 3);
+      const int tap = s / (CIN / 4), q = s % (CIN / 4);
+      const int off = 4 * q * PLANE + cskew<PLANE>(4 * q) + (tap / 3) * WP + (tap % 3);
 #pragma unroll
       for (int i = 0; i < TPW; ++i)
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(Tin[base[i] + off], bf[s], acc[i], 0, 0, 0);
@@ -404,7 +429,7 @@ __device__ __forceinline__ void conv_mfma(const float* Tin, const float (&bf)[(9
     for (int s = 0; s < KS; ++s) {
       const int k = 4 * s + g;
       const int tap = k / CIN, ci = k - tap * CIN;
-      const int off = k < 9 * CIN ? ci * PLANE + (tap / 3) * WP + (tap % 3) : 0;  // pad k: weight 0
+      const int off = k < 9 * CIN ? ci * PLANE + cskew<PLANE>(ci) + (tap / 3) * WP + (tap % 3) : 0;  // pad k: weight 0
 #pragma unroll
       for (int i = 0; i < TPW; ++i)
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(Tin[base[i] + off], bf[s], acc[i], 0, 0, 0);
@@ -434,18 +459,18 @@ __device__ __forceinline__ void to_padded(const float* X, float* T, const float*
   // interior, 4 consecutive x per thread (one ds_read_b128 of X)
   for (int i = threadIdx.x; i < C * H * H / 4; i += kConvThreads) {
     const int e = 4 * i, ch = e >> (2 * LH), y = (e >> LH) & (H - 1), x = e & (H - 1);
-    const float4 v = *reinterpret_cast<const float4*>(X + e);
+    const float4 v = *reinterpret_cast<const float4*>(X + xpos<H * H>(ch, e & (H * H - 1)));
     const float a = sc[ch], b = sh[ch];
     float o0 = fmaf(v.x, a, b), o1 = fmaf(v.y, a, b), o2 = fmaf(v.z, a, b), o3 = fmaf(v.w, a, b);
     if (RELU) { o0 = relu(o0); o1 = relu(o1); o2 = relu(o2); o3 = relu(o3); }
-    float* d = T + ch * PL + (y + 1) * WP + x + 1;
+    float* d = T + ch * PL + cskew<PL>(ch) + (y + 1) * WP + x + 1;
     d[0] = o0; d[1] = o1; d[2] = o2; d[3] = o3;
   }
   if (BORDER) {  // 4 (H + 1) border cells per plane
     for (int i = threadIdx.x; i < C * 4 * (H + 1); i += kConvThreads) {
       const int ch = i / (4 * (H + 1)), r = i - ch * 4 * (H + 1), side = r / (H + 1), k = r - side * (H + 1);
       const int off = side == 0 ? k : side == 1 ? (H + 1) * WP + 1 + k : side == 2 ? (k + 1) * WP : k * WP + WP - 1;
-      T[ch * PL + off] = 0.f;
+      T[ch * PL + cskew<PL>(ch) + off] = 0.f;
     }
   }
 }
@@ -496,7 +521,7 @@ __device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, 
       }
 #pragma unroll
       for (int pr = 0; pr < PRB; ++pr)
-        X[(ch * HO + PRB * b + pr) * HO + px] = fmaxf(fmaxf(hm[2 * pr], hm[2 * pr + 1]), hm[2 * pr + 2]);
+        X[xpos<HO * HO>(ch, (PRB * b + pr) * HO + px)] = fmaxf(fmaxf(hm[2 * pr], hm[2 * pr + 1]), hm[2 * pr + 2]);
     }
     __syncthreads();
     if (a.dbg) {
@@ -525,7 +550,7 @@ __device__ __forceinline__ void res_blocks(float* T, float* X, float (&bf)[(9 * 
   constexpr int WP = H + 2, PLANE = Plane<H>::P, NT = C / 16, MT = H * H / 16;
   constexpr int TPW = (MT * NT + 7) / 8;
   const int n_ = (wave % NT) * 16 + (lane & 15);
-  auto tpos = [&](int n, int m) { return n * PLANE + (m / H + 1) * WP + (m % H) + 1; };
+  auto tpos = [&](int n, int m) { return n * PLANE + cskew<PLANE>(n) + (m / H + 1) * WP + (m % H) + 1; };
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int i0 = stage * 5 + 1 + 2 * r, i1 = i0 + 1;
@@ -556,8 +581,9 @@ __device__ __forceinline__ void res_blocks(float* T, float* X, float (&bf)[(9 * 
         const int m0 = (q / NT) * 16 + (lane >> 4) * 4;
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
-          const float xn = (acc[i][rr] + b1) + X[n_ * H * H + m0 + rr];
-          X[n_ * H * H + m0 + rr] = xn;
+          const int xp = xpos<H * H>(n_, m0) + rr;  // the swizzle keeps the 4 pixels contiguous
+          const float xn = (acc[i][rr] + b1) + X[xp];
+          X[xp] = xn;
           acc[i][rr] = xn;
         }
       }
@@ -565,11 +591,11 @@ __device__ __forceinline__ void res_blocks(float* T, float* X, float (&bf)[(9 * 
       load_frag<C, NT>(pk + L.conv_w[i1 + 1], bf, wave, lane);  // block 1's first conv
     } else if (!LAST) {
       conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) {
-        T[tpos(n, m)] = fmaf((v + b1) + X[n * H * H + m], s2, h2);
+        T[tpos(n, m)] = fmaf((v + b1) + X[xpos<H * H>(n, m)], s2, h2);
       });
     } else {
       conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) {
-        out[n * H * H + m] = relu((v + b1) + X[n * H * H + m]);   // flatten (C, H, W), impala.py:159-160
+        out[n * H * H + m] = relu((v + b1) + X[xpos<H * H>(n, m)]);   // flatten (C, H, W), impala.py:159-160
       });
     }
     __syncthreads();
@@ -647,12 +673,12 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
     res_blocks<16, 32, 0>(T, X, bf, pk, L, 0, bsc, bsh, wave, ln, a, 4, nullptr);  // ends with T = BN5(X1)
   }
   // ---- stage 2: conv 16->32 @32x32 (S2 after T, over the dead X1), pool -> X2 [32][16][16] ----
-  float* X2 = T + 16 * Plane<32>::P + 32 * kBand * 33;
+  float* X2 = T + 16 * Plane<32>::P + kSkewPad + 32 * kBand * 33;
   {
     float bf[36];
     load_frag<16, 2>(pk + L.conv_w[5], bf, wave, ln);
     FDR_STAMP(a, 12);
-    stage_entry<16, 32, 32, Plane<32>::P, kBand>(T, T + 16 * Plane<32>::P, X2, bf, pk + L.conv_b[5], wave, ln, a, 48);
+    stage_entry<16, 32, 32, Plane<32>::P, kBand>(T, T + 16 * Plane<32>::P + kSkewPad, X2, bf, pk + L.conv_b[5], wave, ln, a, 48);
   }
   {
     float bf[72];
@@ -663,12 +689,12 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
     res_blocks<32, 16, 0>(T, X2, bf, pk, L, 1, bsc, bsh, wave, ln, a, 14, nullptr);  // ends with T = BN10(X2)
   }
   // ---- stage 3: conv 32->32 @16x16 in one 17-row band, pool -> X3 [32][8][8] ----
-  float* X3 = T + 32 * Plane<16>::P + 32 * 17 * 17;
+  float* X3 = T + 32 * Plane<16>::P + kSkewPad + 32 * 17 * 17;
   {
     float bf[72];
     load_frag<32, 2>(pk + L.conv_w[10], bf, wave, ln);
     FDR_STAMP(a, 22);
-    stage_entry<32, 32, 16, Plane<16>::P, 17>(T, T + 32 * Plane<16>::P, X3, bf, pk + L.conv_b[10], wave, ln, a, 56);
+    stage_entry<32, 32, 16, Plane<16>::P, 17>(T, T + 32 * Plane<16>::P + kSkewPad, X3, bf, pk + L.conv_b[10], wave, ln, a, 56);
   }
   {
     float bf[72];
