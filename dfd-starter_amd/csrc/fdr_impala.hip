@@ -479,7 +479,7 @@ __device__ __forceinline__ void to_padded(const float* X, float* T, const float*
 // BR = 9) through the scratch S [COUT][BR][1 + H], a RING of conv rows: conv row g lives in slot
 // (g + 1) mod BR, so a band's pool window (rows 8 b - 1 .. 8 b + 7) is the previous band's last row
 // plus the new ones -- no row is computed twice and every band is (BR-1) H / 16 tiles (a multiple
-// of the 8 waves).  Column 0 of S is -inf (the pool's left pad) and conv row -1 (slot 0 before
+// of the 8 waves).  Column -1 of S is -inf (the pool's left pad) and conv row -1 (slot 0 before
 // band 0) is -inf, so the pool is branch-free and separable -- one thread per (channel, pooled
 // column): BR horizontal max3, then vertical max3.  The B fragments are loaded by the caller and
 // reused by every band.
@@ -492,9 +492,16 @@ __device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, 
   static_assert((NR * H) % 16 == 0 && H % NR == 0 && NR % 2 == 0, "band shape");
   const float bn_ = bias[(wave % NT) * 16 + (lane & 15)];
   uint64_t t_conv = 0, t_pool = 0, t0 = a.dbg ? clock64() : 0;  // diagnostics (fdr_impala_debug_clock)
-  for (int i = threadIdx.x; i < COUT * BR; i += kConvThreads) S[i * SW] = -FLT_MAX;  // pad column
-  for (int i = threadIdx.x; i < COUT * H; i += kConvThreads)                         // conv row -1
-    S[(i / H) * BR * SW + 1 + i % H] = -FLT_MAX;
+  // H = 64: a scratch row holds the even columns, the pad (column -1), then the odd columns, so the pool's
+  // reads of columns 2px-1, 2px, 2px+1 are unit-stride across the 32 lanes of one channel (interleaved: stride
+  // 2, 2-way conflicts; stage-1 pool 10.2 K -> 7.5 K clocks).  H <= 32: the pad first, then columns in order --
+  // a 32-lane half spans 2+ channels whose odd channel stride puts them on the other bank parity.
+  constexpr bool DI = HO >= 32;
+  constexpr int PAD = DI ? HO : 0;
+  auto col = [](int x) { return DI ? ((x & 1) ? HO + 1 + (x >> 1) : (x >> 1)) : 1 + x; };
+  for (int i = threadIdx.x; i < COUT * BR; i += kConvThreads) S[i * SW + PAD] = -FLT_MAX;  // pad column
+  for (int i = threadIdx.x; i < COUT * H; i += kConvThreads)                              // conv row -1
+    S[(i / H) * BR * SW + col(i % H)] = -FLT_MAX;
   for (int b = 0; b < H / NR; ++b) {
     const int rot = (NR * b) % BR;  // slot of conv row NR b - 1
     auto slot = [&](int r) { return rot + r >= BR ? rot + r - BR : rot + r; };  // conv row NR b - 1 + r
@@ -502,7 +509,7 @@ __device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, 
     conv_mfma<CIN, NT, TPW, H, WP, PLANE, MT>(T + NR * b * WP, bf, acc, wave, lane);
     conv_out<NT, TPW, MT>(acc, wave, lane, [&](int n, int m, float v) {
       const int r = m / H, x = m % H;
-      S[(n * BR + slot(r + 1)) * SW + 1 + x] = v + bn_;
+      S[(n * BR + slot(r + 1)) * SW + col(x)] = v + bn_;
     });
     __syncthreads();
     if (a.dbg) {
@@ -512,12 +519,14 @@ __device__ __forceinline__ void stage_entry(const float* T, float* S, float* X, 
     }
     for (int i = threadIdx.x; i < COUT * HO; i += kConvThreads) {
       const int ch = i / HO, px = i - ch * HO;
-      const float* sc = S + ch * BR * SW + 2 * px;  // columns 2px-1 .. 2px+1 (+1 for the pad column)
+      // columns 2px-1, 2px, 2px+1
+      const float* sc = S + ch * BR * SW + (DI ? px : 2 * px);
+      constexpr int c0 = DI ? HO : 0, c1 = DI ? 0 : 1, c2 = DI ? HO + 1 : 2;
       float hm[BR];
 #pragma unroll
       for (int r = 0; r < BR; ++r) {  // conv row NR b - 1 + r
         const int sl = slot(r);
-        hm[r] = fmaxf(fmaxf(sc[sl * SW], sc[sl * SW + 1]), sc[sl * SW + 2]);
+        hm[r] = fmaxf(fmaxf(sc[sl * SW + c0], sc[sl * SW + c1]), sc[sl * SW + c2]);
       }
 #pragma unroll
       for (int pr = 0; pr < PRB; ++pr)
