@@ -21,18 +21,21 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// pixel stride (halves) of an MFMA input image: +8 halves keeps the 16 lanes of a fragment read on
-// disjoint banks (48 B / 80 B pixel pitch); the frame image keeps its 4 channel slots
+// pixel stride (halves) of an MFMA input image.  C = 32: +8 halves (80 B pitch) keeps a ds_read_b128 lane
+// group of a fragment read (two lane groups g = lane >> 4 of 8 pixels each, different channel chunks) on
+// disjoint banks.  C = 16: 32 B pitch -- the two chunks of a pixel belong to g and g ^ 1, which a group
+// pairs with disjoint pixel sets, already conflict-free; the unpadded image leaves room for the second
+// residual image (res_blocks_h).  The frame image keeps its 4 channel slots.
 template <int C>
 struct Pix {
-  static constexpr int CS = C == 3 ? 4 : C + 8;
+  static constexpr int CS = C == 3 ? 4 : (C == 16 ? 16 : C + 8);
 };
 
-constexpr int kHGuard = 832;  // halves: one padded row of the widest image (34 * 24) + slack
+constexpr int kHGuard = 832;  // halves: one padded row of the widest entry-conv input (18 * 40) + slack
 constexpr int kBR1 = 33, kBR2 = 17, kBR3 = 17;   // entry-conv band heights (conv rows) per stage
 // region offsets (halves) inside R = lds_h + kHGuard  (DESIGN.md "fp16 mode")
 constexpr int kFrame = 66 * 66 * 4;              // stage-1 input image [66][66][4]
-constexpr int kT1 = 34 * 34 * Pix<16>::CS;       // stage-1 res / stage-2 entry input [34][34][24]
+constexpr int kT1 = 34 * 34 * Pix<16>::CS;       // stage-1 res / stage-2 entry input [34][34][16]
 constexpr int kT2 = 18 * 18 * Pix<32>::CS;       // stage-2 res / stage-3 entry input [18][18][40]
 constexpr int kS1 = kFrame;                       // S1 [33][64][16] after the frame
 constexpr int kX1 = kS1 + kBR1 * 64 * 16;         // X1 [32][32][16]
@@ -41,6 +44,9 @@ constexpr int kX2 = kS2 + kBR2 * 32 * 32;         // X2 [16][16][32] (over the d
 constexpr int kS3 = kT2;                          // S3 [17][16][32] after T2
 constexpr int kX3 = kS3 + kBR3 * 16 * 32;         // X3 [8][8][32]
 constexpr int kRegion = kX1 + 32 * 32 * 16;       // max extent
+constexpr int kT3 = 10 * 10 * Pix<32>::CS;       // stage-3 res input [10][10][40]
+// the residual blocks' second image Tb follows Ta = R: over the dead frame/S1, S2 and T2 regions
+static_assert(2 * kT1 <= kX1 && 2 * kT2 <= kX2 && 2 * kT3 <= kS3, "fp16 LDS plan: second residual image");
 static_assert(kT1 <= kX1 && kX2 + 16 * 16 * 32 <= kRegion && kX3 + 8 * 8 * 32 <= kX2, "fp16 LDS plan");
 // conv weight staging buffer WB (halves): the A fragments of the widest conv (32 -> 32, 9 k-steps x 2
 // channel tiles).  Every wave of the workgroup needs the same fragments; fetched from the pack by
@@ -328,13 +334,30 @@ __device__ __forceinline__ void stage_entry_h(const _Float16* T, _Float16* S, _F
   }
 }
 
+// Zero border of a padded image [H+2][H+2][CS] (the interior is written by a conv epilogue).
+template <int C, int H>
+__device__ __forceinline__ void zero_border_h(_Float16* T) {
+  constexpr int CS = Pix<C>::CS, WP = H + 2, G = C / 8;
+  const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = threadIdx.x; i < 4 * (H + 1) * G; i += kHThreads) {
+    const int cg = i % G, r = i / G, side = r / (H + 1), k = r - side * (H + 1);
+    const int pix = side == 0 ? k : side == 1 ? (H + 1) * WP + 1 + k : side == 2 ? (k + 1) * WP : k * WP + WP - 1;
+    *reinterpret_cast<h8*>(T + pix * CS + 8 * cg) = z;
+  }
+}
+
 // Two residual blocks; same fusion as the f32 path (fdr_impala.hip res_blocks).  af holds block 0's
-// first conv on entry, st the issued copy of its second conv; T holds relu(bn0(X)) with a zero border.
-// Weight pipeline (convs A B C D = i0, i1 of blocks 0 and 1, E = the next stage's entry conv):
-//   conv phase: MFMAs (af), commit the issued block to WB  |  epilogue phase: af <- WB, issue the next.
-// On exit WB holds E (NEXTH halves; NEXTH == 0: last stage, nothing staged).
+// first conv on entry, st the issued copy of its second conv; Ta holds relu(bn0(X)) with a zero border,
+// Tb (same geometry) a zero border.  Each conv reads one image and its epilogue writes the other -- conv0
+// Ta -> Tb, conv1 Tb -> Ta (+ X) -- so the epilogue follows a wave's own MFMAs with no barrier between:
+// one wave's BN / ReLU / residual VALU overlaps the other wave's MFMAs on the SIMD, and a conv costs one
+// full barrier (the other one only follows the fragment load from WB, all waves arriving together).
+// Weight pipeline (convs A B C D = i0, i1 of blocks 0 and 1, E = the next stage's entry conv): a conv
+// phase commits the block issued earlier to WB; after its barrier af <- WB, a barrier, and the next
+// block is issued.  On exit WB holds E (NEXTH halves; NEXTH == 0: last stage, nothing staged) and Ta
+// the next stage's input.
 template <int C, int H, int LAST, int NEXTH>
-__device__ __forceinline__ void res_blocks_h(_Float16* T, _Float16* X, h8 (&af)[KSteps<C>::N][C / 16],
+__device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float16* X, h8 (&af)[KSteps<C>::N][C / 16],
                                              const _Float16* __restrict__ hp, const float* __restrict__ pk,
                                              const Layout& L, int stage, const float* bsc, const float* bsh, int wave,
                                              int lane, const StepArgs& a, int k0, float* __restrict__ out,
@@ -362,38 +385,29 @@ __device__ __forceinline__ void res_blocks_h(_Float16* T, _Float16* X, h8 (&af)[
         h2[nt][k] = (r == 1 && LAST) ? 0.f : bsh[inext * 32 + ch];
       }
     FDR_STAMP(a, k0 + 4 * r);
+    // ---- conv0: Ta -> Tb ----
     f32x4 acc[TPW][NT];
-    conv_h<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
-    st.commit<WH>(wb);  // conv i1
-    __syncthreads();  // every wave is done reading T
-    FDR_STAMP(a, k0 + 4 * r + 1);
-    load_af_lds<C, NT>(wb, af, lane);
-    if (r == 0) {
-      st.issue<WH>(hp + L.conv_h[i1 + 1]);  // block 1 conv0
-    } else if constexpr (NEXTH > 0) {
-      st.issue<NEXTH>(next_w);
-    }
+    conv_h<C, CS, NT, TPW, H, WP, MT>(Ta, af, acc, wave, lane);
     conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
       const int nt = ch0 >> 4;
       float o[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = relu(fmaf(v[k] + b0[nt][k], s1[nt][k], h1[nt][k]));
-      *reinterpret_cast<h4*>(T + tpos(m) + ch0) = to_h4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<h4*>(Tb + tpos(m) + ch0) = to_h4(o[0], o[1], o[2], o[3]);
     });
+    st.commit<WH>(wb);  // conv i1 (every wave loaded conv i0's fragments before the last barrier)
     __syncthreads();
-    FDR_STAMP(a, k0 + 4 * r + 2);
-    conv_h<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
+    FDR_STAMP(a, k0 + 4 * r + 1);
+    load_af_lds<C, NT>(wb, af, lane);
+    __syncthreads();  // WB may be overwritten once every wave holds af
     if (r == 0) {
-      st.commit<WH>(wb);
+      st.issue<WH>(hp + L.conv_h[i1 + 1]);  // block 1 conv0
     } else if constexpr (NEXTH > 0) {
-      st.commit<NEXTH>(wb);
+      st.issue<NEXTH>(next_w);
     }
-    __syncthreads();  // every wave is done reading T
-    FDR_STAMP(a, k0 + 4 * r + 3);
-    if (r == 0) {
-      load_af_lds<C, NT>(wb, af, lane);  // block 1 conv0
-      st.issue<WH>(hp + L.conv_h[i1 + 2]);  // block 1 conv1
-    }
+    FDR_STAMP(a, k0 + 4 * r + 2);
+    // ---- conv1: Tb -> Ta (+ X) ----
+    conv_h<C, CS, NT, TPW, H, WP, MT>(Tb, af, acc, wave, lane);
     conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
       const int nt = ch0 >> 4;
       const h4 xo = *reinterpret_cast<const h4*>(X + m * C + ch0);
@@ -405,18 +419,29 @@ __device__ __forceinline__ void res_blocks_h(_Float16* T, _Float16* X, h8 (&af)[
         float t[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) t[k] = relu(fmaf(xn[k], s2[nt][k], h2[nt][k]));
-        *reinterpret_cast<h4*>(T + tpos(m) + ch0) = to_h4(t[0], t[1], t[2], t[3]);
+        *reinterpret_cast<h4*>(Ta + tpos(m) + ch0) = to_h4(t[0], t[1], t[2], t[3]);
       } else if (!LAST) {
         float t[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) t[k] = fmaf(xn[k], s2[nt][k], h2[nt][k]);
-        *reinterpret_cast<h4*>(T + tpos(m) + ch0) = to_h4(t[0], t[1], t[2], t[3]);
+        *reinterpret_cast<h4*>(Ta + tpos(m) + ch0) = to_h4(t[0], t[1], t[2], t[3]);
       } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) out[(ch0 + k) * H * H + m] = relu(xn[k]);  // flatten (C,H,W)
       }
     });
+    if (r == 0) {
+      st.commit<WH>(wb);
+    } else if constexpr (NEXTH > 0) {
+      st.commit<NEXTH>(wb);
+    }
     __syncthreads();
+    FDR_STAMP(a, k0 + 4 * r + 3);
+    if (r == 0) {
+      load_af_lds<C, NT>(wb, af, lane);  // block 1 conv0
+      __syncthreads();
+      st.issue<WH>(hp + L.conv_h[i1 + 2]);  // block 1 conv1
+    }
   }
 }
 
@@ -501,9 +526,10 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
     load_af_lds<16, 1>(wb, af, ln);
     st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[2]);
     to_padded_h<16, 32, true, true>(R + kX1, R, bsc + 1 * 32, bsh + 1 * 32);
+    zero_border_h<16, 32>(R + kT1);
     __syncthreads();
     FDR_STAMP(a, 3);
-    res_blocks_h<16, 32, 0, kBlockHalves<16, 2>>(R, R + kX1, af, hp, pk, L, 0, bsc, bsh, wave, ln, a, 4, nullptr, st,
+    res_blocks_h<16, 32, 0, kBlockHalves<16, 2>>(R, R + kT1, R + kX1, af, hp, pk, L, 0, bsc, bsh, wave, ln, a, 4, nullptr, st,
                                                  wb, hp + L.conv_h[5]);
   }
   // ---- stage 2 ----
@@ -520,9 +546,10 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
     load_af_lds<32, 2>(wb, af, ln);
     st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[7]);
     to_padded_h<32, 16, true, true>(R + kX2, R, bsc + 6 * 32, bsh + 6 * 32);
+    zero_border_h<32, 16>(R + kT2);
     __syncthreads();
     FDR_STAMP(a, 13);
-    res_blocks_h<32, 16, 0, kBlockHalves<32, 2>>(R, R + kX2, af, hp, pk, L, 1, bsc, bsh, wave, ln, a, 14, nullptr, st,
+    res_blocks_h<32, 16, 0, kBlockHalves<32, 2>>(R, R + kT2, R + kX2, af, hp, pk, L, 1, bsc, bsh, wave, ln, a, 14, nullptr, st,
                                                  wb, hp + L.conv_h[10]);
   }
   // ---- stage 3 ----
@@ -539,9 +566,10 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
     load_af_lds<32, 2>(wb, af, ln);
     st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[12]);
     to_padded_h<32, 8, true, true>(R + kX3, R, bsc + 11 * 32, bsh + 11 * 32);
+    zero_border_h<32, 8>(R + kT3);
     __syncthreads();
     FDR_STAMP(a, 23);
-    res_blocks_h<32, 8, 1, 0>(R, R + kX3, af, hp, pk, L, 2, bsc, bsh, wave, ln, a, 24, a.feat + env * kFeat, st, wb,
+    res_blocks_h<32, 8, 1, 0>(R, R + kT3, R + kX3, af, hp, pk, L, 2, bsc, bsh, wave, ln, a, 24, a.feat + env * kFeat, st, wb,
                               nullptr);
   }
   FDR_STAMP(a, 32);
