@@ -21,22 +21,39 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// pixel stride (halves) of an MFMA input image.  C = 32: +8 halves (80 B pitch) keeps a ds_read_b128 lane
-// group of a fragment read (two lane groups g = lane >> 4 of 8 pixels each, different channel chunks) on
-// disjoint banks.  C = 16: 32 B pitch -- the two chunks of a pixel belong to g and g ^ 1, which a group
-// pairs with disjoint pixel sets, already conflict-free; the unpadded image leaves room for the second
-// residual image (res_blocks_h).  The frame image keeps its 4 channel slots.
+// pixel stride (halves) of an MFMA input image: unpadded (the chunk swizzle below spreads the banks); the
+// frame image keeps its 4 channel slots.
 template <int C>
 struct Pix {
-  static constexpr int CS = C == 3 ? 4 : (C == 16 ? 16 : C + 8);
+  static constexpr int CS = C == 3 ? 4 : C;
 };
+
+// Chunk swizzles (a chunk = 8 channels = one 16-B fragment read; the chunk index is XORed with a few bits of
+// the pixel index, so every access below stays a whole aligned chunk or half chunk).  Chosen with a bank
+// model of every access of the stack over the lane groups of MI355X_MICROARCH.md's LDS table
+// (ds_read_b128 4 x 16 / b64 2 x 32 lanes, 64 banks; ds_write_b64 4 x 16 / b128 8 x 8 lanes, 32 banks):
+//   padded images T: conv B-fragment reads (b128) conflict-free at 16 x 16 / 32 x 32 (2-way: the K = 16 tap-8
+//   read, the 8 x 8 stage's 2-row tiles), epilogue stores (b64) 2-way, to_padded stores (b128) free;
+//   X / S (unpadded [pixel][C]): residual reads free, residual / band-scratch stores 2-way, pool reads 2-way,
+//   to_padded reads and pool stores free.
+// Without them (r05g PMC, conv_kernel_h): SQ_LDS_BANK_CONFLICT = 44 % of SQ_LDS_IDX_ACTIVE -- the residual
+// and band-scratch stores were 8-way at 32 channels (pixel pitch 64 B = 16 banks), the epilogue stores 4-way.
+template <int C>
+__device__ __forceinline__ int tsw(int q) { return C == 16 ? (q >> 2) & 1 : (q >> 1) & 3; }
+template <int C>
+__device__ __forceinline__ int xsw(int m) { return C == 16 ? (m >> 3) & 1 : (m >> 2) & 3; }
+// halves offset of channel ch of padded pixel q (T) / of pixel m (X, S)
+template <int C>
+__device__ __forceinline__ int tidx(int q, int ch) { return q * Pix<C>::CS + (((ch >> 3) ^ tsw<C>(q)) << 3) + (ch & 7); }
+template <int C>
+__device__ __forceinline__ int xidx(int m, int ch) { return m * C + (((ch >> 3) ^ xsw<C>(m)) << 3) + (ch & 7); }
 
 constexpr int kHGuard = 832;  // halves: one padded row of the widest entry-conv input (18 * 40) + slack
 constexpr int kBR1 = 33, kBR2 = 17, kBR3 = 17;   // entry-conv band heights (conv rows) per stage
 // region offsets (halves) inside R = lds_h + kHGuard  (DESIGN.md "fp16 mode")
 constexpr int kFrame = 66 * 66 * 4;              // stage-1 input image [66][66][4]
 constexpr int kT1 = 34 * 34 * Pix<16>::CS;       // stage-1 res / stage-2 entry input [34][34][16]
-constexpr int kT2 = 18 * 18 * Pix<32>::CS;       // stage-2 res / stage-3 entry input [18][18][40]
+constexpr int kT2 = 18 * 18 * Pix<32>::CS;       // stage-2 res / stage-3 entry input [18][18][32]
 constexpr int kS1 = kFrame;                       // S1 [33][64][16] after the frame
 constexpr int kX1 = kS1 + kBR1 * 64 * 16;         // X1 [32][32][16]
 constexpr int kS2 = kT1;                          // S2 [17][32][32] after T1
@@ -44,7 +61,7 @@ constexpr int kX2 = kS2 + kBR2 * 32 * 32;         // X2 [16][16][32] (over the d
 constexpr int kS3 = kT2;                          // S3 [17][16][32] after T2
 constexpr int kX3 = kS3 + kBR3 * 16 * 32;         // X3 [8][8][32]
 constexpr int kRegion = kX1 + 32 * 32 * 16;       // max extent
-constexpr int kT3 = 10 * 10 * Pix<32>::CS;       // stage-3 res input [10][10][40]
+constexpr int kT3 = 10 * 10 * Pix<32>::CS;       // stage-3 res input [10][10][32]
 // the residual blocks' second image Tb follows Ta = R: over the dead frame/S1, S2 and T2 regions
 static_assert(2 * kT1 <= kX1 && 2 * kT2 <= kX2 && 2 * kT3 <= kS3, "fp16 LDS plan: second residual image");
 static_assert(kT1 <= kX1 && kX2 + 16 * 16 * 32 <= kRegion && kX3 + 8 * 8 * 32 <= kX2, "fp16 LDS plan");
@@ -156,9 +173,11 @@ __device__ __forceinline__ int k_offset(int s, int g, int part) {
 // acc[i][nt] += W(nt) * P(tile q = wave + 8 i) over the whole K; Tin = padded HWC image whose row 0 is
 // the padded row of output row 0 (callers offset it for bands).  Pixel tile = 16 consecutive output
 // pixels (row-major, width W).
+// qoff: padded-pixel index of Tin within its image (band offset of an entry conv; the swizzle is a
+// function of the image's own pixel index).
 template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT>
 __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KSteps<CIN>::N][NT],
-                                       f32x4 (&acc)[TPW][NT], int wave, int lane) {
+                                       f32x4 (&acc)[TPW][NT], int wave, int lane, int qoff = 0) {
   constexpr int KS = KSteps<CIN>::N;
   const int g = lane >> 4;
   // tile i of this wave exists (wave-uniform): only the last i of a conv whose MT is not a multiple of 8
@@ -171,7 +190,7 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
     int mt = wave + 8 * i;
     mt = mt < MT ? mt : MT - 1;
     const int m = mt * 16 + (lane & 15);
-    base[i] = ((m / W) * WP + (m % W)) * CS;
+    base[i] = (m / W) * WP + (m % W);  // padded pixel of tap 0
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[i][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -182,8 +201,8 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         if (!live(i)) continue;
-        const h4 lo = *reinterpret_cast<const h4*>(Tin + base[i] + o0);
-        const h4 hi = *reinterpret_cast<const h4*>(Tin + base[i] + o1);
+        const h4 lo = *reinterpret_cast<const h4*>(Tin + base[i] * CS + o0);
+        const h4 hi = *reinterpret_cast<const h4*>(Tin + base[i] * CS + o1);
         const h8 b = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b, acc[i][nt], 0, 0, 0);
@@ -193,11 +212,14 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
   if constexpr (CIN != 3) {
 #pragma unroll
     for (int s = 0; s < KSteps<CIN>::NF; ++s) {
-      const int o = k_offset<CIN, CS, WP>(s, g, 0);
+      // tap and channel chunk of this lane's 8 K-elements (k_offset's decomposition, swizzled chunk)
+      constexpr int cpg = CIN / 8, tpk = 32 / CIN;
+      const int tap = s * tpk + g / cpg, chunk = g % cpg, tq = (tap / 3) * WP + tap % 3;
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         if (!live(i)) continue;
-        const h8 b = *reinterpret_cast<const h8*>(Tin + base[i] + o);
+        const int q = base[i] + tq;
+        const h8 b = *reinterpret_cast<const h8*>(Tin + q * CS + ((chunk ^ tsw<CIN>(q + qoff)) << 3));
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b, acc[i][nt], 0, 0, 0);
       }
@@ -208,11 +230,12 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
   // wrong sums on gfx950 with this hipcc (a mixed-pass-count SrcC dependency; fp16 golden test, measured),
   // the separate form is exact.
   if constexpr (KSteps<CIN>::kRem) {
-    const int o = (2 * WP + 2) * CS + (CIN == 3 ? 0 : 4 * g);
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       if (!live(i)) continue;
-      const h4 b = *reinterpret_cast<const h4*>(Tin + base[i] + o);
+      const int q = base[i] + 2 * WP + 2;  // tap 8
+      const int o = CIN == 3 ? q * CS : q * CS + (((g >> 1) ^ tsw<CIN>(q + qoff)) << 3) + 4 * (g & 1);
+      const h4 b = *reinterpret_cast<const h4*>(Tin + o);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
         const h8 w = af[KS - 1][nt];
@@ -257,7 +280,7 @@ __device__ __forceinline__ void to_padded_h(const _Float16* X, _Float16* T, cons
     const int pix = threadIdx.x / G + it * PPI;
     if (NP % PPI != 0 && pix >= NP) break;
     const int y = pix / H, x = pix % H;
-    const h8 v = *reinterpret_cast<const h8*>(X + pix * C + 8 * cg);
+    const h8 v = *reinterpret_cast<const h8*>(X + xidx<C>(pix, 8 * cg));
     h8 o;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -265,7 +288,7 @@ __device__ __forceinline__ void to_padded_h(const _Float16* X, _Float16* T, cons
       if (RELU) f = relu(f);
       o[k] = (_Float16)f;
     }
-    *reinterpret_cast<h8*>(T + ((y + 1) * WP + x + 1) * CS + 8 * cg) = o;
+    *reinterpret_cast<h8*>(T + tidx<C>((y + 1) * WP + x + 1, 8 * cg)) = o;
   }
   if (BORDER) {
     const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -294,12 +317,12 @@ __device__ __forceinline__ void stage_entry_h(const _Float16* T, _Float16* S, _F
     for (int r = 0; r < 4; ++r) bz[nt][r] = bias[nt * 16 + 4 * (lane >> 4) + r];
   for (int b = 0; b < H / (BR - 1); ++b) {
     f32x4 acc[TPW][NT];
-    conv_h<CIN, CS, NT, TPW, H, WP, MT>(T + ((BR - 1) * b - 1) * WP * CS, af, acc, wave, lane);
+    conv_h<CIN, CS, NT, TPW, H, WP, MT>(T + ((BR - 1) * b - 1) * WP * CS, af, acc, wave, lane, ((BR - 1) * b - 1) * WP);
     conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
       const int nt = ch0 >> 4;
       const bool neg = b == 0 && m < H;  // conv row -1
       const float ninf = -INFINITY;
-      *reinterpret_cast<h4*>(S + m * COUT + ch0) =
+      *reinterpret_cast<h4*>(S + xidx<COUT>(m, ch0)) =
           neg ? to_h4(ninf, ninf, ninf, ninf)
               : to_h4(v[0] + bz[nt][0], v[1] + bz[nt][1], v[2] + bz[nt][2], v[3] + bz[nt][3]);
     });
@@ -314,20 +337,20 @@ __device__ __forceinline__ void stage_entry_h(const _Float16* T, _Float16* S, _F
       const int i = threadIdx.x + it * kHThreads;
       if (NI % kHThreads != 0 && i >= NI) break;
       const int cg = i % G, r = i / G, px = r % HO, pr = r / HO;
-      const _Float16* base = S + (2 * pr * H) * COUT + 8 * cg;
       const int xl = 2 * px > 0 ? 2 * px - 1 : 0;
       h8 v[9];
 #pragma unroll
       for (int dr = 0; dr < 3; ++dr) {
-        v[3 * dr] = *reinterpret_cast<const h8*>(base + (dr * H + xl) * COUT);
-        v[3 * dr + 1] = *reinterpret_cast<const h8*>(base + (dr * H + 2 * px) * COUT);
-        v[3 * dr + 2] = *reinterpret_cast<const h8*>(base + (dr * H + 2 * px + 1) * COUT);
+        const int row = (2 * pr + dr) * H;
+        v[3 * dr] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + xl, 8 * cg));
+        v[3 * dr + 1] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + 2 * px, 8 * cg));
+        v[3 * dr + 2] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + 2 * px + 1, 8 * cg));
       }
       const h8 m01 = __builtin_elementwise_max(v[0], v[1]), m23 = __builtin_elementwise_max(v[2], v[3]);
       const h8 m45 = __builtin_elementwise_max(v[4], v[5]), m67 = __builtin_elementwise_max(v[6], v[7]);
       const h8 mx = __builtin_elementwise_max(
           __builtin_elementwise_max(__builtin_elementwise_max(m01, m23), __builtin_elementwise_max(m45, m67)), v[8]);
-      *reinterpret_cast<h8*>(X + ((PRB * b + pr) * HO + px) * COUT + 8 * cg) = mx;
+      *reinterpret_cast<h8*>(X + xidx<COUT>((PRB * b + pr) * HO + px, 8 * cg)) = mx;
     }
     __syncthreads();
     FDR_STAMP(a, kst + 2 * b + 1);  // band b pool done
@@ -364,7 +387,7 @@ __device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float1
                                              WStage& st, _Float16* wb, const _Float16* __restrict__ next_w) {
   constexpr int CS = Pix<C>::CS, WP = H + 2, NT = C / 16, MT = H * H / 16;
   constexpr int TPW = (MT + 7) / 8, WH = kBlockHalves<C, C / 16>;
-  auto tpos = [&](int m) { return ((m / H + 1) * WP + (m % H) + 1) * CS; };
+  auto tpos = [&](int m, int ch0) { return tidx<C>((m / H + 1) * WP + (m % H) + 1, ch0); };
   const int cl = 4 * (lane >> 4);  // this lane's 4 channels within an output-channel tile
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
@@ -393,7 +416,7 @@ __device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float1
       float o[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = relu(fmaf(v[k] + b0[nt][k], s1[nt][k], h1[nt][k]));
-      *reinterpret_cast<h4*>(Tb + tpos(m) + ch0) = to_h4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<h4*>(Tb + tpos(m, ch0)) = to_h4(o[0], o[1], o[2], o[3]);
     });
     st.commit<WH>(wb);  // conv i1 (every wave loaded conv i0's fragments before the last barrier)
     __syncthreads();
@@ -410,21 +433,21 @@ __device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float1
     conv_h<C, CS, NT, TPW, H, WP, MT>(Tb, af, acc, wave, lane);
     conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
       const int nt = ch0 >> 4;
-      const h4 xo = *reinterpret_cast<const h4*>(X + m * C + ch0);
+      const h4 xo = *reinterpret_cast<const h4*>(X + xidx<C>(m, ch0));
       float xn[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) xn[k] = (float)(_Float16)((v[k] + b1[nt][k]) + (float)xo[k]);
       if (r == 0) {
-        *reinterpret_cast<h4*>(X + m * C + ch0) = to_h4(xn[0], xn[1], xn[2], xn[3]);
+        *reinterpret_cast<h4*>(X + xidx<C>(m, ch0)) = to_h4(xn[0], xn[1], xn[2], xn[3]);
         float t[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) t[k] = relu(fmaf(xn[k], s2[nt][k], h2[nt][k]));
-        *reinterpret_cast<h4*>(Ta + tpos(m) + ch0) = to_h4(t[0], t[1], t[2], t[3]);
+        *reinterpret_cast<h4*>(Ta + tpos(m, ch0)) = to_h4(t[0], t[1], t[2], t[3]);
       } else if (!LAST) {
         float t[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) t[k] = fmaf(xn[k], s2[nt][k], h2[nt][k]);
-        *reinterpret_cast<h4*>(Ta + tpos(m) + ch0) = to_h4(t[0], t[1], t[2], t[3]);
+        *reinterpret_cast<h4*>(Ta + tpos(m, ch0)) = to_h4(t[0], t[1], t[2], t[3]);
       } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) out[(ch0 + k) * H * H + m] = relu(xn[k]);  // flatten (C,H,W)
