@@ -71,7 +71,7 @@ static_assert(kT1 <= kX1 && kX2 + 16 * 16 * 32 <= kRegion && kX3 + 8 * 8 * 32 <=
 // waves stall on).  Instead the workgroup copies each conv's block ONCE into WB (16 B per thread per
 // chunk) and the waves read their fragments from LDS.
 constexpr int kWB = 9 * 2 * 64 * 8;
-constexpr int kHLdsBytes = (kHGuard + kRegion) * 2 + 2 * kBnTab * 4 + kWB * 2;
+constexpr int kHLdsBytes = (kHGuard + kRegion) * 2 + 3 * kBnTab * 4 + kWB * 2;  // + BN scale / shift, conv bias
 static_assert(kHLdsBytes <= 160 * 1024, "fp16 conv LDS");
 
 // ---- conv on f16 MFMA ---------------------------------------------------------------------------
@@ -382,7 +382,7 @@ __device__ __forceinline__ void zero_border_h(_Float16* T) {
 template <int C, int H, int LAST, int NEXTH>
 __device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float16* X, h8 (&af)[KSteps<C>::N][C / 16],
                                              const _Float16* __restrict__ hp, const float* __restrict__ pk,
-                                             const Layout& L, int stage, const float* bsc, const float* bsh, int wave,
+                                             const Layout& L, int stage, const float* bsc, const float* bsh, const float* bcb, int wave,
                                              int lane, const StepArgs& a, int k0, float* __restrict__ out,
                                              WStage& st, _Float16* wb, const _Float16* __restrict__ next_w) {
   constexpr int CS = Pix<C>::CS, WP = H + 2, NT = C / 16, MT = H * H / 16;
@@ -400,8 +400,8 @@ __device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float1
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int ch = nt * 16 + cl + k;
-        b0[nt][k] = pk[L.conv_b[i0] + ch];
-        b1[nt][k] = pk[L.conv_b[i1] + ch];
+        b0[nt][k] = bcb[i0 * 32 + ch];  // LDS: a global load here would wait (vmcnt) on the issued WB block
+        b1[nt][k] = bcb[i1 * 32 + ch];
         s1[nt][k] = bsc[i1 * 32 + ch];
         h1[nt][k] = bsh[i1 * 32 + ch];
         s2[nt][k] = (r == 1 && LAST) ? 0.f : bsc[inext * 32 + ch];
@@ -479,27 +479,54 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
   const _Float16* hp = a.hpack + (int64_t)lane * a.hpack_stride;
   float* bsc = reinterpret_cast<float*>(smem);
   float* bsh = bsc + kBnTab;
-  _Float16* R = reinterpret_cast<_Float16*>(smem + 2 * kBnTab * 4) + kHGuard;
+  float* bcb = bsh + kBnTab;  // conv biases [15][32]
+  _Float16* R = reinterpret_cast<_Float16*>(smem + 3 * kBnTab * 4) + kHGuard;
 
   _Float16* wb = reinterpret_cast<_Float16*>(smem + kHLdsBytes - kWB * 2);
+  // BN / bias table inputs first (global loads; vmcnt retires in order, so they go ahead of the weight
+  // loads), folded after the frame hash below has covered their latency
+  static_assert(kBnTab <= kHThreads, "one table entry per thread");
+  const int bi = threadIdx.x, bidx = bi >> 5, bch = bi & 31;
+  const bool has_bn = bi < kBnTab && bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
+  const bool has_cb = bi < kBnTab && bch < (bidx < 5 ? 16 : 32);  // kConvs == 15: conv bidx's bias
+  float rm = 0.f, rv = 1.f, bnw = 0.f, bnb = 0.f, cbv = 0.f;
+  if (has_bn) {
+    if (a.bn_mean) rm = a.bn_mean[L.bn_stat[bidx] + bch];
+    if (a.bn_var) rv = a.bn_var[L.bn_stat[bidx] + bch];
+    bnw = pk[L.bn_w[bidx] + bch];
+    bnb = pk[L.bn_b[bidx] + bch];
+  }
+  if (has_cb) cbv = pk[L.conv_b[bidx] + bch];
   h8 af3[KSteps<3>::N][1];
   load_af<3, 1>(hp + L.conv_h[0], af3, ln);
   WStage st;
   st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);  // committed in the stage-1 entry
   FDR_STAMP(a, 0);
-  for (int i = threadIdx.x; i < kBnTab; i += kHThreads) {
-    const int idx = i >> 5, ch = i & 31;
-    const int nch = idx == 0 ? 3 : (idx == 5 ? 16 : (idx < 5 ? 16 : 32));
-    float sc = 0.f, sh = 0.f;
-    if (ch < nch) {
-      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[idx] + ch] : 0.f;
-      const float rv = a.bn_var ? a.bn_var[L.bn_stat[idx] + ch] : 1.f;
-      const float inv = 1.f / sqrtf(rv + kBnEps);
-      sc = pk[L.bn_w[idx] + ch] * inv;
-      sh = pk[L.bn_b[idx] + ch] - rm * sc;
+  // ---- frame (policies/impala.py:147: frame / 255): values of this thread's 8 pixels x 3 channels ----
+  const int fw = threadIdx.x;  // 512 threads x 8 pixels = 64 x 64
+  const int fy = fw >> 3, fx0 = (fw & 7) * 8;
+  float fv[3][8];
+  if (a.frames) {
+    const float* fr = a.frames + (a.shared_frames ? (int64_t)e : env) * kFramePix;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fv[c][j] = fr[c * 4096 + fy * 64 + fx0 + j];
+  } else {
+    const uint64_t gid = (uint64_t)(a.lane_offset * a.envs + env);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const uint64_t word = (uint64_t)(c * 512 + fw);
+      const uint64_t hb = mix64(a.fkey + ((gid << 32) | ((uint64_t)a.t << 11) | word) * kGolden);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fv[c][j] = (float)((uint32_t)(hb >> (8 * j)) & 255u);
     }
-    bsc[i] = sc;
-    bsh[i] = sh;
+  }
+  if (bi < kBnTab) {  // eval-mode BN folded per channel: y = x * (w / sqrt(rv + eps)) + (b - rm * scale)
+    const float sc = has_bn ? bnw * (1.f / sqrtf(rv + kBnEps)) : 0.f;
+    bsc[bi] = sc;
+    bsh[bi] = has_bn ? bnb - rm * sc : 0.f;
+    bcb[bi] = cbv;
   }
   {  // zero the guard + frame image (its border and 4th channel slot stay 0)
     uint4* z = reinterpret_cast<uint4*>(R - kHGuard);
@@ -508,41 +535,20 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
   __syncthreads();
   FDR_STAMP(a, 1);
 
-  // ---- frame -> BN2d(3) -> padded HWC [66][66][4] f16: one thread per 8 consecutive pixels ----
-  {
-    const int w = threadIdx.x;  // 512 threads x 8 pixels = 64 x 64
-    const int y = w >> 3, x0 = (w & 7) * 8;
-    float v[3][8];
-    if (a.frames) {
-      const float* fr = a.frames + (a.shared_frames ? (int64_t)e : env) * kFramePix;
+  // ---- frame -> BN2d(3) -> padded HWC [66][66][4] f16 ----
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
+  for (int j = 0; j < 8; ++j) {
+    h4 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[c][j] = fr[c * 4096 + y * 64 + x0 + j];
-    } else {
-      const uint64_t gid = (uint64_t)(a.lane_offset * a.envs + env);
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const uint64_t word = (uint64_t)(c * 512 + w);
-        const uint64_t hb = mix64(a.fkey + ((gid << 32) | ((uint64_t)a.t << 11) | word) * kGolden);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[c][j] = (float)((uint32_t)(hb >> (8 * j)) & 255u);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      h4 o;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) o[c] = (_Float16)fmaf(v[c][j] / 255.0f, bsc[c], bsh[c]);
-      o[3] = (_Float16)0.f;
-      *reinterpret_cast<h4*>(R + ((y + 1) * 66 + x0 + j + 1) * 4) = o;
-    }
+    for (int c = 0; c < 3; ++c) o[c] = (_Float16)fmaf(fv[c][j] / 255.0f, bsc[c], bsh[c]);
+    o[3] = (_Float16)0.f;
+    *reinterpret_cast<h4*>(R + ((fy + 1) * 66 + fx0 + j + 1) * 4) = o;
   }
   __syncthreads();
   FDR_STAMP(a, 2);
 
   // ---- stage 1 ----
-  stage_entry_h<3, 16, 64, kBR1, kBlockHalves<16, 1>>(R, R + kS1, R + kX1, af3, pk + L.conv_b[0], wave, ln, a, 40,
+  stage_entry_h<3, 16, 64, kBR1, kBlockHalves<16, 1>>(R, R + kS1, R + kX1, af3, bcb + 0 * 32, wave, ln, a, 40,
                                                      st, wb);
   {
     h8 af[KSteps<16>::N][1];
@@ -552,7 +558,7 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
     zero_border_h<16, 32>(R + kT1);
     __syncthreads();
     FDR_STAMP(a, 3);
-    res_blocks_h<16, 32, 0, kBlockHalves<16, 2>>(R, R + kT1, R + kX1, af, hp, pk, L, 0, bsc, bsh, wave, ln, a, 4, nullptr, st,
+    res_blocks_h<16, 32, 0, kBlockHalves<16, 2>>(R, R + kT1, R + kX1, af, hp, pk, L, 0, bsc, bsh, bcb, wave, ln, a, 4, nullptr, st,
                                                  wb, hp + L.conv_h[5]);
   }
   // ---- stage 2 ----
@@ -561,7 +567,7 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
     load_af_lds<16, 2>(wb, af, ln);
     st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
     FDR_STAMP(a, 12);
-    stage_entry_h<16, 32, 32, kBR2, kBlockHalves<32, 2>>(R, R + kS2, R + kX2, af, pk + L.conv_b[5], wave, ln, a, 48,
+    stage_entry_h<16, 32, 32, kBR2, kBlockHalves<32, 2>>(R, R + kS2, R + kX2, af, bcb + 5 * 32, wave, ln, a, 48,
                                                          st, wb);
   }
   {
@@ -572,7 +578,7 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
     zero_border_h<32, 16>(R + kT2);
     __syncthreads();
     FDR_STAMP(a, 13);
-    res_blocks_h<32, 16, 0, kBlockHalves<32, 2>>(R, R + kT2, R + kX2, af, hp, pk, L, 1, bsc, bsh, wave, ln, a, 14, nullptr, st,
+    res_blocks_h<32, 16, 0, kBlockHalves<32, 2>>(R, R + kT2, R + kX2, af, hp, pk, L, 1, bsc, bsh, bcb, wave, ln, a, 14, nullptr, st,
                                                  wb, hp + L.conv_h[10]);
   }
   // ---- stage 3 ----
@@ -581,7 +587,7 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
     load_af_lds<32, 2>(wb, af, ln);
     st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
     FDR_STAMP(a, 22);
-    stage_entry_h<32, 32, 16, kBR3, kBlockHalves<32, 2>>(R, R + kS3, R + kX3, af, pk + L.conv_b[10], wave, ln, a, 56,
+    stage_entry_h<32, 32, 16, kBR3, kBlockHalves<32, 2>>(R, R + kS3, R + kX3, af, bcb + 10 * 32, wave, ln, a, 56,
                                                          st, wb);
   }
   {
@@ -592,7 +598,7 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
     zero_border_h<32, 8>(R + kT3);
     __syncthreads();
     FDR_STAMP(a, 23);
-    res_blocks_h<32, 8, 1, 0>(R, R + kT3, R + kX3, af, hp, pk, L, 2, bsc, bsh, wave, ln, a, 24, a.feat + env * kFeat, st, wb,
+    res_blocks_h<32, 8, 1, 0>(R, R + kT3, R + kX3, af, hp, pk, L, 2, bsc, bsh, bcb, wave, ln, a, 24, a.feat + env * kFeat, st, wb,
                               nullptr);
   }
   FDR_STAMP(a, 32);
