@@ -389,17 +389,55 @@ __device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float1
   constexpr int TPW = (MT + 7) / 8, WH = kBlockHalves<C, C / 16>;
   auto tpos = [&](int m, int ch0) { return tidx<C>((m / H + 1) * WP + (m % H) + 1, ch0); };
   const int cl = 4 * (lane >> 4);  // this lane's 4 channels within an output-channel tile
+  // SPLIT (8 x 8 stage: 4 pixel tiles x 2 channel tiles): one (tile, channel tile) pair per wave instead of
+  // 2 channel tiles on waves 0-3 and nothing on waves 4-7.  ntw is wave-uniform; the wave's fragments and
+  // epilogue constants are those of its channel tile only (constant register indices).
+  constexpr bool SPLIT = MT < 8 && MT * NT == 8;
+  static_assert(!SPLIT || NT == 2, "split: two channel tiles");
+  constexpr int NTC = SPLIT ? 1 : NT, TPC = SPLIT ? 1 : TPW;
+  const int ntw = SPLIT ? wave % NT : 0, mtw = SPLIT ? wave / NT : wave;
+  h8 af1[KSteps<C>::N][1];
+  // this wave's fragments from WB: all channel tiles (af) or, SPLIT, channel tile ntw only (af1; a select
+  // between af[s][0] and af[s][1] became a dynamically indexed scratch copy)
+  auto load_frags = [&]() {
+    if constexpr (SPLIT) {
+      static_assert(!KSteps<C>::kRem, "split: full K-steps only");
+#pragma unroll
+      for (int s = 0; s < KSteps<C>::N; ++s) af1[s][0] = *reinterpret_cast<const h8*>(wb + (((s * NT + ntw) * 64) + lane) * 8);
+    } else {
+      load_af_lds<C, NT>(wb, af, lane);
+    }
+  };
+  auto conv = [&](const _Float16* Tin, f32x4 (&acc)[TPC][NTC]) {
+    if constexpr (SPLIT) {
+      conv_h<C, CS, 1, 1, H, WP, MT>(Tin, af1, acc, mtw, lane);
+    } else {
+      conv_h<C, CS, NT, TPW, H, WP, MT>(Tin, af, acc, wave, lane);
+    }
+  };
+  // f(ch0, ci, m, v): ci = the index of ch0's channel tile in this wave's constants
+  auto visit = [&](const f32x4 (&acc)[TPC][NTC], auto&& f) {
+    if constexpr (SPLIT) {
+      conv_out_h<1, 1, MT>(acc, mtw, lane, [&](int ch0, int m, f32x4 v) { f(ch0 + 16 * ntw, 0, m, v); });
+    } else {
+      conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) { f(ch0, ch0 >> 4, m, v); });
+    }
+  };
+  if constexpr (SPLIT) {  // the caller's af came from the same WB block, still in place
+    load_frags();
+    __syncthreads();  // before any wave's first commit overwrites WB
+  }
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int i0 = stage * 5 + 1 + 2 * r, i1 = i0 + 1;
     const int inext = r == 0 ? i1 + 1 : (stage + 1) * 5;
     // per-lane epilogue constants: bias of both convs, BN after conv0, BN after conv1
-    float b0[NT][4], s1[NT][4], h1[NT][4], b1[NT][4], s2[NT][4], h2[NT][4];
+    float b0[NTC][4], s1[NTC][4], h1[NTC][4], b1[NTC][4], s2[NTC][4], h2[NTC][4];
 #pragma unroll
-    for (int nt = 0; nt < NT; ++nt)
+    for (int nt = 0; nt < NTC; ++nt)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int ch = nt * 16 + cl + k;
+        const int ch = (SPLIT ? ntw : nt) * 16 + cl + k;
         b0[nt][k] = bcb[i0 * 32 + ch];  // LDS: a global load here would wait (vmcnt) on the issued WB block
         b1[nt][k] = bcb[i1 * 32 + ch];
         s1[nt][k] = bsc[i1 * 32 + ch];
@@ -409,10 +447,9 @@ __device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float1
       }
     FDR_STAMP(a, k0 + 4 * r);
     // ---- conv0: Ta -> Tb ----
-    f32x4 acc[TPW][NT];
-    conv_h<C, CS, NT, TPW, H, WP, MT>(Ta, af, acc, wave, lane);
-    conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
-      const int nt = ch0 >> 4;
+    f32x4 acc[TPC][NTC];
+    conv(Ta, acc);
+    visit(acc, [&](int ch0, int nt, int m, f32x4 v) {
       float o[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = relu(fmaf(v[k] + b0[nt][k], s1[nt][k], h1[nt][k]));
@@ -421,7 +458,7 @@ __device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float1
     st.commit<WH>(wb);  // conv i1 (every wave loaded conv i0's fragments before the last barrier)
     __syncthreads();
     FDR_STAMP(a, k0 + 4 * r + 1);
-    load_af_lds<C, NT>(wb, af, lane);
+    load_frags();
     __syncthreads();  // WB may be overwritten once every wave holds af
     if (r == 0) {
       st.issue<WH>(hp + L.conv_h[i1 + 1]);  // block 1 conv0
@@ -430,9 +467,8 @@ __device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float1
     }
     FDR_STAMP(a, k0 + 4 * r + 2);
     // ---- conv1: Tb -> Ta (+ X) ----
-    conv_h<C, CS, NT, TPW, H, WP, MT>(Tb, af, acc, wave, lane);
-    conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
-      const int nt = ch0 >> 4;
+    conv(Tb, acc);
+    visit(acc, [&](int ch0, int nt, int m, f32x4 v) {
       const h4 xo = *reinterpret_cast<const h4*>(X + xidx<C>(m, ch0));
       float xn[4];
 #pragma unroll
@@ -461,7 +497,7 @@ __device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float1
     __syncthreads();
     FDR_STAMP(a, k0 + 4 * r + 3);
     if (r == 0) {
-      load_af_lds<C, NT>(wb, af, lane);  // block 1 conv0
+      load_frags();  // block 1 conv0
       __syncthreads();
       st.issue<WH>(hp + L.conv_h[i1 + 2]);  // block 1 conv1
     }
