@@ -115,6 +115,8 @@ Context& default_context() {
                          : strcmp(e, "single") == 0 ? FDR_ROLLOUT_SINGLE
                          : strcmp(e, "wide") == 0   ? FDR_ROLLOUT_WIDE
                                                     : strcmp(e, "pair") == 0 ? FDR_ROLLOUT_PAIR : FDR_ROLLOUT_AUTO;
+    const char* m = getenv("FDR_CORE_MFMA");  // A/B switch: "0" selects the VALU fp16 pair core
+    c->core_mfma = !(m && strcmp(m, "0") == 0);
     return c;
   }();
   return *d;
@@ -172,6 +174,10 @@ int fdr_ctx_set_replay_gemm(fdr_ctx* ctx, int32_t on) {
   (ctx ? ctx->c : default_context()).replay_gemm = on != 0;
   return FDR_OK;
 }
+int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on) {
+  (ctx ? ctx->c : default_context()).core_mfma = on != 0;
+  return FDR_OK;
+}
 int fdr_ctx_impala_profile(fdr_ctx* ctx, int32_t enable) { return impala::set_profile(ctx ? ctx->c : default_context(), enable); }
 int fdr_ctx_impala_profile_read(fdr_ctx* ctx, double* ms) {
   if (!ms) return set_error(FDR_ERR_INVALID, "NULL pointer");
@@ -194,6 +200,7 @@ int fdr_ctx_create(int device, fdr_ctx** out) {
   c->c.device = device;
   c->c.cus = cus;
   c->c.rollout_impl = default_context().rollout_impl;  // FDR_ROLLOUT applies to new contexts too
+  c->c.core_mfma = default_context().core_mfma;        // and FDR_CORE_MFMA
   *out = c;
   return FDR_OK;
 }

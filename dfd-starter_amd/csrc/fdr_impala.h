@@ -19,6 +19,14 @@ constexpr int kCoreIn = 257; // fc output + clipped reward (policies/impala.py:1
 #ifndef FDR_CORE_UNROLL_H
 #define FDR_CORE_UNROLL_H 2  // fp16 step kernel's fc / gate streams (A/B: 0.377 -> 0.360 ms per step vs 4)
 #endif
+// fp16 pair-form core step on MFMA (core_kernel_hpm): fc W^T and [W_ih | W_hh]^T as v_mfma_f32_16x16x32_f16
+// A-fragment images [k-step][16-column tile][64 lanes][8 halves] (lane l: W[16 nt + (l & 15)][32 ks + 8 (l >> 4) ..
+// + 7]), one for theta and one per pair for sigma-eps; K of the gates (513) zero-padded to 17 k-steps.
+constexpr int kFcKS = kFeat / 32, kFcNT = kHid / 16;
+constexpr int kGateK = kCoreIn + kHid, kGateKS = (kGateK + 31) / 32, kGateNT = kGates / 16;
+constexpr int64_t kFcImg = (int64_t)kFcKS * kFcNT * 512;      // halves
+constexpr int64_t kGateImg = (int64_t)kGateKS * kGateNT * 512;
+constexpr int64_t kMImg = kFcImg + kGateImg;                    // halves per image (2.2 MB)
 constexpr int kReplayChunk = 64;  // entropy replay: steps per batched input-projection GEMM
 constexpr int kMaxAct = 32;
 constexpr int kMaxSections = 64;
@@ -88,6 +96,9 @@ struct StepArgs {
   const float* ep32;
   int64_t ep_stride;
   const int8_t* sign;
+  // MFMA form (fp16 pairs, ctx core_mfma): theta's image and the pairs' sigma-eps images [n_lanes / 2][kMImg]
+  const _Float16* thm;
+  const _Float16* epm;
 };
 
 // phase clock of the first conv workgroup (s_memtime), for the phase breakdown in DESIGN.md
@@ -216,10 +227,14 @@ template <int E>
 __global__ void core_kernel_pr(Layout L, StepArgs a);  // f32 pair form of the replay (with a.gx)
 template <int E>
 __global__ void core_kernel_hpr(Layout L, StepArgs a); // fp16 pair form of the replay (with a.gx)
+template <int E>
+__global__ void core_kernel_hpm(Layout L, StepArgs a); // fp16 pair form on MFMA (rollout mode), grid n_lanes / 2
+// MFMA images (kMImg halves each) of n half packs: grid (kFcKS + 4 kGateKS, n)
+__global__ void mfma_image_kernel(Layout L, const _Float16* src, int64_t src_stride, _Float16* dst);
 constexpr int kHThreads = 512;
 
 struct Plan {  // workspace carve-up (byte offsets)
-  int64_t pack, hpack, feat, h, c, rprev, ci, gx, n2, zeros, thpack, epack, idxe, n2x, total;
+  int64_t pack, hpack, feat, h, c, rprev, ci, gx, n2, zeros, thpack, epack, idxe, n2x, mimg, total;
   int nblk;    // prep blocks per lane
 };
 // pairs: the fp16 pair form (theta half pack, one sigma-eps half pack per pair, a zero base, pair offsets)

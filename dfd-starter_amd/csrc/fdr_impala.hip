@@ -143,6 +143,7 @@ Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16
   p.epack = take(pr ? (int64_t)(n_lanes / 2) * plen : 0);
   p.idxe = take(pr ? (int64_t)(n_lanes / 2) * 8 : 0);
   p.n2x = take(pr && !fp16 ? (int64_t)(n_lanes / 2 + 1) * p.nblk * 8 : 0);  // the f32 pack kernels' n2 partials
+  p.mimg = take(pr && fp16 ? (int64_t)(n_lanes / 2 + 1) * kMImg * 2 : 0);  // theta's + the pairs' MFMA images
   p.total = o;
   return p;
 }
@@ -1353,7 +1354,10 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
     mark(prof, stream);
     bool pair_done = false;
     if constexpr (E <= 4) {
-      if (h && a.ep) {
+      if (h && a.epm) {
+        hipLaunchKernelGGL((core_kernel_hpm<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
+        pair_done = true;
+      } else if (h && a.ep) {
         hipLaunchKernelGGL((core_kernel_hp<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
         pair_done = true;
       } else if (!h && a.ep32) {
@@ -1467,6 +1471,14 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
       a.th = th;
       a.ep = ep;
       a.ep_stride = L.hpack;
+      if (c.ctx->core_mfma) {  // MFMA-fragment images of theta's and the pairs' fc / LSTM weights
+        _Float16* im = reinterpret_cast<_Float16*>(w + p.mimg);
+        const unsigned nb = kFcKS + 4 * kGateKS;
+        hipLaunchKernelGGL(mfma_image_kernel, dim3(nb, 1), dim3(256), 0, stream, L, th, (int64_t)0, im);
+        hipLaunchKernelGGL(mfma_image_kernel, dim3(nb, np), dim3(256), 0, stream, L, ep, (int64_t)L.hpack, im + kMImg);
+        a.thm = im;
+        a.epm = im + kMImg;
+      }
     } else {  // f32: w = fl32(theta +- fl32(sigma eps)) in registers is the pack's value bit for bit
       float* th = reinterpret_cast<float*>(w + p.thpack);
       float* ep = reinterpret_cast<float*>(w + p.epack);

@@ -1094,6 +1094,290 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_hpr(Layout L, StepAr
   __syncthreads();
   if (j < E2) core_finish<E, kReplay>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
 }
+// ---- MFMA form of the fp16 pair core step (ctx core_mfma, the default) ---------------------------------------
+// The pair's lanes share theta and sigma-eps E, so each GEMM of the step is  W_l x = theta x + s_l (E x):
+// one v_mfma_f32_16x16x32_f16 of theta's A fragment against the B fragment X (the pair's 2E envs as columns,
+// repeated to 16) and one of E's fragment against S X (the columns of the minus lane sign-flipped), chained
+// into ONE f32 accumulator per 16-column tile.  The VALU form (core_kernel_hp) issues 96 VALU instructions per
+// 32 streamed bytes and leaves the HBM stream latency-bound at 2 waves/SIMD; here the VALU work is gone and
+// the weights stream through a 4-deep register ring (the images hold the A fragments in HBM order, 1 KB per
+// wave-load).  Activations x, the fc output and h are rounded to f16 as the B operand (fp16 tolerance).
+
+// MFMA images of n half packs: block (k-step, 256-column quarter) of W^T -> LDS -> fragments [ks][nt][l][8].
+__global__ __launch_bounds__(256) void mfma_image_kernel(Layout L, const _Float16* src, int64_t src_stride,
+                                                          _Float16* dst) {
+  constexpr int TP = 256 + 8;  // LDS tile pitch (halves)
+  __shared__ __attribute__((aligned(16))) _Float16 tile[32 * TP];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const bool fc = b < kFcKS;
+  const int ks = fc ? b : (b - kFcKS) >> 2, q = fc ? 0 : (b - kFcKS) & 3;
+  const int ncol = fc ? kHid : kGates, nt_n = fc ? kFcNT : kGateNT, krows = fc ? kFeat : kGateK;
+  const _Float16* s = src + (int64_t)blockIdx.y * src_stride + (fc ? L.fc_wt_h : L.lstm_wt_h);
+  _Float16* d = dst + (int64_t)blockIdx.y * kMImg + (fc ? 0 : kFcImg);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = t + 256 * i, r = idx >> 5, cc = idx & 31, k = 32 * ks + r;
+    h8 v = h8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (k < krows) v = *reinterpret_cast<const h8*>(s + (int64_t)k * ncol + 256 * q + 8 * cc);
+    *reinterpret_cast<h8*>(tile + r * TP + 8 * cc) = v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = t + 256 * i, nt = idx >> 6, l = idx & 63;
+    h8 v;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) v[jj] = tile[(8 * (l >> 4) + jj) * TP + 16 * nt + (l & 15)];
+    *reinterpret_cast<h8*>(d + (((int64_t)ks * nt_n + 16 * q + nt) * 64 + l) * 8) = v;
+  }
+}
+
+// Stream NQ k-steps of 4 column tiles through a D-deep register ring: frag(q) = the images' offset (halves)
+// of step q's first tile (the next 3 follow at +512).  prime() issues the first D - 1 steps (called ahead of
+// the phase before the stream, so the loads overlap it); run(mma) consumes step q with mma(q, th, ep).
+template <int NQ, class Frag>
+struct MfmaRing {
+  static constexpr int D = 4;
+  static_assert(NQ % D == 0, "ring depth divides the step count");
+  const _Float16* thm;
+  const _Float16* epm;
+  Frag frag;
+  h8 rt[D][4], re[D][4];
+  __device__ __forceinline__ void issue(int q, h8 (&t)[4], h8 (&e)[4]) {
+    const int64_t o = frag(q);
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) {
+      t[jt] = *reinterpret_cast<const h8*>(thm + o + 512 * jt);
+      e[jt] = ld_stream(reinterpret_cast<const h8*>(epm + o + 512 * jt));
+    }
+  }
+  __device__ __forceinline__ void prime() {
+#pragma unroll
+    for (int u = 0; u < D - 1; ++u) issue(u, rt[u], re[u]);
+  }
+  template <class Mma>
+  __device__ __forceinline__ void run(Mma&& mma) {
+#pragma unroll 1
+    for (int q0 = 0; q0 < NQ; q0 += D) {
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        const int q = q0 + u;
+        issue(min(q + D - 1, NQ - 1), rt[(u + D - 1) % D], re[(u + D - 1) % D]);  // past the end: a re-read
+        __builtin_amdgcn_sched_barrier(0);  // keep the ring: the scheduler would sink each load to its use
+        mma(q, rt[u], re[u]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+};
+template <int NQ, class Frag>
+__device__ __forceinline__ MfmaRing<NQ, Frag> mfma_ring(const _Float16* thm, const _Float16* epm, Frag f) {
+  return MfmaRing<NQ, Frag>{thm, epm, f};
+}
+
+template <int E>
+__global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2))) void core_kernel_hpm(Layout L,
+                                                                                                       StepArgs a) {
+  constexpr int E2 = 2 * E;
+  static_assert(E2 <= 16 && (E2 & (E2 - 1)) == 0, "the pair's envs are the B operand's columns (mod E2)");
+  constexpr int XP = kFeat + 16;         // f16 pitch of BN(features) rows [env][k]
+  constexpr int GP = kGateKS * 32 + 16;  // f16 pitch of the gate input rows [env][cis (257) | h (256) | 0]
+  constexpr int kXBytes = E2 * XP * 2, kGBytes = kGates * E2 * 4;
+  __shared__ __attribute__((aligned(16))) char xg[kXBytes > kGBytes ? kXBytes : kGBytes];
+  __shared__ __attribute__((aligned(16))) _Float16 gh[E2 * GP];
+  __shared__ float hs[kHid * E2];
+  __shared__ float logit[E2 * kMaxAct];
+  __shared__ float bsum[2 * kGates];               // b_ih + b_hh of the pair's two lanes
+  _Float16* xh = reinterpret_cast<_Float16*>(xg);  // fc input, dead after the fc MFMAs
+  float* gates = reinterpret_cast<float*>(xg);     // gate pre-activations [1024][E2] (over xh)
+  const int pr = blockIdx.x, j = threadIdx.x, w = j >> 6, l = j & 63;
+  const int l0 = 2 * pr;
+  const float* pk0 = a.pack + (int64_t)l0 * a.pack_stride;
+  const float* pk1 = pk0 + a.pack_stride;
+  const _Float16* epm = a.epm + (int64_t)pr * kMImg;
+  // the weight streams (issued first: their first steps load during the BN prologue)
+  auto fc_ring = mfma_ring<kFcKS>(a.thm, epm, [w, l](int q) { return ((int64_t)(q * kFcNT + 4 * w) * 64 + l) * 8; });
+  fc_ring.prime();
+  auto gate_ring = mfma_ring<4 * kGateKS>(a.thm + kFcImg, epm + kFcImg, [w, l](int q) {
+    const int g = q / kGateKS, ks = q - g * kGateKS;
+    return ((int64_t)(ks * kGateNT + 16 * w + 4 * g) * 64 + l) * 8;
+  });
+  const bool neg0 = a.sign && a.sign[l0] < 0, neg1 = a.sign && a.sign[l0 + 1] < 0;
+  const int64_t e0 = (int64_t)l0 * E;
+  const int A = a.n_act;
+  auto pkof = [&](int e) { return e < E ? pk0 : pk1; };
+  // this lane's B column: env (l & 15) mod E2; S X flips the sign bits of the minus lane's column
+  const int benv = (l & 15) & (E2 - 1);
+  const unsigned smask = (benv < E ? neg0 : neg1) ? 0x80008000u : 0u;
+  auto bfrag = [&](const _Float16* rowp, int k0, h8& x, h8& sx) {
+    x = *reinterpret_cast<const h8*>(rowp + k0 + 8 * (l >> 4));
+    u32x4 u = __builtin_bit_cast(u32x4, x);
+    u ^= u32x4{smask, smask, smask, smask};
+    sx = __builtin_bit_cast(h8, u);
+  };
+
+  // the fc biases of this lane's 16 outputs (rows 4 (l >> 4) .. +3 of its 4 tiles; env column l & 15)
+  float4 fcb[4];
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+    fcb[jt] = *reinterpret_cast<const float4*>(pkof(benv) + L.fc_b + 16 * (4 * w + jt) + 4 * (l >> 4));
+  for (int i = j; i < 2 * kGates; i += kCoreThreads) {  // b_ih + b_hh per lane of the pair
+    const float* pk = i < kGates ? pk0 : pk1;
+    const int col = i & (kGates - 1);
+    bsum[i] = pk[L.lstm_bih + col] + pk[L.lstm_bhh + col];
+  }
+  // branch-free loads (a conditional load ends its block with a full vmcnt wait): without running statistics
+  // the loads read the pack and the values are replaced by 0 / 1
+  const bool has_m = a.bn_mean != nullptr, has_v = a.bn_var != nullptr;
+  const float* bmp = has_m ? a.bn_mean + L.bn_stat[15] : pk0;
+  const float* bvp = has_v ? a.bn_var + L.bn_stat[15] : pk0;
+  typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int it = 0; it < kFeat / (4 * kCoreThreads); ++it) {  // BN1d(2048) -> f16 rows; 4 features per thread
+    const int k = 4 * j + 4 * kCoreThreads * it;
+    float rm[4], rv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float rmv = bmp[k + c], rvv = bvp[k + c];
+      rm[c] = has_m ? rmv : 0.f;
+      rv[c] = has_v ? rvv : 1.f;
+    }
+    float4 f[E2];
+#pragma unroll
+    for (int e = 0; e < E2; ++e) f[e] = *reinterpret_cast<const float4*>(a.feat + (e0 + e) * kFeat + k);
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const float* pk = hf ? pk1 : pk0;
+      const float4 w4 = *reinterpret_cast<const float4*>(pk + L.bn_w[15] + k);
+      const float4 b4 = *reinterpret_cast<const float4*>(pk + L.bn_b[15] + k);
+      float sc[4], sh[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        sc[c] = w4[c] * (1.f / sqrtf(rv[c] + kBnEps));
+        sh[c] = b4[c] - rm[c] * sc[c];
+      }
+#pragma unroll
+      for (int e = hf * E; e < hf * E + E; ++e)
+        *reinterpret_cast<h4v*>(xh + e * XP + k) =
+            h4v{(_Float16)fmaf(f[e][0], sc[0], sh[0]), (_Float16)fmaf(f[e][1], sc[1], sh[1]),
+                (_Float16)fmaf(f[e][2], sc[2], sh[2]), (_Float16)fmaf(f[e][3], sc[3], sh[3])};
+    }
+  }
+  float cj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    gh[e * GP + kCoreIn + j] = (_Float16)a.h[(e0 + e) * kHid + j];
+    cj[e] = a.c[(e0 + e) * kHid + j];
+  }
+  for (int i = j; i < E2 * (GP - kGateK); i += kCoreThreads) {
+    const int e = i / (GP - kGateK);
+    gh[e * GP + kGateK + i - e * (GP - kGateK)] = (_Float16)0.f;
+  }
+  float* ci = a.ci ? a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn : nullptr;
+  if (j < E2) {
+    const float r = fminf(fmaxf(a.rprev[e0 + j], -1.f), 1.f);
+    gh[j * GP + kHid] = (_Float16)r;
+    if (ci) ci[j * kCoreIn + kHid] = r;
+  }
+  __syncthreads();
+  {  // fc: wave w owns column tiles 4w .. 4w+3 over the 64 k-steps
+    f32x4 acc[4];
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const _Float16* xrow = xh + benv * XP;
+    fc_ring.run(
+        [&](int q, const h8 (&tf)[4], const h8 (&ef)[4]) {
+          h8 x, sx;
+          bfrag(xrow, 32 * q, x, sx);
+#pragma unroll
+          for (int jt = 0; jt < 4; ++jt) {
+            acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(tf[jt], x, acc[jt], 0, 0, 0);
+            acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ef[jt], sx, acc[jt], 0, 0, 0);
+          }
+        });
+    gate_ring.prime();  // the gate weights' first steps load during the epilogue and the barrier
+    if ((l & 15) < E2) {  // lane: rows 4 (l >> 4) .. +3 of each tile, env column l & 15
+      const int e = l & 15;
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = 16 * (4 * w + jt) + 4 * (l >> 4) + i;
+          const float y = relu(acc[jt][i] + fcb[jt][i]);
+          gh[e * GP + n] = (_Float16)y;
+          if (ci) ci[e * kCoreIn + n] = y;
+        }
+    }
+  }
+  __syncthreads();  // gate input complete; xh dead (the gates region reuses it)
+  {  // gates: wave w owns column tiles 16w .. 16w+15, four at a time over the 17 k-steps
+    f32x4 acc[4];
+    const _Float16* grow = gh + benv * GP;
+    gate_ring.run(
+        [&](int q, const h8 (&tf)[4], const h8 (&ef)[4]) {
+          const int g = q / kGateKS, ks = q - g * kGateKS;
+          if (ks == 0)
+#pragma unroll
+            for (int jt = 0; jt < 4; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          h8 x, sx;
+          bfrag(grow, 32 * ks, x, sx);
+#pragma unroll
+          for (int jt = 0; jt < 4; ++jt) {
+            acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(tf[jt], x, acc[jt], 0, 0, 0);
+            acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ef[jt], sx, acc[jt], 0, 0, 0);
+          }
+          if (ks == kGateKS - 1 && (l & 15) < E2) {
+#pragma unroll
+            for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                gates[(16 * (16 * w + 4 * g + jt) + 4 * (l >> 4) + i) * E2 + (l & 15)] = acc[jt][i];
+          }
+        });
+  }
+  __syncthreads();
+  float hj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    float pre[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int col = g * kHid + j;
+      pre[g] = gates[col * E2 + e] + bsum[(e < E ? 0 : kGates) + col];
+    }
+    const float gi = sigm(pre[0]), gf = sigm(pre[1]), gg = tanhf(pre[2]), go = sigm(pre[3]);
+    cj[e] = gf * cj[e] + gi * gg;
+    hj[e] = go * tanhf(cj[e]);
+    a.h[(e0 + e) * kHid + j] = hj[e];
+    a.c[(e0 + e) * kHid + j] = cj[e];
+  }
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const float* pk = hf ? pk1 : pk0;
+    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
+    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
+    const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
+    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+#pragma unroll
+    for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
+  }
+  __syncthreads();
+  if (j < A * E2) {  // head in f32 (A x 256, tiny), each lane's own
+    const int ai = j / E2, e = j - ai * E2;
+    const float* pk = pkof(e);
+    const float* wh = pk + L.head_w + ai * kHid;
+    float s = 0.f;
+    for (int k = 0; k < kHid; ++k) s = fmaf(wh[k], hs[k * E2 + e], s);
+    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
+  }
+  __syncthreads();
+  if (j < E2) core_finish<E, kRollout>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
+}
+
+template __global__ void core_kernel_hpm<1>(Layout, StepArgs);
+template __global__ void core_kernel_hpm<2>(Layout, StepArgs);
+template __global__ void core_kernel_hpm<4>(Layout, StepArgs);
+
 template __global__ void core_kernel_hpr<1>(Layout, StepArgs);
 template __global__ void core_kernel_hpr<2>(Layout, StepArgs);
 template __global__ void core_kernel_hpr<4>(Layout, StepArgs);

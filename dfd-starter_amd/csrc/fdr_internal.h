@@ -21,6 +21,7 @@ struct Context {
   int cus = 0;          // compute units of `device` (0: query the current device)
   int rollout_impl = 2; // FDR_ROLLOUT_AUTO
   int replay_gemm = 1;
+  int core_mfma = 1;    // fp16 pair-form core step on MFMA (core_kernel_hpm); 0: the VALU form (core_kernel_hp)
   uint64_t* debug_clock = nullptr;
   impala::Profile* prof = nullptr;  // owned, created on first enable
 };

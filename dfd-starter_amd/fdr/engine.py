@@ -42,6 +42,10 @@ class Context(object):
     def set_replay_gemm(self, on):
         check(lib.fdr_ctx_set_replay_gemm(self.handle, 1 if on else 0), "fdr_ctx_set_replay_gemm")
 
+    def set_core_mfma(self, on):
+        """fp16 pair-form Impala core step: MFMA (True, default) or the VALU form (False)."""
+        check(lib.fdr_ctx_set_core_mfma(self.handle, 1 if on else 0), "fdr_ctx_set_core_mfma")
+
     def impala_profile(self, enable):
         check(lib.fdr_ctx_impala_profile(self.handle, 1 if enable else 0), "fdr_ctx_impala_profile")
 

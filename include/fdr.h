@@ -100,6 +100,10 @@ int fdr_ctx_device(const fdr_ctx* ctx);
 /* per-context settings (ctx = NULL: the default context) */
 int fdr_ctx_set_rollout_impl(fdr_ctx* ctx, int32_t impl);  /* FDR_ROLLOUT_* below */
 int fdr_ctx_set_replay_gemm(fdr_ctx* ctx, int32_t on);     /* see fdr_impala_set_replay_gemm */
+/* fp16 pair-form Impala core step (fdr_impala_desc.fp16 && .pairs): 1 (default) = fc / LSTM GEMMs on
+   v_mfma_f32_16x16x32_f16 as theta X + E (S X) over MFMA-fragment images of theta and each pair's sigma-eps
+   (activations rounded to f16); 0 = the VALU form (w = f16(theta) + s f16(sigma eps) formed per element) */
+int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on);
 int fdr_ctx_impala_profile(fdr_ctx* ctx, int32_t enable);  /* see fdr_impala_profile */
 int fdr_ctx_impala_profile_read(fdr_ctx* ctx, double* ms);
 int fdr_ctx_impala_debug_clock(fdr_ctx* ctx, uint64_t* buf);

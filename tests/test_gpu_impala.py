@@ -325,9 +325,9 @@ def test_fp16_multistep_drift_bound_vs_f32_oracle(engine, table):
 
 
 def test_fp16_pair_core_matches_per_lane_core(engine, table):
-    """fdr_impala_desc.pairs (config 5's antithetic pairs): the core step forms w = f16(theta) + s f16(sigma eps)
-    from theta's shared half pack and the pair's sigma-eps half pack instead of streaming each lane's
-    f16(theta + s sigma eps).  Step 0 sees identical conv features in both forms: probabilities within the fp16
+    """fdr_impala_desc.pairs (config 5's antithetic pairs): the core step computes W_l x = theta x + s_l (E x) on MFMA
+    from theta's and the pair's sigma-eps fragment images (default), or forms w = f16(theta) + s f16(sigma eps) per
+    element on the VALU (core_mfma off), instead of streaming each lane's f16(theta + s sigma eps).  Step 0 sees identical conv features in both forms: probabilities within the fp16
     tolerance of the per-lane form and of the f32 path; norms identical; whole episodes finite."""
     A, E, T = 4, 4, 5
     theta = _theta(A)
@@ -336,17 +336,21 @@ def test_fp16_pair_core_matches_per_lane_core(engine, table):
     dev = "cuda"
     lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
                               torch.tensor(idx, device=dev), torch.tensor(sign, device=dev), 0.02)
+    valu = engine.Context()   # the VALU pair form (core_kernel_hp); the default context runs the MFMA form
+    valu.set_core_mfma(False)
     outs = {}
-    for name, fp16, pairs in (("lane", True, False), ("pair", True, True), ("f32", False, False)):
+    for name, fp16, pairs, ctx in (("lane", True, False, None), ("pair", True, True, None),
+                                   ("pair_valu", True, True, valu), ("f32", False, False, None)):
         outs[name] = engine.impala_rollout(engine.ImpalaSpec(A, E, T, env_seed=5, fp16=fp16, pairs=pairs), lanes,
-                                           len(idx), 11, record=True)
+                                           len(idx), 11, record=True, ctx=ctx)
     torch.cuda.synchronize()
-    p_pair = outs["pair"].probs.cpu().numpy()[:, 0]
-    np.testing.assert_allclose(p_pair, outs["lane"].probs.cpu().numpy()[:, 0], rtol=F16_RTOL / 4)
-    np.testing.assert_allclose(p_pair, outs["f32"].probs.cpu().numpy()[:, 0], rtol=F16_RTOL)
-    np.testing.assert_array_equal(outs["pair"].norm2.cpu().numpy(), outs["lane"].norm2.cpu().numpy())
-    for t in (outs["pair"].reward, outs["pair"].entropy):
-        assert np.all(np.isfinite(t.cpu().numpy()))
+    for form in ("pair", "pair_valu"):
+        p_pair = outs[form].probs.cpu().numpy()[:, 0]
+        np.testing.assert_allclose(p_pair, outs["lane"].probs.cpu().numpy()[:, 0], rtol=F16_RTOL / 4)
+        np.testing.assert_allclose(p_pair, outs["f32"].probs.cpu().numpy()[:, 0], rtol=F16_RTOL)
+        np.testing.assert_array_equal(outs[form].norm2.cpu().numpy(), outs["lane"].norm2.cpu().numpy())
+        for t in (outs[form].reward, outs[form].entropy):
+            assert np.all(np.isfinite(t.cpu().numpy()))
 
 
 def test_f32_pair_core_bit_identical(engine, table):
