@@ -1345,9 +1345,12 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
       const int col = g * kHid + j;
       pre[g] = gates[col * E2 + e] + bsum[(e < E ? 0 : kGates) + col];
     }
-    const float gi = sigm(pre[0]), gf = sigm(pre[1]), gg = tanhf(pre[2]), go = sigm(pre[3]);
+    // v_exp / v_rcp forms (abs error ~3e-7, inside the fp16 tolerance): the cell phase has no HBM stream
+    // under it, and the accurate expf / tanhf / IEEE division were ~1,500 instructions per thread
+    auto sg = [](float x) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x)); };
+    const float gi = sg(pre[0]), gf = sg(pre[1]), gg = tanh_fast(pre[2]), go = sg(pre[3]);
     cj[e] = gf * cj[e] + gi * gg;
-    hj[e] = go * tanhf(cj[e]);
+    hj[e] = go * tanh_fast(cj[e]);
     a.h[(e0 + e) * kHid + j] = hj[e];
     a.c[(e0 + e) * kHid + j] = cj[e];
   }
