@@ -1355,7 +1355,7 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
     bool pair_done = false;
     if constexpr (E <= 4) {
       if (h && a.epm) {
-        hipLaunchKernelGGL((core_kernel_hpm<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
+        hipLaunchKernelGGL((core_kernel_hpm<E, kRollout>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
         pair_done = true;
       } else if (h && a.ep) {
         hipLaunchKernelGGL((core_kernel_hp<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
@@ -1390,7 +1390,11 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
         a.t = t;
         bool pair_done = false;
         if constexpr (E <= 4) {
-          if (a.gx && h && a.ep) {
+          if (a.gx && h && a.epm) {
+            hipLaunchKernelGGL((core_kernel_hpm<E, kReplay>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L,
+                               a);
+            pair_done = true;
+          } else if (a.gx && h && a.ep) {
             hipLaunchKernelGGL((core_kernel_hpr<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
             pair_done = true;
           } else if (a.gx && !h && a.ep32) {

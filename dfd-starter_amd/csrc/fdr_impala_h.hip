@@ -1175,10 +1175,14 @@ __device__ __forceinline__ MfmaRing<NQ, Frag> mfma_ring(const _Float16* thm, con
   return MfmaRing<NQ, Frag>{thm, epm, f};
 }
 
-template <int E>
+// MODE kRollout: the step (fc + gates).  MODE kReplay (entropy pass, a.gx = x W_ih^T of the chunk): the W_hh
+// product only -- the gate images' k-steps 8 .. 16 (rows 256 .. 543) against B rows [0 | h | 0].
+template <int E, int MODE>
 __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2))) void core_kernel_hpm(Layout L,
                                                                                                        StepArgs a) {
   constexpr int E2 = 2 * E;
+  constexpr bool kRep = MODE == kReplay;
+  constexpr int kKs0 = kRep ? kCoreIn / 32 : 0, kNks = kGateKS - kKs0;  // the gate k-steps streamed
   static_assert(E2 <= 16 && (E2 & (E2 - 1)) == 0, "the pair's envs are the B operand's columns (mod E2)");
   constexpr int XP = kFeat + 16;         // f16 pitch of BN(features) rows [env][k]
   constexpr int GP = kGateKS * 32 + 16;  // f16 pitch of the gate input rows [env][cis (257) | h (256) | 0]
@@ -1197,11 +1201,14 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
   const _Float16* epm = a.epm + (int64_t)pr * kMImg;
   // the weight streams (issued first: their first steps load during the BN prologue)
   auto fc_ring = mfma_ring<kFcKS>(a.thm, epm, [w, l](int q) { return ((int64_t)(q * kFcNT + 4 * w) * 64 + l) * 8; });
-  fc_ring.prime();
-  auto gate_ring = mfma_ring<4 * kGateKS>(a.thm + kFcImg, epm + kFcImg, [w, l](int q) {
-    const int g = q / kGateKS, ks = q - g * kGateKS;
+  auto gate_ring = mfma_ring<4 * kNks>(a.thm + kFcImg, epm + kFcImg, [w, l](int q) {
+    const int g = q / kNks, ks = kKs0 + q - g * kNks;
     return ((int64_t)(ks * kGateNT + 16 * w + 4 * g) * 64 + l) * 8;
   });
+  if constexpr (kRep)
+    gate_ring.prime();
+  else
+    fc_ring.prime();
   const bool neg0 = a.sign && a.sign[l0] < 0, neg1 = a.sign && a.sign[l0 + 1] < 0;
   const int64_t e0 = (int64_t)l0 * E;
   const int A = a.n_act;
@@ -1216,16 +1223,29 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
     sx = __builtin_bit_cast(h8, u);
   };
 
-  // the fc biases of this lane's 16 outputs (rows 4 (l >> 4) .. +3 of its 4 tiles; env column l & 15)
-  float4 fcb[4];
+  float cj[E2];
 #pragma unroll
-  for (int jt = 0; jt < 4; ++jt)
-    fcb[jt] = *reinterpret_cast<const float4*>(pkof(benv) + L.fc_b + 16 * (4 * w + jt) + 4 * (l >> 4));
+  for (int e = 0; e < E2; ++e) {
+    gh[e * GP + kCoreIn + j] = (_Float16)a.h[(e0 + e) * kHid + j];
+    cj[e] = a.c[(e0 + e) * kHid + j];
+  }
+  for (int i = j; i < E2 * (GP - kGateK); i += kCoreThreads) {
+    const int e = i / (GP - kGateK);
+    gh[e * GP + kGateK + i - e * (GP - kGateK)] = (_Float16)0.f;
+  }
   for (int i = j; i < 2 * kGates; i += kCoreThreads) {  // b_ih + b_hh per lane of the pair
     const float* pk = i < kGates ? pk0 : pk1;
     const int col = i & (kGates - 1);
     bsum[i] = pk[L.lstm_bih + col] + pk[L.lstm_bhh + col];
   }
+  if constexpr (kRep) {
+    if (j < E2) gh[j * GP + kHid] = (_Float16)0.f;  // W_ih's reward row: its product is inside a.gx
+  } else {
+  // the fc biases of this lane's 16 outputs (rows 4 (l >> 4) .. +3 of its 4 tiles; env column l & 15)
+  float4 fcb[4];
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+    fcb[jt] = *reinterpret_cast<const float4*>(pkof(benv) + L.fc_b + 16 * (4 * w + jt) + 4 * (l >> 4));
   // branch-free loads (a conditional load ends its block with a full vmcnt wait): without running statistics
   // the loads read the pack and the values are replaced by 0 / 1
   const bool has_m = a.bn_mean != nullptr, has_v = a.bn_var != nullptr;
@@ -1263,16 +1283,6 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
                 (_Float16)fmaf(f[e][2], sc[2], sh[2]), (_Float16)fmaf(f[e][3], sc[3], sh[3])};
     }
   }
-  float cj[E2];
-#pragma unroll
-  for (int e = 0; e < E2; ++e) {
-    gh[e * GP + kCoreIn + j] = (_Float16)a.h[(e0 + e) * kHid + j];
-    cj[e] = a.c[(e0 + e) * kHid + j];
-  }
-  for (int i = j; i < E2 * (GP - kGateK); i += kCoreThreads) {
-    const int e = i / (GP - kGateK);
-    gh[e * GP + kGateK + i - e * (GP - kGateK)] = (_Float16)0.f;
-  }
   float* ci = a.ci ? a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn : nullptr;
   if (j < E2) {
     const float r = fminf(fmaxf(a.rprev[e0 + j], -1.f), 1.f);
@@ -1309,14 +1319,15 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
         }
     }
   }
+  }  // !kRep
   __syncthreads();  // gate input complete; xh dead (the gates region reuses it)
-  {  // gates: wave w owns column tiles 16w .. 16w+15, four at a time over the 17 k-steps
+  {  // gates: wave w owns column tiles 16w .. 16w+15, four at a time over the kNks k-steps
     f32x4 acc[4];
     const _Float16* grow = gh + benv * GP;
     gate_ring.run(
         [&](int q, const h8 (&tf)[4], const h8 (&ef)[4]) {
-          const int g = q / kGateKS, ks = q - g * kGateKS;
-          if (ks == 0)
+          const int g = q / kNks, ks = kKs0 + q - g * kNks;
+          if (ks == kKs0)
 #pragma unroll
             for (int jt = 0; jt < 4; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
           h8 x, sx;
@@ -1344,6 +1355,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
     for (int g = 0; g < 4; ++g) {
       const int col = g * kHid + j;
       pre[g] = gates[col * E2 + e] + bsum[(e < E ? 0 : kGates) + col];
+      if constexpr (kRep) pre[g] += a.gx[((int64_t)(a.t - a.gx_t0) * a.n_lanes * E + e0 + e) * kGates + col];
     }
     // v_exp / v_rcp forms (abs error ~3e-7, inside the fp16 tolerance): the cell phase has no HBM stream
     // under it, and the accurate expf / tanhf / IEEE division were ~1,500 instructions per thread
@@ -1374,12 +1386,15 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
     logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
   }
   __syncthreads();
-  if (j < E2) core_finish<E, kRollout>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
+  if (j < E2) core_finish<E, MODE>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
 }
 
-template __global__ void core_kernel_hpm<1>(Layout, StepArgs);
-template __global__ void core_kernel_hpm<2>(Layout, StepArgs);
-template __global__ void core_kernel_hpm<4>(Layout, StepArgs);
+template __global__ void core_kernel_hpm<1, kRollout>(Layout, StepArgs);
+template __global__ void core_kernel_hpm<2, kRollout>(Layout, StepArgs);
+template __global__ void core_kernel_hpm<4, kRollout>(Layout, StepArgs);
+template __global__ void core_kernel_hpm<1, kReplay>(Layout, StepArgs);
+template __global__ void core_kernel_hpm<2, kReplay>(Layout, StepArgs);
+template __global__ void core_kernel_hpm<4, kReplay>(Layout, StepArgs);
 
 template __global__ void core_kernel_hpr<1>(Layout, StepArgs);
 template __global__ void core_kernel_hpr<2>(Layout, StepArgs);

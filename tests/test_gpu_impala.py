@@ -351,6 +351,10 @@ def test_fp16_pair_core_matches_per_lane_core(engine, table):
         np.testing.assert_array_equal(outs[form].norm2.cpu().numpy(), outs["lane"].norm2.cpu().numpy())
         for t in (outs[form].reward, outs[form].entropy):
             assert np.all(np.isfinite(t.cpu().numpy()))
+    # the entropy replay in both pair forms (MFMA: core_kernel_hpm<kReplay>; VALU: core_kernel_hpr)
+    np.testing.assert_allclose(outs["pair"].entropy.cpu().numpy(), outs["pair_valu"].entropy.cpu().numpy(),
+                               rtol=F16_RTOL)
+    np.testing.assert_allclose(outs["pair"].entropy.cpu().numpy(), outs["f32"].entropy.cpu().numpy(), rtol=F16_RTOL)
 
 
 def test_f32_pair_core_bit_identical(engine, table):
