@@ -936,12 +936,19 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_p(Layout L, StepArgs
     }
   };
 
-  for (int k = j; k < kFeat; k += kCoreThreads) {
+  // branch-free BN1d loads (a conditional load ends its block with a full vmcnt wait; without running
+  // statistics the loads read the pack and the values are replaced by 0 / 1) -- the same values
+  const bool has_m = a.bn_mean != nullptr, has_v = a.bn_var != nullptr;
+  const float* bmp = has_m ? a.bn_mean + L.bn_stat[15] : pk0;
+  const float* bvp = has_v ? a.bn_var + L.bn_stat[15] : pk0;
+#pragma unroll
+  for (int it = 0; it < kFeat / kCoreThreads; ++it) {
+    const int k = j + it * kCoreThreads;
+    const float rmv = bmp[k], rvv = bvp[k];
+    const float rm = has_m ? rmv : 0.f, rv = has_v ? rvv : 1.f;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       const float* pk = hf ? pk1 : pk0;
-      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + k] : 0.f;
-      const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + k] : 1.f;
       const float sc = pk[L.bn_w[15] + k] * (1.f / sqrtf(rv + kBnEps));
       const float sh = pk[L.bn_b[15] + k] - rm * sc;
 #pragma unroll
