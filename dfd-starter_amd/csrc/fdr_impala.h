@@ -229,6 +229,9 @@ template <int E>
 __global__ void core_kernel_hpr(Layout L, StepArgs a); // fp16 pair form of the replay (with a.gx)
 template <int E, int MODE>
 __global__ void core_kernel_hpm(Layout L, StepArgs a); // fp16 pair form on MFMA (kRollout / kReplay), grid n_lanes / 2
+// replay input projection of a chunk in the fp16 pair form on MFMA: grid (n_lanes / 2, kGateNT / 4)
+template <int E>
+__global__ void xproj_pair_kernel(Layout L, StepArgs a, int t0, int tc, float* gx);
 // MFMA images (kMImg halves each) of n half packs: grid (kFcKS + 4 kGateKS, n)
 __global__ void mfma_image_kernel(Layout L, const _Float16* src, int64_t src_stride, _Float16* dst);
 constexpr int kHThreads = 512;

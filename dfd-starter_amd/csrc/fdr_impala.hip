@@ -1386,7 +1386,16 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
       const int tc = std::min(kReplayChunk, a.T - t0);
       if (ctx.replay_gemm && gx) {
         const dim3 grid(a.n_lanes, (tc * E + 63) / 64, kGates / 256);
-        if (h)
+        bool pair_xproj = false;
+        if constexpr (E <= 4) {
+          if (h && a.epm) {  // fp16 pair form on MFMA: theta X + s (E X) from the gate images
+            hipLaunchKernelGGL((xproj_pair_kernel<E>), dim3(a.n_lanes / 2, kGateNT / 4), dim3(256), 0, stream, L, a,
+                               t0, tc, gx);
+            pair_xproj = true;
+          }
+        }
+        if (pair_xproj) {
+        } else if (h)
           hipLaunchKernelGGL(lstm_xproj_kernel<true>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);
         else
           hipLaunchKernelGGL(lstm_xproj_kernel<false>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);

@@ -1389,6 +1389,65 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
   if (j < E2) core_finish<E, MODE>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
 }
 
+// Entropy replay, input projection of one chunk in the fp16 pair form on MFMA: gx = theta X + s (E X) with the
+// gate images' k-steps 0 .. 8 (rows 0 .. 287 = W_ih^T's 257 rows; X is zero beyond k = 256) -- the per-lane
+// f32 GEMM (lstm_xproj_kernel<true>) ran at the f32 MFMA rate and re-read each lane's W_ih per row block.
+// Grid (n_pairs, kGateNT / 4): a workgroup holds its 4 column tiles' theta / E fragments in LDS (72 KiB) and
+// its 4 waves take the pair's row tiles (rows = (t, env of the pair), B columns; X rounded to f16).
+template <int E>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void xproj_pair_kernel(Layout L, StepArgs a, int t0,
+                                                                                            int tc, float* __restrict__ gx) {
+  constexpr int E2 = 2 * E, KS = (kCoreIn + 31) / 32;
+  __shared__ h8 af[2][KS][4][64];
+  const int pr = blockIdx.x, nt0 = 4 * blockIdx.y, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const _Float16* src[2] = {a.thm + kFcImg, a.epm + (int64_t)pr * kMImg + kFcImg};
+  for (int i = tid; i < 2 * KS * 4 * 64; i += 256) {
+    const int sidx = i / (KS * 256), rem = i - sidx * (KS * 256), ks = rem >> 8, jt = (rem >> 6) & 3, ll = rem & 63;
+    af[sidx][ks][jt][ll] = *reinterpret_cast<const h8*>(src[sidx] + (((int64_t)ks * kGateNT + nt0 + jt) * 64 + ll) * 8);
+  }
+  const int l0 = 2 * pr;
+  const bool neg0 = a.sign && a.sign[l0] < 0, neg1 = a.sign && a.sign[l0 + 1] < 0;
+  const int64_t e0 = (int64_t)l0 * E, ne = (int64_t)a.n_lanes * E;
+  const int rows = tc * E2;
+  __syncthreads();
+  for (int rt = w; rt < (rows + 15) / 16; rt += 4) {
+    const int row = rt * 16 + (l & 15);  // this lane's B column
+    const bool ok = row < rows;
+    const int rr = ok ? row : 0, t = rr / E2, env = rr - t * E2;
+    const float* xr = a.ci + ((int64_t)(t0 + t) * ne + e0 + env) * kCoreIn;
+    const unsigned smask = (env < E ? neg0 : neg1) ? 0x80008000u : 0u;
+    f32x4 acc[4];
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 3
+    for (int ks = 0; ks < KS; ++ks) {
+      h8 x;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int k = 32 * ks + 8 * (l >> 4) + i;
+        const float v = xr[k < kCoreIn ? k : 0];  // branch-free: the clamped load is discarded
+        x[i] = (_Float16)(ok && k < kCoreIn ? v : 0.f);
+      }
+      u32x4 u = __builtin_bit_cast(u32x4, x);
+      u ^= u32x4{smask, smask, smask, smask};
+      const h8 sx = __builtin_bit_cast(h8, u);
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt) {
+        acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[0][ks][jt][l], x, acc[jt], 0, 0, 0);
+        acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[1][ks][jt][l], sx, acc[jt], 0, 0, 0);
+      }
+    }
+    if (ok) {  // lane: gate columns 16 (nt0 + jt) + 4 (l >> 4) .. +3 of its row
+      float* dst = gx + ((int64_t)t * ne + e0 + env) * kGates + 16 * nt0 + 4 * (l >> 4);
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt) *reinterpret_cast<f32x4*>(dst + 16 * jt) = acc[jt];
+    }
+  }
+}
+template __global__ void xproj_pair_kernel<1>(Layout, StepArgs, int, int, float*);
+template __global__ void xproj_pair_kernel<2>(Layout, StepArgs, int, int, float*);
+template __global__ void xproj_pair_kernel<4>(Layout, StepArgs, int, int, float*);
+
 template __global__ void core_kernel_hpm<1, kRollout>(Layout, StepArgs);
 template __global__ void core_kernel_hpm<2, kRollout>(Layout, StepArgs);
 template __global__ void core_kernel_hpm<4, kRollout>(Layout, StepArgs);
