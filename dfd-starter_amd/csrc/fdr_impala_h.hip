@@ -1209,8 +1209,18 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
     gate_ring.prime();
   else
     fc_ring.prime();
-  const bool neg0 = a.sign && a.sign[l0] < 0, neg1 = a.sign && a.sign[l0 + 1] < 0;
   const int64_t e0 = (int64_t)l0 * E;
+  // replay: this thread's x W_ih^T gate inputs (unit j of the 4 gates, every env), loaded ahead of the stream
+  // (used after it: a load there is a dependent round trip per env)
+  float gxv[kRep ? E2 : 1][4];
+  if constexpr (kRep) {
+    const float* g = a.gx + ((int64_t)(a.t - a.gx_t0) * a.n_lanes * E + e0) * kGates + j;
+#pragma unroll
+    for (int e = 0; e < E2; ++e)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gxv[e][q] = g[(int64_t)e * kGates + q * kHid];
+  }
+  const bool neg0 = a.sign && a.sign[l0] < 0, neg1 = a.sign && a.sign[l0 + 1] < 0;
   const int A = a.n_act;
   auto pkof = [&](int e) { return e < E ? pk0 : pk1; };
   // this lane's B column: env (l & 15) mod E2; S X flips the sign bits of the minus lane's column
@@ -1355,7 +1365,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
     for (int g = 0; g < 4; ++g) {
       const int col = g * kHid + j;
       pre[g] = gates[col * E2 + e] + bsum[(e < E ? 0 : kGates) + col];
-      if constexpr (kRep) pre[g] += a.gx[((int64_t)(a.t - a.gx_t0) * a.n_lanes * E + e0 + e) * kGates + col];
+      if constexpr (kRep) pre[g] += gxv[e][g];
     }
     // v_exp / v_rcp forms (abs error ~3e-7, inside the fp16 tolerance): the cell phase has no HBM stream
     // under it, and the accurate expf / tanhf / IEEE division were ~1,500 instructions per thread
@@ -1369,8 +1379,9 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
     const float* pk = hf ? pk1 : pk0;
-    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
-    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
+    const float rmv = (a.bn_mean ? a.bn_mean + L.bn_stat[16] : pk0)[j];  // branch-free (see the BN1d prologue)
+    const float rvv = (a.bn_var ? a.bn_var + L.bn_stat[16] : pk0)[j];
+    const float rm = a.bn_mean ? rmv : 0.f, rv = a.bn_var ? rvv : 1.f;
     const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
     const float sh = pk[L.bn_b[16] + j] - rm * sc;
 #pragma unroll
