@@ -1220,7 +1220,10 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
       for (int q = 0; q < 4; ++q) gxv[e][q] = g[(int64_t)e * kGates + q * kHid];
   }
-  const bool neg0 = a.sign && a.sign[l0] < 0, neg1 = a.sign && a.sign[l0 + 1] < 0;
+  // branch-free sign loads (a conditional load would end its block with a full vmcnt wait behind the ring)
+  const int8_t* sgp = a.sign ? a.sign + l0 : reinterpret_cast<const int8_t*>(pk0);
+  const int8_t sg0v = sgp[0], sg1v = sgp[1];
+  const bool neg0 = a.sign && sg0v < 0, neg1 = a.sign && sg1v < 0;
   const int A = a.n_act;
   auto pkof = [&](int e) { return e < E ? pk0 : pk1; };
   // this lane's B column: env (l & 15) mod E2; S X flips the sign bits of the minus lane's column
@@ -1243,7 +1246,9 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
     const int e = i / (GP - kGateK);
     gh[e * GP + kGateK + i - e * (GP - kGateK)] = (_Float16)0.f;
   }
-  for (int i = j; i < 2 * kGates; i += kCoreThreads) {  // b_ih + b_hh per lane of the pair
+#pragma unroll
+  for (int it = 0; it < 2 * kGates / kCoreThreads; ++it) {  // b_ih + b_hh per lane of the pair
+    const int i = j + it * kCoreThreads;
     const float* pk = i < kGates ? pk0 : pk1;
     const int col = i & (kGates - 1);
     bsum[i] = pk[L.lstm_bih + col] + pk[L.lstm_bhh + col];
@@ -1294,10 +1299,12 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
     }
   }
   float* ci = a.ci ? a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn : nullptr;
-  if (j < E2) {
-    const float r = fminf(fmaxf(a.rprev[e0 + j], -1.f), 1.f);
-    gh[j * GP + kHid] = (_Float16)r;
-    if (ci) ci[j * kCoreIn + kHid] = r;
+  {
+    const float r = fminf(fmaxf(a.rprev[e0 + (j & (E2 - 1))], -1.f), 1.f);  // every thread loads: no branch
+    if (j < E2) {
+      gh[j * GP + kHid] = (_Float16)r;
+      if (ci) ci[j * kCoreIn + kHid] = r;
+    }
   }
   __syncthreads();
   {  // fc: wave w owns column tiles 4w .. 4w+3 over the 64 k-steps
