@@ -918,7 +918,10 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_p(Layout L, StepArgs
   const int l0 = 2 * pr;
   const float* pk0 = a.pack + (int64_t)l0 * a.pack_stride;
   const float* pk1 = pk0 + a.pack_stride;
-  const float sg0 = a.sign ? (float)a.sign[l0] : 1.f, sg1 = a.sign ? (float)a.sign[l0 + 1] : 1.f;
+  // branch-free sign loads (a conditional load ends its block with a full vmcnt wait)
+  const int8_t* sgp = a.sign ? a.sign + l0 : reinterpret_cast<const int8_t*>(pk0);
+  const int8_t sg0v = sgp[0], sg1v = sgp[1];
+  const float sg0 = a.sign ? (float)sg0v : 1.f, sg1 = a.sign ? (float)sg1v : 1.f;
   const float* ep = a.ep32 + (int64_t)pr * a.ep_stride;
   const int64_t e0 = (int64_t)l0 * E;
   const int A = a.n_act;
