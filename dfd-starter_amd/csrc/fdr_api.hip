@@ -412,8 +412,6 @@ static int fd_grad_fused_impl(const float* table, int64_t table_size, const int6
   const int n_local = n_dirs * lanes_per_dir;
   if (!idx_local || !rewards_all || !sign_local || !norm2_local) return set_error(FDR_ERR_INVALID, "NULL pointer");
   if (n_all <= 0 || lane_lo < 0 || lane_lo + n_local > n_all) return set_error(FDR_ERR_INVALID, "bad lane range");
-  if (mode == FDR_WEIGHT_MOMENTS && (lane_lo != 0 || n_all != n_local))
-    return set_error(FDR_ERR_INVALID, "moments form takes the local rewards only (lane_lo = 0, n_all = n_local)");
   return launch_fd_grad_fused(table, table_size, idx_local, n_dirs, n_params, rewards_all, n_all, policy_reward,
                               lane_lo, sign_local, norm2_local, lanes_per_dir, sigma, mode, out, theta, lr, lr_scale,
                               hist, dsgd_out, workspace, workspace_bytes, (hipStream_t)stream);

@@ -557,10 +557,10 @@ struct FdArgs {
   const int64_t* idx;    // per LOCAL lane [n_dirs * lpd]; direction d's row starts at idx[d * lpd]
   int n_dirs;
   int64_t P;
-  const double* r_all;   // [n_all]
-  int n_all;
+  const double* r_all;   // [n_all]; MOMENTS: the local lanes' rewards only
+  int n_all;             // lanes over all ranks
   double pr;
-  int lo;
+  int lo;                // this rank's first global lane
   const int8_t* sign;    // [n_dirs * lpd] (local lanes)
   const double* n2;      // [n_dirs * lpd]
   const double* w;       // centred-rank weights of the local lanes
@@ -569,7 +569,7 @@ struct FdArgs {
   int rows_per_chunk, n_chunks, col_blocks;
   double* partial;       // [n_chunks][P] (x2 in MOMENTS mode)
   unsigned* cnt;         // [col_blocks] chunk tickets, [col_blocks] the DSGD ticket
-  double* out;           // g [P]; MOMENTS: [A | B | sum r' | sum r'^2 | n]
+  double* out;           // g [P]; MOMENTS: [A | B | n_local | r' slots [n_all]]
   double* gsq;           // [col_blocks] sum fl32(-g)^2 per column block (fdr_fd_step), or NULL
 };
 
@@ -658,6 +658,7 @@ __global__ __launch_bounds__(256) void fd_grad_fused_kernel(FdArgs a) {
   // vmcnt(0) wait, which serialised these ~30 loads into as many L2 round trips (measured: the kernel's
   // 24 us vs 10.5 us for the bare 50 MB stream, tools/learner_bench.py).
   double xin[kMaxLpd], vin[kMaxLpd];
+  const int roff = MODE == FDR_WEIGHT_MOMENTS ? 0 : a.lo;  // MOMENTS: r_all holds the local lanes only
   {
     const int nloc = max(1, (d1 - d0) * a.lpd);  // this chunk's local lanes: [d0 * lpd, d1 * lpd)
     int sg[kMaxLpd];
@@ -668,7 +669,7 @@ __global__ __launch_bounds__(256) void fd_grad_fused_kernel(FdArgs a) {
       sg[k] = a.sign[i];
       n2v[k] = a.n2[i];
       if constexpr (MODE == FDR_WEIGHT_CENTERED_RANK) xv[k] = a.w[i];
-      else xv[k] = a.r_all[a.lo + i];
+      else xv[k] = a.r_all[roff + i];
     }
 #pragma unroll
     for (int k = 0; k < kMaxLpd; ++k) {
@@ -715,20 +716,25 @@ __global__ __launch_bounds__(256) void fd_grad_fused_kernel(FdArgs a) {
     if constexpr (MODE == FDR_WEIGHT_ZSCORE) return sd == 0.0 ? x : (x - mean) / sd;  // math_helpers.py:127-134
     else return x;
   };
+  // MOMENTS: c = sum_k (r'_k - r'_0) v_k + r'_0 b, b = sum_k v_k -- the same value in real arithmetic, but an
+  // antithetic pair (v_1 = -v_0, so b = 0 exactly) gives c = (r'_1 - r'_0) v_1 with the difference exact
+  // (Sterbenz) instead of r'_0 v_0 + r'_1 v_1, whose products cancel when the returns are near-constant
   if (dmine < d1 && a.lpd <= kMaxLpd) {
     double c = 0.0, b = 0.0;
+    const double x0 = MODE == FDR_WEIGHT_MOMENTS ? xin[0] : 0.0;
 #pragma unroll
     for (int k = 0; k < kMaxLpd; ++k)
       if (k < a.lpd && vin[k] != 0.0) {
-        c += weight(xin[k]) * vin[k];
+        c += weight(xin[k] - x0) * vin[k];
         b += vin[k];
       }
+    if constexpr (MODE == FDR_WEIGHT_MOMENTS) c = fma(x0, b, c);
     if (row_off(dmine) < 0) c = b = __builtin_nan("");
     cA[dmine - d0] = c;
     if constexpr (MODE == FDR_WEIGHT_MOMENTS) cB[dmine - d0] = b;
   }
   for (int d = d0 + tid + (a.lpd <= kMaxLpd ? 256 : 0); d < d1; d += 256) {  // further directions of this thread
-    double c = 0.0, b = 0.0;
+    double c = 0.0, b = 0.0, x0 = 0.0;
     for (int k = 0; k < a.lpd; ++k) {
       const int i = d * a.lpd + k;
       const int sg = a.sign[i];
@@ -736,10 +742,12 @@ __global__ __launch_bounds__(256) void fd_grad_fused_kernel(FdArgs a) {
       const double vi = (double)sg * (double)a.sigma / a.n2[i];
       double x;
       if constexpr (MODE == FDR_WEIGHT_CENTERED_RANK) x = a.w[i];
-      else x = a.r_all[a.lo + i] - a.pr;
-      c += weight(x) * vi;
+      else x = a.r_all[roff + i] - a.pr;
+      if (MODE == FDR_WEIGHT_MOMENTS && k == 0) x0 = x;  // as above
+      c += weight(x - x0) * vi;
       b += vi;
     }
+    if constexpr (MODE == FDR_WEIGHT_MOMENTS) c = fma(x0, b, c);
     if (row_off(d) < 0) c = b = __builtin_nan("");
     cA[d - d0] = c;
     if constexpr (MODE == FDR_WEIGHT_MOMENTS) cB[d - d0] = b;
@@ -792,20 +800,18 @@ __global__ __launch_bounds__(256) void fd_grad_fused_kernel(FdArgs a) {
     }
   }
   if constexpr (MODE == FDR_WEIGHT_MOMENTS) {
-    if (cb == 0 && chunk == 0) {  // the local reward moments [sum r' | sum r'^2 | n]
-      double s = 0.0, q = 0.0;
+    if (cb == 0 && chunk == 0) {
+      // [n_local | r' slots]: this rank's r' at its global lanes, 0 elsewhere -- the all-reduce's sum is then
+      // every rank's r' (x + 0 = x exactly) and the lane count, from which the DSGD launch forms the z-score
+      // statistics in two passes as standardize_arr does (a one-pass sum r'^2 / n - m^2 cancels when the
+      // returns are near-constant)
+      const int n_local = a.n_dirs * a.lpd;
+      double* slots = a.out + 2 * P + 1;
       for (int i = tid; i < a.n_all; i += 256) {
-        const double x = a.r_all[a.lo + i] - a.pr;
-        s += x;
-        q += x * x;
+        const int k = i - a.lo;
+        slots[i] = (k >= 0 && k < n_local) ? a.r_all[k] - a.pr : 0.0;
       }
-      s = block_sum_256(s, red);
-      q = block_sum_256(q, red);
-      if (tid == 0) {
-        a.out[2 * P] = s;
-        a.out[2 * P + 1] = q;
-        a.out[2 * P + 2] = (double)a.n_all;
-      }
+      if (tid == 0) a.out[2 * P] = (double)n_local;
     }
   } else {
     if (a.gsq && owner) {  // fdr_fd_step: this column block's sum fl32(-g)^2 for the DSGD launch
@@ -998,19 +1004,28 @@ int launch_rank_weights(const double* r_all, int n_all, int lo, int n_local, dou
 // ------------------------------------------------------------------------------------------
 constexpr int64_t kDsgdFusedMaxP = 1 << 16;
 
-__device__ __forceinline__ double grad_elem(const double* src, int64_t P, int64_t p, bool mom, double m, double inv_sd,
-                                            bool unit) {
+__device__ __forceinline__ double grad_elem(const double* src, int64_t P, int64_t p, bool mom, double m, double sd) {
   if (!mom) return src[p];
   const double A = src[p], B = src[P + p];
-  return unit ? A : (A - m * B) * inv_sd;
+  return sd == 0.0 ? A : (A - m * B) / sd;  // standardize_arr returns its input unchanged when std == 0
 }
 
-__device__ __forceinline__ void moment_stats(const double* src, int64_t P, double& m, double& inv_sd, bool& unit) {
-  const double s = src[2 * P], q = src[2 * P + 1], n = src[2 * P + 2];
-  m = s / n;
-  const double var = fmax(q / n - m * m, 0.0);
-  unit = var == 0.0;  // standardize_arr returns the input unchanged when std == 0
-  inv_sd = unit ? 1.0 : 1.0 / sqrt(var);
+__device__ double block_sum_1024x(double v, double* red);
+
+// z-score statistics of the summed moments [A | B | n | r'_0 .. r'_{n-1}]: mean and population std of all
+// ranks' r' in two f64 passes (utils/math_helpers.py:127-134), by a 1024-thread workgroup in a fixed order
+__device__ void moment_stats_1024(const double* src, int64_t P, double* red, double& m, double& sd) {
+  const int n = (int)src[2 * P];
+  const double* r = src + 2 * P + 1;
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) s += r[i];
+  m = block_sum_1024x(s, red) / (double)n;
+  double q = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) {
+    const double d = r[i] - m;
+    q += d * d;
+  }
+  sd = sqrt(block_sum_1024x(q, red) / (double)n);
 }
 
 __device__ double block_sum_1024x(double v, double* red) {
@@ -1029,12 +1044,11 @@ __global__ __launch_bounds__(1024) void dsgd_fused_kernel(float* __restrict__ th
                                                           double* __restrict__ g_out, double* __restrict__ out) {
 #pragma clang fp contract(off)
   __shared__ double red[16];
-  double m = 0.0, inv_sd = 1.0;
-  bool unit = true;
-  if (mom) moment_stats(src, P, m, inv_sd, unit);
+  double m = 0.0, sd = 0.0;
+  if (mom) moment_stats_1024(src, P, red, m, sd);
   double s = 0.0;
   for (int64_t p = threadIdx.x; p < P; p += 1024) {
-    const double g = grad_elem(src, P, p, mom, m, inv_sd, unit);
+    const double g = grad_elem(src, P, p, mom, m, sd);
     if (mom && g_out) g_out[p] = g;
     const float gr = (float)(-g);
     s += (double)gr * (double)gr;
@@ -1045,7 +1059,7 @@ __global__ __launch_bounds__(1024) void dsgd_fused_kernel(float* __restrict__ th
     const double coef = lr * sqrt((double)P) * lr_scale / (double)norm;
     const float c32 = (float)coef;
     for (int64_t p = threadIdx.x; p < P; p += 1024) {
-      const float gr = (float)(-grad_elem(src, P, p, mom, m, inv_sd, unit));
+      const float gr = (float)(-grad_elem(src, P, p, mom, m, sd));
       const float old = theta[p];
       const float nw = old - c32 * gr;
       theta[p] = nw;
@@ -1060,14 +1074,24 @@ __global__ __launch_bounds__(1024) void dsgd_fused_kernel(float* __restrict__ th
   }
 }
 
-// multi-block path for large P (ImpalaPolicy), moments-aware
+// multi-block path for large P (ImpalaPolicy): the statistics once, then g = (A - m B) / sd
+__global__ __launch_bounds__(1024) void moment_stats_kernel(const double* __restrict__ src, int64_t P,
+                                                            double* __restrict__ stats) {
+  __shared__ double red[16];
+  double m, sd;
+  moment_stats_1024(src, P, red, m, sd);
+  if (threadIdx.x == 0) {
+    stats[0] = m;
+    stats[1] = sd;
+  }
+}
+
 __global__ __launch_bounds__(256) void moments_to_grad_kernel(const double* __restrict__ src, int64_t P,
+                                                              const double* __restrict__ stats,
                                                               double* __restrict__ g) {
-  double m, inv_sd;
-  bool unit;
-  moment_stats(src, P, m, inv_sd, unit);
+  const double m = stats[0], sd = stats[1];
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < P; p += (int64_t)gridDim.x * blockDim.x)
-    g[p] = grad_elem(src, P, p, true, m, inv_sd, unit);
+    g[p] = grad_elem(src, P, p, true, m, sd);
 }
 
 int launch_dsgd_ex(float* theta, const double* src, int mom, int64_t P, double lr, double lr_scale, double* g_out,
@@ -1079,9 +1103,15 @@ int launch_dsgd_ex(float* theta, const double* src, int mom, int64_t P, double l
   const double* g = src;
   if (mom) {
     if (!g_out) return set_error(FDR_ERR_INVALID, "moments form needs g_out for large P");
+    if (ws == nullptr || ws_bytes < dsgd_workspace_bytes(P))
+      return set_error(FDR_ERR_WORKSPACE, "dsgd workspace too small");
+    double* stats = static_cast<double*>(ws) + 2 * kDsgdBlocks + 2;  // past launch_dsgd's partials
+    hipLaunchKernelGGL(moment_stats_kernel, dim3(1), dim3(1024), 0, stream, src, P, stats);
+    int rc = check_launch("moment_stats_kernel");
+    if (rc) return rc;
     const int rb = (int)std::min<int64_t>((P + 255) / 256, 2048);
-    hipLaunchKernelGGL(moments_to_grad_kernel, dim3(rb), dim3(256), 0, stream, src, P, g_out);
-    int rc = check_launch("moments_to_grad_kernel");
+    hipLaunchKernelGGL(moments_to_grad_kernel, dim3(rb), dim3(256), 0, stream, src, P, stats, g_out);
+    rc = check_launch("moments_to_grad_kernel");
     if (rc) return rc;
     g = g_out;
   }

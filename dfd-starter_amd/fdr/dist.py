@@ -4,10 +4,11 @@ One process per GPU; the perturbation set is split into contiguous lane slices, 
   * every rank draws the FULL index list from its own copy of the shared noise table stream, in
     the reference's order (utils/noise_sources.py:44-47), and keeps its slice -- no index exchange;
   * antithetic pairs are never split across ranks (slices are whole directions);
-  * the only data-path exchange per FD step is (1) an all-gather of the per-lane returns (a few KB,
-    needed because the z-score is global: learner/finite_differences.py:43) and (2) ONE all-reduce
-    of the f64 gradient vector (P * 8 bytes); DSGD then runs replicated and bit-identically on
-    every rank.
+  * the data-path exchange per FD step (z-score, antithetic, the default) is ONE all-reduce of the f64
+    moments [A | B | n | r' slots] (2P + 1 + n_lanes doubles: each rank's r' at its global lanes, so the
+    sum carries every return for the global z-score, learner/finite_differences.py:43); centred-rank and
+    one-sided steps take (1) an all-gather of the per-lane returns (a few KB) and (2) an all-reduce of g
+    (P * 8 bytes).  DSGD then runs replicated and bit-identically on every rank.
 Backend "nccl" is RCCL on ROCm (xGMI); the same helpers run on gloo for CPU tests.
 """
 import torch

@@ -226,26 +226,53 @@ def _workspace(key, nbytes, device, zeroed=False):
     return buf
 
 
+_WS_ZERO_PREFIX = {}
+
+
+def _fused_workspace(mode, n_dirs, lanes_per_dir, n_params, device):
+    """The fdr_fd_grad_fused / fdr_fd_step workspace with its ticket-counter prefix guaranteed zero.
+
+    A call leaves exactly its own counter prefix, fdr_fd_grad_fused_counter_bytes(n_dirs, P), at zero; the bytes
+    behind it hold that call's slabs / partials.  A later call whose prefix is longer (more column blocks) would
+    find non-zero counters there, so the prefix is re-zeroed (on the current stream, ahead of the launch)
+    whenever it grows past what is known to be zero."""
+    key = ("fused_%d" % mode, device)
+    old = _WS.get(key)
+    nb = lib.fdr_fd_grad_fused_workspace_bytes(n_dirs, int(lanes_per_dir), n_params, mode)
+    ws = _workspace(key[0], nb, device, zeroed=True)
+    if ws is not old:
+        _WS_ZERO_PREFIX[key] = ws.numel()
+    cb = int(lib.fdr_fd_grad_fused_counter_bytes(n_dirs, n_params))
+    if cb > _WS_ZERO_PREFIX.get(key, 0):
+        ws[:cb].zero_()
+    _WS_ZERO_PREFIX[key] = cb
+    return ws
+
+
 WEIGHT_MODES = {"zscore": _lib.FDR_WEIGHT_ZSCORE, "centred_rank": _lib.FDR_WEIGHT_CENTERED_RANK,
                 "moments": _lib.FDR_WEIGHT_MOMENTS}
 
 
 def fd_grad_fused(table, idx_local, rewards_all, policy_reward, lane_lo, sign_local, norm2_local, lanes_per_dir, sigma,
-                  n_params, mode="zscore", out=None):
+                  n_params, mode="zscore", out=None, n_all=None):
     """Weights + noise-weighted gradient in one launch (fdr_fd_grad_fused).  idx_local / sign_local / norm2_local:
-    one entry per local lane.  mode "zscore" / "centred_rank" -> g f64 [P]; "moments" (local rewards only) ->
-    [A | B | sum r' | sum r'^2 | n] f64 [2P + 3]."""
+    one entry per local lane.  mode "zscore" / "centred_rank" -> g f64 [P]; "moments" (rewards_all = the local
+    rewards, n_all = the lanes of all ranks, lane_lo = this rank's first global lane) ->
+    [A | B | n_local | r' slots [n_all]] f64 [2P + 1 + n_all]."""
     _check_dev(table, idx_local, rewards_all, sign_local, norm2_local)
     dev = table.device
     n_dirs = idx_local.numel() // int(lanes_per_dir)
     m = WEIGHT_MODES[mode]
-    n_out = 2 * n_params + 3 if mode == "moments" else n_params
+    if n_all is None:
+        n_all = rewards_all.numel() + (int(lane_lo) if mode == "moments" else 0)
+    n_out = 2 * n_params + 1 + int(n_all) if mode == "moments" else n_params
     if out is None:
         out = torch.empty(n_out, dtype=torch.float64, device=dev)
-    nb = lib.fdr_fd_grad_fused_workspace_bytes(n_dirs, int(lanes_per_dir), n_params, m)
-    ws = _workspace("fused_%d" % m, nb, dev, zeroed=True)
+    elif out.numel() < n_out:
+        raise ValueError("fd_grad_fused: out holds %d doubles, needs %d" % (out.numel(), n_out))
+    ws = _fused_workspace(m, n_dirs, lanes_per_dir, n_params, dev)
     check(lib.fdr_fd_grad_fused(_c(dev), _p(table), table.numel(), _p(idx_local), n_dirs, n_params, _p(rewards_all),
-                                rewards_all.numel(), float(policy_reward), int(lane_lo), _p(sign_local), _p(norm2_local),
+                                int(n_all), float(policy_reward), int(lane_lo), _p(sign_local), _p(norm2_local),
                                 int(lanes_per_dir), float(sigma), m, _p(out), _p(ws), ws.numel(), _stream(dev)),
           "fdr_fd_grad_fused")
     return out
@@ -265,8 +292,7 @@ def fd_step(table, idx_local, rewards, policy_reward, sign_local, norm2_local, l
         g = torch.empty(P, dtype=torch.float64, device=dev)
     if out is None:
         out = torch.empty(2, dtype=torch.float64, device=dev)
-    nb = lib.fdr_fd_grad_fused_workspace_bytes(n_dirs, int(lanes_per_dir), P, m)
-    ws = _workspace("fused_%d" % m, nb, dev, zeroed=True)
+    ws = _fused_workspace(m, n_dirs, lanes_per_dir, P, dev)
     check(lib.fdr_fd_step(_c(dev), _p(table), table.numel(), _p(idx_local), n_dirs, P, _p(rewards), rewards.numel(),
                           float(policy_reward), _p(sign_local), _p(norm2_local), int(lanes_per_dir), float(sigma), m,
                           _p(theta), float(lr), float(lr_scale), _p(g), _p(theta_hist), _p(out), _p(ws), ws.numel(),

@@ -9,8 +9,11 @@ list of FDReturn or an FDBatch (device SoA from Worker.evaluate) and runs, all o
     fdr_dsgd_step      ONE launch (P <= 65536): theta <- theta - lr*sqrt(P)*lr_scale * fl32(-g) / ||fl32(-g)||
 
 Sharded over ranks (DESIGN.md "Multi-GPU") the z-score step needs ONE collective: every rank reduces its lanes
-to the moments [A | B | sum r' | sum r'^2 | n] (A = sum r'_i v_i, B = sum v_i), one RCCL all-reduce sums them,
-and DSGD forms g = (A - m B) / sd on the fly (equal to the z-weighted sum in real arithmetic).
+to the moments [A | B | n | r' slots] (A = sum r'_i v_i, B = sum v_i; its r' at its global lanes, 0 elsewhere),
+one RCCL all-reduce sums them, and DSGD forms m, sd in two passes over all r' and g = (A - m B) / sd on the fly
+(equal to the z-weighted sum in real arithmetic, B = 0 exactly for antithetic pairs).  One-sided
+batches, and batches whose lane split is not known on every rank (a list of FDReturn), all-gather the returns
+instead.
 ``weighting="centred_rank"`` (build extension named by the north star; the reference's weighting is the
 z-score) ranks all returns, so it keeps the all-gather of the per-lane returns + the all-reduce of g.
 
@@ -99,9 +102,14 @@ class FiniteDifferences(object):
             g = engine.fd_grad_fused(table, b.idx, b.reward, policy_reward, 0, b.sign, b.norm2, b.lanes_per_dir,
                                      self.noise_std, P, mode=self.weighting, out=self.gradient_memory)
             return self._apply(g)
-        if self.weighting == "zscore" and self.one_collective:
-            mom = engine.fd_grad_fused(table, b.idx, b.reward, policy_reward, 0, b.sign, b.norm2, b.lanes_per_dir,
-                                       self.noise_std, P, mode="moments")
+        sizes = getattr(b, "rank_lanes", None)
+        if self.weighting == "zscore" and self.one_collective and sizes is not None and b.lanes_per_dir == 2:
+            # the split is known on every rank (Worker.evaluate's lane_range): [A | B | n | r' slots], ONE all-reduce.
+            # Antithetic only: there B = 0 exactly, so A - m B carries no cancellation; one-sided batches with
+            # near-constant returns (|m| >> sd) would lose digits in it, and take the exact gather path below.
+            _, rank = fdist.world_rank(self.process_group)
+            mom = engine.fd_grad_fused(table, b.idx, b.reward, policy_reward, int(sum(sizes[:rank])), b.sign, b.norm2,
+                                       b.lanes_per_dir, self.noise_std, P, mode="moments", n_all=int(sum(sizes)))
             fdist.allreduce_grad(mom, self.process_group)            # the step's one collective
             return self._apply(mom, moments=True)
         rewards_all, lane_lo = fdist.gather_rewards(b.reward, self.process_group, getattr(b, "rank_lanes", None))

@@ -219,7 +219,11 @@ class SequentialRunner(object):
             self.agent.cumulative_timesteps += steps
             n_train = n_dirs * lpd * E
             eval_states = self.worker.eval_states(self.zeta_size) if is_eval.any() else None
-            for r, e, nv in zip(rew[n_train:], ent[n_train:], nov[n_train:]):
+            # run_sequential.py:142-151 runs once per eval EPISODE of the reference's single env; an eval lane with
+            # E envs is one such evaluation, so its E returns are averaged and the EMAs / zeta move once per lane
+            # (per-env updates would make the 0.9 time constants and the zeta churn depend on E)
+            ev = [a[n_train:].reshape(-1, E).mean(1) for a in (rew, ent, nov)]
+            for r, e, nv in zip(*ev):
                 self.policy_reward = self.policy_reward * 0.9 + r * 0.1
                 self.policy_entropy = self.policy_entropy * 0.9 + e * 0.1
                 self.policy_novelty = self.policy_novelty * 0.9 + nv * 0.1

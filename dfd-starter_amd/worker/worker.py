@@ -109,9 +109,11 @@ class Worker(object):
             roll = engine.impala_rollout if p.KIND == "impala" else engine.atari_rollout
             spec = self.agent.env.spec()
             if pairs and p.KIND == "impala":
-                ii, ss = np.asarray(idx), np.asarray(sign)
-                spec.pairs = bool(n % 2 == 0 and np.array_equal(ii[0::2], ii[1::2])
-                                  and np.all(ss[0::2].astype(np.int32) == -ss[1::2].astype(np.int32)))
+                ii, ss, dd = np.asarray(idx), np.asarray(sign).astype(np.int32), np.asarray(det)
+                # +eps / -eps lanes only: a sign-0 (eval) pair also satisfies s0 == -s1, but the pair cores take
+                # the pair's sign from its first lane and would perturb an eval lane
+                spec.pairs = bool(n % 2 == 0 and np.array_equal(ii[0::2], ii[1::2]) and np.all(ss[0::2] == 1)
+                                  and np.all(ss[1::2] == -1) and not np.any(dd))
             res = roll(spec, lanes, n, seed, jiggle=jiggle, bn_mean=bm, bn_var=bv, device=p.flat.device)
             if E > 1:
                 res.norm2 = res.norm2.repeat_interleave(E)

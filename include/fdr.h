@@ -213,12 +213,15 @@ int fdr_fd_grad(fdr_ctx* ctx, const float* table, int64_t table_size, const int6
  *   FDR_WEIGHT_CENTERED_RANK  w_i = rank_i / (n_all - 1) - 0.5, rank over rewards_all with ties broken by
  *                             lane index (build extension named by the north star; the standard ES
  *                             centred rank); out = g [P]
- *   FDR_WEIGHT_MOMENTS        the one-collective multi-GPU form of the z-score: with r' = r -
- *                             policy_reward over the LOCAL lanes (rewards_all = the local rewards,
- *                             n_all = n_local, lane_lo = 0), out = [A | B | sum r' | sum r'^2 | n]
- *                             (2P + 3 f64): A = sum_i r'_i v_i, B = sum_i v_i, v_i = sign_i sigma eps_i /
- *                             norm2_i.  Summed over ranks (one all-reduce) it gives g = (A - m B) / sd
- *                             exactly in real arithmetic; fdr_dsgd_step_ex consumes it.
+ *   FDR_WEIGHT_MOMENTS        the one-collective multi-GPU form of the z-score: rewards_all = the
+ *                             n_local LOCAL rewards, n_all = the lanes of all ranks, lane_lo = this rank's
+ *                             first global lane; with r' = r - policy_reward, out = [A | B | n_local |
+ *                             r' slots [n_all]] (2P + 1 + n_all f64): A = sum_i r'_i v_i, B = sum_i v_i,
+ *                             v_i = sign_i sigma eps_i / norm2_i, the slots hold this rank's r' at its
+ *                             global lanes and 0 elsewhere.  Summed over ranks (one all-reduce) it holds
+ *                             n_all and every lane's r', so fdr_dsgd_step_ex forms m and sd in two passes
+ *                             as standardize_arr does and g = (A - m B) / sd (exact in real arithmetic;
+ *                             antithetic pairs give B = 0 exactly).
  * Chunk partials are combined inside the launch (deterministic order).  workspace:
  * fdr_fd_grad_fused_workspace_bytes(n_dirs, lanes_per_dir, P, mode) bytes whose first
  * fdr_fd_grad_fused_counter_bytes(n_dirs, P) bytes must be zero before the first call on that workspace
@@ -287,7 +290,8 @@ int fdr_dsgd_step(fdr_ctx* ctx, float* theta, const double* g, int64_t n_params,
                   fdr_stream stream);
 
 /* DSGD from a gradient or from the summed moments of FDR_WEIGHT_MOMENTS (src_is_moments = 1: g = (A - m B) /
- * sd with m, sd from [sum r' | sum r'^2 | n]; sd == 0 -> g = A, as standardize_arr; g is written to g_out).
+ * sd with m, sd the two-pass mean / population std of the n r' slots; sd == 0 -> g = A, as standardize_arr; g is
+ * written to g_out).
  * P <= 65536: one fused launch (norm + update + ||d theta||).  out, workspace as fdr_dsgd_step. */
 int fdr_dsgd_step_ex(fdr_ctx* ctx, float* theta, const double* src, int32_t src_is_moments, int64_t n_params,
                      double lr, double lr_scale, double* g_out, double* out, void* workspace, int64_t workspace_bytes,

@@ -73,21 +73,32 @@ def fd_gradient_weights(table, P, idx, sign, weights, sigma):
     return np.dot(np.asarray(weights, np.float64), V)
 
 
-def fd_moments(table, P, idx, sign, rewards, policy_reward, sigma):
-    """One rank's share of the one-collective z-score step: [A | B | sum r' | sum r'^2 | n] with
-    r' = r - policy_reward, A = sum r'_i v_i, B = sum v_i (f64)."""
+def fd_moments(table, P, idx, sign, rewards, policy_reward, sigma, lane_lo=0, n_all=None, lanes_per_dir=1):
+    """One rank's share of the one-collective z-score step: [A | B | n_local | r' slots [n_all]] with
+    r' = r - policy_reward, A = sum r'_i v_i, B = sum v_i (f64); this rank's r' sit at its global lanes
+    [lane_lo, lane_lo + n_local), zeros elsewhere, so the all-reduce's sum holds every lane's r'.
+    A is accumulated per direction as sum_k (r'_k - r'_0) v_k + r'_0 sum_k v_k (the build's fdr_fd_grad_fused
+    order: for an antithetic pair sum_k v_k = 0 exactly and the near-constant-return products do not cancel)."""
     V, _ = perturbation_vectors(table, P, idx, sign, sigma)
+    V = V.astype(np.float64)
     r = np.subtract(rewards, policy_reward).astype(np.float64)
-    return np.concatenate([np.dot(r, V), V.astype(np.float64).sum(0), [r.sum(), (r * r).sum(), float(r.size)]])
+    R = r.reshape(-1, lanes_per_dir)
+    VB = V.reshape(R.shape[0], lanes_per_dir, P).sum(1)
+    A = np.dot((R - R[:, :1]).reshape(-1), V) + np.dot(R[:, 0], VB)
+    n_all = r.size + lane_lo if n_all is None else n_all
+    slots = np.zeros(n_all)
+    slots[lane_lo:lane_lo + r.size] = r
+    return np.concatenate([A, VB.sum(0), [float(r.size)], slots])
 
 
 def grad_from_moments(mom, P):
-    """g = (A - m B) / sd from summed moments (sd == 0: A, as standardize returns its input unchanged)."""
+    """g = (A - m B) / sd from summed moments; m, sd over the r' slots as standardize (utils/math_helpers.py:127-134:
+    two-pass, population std; sd == 0: A, as standardize returns its input unchanged)."""
     A, B = mom[:P], mom[P:2 * P]
-    s, q, n = mom[2 * P:2 * P + 3]
-    m = s / n
-    var = max(q / n - m * m, 0.0)
-    return A if var == 0 else (A - m * B) / np.sqrt(var)
+    n = int(mom[2 * P])
+    r = mom[2 * P + 1:2 * P + 1 + n]
+    m, sd = r.mean(), r.std()
+    return A if sd == 0 else (A - m * B) / sd
 
 
 def dsgd_step(theta, g, lr, omega=0.0, omega_min=0.0, omega_max=1.0, min_scale=0.23, max_scale=1.0):

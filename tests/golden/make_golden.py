@@ -596,9 +596,82 @@ def g12_history():
     save("g12_history.npz", **out)
 
 
+def g12_impala():
+    """G12 for ImpalaPolicy (config 5's archive): the reference StrategyHandler / SparseHistoryManager
+    (strategy/strategy_handler.py:6-31, sparse_history_manager.py:17-148) over a reference ImpalaPolicy
+    (policies/impala.py:8-45) with categorical_tvd -- 6 points added, zeta set (8 obs dicts), 14 more
+    submit_policy calls.  Harness patch: ImpalaPolicy.get_strategy resets the LSTM state first, the build's
+    documented zero-state rule (StrategyPoint.evaluate_strategy would otherwise start
+    each point from the state the previous call left in the shared policy object, policies/impala.py:24-27).
+    The parameter vectors are not committed (4.6 MB each): theta = 0.1 * table[1000:], point k =
+    theta + scale_k * table[off_k:] with table = RandomState(7).randn(2^22) f32; BN running stats as G8."""
+    from policies.impala import ImpalaPolicy
+    A, H, N, Z = 4, 6, 20, 8
+    orig = ImpalaPolicy.get_strategy
+
+    def get_strategy_from_reset(self, x):
+        self.reset()
+        return orig(self, x)
+
+    ImpalaPolicy.get_strategy = get_strategy_from_reset
+    try:
+        torch.manual_seed(124)
+        pol = ImpalaPolicy((64, 64, 3), A, seed=124)
+        P = pol.num_params
+        rs = np.random.RandomState(7)
+        table = rs.randn(2 ** 22).astype(np.float32)
+        theta = (table[1000:1000 + P] * np.float32(0.1)).astype(np.float32)
+        bns = [m for m in pol.modules() if isinstance(m, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d))]
+        nbn = sum(m.num_features for m in bns)
+        rm = (table[2000000:2000000 + nbn] * np.float32(0.1)).astype(np.float32)
+        rv = (1.0 + 0.5 * np.abs(table[3000000:3000000 + nbn])).astype(np.float32)
+        with torch.no_grad():
+            o = 0
+            for m in bns:
+                n = m.num_features
+                m.running_mean.copy_(torch.as_tensor(rm[o:o + n]))
+                m.running_var.copy_(torch.as_tensor(rv[o:o + n]))
+                o += n
+        prs = np.random.RandomState(12)
+        scales = prs.choice([0.02, 0.05, 0.1, 0.2, 0.4], size=N).astype(np.float32)
+        offs = prs.randint(0, table.size - P, size=N)
+        frames = prs.randint(0, 256, size=(Z, 3, 64, 64)).astype(np.uint8)
+        zrew = prs.choice([-1.0, 0.0, 1.0], size=Z).astype(np.float32)
+        zeta = [{"frame": torch.as_tensor(frames[z].astype(np.float32)).view(1, 1, 3, 64, 64),
+                 "reward": torch.as_tensor(zrew[z]).view(1, 1),
+                 "done": torch.as_tensor(False).view(1, 1)} for z in range(Z)]
+        handler = StrategyHandler(pol, math_helpers.categorical_tvd, max_history_size=H)
+        mgr = handler.strategy_history_manager
+        for k in range(H):
+            pol.set_trainable_flat((theta + scales[k] * table[offs[k]:offs[k] + P]).astype(np.float32))
+            handler.add_policy(pol)
+        handler.set_zeta(zeta)
+        worst, rets = [mgr.worst_point_idx], []
+        for k in range(H, N):
+            pol.set_trainable_flat((theta + scales[k] * table[offs[k]:offs[k] + P]).astype(np.float32))
+            r = mgr.submit_policy(pol)
+            rets.append(-2 if r is None else int(r))
+            worst.append(mgr.worst_point_idx)
+        D = np.full((H, H), np.inf)
+        for (i, j), d in mgr.known_dists.items():
+            D[i, j] = D[j, i] = d
+        # novelty of two more policies against the final archive (strategy_handler.py:26-31)
+        nov = []
+        for k in (0, N - 1):
+            pol.set_trainable_flat((theta - scales[k] * table[offs[k]:offs[k] + P]).astype(np.float32))
+            nov.append(handler.compute_novelty(pol))
+    finally:
+        ImpalaPolicy.get_strategy = orig
+    save("g12_impala.npz", A=np.array(A), H=np.array(H), P=np.array(P), table_seed=np.array(7),
+         param_offset=np.array(1000), rm=rm, rv=rv, scales=scales, offs=offs, zeta_frames=frames, zeta_rewards=zrew,
+         returns=np.array(rets), worst=np.array(worst), strategies=np.asarray(mgr.strategy_tensor, np.float32),
+         dists=D, novelty=np.array(nov))
+
+
 GENERATORS = {"g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
               "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g8": g8_impala,
-              "g9": g9_novelty, "g10": g10_welford, "g11": g11_atari, "g12": g12_history}
+              "g9": g9_novelty, "g10": g10_welford, "g11": g11_atari, "g12": g12_history,
+              "g12i": g12_impala}
 
 if __name__ == "__main__":
     torch.set_num_threads(1)

@@ -1,0 +1,44 @@
+"""GPU: the N-rank product path equals the 1-rank path.
+
+tools/dist_check.py runs Worker.evaluate(lane_range="auto") + FiniteDifferences.step for 3 FD steps of a
+HalfCheetah-shaped MujocoPolicy (96 antithetic directions, T = 200) once in one process and once as 2 ranks
+(torch.distributed.run, gloo, both on cuda:0).  The z-score case exercises the one-collective moments form
+(ONE all-reduce of [A | B | n | r' slots] per step), centred rank the all-gather + all-reduce form
+(learner/finite_differences.py:24-64 in the reference).  Both ranks' theta must be bitwise equal (replicated
+DSGD), and within 1e-6 of the single-process theta (the collective only changes the summation order)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCRIPT = os.path.join(ROOT, "tools", "dist_check.py")
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("weighting,port", [("zscore", 29541), ("centred_rank", 29542)])
+def test_two_rank_fd_steps_equal_one_rank(tmp_path, weighting, port):
+    out = str(tmp_path)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.run([sys.executable, SCRIPT, "single", weighting, out], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-2000:]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), SCRIPT, "multi", weighting, out],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-2000:]
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import dist_check
+    finally:
+        sys.path.pop(0)
+    err = dist_check.compare(out)
+    assert err <= 1e-6, err
+    u1 = np.load(os.path.join(out, "upd_single.npy"))
+    u0 = np.load(os.path.join(out, "upd_rank0.npy"))
+    np.testing.assert_array_equal(u0, np.load(os.path.join(out, "upd_rank1.npy")))
+    np.testing.assert_allclose(u0, u1, rtol=1e-6)
+    assert np.all(u0 > 0)

@@ -375,24 +375,98 @@ def test_f32_pair_core_bit_identical(engine, table):
         np.testing.assert_array_equal(getattr(o[0], f).cpu().numpy(), getattr(o[1], f).cpu().numpy())
 
 
+def _check_vs_followed_oracle(out_probs, out_acts, out_ret, out_ent, ref, seed, lane_ids, E, tol):
+    """A kernel's recorded trajectories [L, E, T] against oi.follow_lanes along the same actions: every step's
+    probabilities within tol (abs), the replayed entropy within tol (rel), returns equal up to the +-1e-12
+    jiggle, and every sampled action equal to the inverse CDF of the REFERENCE probabilities at the step's
+    counter uniform -- except where u * sum(p) lies closer to a partition boundary than the two probability
+    vectors' largest cumulative difference (then the kernel's own, slightly different, probabilities may
+    legitimately pick the neighbour; such a flip is explained, and counted).
+    Returns (worst prob diff, worst rel entropy diff, explained flips)."""
+    from oracle import rng as crng
+    from oracle.policies import categorical_inverse_cdf
+    T = out_acts.shape[2]
+    dp = np.abs(out_probs - ref["probs"]).max()
+    assert dp <= tol, dp
+    de = np.abs(out_ent - ref["ent"]) / np.abs(ref["ent"])
+    assert de.max() <= tol, de.max()
+    np.testing.assert_allclose(out_ret - ref["ret"], 0.0, rtol=0, atol=2e-12)
+    flips = 0
+    for li, l in enumerate(lane_ids):
+        envs = np.uint64(l) * np.uint64(E) + np.arange(E, dtype=np.uint64)
+        for t in range(T):
+            u = crng.uniform(seed, envs, t, 0)
+            pr, pk = ref["probs"][li, :, t], out_probs[li, :, t]
+            margin = oi.sample_margin(pr, u)
+            dcs = np.abs(np.cumsum(pk.astype(np.float64), -1) - np.cumsum(pr.astype(np.float64), -1)).max(-1)
+            for e in range(E):
+                if out_acts[li, e, t] == categorical_inverse_cdf(pr[e], u[e]):
+                    continue
+                assert margin[e] <= dcs[e] + 1e-6, (l, e, t, out_acts[li, e, t], margin[e], dcs[e])
+                flips += 1
+    return dp, de.max(), flips
+
+
+@pytest.mark.parametrize("core_mfma", [True, False])
+def test_fp16_pair_default_path_whole_episode_vs_f32_oracle(engine, table, core_mfma):
+    """the kernels config 5 actually runs -- Worker.evaluate(antithetic) sets pairs, and the
+    default context's fp16 pair core is core_kernel_hpm (MFMA step: theta x + s (E x) on f16 fragment images)
+    with the replay's input projection on xproj_pair_kernel and core_kernel_hpm<kReplay>; core_mfma=False runs
+    the VALU pair forms (core_kernel_hp / core_kernel_hpr).  2 antithetic pairs, A = 4, E = 4, T = 130 (the
+    replay crosses two 64-step chunk boundaries), stochastic actions; the f32 oracle follows the kernel's own
+    actions (policies/impala.py:136-186, worker/agent.py:20-71): per-step probabilities within 2e-2, replayed
+    entropies within 2e-2, returns exact up to the jiggle, sampled actions consistent with the reference."""
+    A, E, T, L, seed = 4, 4, 130, 4, 11
+    theta = _theta(A)
+    idx = np.repeat(np.array([555, 1_234_567], np.int64), 2)
+    sign = np.tile(np.array([1, -1], np.int8), 2)
+    dev = "cuda"
+    lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
+                              torch.tensor(idx, device=dev), torch.tensor(sign, device=dev), 0.02)
+    ctx = None
+    if not core_mfma:
+        ctx = engine.Context()
+        ctx.set_core_mfma(False)
+    spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=True, pairs=True)
+    out = engine.impala_rollout(spec, lanes, L, seed, record=True, ctx=ctx)
+    torch.cuda.synchronize()
+    acts = out.actions.cpu().numpy().reshape(L, E, T)
+    nb = oi.num_bn()
+    ref = oi.follow_lanes(theta, table, idx, sign, 0.02, A, E, T, 5, np.zeros(nb, np.float32),
+                          np.ones(nb, np.float32), acts)
+    from oracle import rng as crng
+    jig = np.stack([crng.jiggle(seed, np.uint64(l) * np.uint64(E) + np.arange(E, dtype=np.uint64)) for l in range(L)])
+    dp, de, amb = _check_vs_followed_oracle(out.probs.cpu().numpy().reshape(L, E, T, A), acts,
+                                            out.reward.cpu().numpy().reshape(L, E) - jig,
+                                            out.entropy.cpu().numpy().reshape(L, E), ref, seed, range(L), E, F16_RTOL)
+    print("fp16 pair core (%s): max |dp| %.3g, max rel d(ent) %.3g, %d / %d explained action flips"
+          % ("mfma" if core_mfma else "valu", dp, de, amb, L * E * T))
+    assert amb <= 0.01 * L * E * T
+
+
 @pytest.mark.parametrize("fp16,pairs", [(False, False), (False, True), (True, False), (True, True)])
 def test_full_size_rollout_properties(engine, fp16, pairs):
-    """BASELINE configs 4/5 at full size (1024 lanes x 4 envs x T = 1000, A = 6 / 4): bitwise reproducible,
-    antithetic lanes have identical ||lambda||^2, returns integer (+- jiggle) within [-T, T], entropies finite
-    in (0, ln A]."""
+    """BASELINE configs 4/5 at full size (1024 lanes x 4 envs x T = 1000, A = 6 / 4): bitwise reproducible (a
+    second launch that also records per-step probabilities / actions), antithetic lanes have identical
+    ||lambda||^2, returns integer (+- jiggle) within [-T, T], entropies finite in (0, ln A] -- and (VERDICT r2
+    item 2) sampled lanes {0, 1, 511, 1023} of the full launch, all 4 envs, whole 1000-step episodes, against the
+    f32 oracle along the kernel's trajectories (worker/agent.py:20-71): f32 every step's probabilities and the
+    entropies within 1e-5 and every sampled action the reference's (outside a 1e-5 boundary margin); fp16 the
+    drift bound of config 5 (2e-2); returns exact up to the jiggle in both."""
     A = 4 if fp16 else 6
-    L, E, T = 1024, 4, 1000
+    L, E, T, seed = 1024, 4, 1000, 123
     theta = _theta(A)
     P = theta.size
     dev = "cuda"
-    tab = torch.randn(25_000_000, generator=torch.Generator().manual_seed(124)).to(dev)
-    idx = torch.as_tensor(np.repeat(np.random.RandomState(4).randint(0, 25_000_000 - P, size=L // 2), 2), device=dev)
-    sign = torch.as_tensor(np.tile(np.array([1, -1], np.int8), L // 2), device=dev)
-    lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, tab, idx, sign, 0.02)
+    tab = torch.randn(25_000_000, generator=torch.Generator().manual_seed(124))
+    idx_h = np.repeat(np.random.RandomState(4).randint(0, 25_000_000 - P, size=L // 2), 2)
+    sign_h = np.tile(np.array([1, -1], np.int8), L // 2)
+    lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, tab.to(dev), torch.as_tensor(idx_h, device=dev),
+                              torch.as_tensor(sign_h, device=dev), 0.02)
     spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=fp16, pairs=pairs)
     outs = []
-    for _ in range(2):
-        o = engine.impala_rollout(spec, lanes, L, 123)
+    for rec in (False, True):
+        o = engine.impala_rollout(spec, lanes, L, seed, record=rec)
         torch.cuda.synchronize()
         outs.append([t.cpu().numpy().copy() for t in (o.reward, o.entropy, o.timesteps, o.norm2)])
     for a, b in zip(*outs):
@@ -404,3 +478,25 @@ def test_full_size_rollout_properties(engine, fp16, pairs):
     assert np.all(np.isfinite(ent)) and np.all(ent > 0) and np.all(ent <= np.log(A) + 1e-6)
     np.testing.assert_array_equal(n2[0::2], n2[1::2])
     assert np.all(n2 > 0)
+    # sampled lanes against the oracle (each lane evaluated with its own global lane id)
+    from oracle import rng as crng
+    sample = [0, 1, 511, 1023]
+    probs = o.probs.view(L, E, T, A)[sample].cpu().numpy()
+    acts = o.actions.view(L, E, T)[sample].cpu().numpy()
+    del o
+    nb = oi.num_bn()
+    table = tab.numpy()
+    ref = {"probs": [], "ret": [], "ent": []}
+    for k, l in enumerate(sample):
+        r = oi.follow_lanes(theta, table, idx_h[l:l + 1], sign_h[l:l + 1], 0.02, A, E, T, 5,
+                            np.zeros(nb, np.float32), np.ones(nb, np.float32), acts[k:k + 1], lane_offset=l)
+        for key in ref:
+            ref[key].append(r[key][0])
+    ref = {k: np.stack(v) for k, v in ref.items()}
+    jig = np.stack([crng.jiggle(seed, np.uint64(l) * np.uint64(E) + np.arange(E, dtype=np.uint64)) for l in sample])
+    tol = F16_RTOL if fp16 else ATOL
+    dp, de, amb = _check_vs_followed_oracle(probs, acts, ret.reshape(L, E)[sample] - jig, ent.reshape(L, E)[sample],
+                                            ref, seed, sample, E, tol)
+    print("full size fp16=%s pairs=%s: max |dp| %.3g, max rel d(ent) %.3g, %d / %d explained action flips"
+          % (fp16, pairs, dp, de, amb, len(sample) * E * T))
+    assert amb <= (0.01 if fp16 else 0.001) * len(sample) * E * T

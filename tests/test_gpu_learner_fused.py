@@ -83,28 +83,61 @@ def test_centred_rank_weights_and_gradient(eng, ties):
     assert _rel(g, g_ref) <= 1e-5
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
-def test_moments_one_collective_equals_zscore_path(eng, world):
-    """Per-rank moments summed (the all-reduce) -> DSGD from moments == the z-score gradient + DSGD."""
+@pytest.mark.parametrize("world,P,near_constant", [(1, 6092, False), (2, 6092, False), (3, 6092, False),
+                                                   (2, 6092, True), (3, 200_000, False), (2, 200_000, True)])
+def test_moments_one_collective_equals_zscore_path(eng, world, P, near_constant):
+    """Per-rank moments [A | B | n_local | r' slots] summed (the all-reduce) -> DSGD from moments == the z-score
+    gradient + DSGD (fused one-workgroup DSGD for P <= 65536, stats + multi-block path above).  near_constant:
+    returns 500 +- 1e-12 (|m| / sd ~ 1e13), where a one-pass variance is rounding noise -- the slots give the
+    two-pass statistics of standardize_arr, and the pair-shifted coefficients keep A free of cancellation."""
     from fdr import dist as fdist
-    n_dirs, P = 512, 6092
-    _, _, _, _, d = _case(n_dirs, P, seed=6, mean=40.0)
+    n_dirs = 512 if P <= 6092 else 64
+    table, idx, sign, rew, d = _case(n_dirs, P, seed=6, mean=40.0)
+    if near_constant:
+        rew = 500.0 + np.random.RandomState(9).choice([-1e-12, 1e-12], rew.size)
+        d["rew"] = torch.as_tensor(rew, device="cuda")
     theta0 = torch.as_tensor(np.random.RandomState(1).randn(P).astype(np.float32) * 0.1, device="cuda")
     g_z = eng.fd_grad_fused(d["table"], d["idx"], d["rew"], 0.5, 0, d["sign"], d["n2"], 2, 0.02, P)
     th_z = theta0.clone()
     out_z = eng.dsgd_step_ex(th_z, g_z, False, 0.01, 0.6).cpu().numpy()
-    mom = torch.zeros(2 * P + 3, dtype=torch.float64, device="cuda")
+    mom = torch.zeros(2 * P + 1 + rew.size, dtype=torch.float64, device="cuda")
     for r in range(world):
         lo, hi = fdist.lane_range(n_dirs, 2, world, r)
         mom += eng.fd_grad_fused(d["table"], d["idx"][lo:hi].contiguous(), d["rew"][lo:hi].contiguous(),
-                                 0.5, 0, d["sign"][lo:hi].contiguous(), d["n2"][lo:hi].contiguous(), 2, 0.02, P,
-                                 mode="moments")
+                                 0.5, lo, d["sign"][lo:hi].contiguous(), d["n2"][lo:hi].contiguous(), 2, 0.02, P,
+                                 mode="moments", n_all=rew.size)
+    assert mom[2 * P].item() == rew.size
+    np.testing.assert_array_equal(mom[2 * P + 1:].cpu().numpy(), rew - 0.5)
     th_m = theta0.clone()
     g_m = torch.empty(P, dtype=torch.float64, device="cuda")
     out_m = eng.dsgd_step_ex(th_m, mom, True, 0.01, 0.6, g_out=g_m).cpu().numpy()
-    assert _rel(g_m.cpu().numpy(), g_z.cpu().numpy()) <= 1e-12
+    assert _rel(g_m.cpu().numpy(), g_z.cpu().numpy()) <= (1e-12 if not near_constant else 1e-9)
     np.testing.assert_allclose(th_m.cpu().numpy(), th_z.cpu().numpy(), rtol=0, atol=1e-7)
     np.testing.assert_allclose(out_m, out_z, rtol=1e-6)
+    if near_constant and P <= 6092:
+        g_ref, _ = olearn.fd_gradient(table, P, idx, sign, rew, 0.5, 0.02)
+        assert _rel(g_m.cpu().numpy(), g_ref) <= 1e-5
+
+
+def test_fused_workspace_counters_rezeroed_when_prefix_grows(eng):
+    """ADVICE r2: a fused call at small P leaves only ITS ticket-counter prefix at zero and writes slabs behind it;
+    a later call at a larger P (more column blocks, n_chunks > 1) reusing the workspace must find its longer
+    counter prefix zero, or a column block's owner never fires and g keeps stale values."""
+    big_dirs, big_P = 2048, 40_000           # 157 column blocks -> 768 B counter prefix, 6 row chunks
+    _, _, _, _, d = _case(big_dirs, big_P, seed=31)
+    _, _, _, _, ds = _case(64, 6092, seed=30)  # 24 column blocks -> 256 B prefix; gsq / DSGD partials behind it
+    coef = eng.fd_weights(d["rew"], 0.0, 0, d["sign"], d["n2"], 2, 0.02)
+    g_staged = eng.fd_grad(d["table"], d["idx"][::2].contiguous(), coef, big_P).cpu().numpy()
+
+    def big():
+        return eng.fd_grad_fused(d["table"], d["idx"], d["rew"], 0.0, 0, d["sign"], d["n2"], 2, 0.02,
+                                 big_P).cpu().numpy()
+
+    assert _rel(big(), g_staged) <= 1e-12     # sizes the shared workspace for the big call
+    theta = torch.zeros(6092, dtype=torch.float32, device="cuda")
+    eng.fd_step(ds["table"], ds["idx"], ds["rew"], 0.0, ds["sign"], ds["n2"], 2, 0.02, theta, 0.01, 1.0)
+    torch.cuda.synchronize()                  # the small step wrote its gsq / partials into bytes 256..704
+    assert _rel(big(), g_staged) <= 1e-12
 
 
 @pytest.mark.parametrize("P", [6092, 200_000])

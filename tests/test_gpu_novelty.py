@@ -142,3 +142,50 @@ def test_archive_replacement_matches_reference(engine, golden, tag, kind, n_in, 
     np.testing.assert_array_equal(worst, z[tag + "_worst"])
     np.testing.assert_allclose(h.archive.cpu().numpy(), z[tag + "_strategies"], rtol=0, atol=1e-5)
     np.testing.assert_allclose(h.pair, z[tag + "_dists"], rtol=1e-5)
+
+
+def test_impala_archive_replacement_matches_reference(engine, golden):
+    """the device StrategyHandler over an ImpalaPolicy (fdr_impala_strategies: conv stack on
+    the shared zeta frames, the zeta obs as ONE LSTM sequence from the reset state) against G12-impala, made by
+    the reference's StrategyHandler / SparseHistoryManager with get_strategy from reset (the build's documented
+    zero-state rule): every submit's return and worst_point_idx, the archive (f32, 1e-5), the distance table
+    and compute_novelty."""
+    from policies import ImpalaPolicy
+    from strategy import StrategyHandler
+    from utils import math_helpers
+    z = golden("g12_impala.npz")
+    A, H, P = int(z["A"]), int(z["H"]), int(z["P"])
+    table = np.random.RandomState(int(z["table_seed"])).randn(2 ** 22).astype(np.float32)
+    off = int(z["param_offset"])
+    theta = (table[off:off + P] * np.float32(0.1)).astype(np.float32)
+    flats = [(theta + s * table[o:o + P]).astype(np.float32) for s, o in zip(z["scales"], z["offs"])]
+    pol = ImpalaPolicy((64, 64, 3), A, seed=124)
+    assert pol.num_params == P
+    o = 0
+    for m in pol.model.bn_layers():
+        n = m.num_features
+        m.running_mean.copy_(torch.as_tensor(z["rm"][o:o + n]))
+        m.running_var.copy_(torch.as_tensor(z["rv"][o:o + n]))
+        o += n
+    Z = z["zeta_frames"].shape[0]
+    zeta = {"frame": torch.as_tensor(z["zeta_frames"].astype(np.float32)).view(Z, 1, 3, 64, 64),
+            "reward": torch.as_tensor(z["zeta_rewards"]).view(Z, 1),
+            "done": torch.zeros(Z, 1, dtype=torch.bool)}
+    h = StrategyHandler(pol, math_helpers.categorical_tvd, max_history_size=H)
+    for k in range(H):
+        pol.set_trainable_flat(flats[k])
+        assert h.add_policy(pol) is None
+    h.set_zeta(zeta)
+    worst, rets = [h.worst_point_idx], []
+    for k in range(H, len(flats)):
+        pol.set_trainable_flat(flats[k])
+        r = h.add_policy(pol)
+        rets.append(-2 if r is None else r)
+        worst.append(h.worst_point_idx)
+    np.testing.assert_array_equal(rets, z["returns"])
+    np.testing.assert_array_equal(worst, z["worst"])
+    np.testing.assert_allclose(h.archive.cpu().numpy(), z["strategies"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(h.pair, z["dists"], rtol=1e-5)
+    for k, want in zip((0, len(flats) - 1), z["novelty"]):
+        pol.set_trainable_flat((theta - z["scales"][k] * table[z["offs"][k]:z["offs"][k] + P]).astype(np.float32))
+        assert abs(h.compute_novelty(pol) - want) <= 1e-5 * max(1.0, want)

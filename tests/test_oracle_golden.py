@@ -221,3 +221,51 @@ def test_history_replacement_matches_reference(golden):
         for (i, j), d in hist.known.items():
             D[i, j] = D[j, i] = d
         np.testing.assert_allclose(D, z[tag + "_dists"], rtol=1e-6)
+
+
+def _g12i_flats(z):
+    """The G12-impala parameter vectors, regenerated from the committed seeds (4.6 MB each, not committed)."""
+    P = int(z["P"])
+    table = np.random.RandomState(int(z["table_seed"])).randn(2 ** 22).astype(np.float32)
+    off = int(z["param_offset"])
+    theta = (table[off:off + P] * np.float32(0.1)).astype(np.float32)
+    return theta, table, [(theta + s * table[o:o + P]).astype(np.float32) for s, o in zip(z["scales"], z["offs"])]
+
+
+def test_impala_history_replacement_matches_reference(golden):
+    """G12-impala: oracle.history over ImpalaPolicy strategies (oracle.impala.strategy from the reset state:
+    the zeta obs as ONE LSTM sequence, policies/impala.py:24-27) reproduces the reference StrategyHandler /
+    SparseHistoryManager run with get_strategy from reset -- returns, worst_point_idx trace, archive, distances
+    and compute_novelty."""
+    from oracle import history
+    from oracle import impala as oi
+    from oracle import novelty as onov
+    z = golden("g12_impala.npz")
+    A, H = int(z["A"]), int(z["H"])
+    _, _, flats = _g12i_flats(z)
+    bn = oi.split_bn(z["rm"], z["rv"])
+    fr = z["zeta_frames"].astype(np.float32)
+
+    def strat(f):
+        return oi.strategy(oi.unflatten(f, A), bn, fr, z["zeta_rewards"])[0]
+    hist = history.History("tvd", H)
+    for k in range(H):
+        hist.submit(None, False)
+    hist.evaluate([strat(f) for f in flats[:H]])
+    worst, rets = [hist.worst_point_idx], []
+    for k in range(H, len(flats)):
+        r = hist.submit(strat(flats[k]), True)
+        rets.append(-2 if r is None else r)
+        worst.append(hist.worst_point_idx)
+    np.testing.assert_array_equal(rets, z["returns"])
+    np.testing.assert_array_equal(worst, z["worst"])
+    np.testing.assert_allclose(np.stack(hist.strategies), z["strategies"], rtol=0, atol=1e-5)
+    D = np.full((H, H), np.inf)
+    for (i, j), d in hist.known.items():
+        D[i, j] = D[j, i] = d
+    np.testing.assert_allclose(D, z["dists"], rtol=1e-5)
+    theta, table, _ = _g12i_flats(z)
+    P = int(z["P"])
+    for k, want in zip((0, len(flats) - 1), z["novelty"]):
+        f = (theta - z["scales"][k] * table[z["offs"][k]:z["offs"][k] + P]).astype(np.float32)
+        assert abs(onov.novelty(strat(f), np.stack(hist.strategies), "tvd") - want) <= 1e-5 * max(1.0, want)

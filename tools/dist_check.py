@@ -1,27 +1,28 @@
 """Multi-rank rehearsal of the sharded FD step on ONE GPU (all ranks share cuda:0, gloo backend).
 
-    python tools/dist_check.py single                  # 1 process  -> gpurun_out/dist/theta_single.npy
+    python tools/dist_check.py single <weighting> <out_dir>        # 1 process -> <out_dir>/theta_single.npy
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
-        tools/dist_check.py multi                      # 2 ranks   -> gpurun_out/dist/theta_rank{r}.npy
-    python tools/dist_check.py compare
+        tools/dist_check.py multi <weighting> <out_dir>            # 2 ranks  -> <out_dir>/theta_rank{r}.npy
+    python tools/dist_check.py compare <weighting> <out_dir>
 
-Every rank draws the full index stream, evaluates its lane slice, all-gathers rewards, all-reduces
-the gradient and applies the replicated DSGD step: all ranks must end bit-identical, and equal to
-the single-process run up to the all-reduce summation order.
+weighting: "zscore" (the default one-collective moments form) or "centred_rank" (all-gather + all-reduce).
+The product path end to end: every rank draws the full index stream (SharedNoiseTable), Worker.evaluate runs its
+lane slice (lane_range="auto", lanes keyed by their GLOBAL index), FiniteDifferences.step exchanges and applies
+the replicated DSGD step -- for STEPS FD steps.  All ranks must end bit-identical, and equal to the
+single-process run up to the collective's summation order.  tests/test_gpu_dist_equivalence.py drives it.
 """
 import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "dfd-starter_amd")]
-OUT = os.path.join(REPO, "gpurun_out", "dist")
+STEPS = 3
 
 
-def run(mode):
+def run(mode, weighting, out):
     import numpy as np
     import torch
     import torch.distributed as dist
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if mode == "multi":
         dist.init_process_group("gloo")
@@ -39,32 +40,39 @@ def run(mode):
     table = SharedNoiseTable(1 << 22, policy.num_params, random_seed=124)
     agent = Agent(policy, env, random_seed=7)
     worker = Worker(policy, agent, table, None, sigma=0.02, random_seed=124)
-    learner = FiniteDifferences(policy, DSGD(policy.parameters(), lr=0.01), AdaptiveOmega(), table, noise_std=0.02)
+    learner = FiniteDifferences(policy, DSGD(policy.parameters(), lr=0.01), AdaptiveOmega(), table, noise_std=0.02,
+                                weighting=weighting)
     n_dirs = 96
-    for step in range(3):
+    upd = []
+    for step in range(STEPS):
         # the same counter-stream key for a lane whatever rank evaluates it: seed by step only,
-        # and lanes are keyed by their GLOBAL index through lane_base
+        # and lanes are keyed by their GLOBAL index through lane_offset
         batch = worker.evaluate(n_dirs, antithetic=True, lane_range="auto", seed=1000 + step)
-        learner.step(batch, 0.0, 0.0, 0.0)
-    os.makedirs(OUT, exist_ok=True)
-    name = "theta_single.npy" if mode == "single" else "theta_rank%d.npy" % rank
-    np.save(os.path.join(OUT, name), policy.get_trainable_flat())
+        upd.append(learner.step(batch, 0.25, 0.0, 0.0))
+    os.makedirs(out, exist_ok=True)
+    name = "single" if mode == "single" else "rank%d" % rank
+    np.save(os.path.join(out, "theta_%s.npy" % name), policy.get_trainable_flat())
+    np.save(os.path.join(out, "upd_%s.npy" % name), np.asarray(upd))
     if mode == "multi":
         dist.destroy_process_group()
 
 
-def compare():
+def compare(out, world=2):
+    """-> max |theta_Nrank - theta_1rank|; raises if the ranks differ."""
     import numpy as np
-    single = np.load(os.path.join(OUT, "theta_single.npy"))
-    r0 = np.load(os.path.join(OUT, "theta_rank0.npy"))
-    r1 = np.load(os.path.join(OUT, "theta_rank1.npy"))
-    assert np.array_equal(r0, r1), "ranks diverged"
-    err = np.abs(r0 - single).max()
-    print("max |theta_2rank - theta_1rank| = %.3e" % err)
-    assert err < 1e-5, err
-    print("dist_check ok")
+    single = np.load(os.path.join(out, "theta_single.npy"))
+    ranks = [np.load(os.path.join(out, "theta_rank%d.npy" % r)) for r in range(world)]
+    for r in ranks[1:]:
+        assert np.array_equal(r, ranks[0]), "ranks diverged"
+    err = float(np.abs(ranks[0] - single).max())
+    print("max |theta_%drank - theta_1rank| = %.3e" % (world, err))
+    return err
 
 
 if __name__ == "__main__":
-    mode = sys.argv[1]
-    compare() if mode == "compare" else run(mode)
+    mode, weighting, out = sys.argv[1], sys.argv[2], sys.argv[3]
+    if mode == "compare":
+        assert compare(out) <= 1e-6
+        print("dist_check ok")
+    else:
+        run(mode, weighting, out)
