@@ -73,8 +73,10 @@ def lane_step_flops(kind, n_in, n_act):
 # CPU baseline (oracle restatement of the reference's per-lane loop), forked before any GPU use
 # ------------------------------------------------------------------------------------------------
 def _cpu_worker_impala(wid, seconds, T):
-    """Per-env reference loop on one core: ImpalaCNN torch-CPU forward per step (oracle restatement of
-    policies/impala.py + worker/agent.py), perturbed theta, synthetic frames."""
+    """Per-env reference loop on one core, WHOLE episodes (at least one, then until `seconds`): ImpalaCNN torch-CPU
+    forward per step (oracle restatement of policies/impala.py + worker/agent.py:35-55), perturbed theta, synthetic
+    frames, then the end-of-episode entropy pass over every visited obs (worker/agent.py:60-66, the LSTM replayed
+    from the end state).  -> (env steps, whole episodes, elapsed s)."""
     import numpy as np
     import torch
     from oracle import impala as oi
@@ -82,18 +84,27 @@ def _cpu_worker_impala(wid, seconds, T):
     torch.manual_seed(124)
     P = oi.num_params(6)
     theta = (torch.randn(P) * 0.01).numpy()
-    eps = np.random.RandomState(wid).randn(P).astype(np.float32)
-    p = oi.unflatten((theta + np.float32(0.02) * eps).astype(np.float32), 6)
     bn = oi.split_bn(np.zeros(oi.num_bn(), np.float32), np.ones(oi.num_bn(), np.float32))
-    h, c, r = torch.zeros(1, 256), torch.zeros(1, 256), np.zeros(1, np.float32)
-    steps, t0, t = 0, time.perf_counter(), 0
-    while time.perf_counter() - t0 < seconds:
-        fr = oi.frames(5, [wid], t).astype(np.float32)
-        pr, h, c, _, _ = oi.forward(p, bn, fr, r, h, c)
-        a = oi.categorical_inverse_cdf(pr.numpy()[0], crng.uniform(7, wid, t, 0))
-        r = oi.rewards(5, [wid], t, [a], 6)
-        steps, t = steps + 1, (t + 1) % T
-    return steps, time.perf_counter() - t0
+    rs = np.random.RandomState(wid)
+    steps = episodes = 0
+    t0 = time.perf_counter()
+    while episodes == 0 or time.perf_counter() - t0 < seconds:
+        p = oi.unflatten((theta + np.float32(0.02) * rs.randn(P).astype(np.float32)).astype(np.float32), 6)
+        h, c, r = torch.zeros(1, 256), torch.zeros(1, 256), np.zeros(1, np.float32)
+        cis = []
+        for t in range(T):
+            fr = oi.frames(5, [wid], t).astype(np.float32)
+            pr, h, c, _, ci = oi.forward(p, bn, fr, r, h, c)
+            cis.append(ci)
+            a = oi.categorical_inverse_cdf(pr.numpy()[0], crng.uniform(7, wid, t, 0))
+            r = oi.rewards(5, [wid], t, [a], 6)
+        eh, ec = h, c
+        for t in range(T):
+            pe, eh, ec = oi.lstm_head(p, bn, cis[t], eh, ec)
+            oi.categorical_entropy(pe)
+        steps += T
+        episodes += 1
+    return steps, episodes, time.perf_counter() - t0
 
 
 def _cpu_worker(args):
@@ -102,8 +113,7 @@ def _cpu_worker(args):
     torch.set_num_threads(1)                      # run_client.py:15
     kind, n_in, n_act, _, T = CONFIGS[cfg]
     if kind == "impala":
-        steps, el = _cpu_worker_impala(wid, seconds, T)
-        return steps, 0, el
+        return _cpu_worker_impala(wid, seconds, T)
     from oracle import agent
     return agent.reference_collect_loop(kind, n_in, n_act, T, seconds, wid)
 
@@ -140,13 +150,68 @@ def cpu_baseline(cfg, seconds, cores, lanes, n_params, T):
     return rate, steps, episodes, lanes * T / rate + learn_s, learn_s, n_learn
 
 
+def bench_trap(args):
+    """BASELINE config 1: run_sequential.py on custom_envs.simple_trap_env, DiscretePolicy(2, 9), 16 perturbations.
+    The reference runs it on the CPU only; its cpu_baseline here is the restated SequentialRunner.train loop
+    (oracle/runner.run_trap, run_sequential.py:113-179) timed epoch by epoch on one core (the reference's runner is
+    one single-threaded process), and `value` is the product SequentialRunner (one rollout launch of the trap env
+    per epoch + the device learner) on cuda:0.  A step is one train epoch."""
+    import numpy as np
+    cpu = None
+    if not args.no_cpu_baseline:
+        import torch
+        torch.set_num_threads(1)
+        from oracle import runner as orun
+        secs = []
+        n_ep = max(3, int(args.cpu_seconds / 0.6))
+        t0 = time.perf_counter()
+        out = orun.run_trap(n_ep, epoch_seconds=secs)
+        wall = time.perf_counter() - t0
+        rate = out["cum_steps"] / sum(secs)
+        cpu = {"value": round(rate, 1), "unit": "env steps/s", "cores": 1, "kind": "port",
+               "sec_per_fd_step": round(float(np.median(secs)), 4),
+               "sample": "%d epochs of oracle/runner.run_trap (SequentialRunner.train restated: 16 returns per epoch, "
+                         "per-step torch forward + injected-uniform sampling, learner step; %.1f s incl. setup), "
+                         "%d env steps; sec_per_fd_step = median epoch" % (n_ep, wall, out["cum_steps"]),
+               "calibration": "profiles/r06_cpu_calibration.txt: the reference's own SequentialRunner.train on the "
+                              "trap env ran at 0.56x this restatement's rate in the build container (same machine)"}
+    import torch
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    from run_sequential import SequentialRunner
+    runner = SequentialRunner(env_id="SimpleTrapEnv-v0", batch_size=16, random_seed=124, zeta_size=4,
+                              max_strategy_history_size=4, device=dev, verbose=False)
+    for _ in range(max(1, args.warmup)):
+        runner.train(1)
+    torch.cuda.synchronize()
+    s0 = runner.agent.cumulative_timesteps
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        runner.train(1)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    steps = runner.agent.cumulative_timesteps - s0
+    line = {"metric": METRIC, "value": round(steps / el, 1), "unit": "env steps/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 4),
+            "sec_per_fd_step": round(el / args.steps, 6), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "BASELINE config 1: run_sequential.py SequentialRunner on custom_envs.simple_trap_env "
+                                   "(the reference's map, integer-exact GPU env), DiscretePolicy(2, 9) P=%d, 16 "
+                                   "perturbations per epoch, T=201; a step = one train epoch (rollout launch + FD "
+                                   "step + the host bookkeeping of run_sequential.py:113-179)" % runner.policy.num_params,
+                       "parallelism": "dp1"},
+            "roofline": None, "cpu_baseline": cpu,
+            "note": "plumbing config (the reference's CPU-only smoke test): launch- and host-bound by construction"}
+    print(json.dumps(line), flush=True)
+
+
 # ------------------------------------------------------------------------------------------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="halfcheetah", choices=list(CONFIGS))
+    ap.add_argument("--config", default="halfcheetah", choices=list(CONFIGS) + ["trap"])
     ap.add_argument("--perturbations", type=int, default=None,
                     help="antithetic lanes per GPU (default: the BASELINE config's -- 4096 halfcheetah, "
                          "1024 cartpole, 1024 x 4 envs impala)")
@@ -165,6 +230,8 @@ def main():
     ap.add_argument("--no-novelty", action="store_true", help="config 5 without the novelty archive / omega "
                     "(rocprof passes: the archive's conv launches would mix into the rollout conv's average)")
     args = ap.parse_args()
+    if args.config == "trap":
+        return bench_trap(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -119,6 +119,16 @@ __device__ __forceinline__ float disc_entropy_term(float p, float tot) {
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+// c + a * (b.x, b.x) / c + a * (b.y, b.y): one element of a register pair broadcast by op_sel (hipcc 7.2 moves an
+// odd element of a b128 load to an even register first: a v_mov per broadcast operand otherwise)
+__device__ __forceinline__ f2 pk_fma_blo(f2 a, f2 b, f2 c) {
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[1,0,1]" : "+v"(c) : "v"(a), "v"(b));
+  return c;
+}
+__device__ __forceinline__ f2 pk_fma_bhi(f2 a, f2 b, f2 c) {
+  asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(c) : "v"(a), "v"(b));
+  return c;
+}
 
 __host__ __device__ constexpr int l2_sigma(int i) { return i < 4 ? i : 11 - i; }
 
@@ -837,7 +847,13 @@ struct MlpPair {
     auto w1v = [&](int u, int k) {
       return k < NIN ? src.get(L::L1W + (int64_t)u * NIN + k) : (k == NIN ? src.get(L::L1B + u) : 0.f);
     };
-    if constexpr (kW1Lds) {
+    if constexpr (kPk) {
+#pragma unroll
+      for (int j = 0; j < 2 * kW1Chunks; ++j) {
+        const float e0 = w1v(ua, 2 * j), f0 = w1v(ub, 2 * j), e1 = w1v(ua, 2 * j + 1), f1 = w1v(ub, 2 * j + 1);
+        my[j * kWave] = float4{e0, f0, e1, f1};
+      }
+    } else if constexpr (kW1Lds) {
 #pragma unroll
       for (int m = 0; m < kW1Chunks; ++m) {
         const float e0 = w1v(ua, 4 * m), e1 = w1v(ua, 4 * m + 1), e2 = w1v(ua, 4 * m + 2), e3 = w1v(ua, 4 * m + 3);
@@ -866,8 +882,9 @@ struct MlpPair {
         w2[p * 8 + k] = f2{e0, e1};
       }
     }
-    b2a = src.get(L::L2B + 16 * r + c);
-    b2b = src.get(L::L2B + 16 * r + 8 + c);
+    const int u2a = 16 * r + c, u2b = 16 * r + 8 + c;  // this thread's layer-2 units
+    b2a = src.get(L::L2B + u2a);
+    b2b = src.get(L::L2B + u2b);
     if (o < NOUT) {
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
@@ -899,8 +916,8 @@ struct MlpPair {
       };
       fold(L::BN1W, L::BN1B, NIN, ua, a1a, c1a);
       fold(L::BN1W, L::BN1B, NIN, ub, a1b, c1b);
-      fold(L::BN2W, L::BN2B, NIN + kHidden, 16 * r + c, a2a, c2a);
-      fold(L::BN2W, L::BN2B, NIN + kHidden, 16 * r + 8 + c, a2b, c2b);
+      fold(L::BN2W, L::BN2B, NIN + kHidden, u2a, a2a, c2a);
+      fold(L::BN2W, L::BN2B, NIN + kHidden, u2b, a2b, c2b);
     }
   }
 
@@ -922,18 +939,41 @@ struct MlpPair {
 
   // Loop-invariant LDS rows of layer 1 (W1 rows 2t, 2t+1 when kW1Lds) and the env's M row t, loaded
   // a phase ahead of their use (after the head of the previous step), off the step's dependency chain.
+  // NIN = 4k + 1 with the folded bias (HalfCheetah's 17): the last input chunk is [x_{NIN-1}, 1, 0, 0] and the
+  // W1 / M chunks [w, b, 0, 0] / [m, 0, 0, 0] -- taken as one scalar input (a ds_read_b32 of x, a float2 of
+  // W1, a float of M) and 3 FMAs instead of a fifth b128 chunk and 6 packed FMAs
+  static constexpr bool kTail = kW1Lds && kBiasCol && NX - NIN == 3;
+  static constexpr int NQ = kTail ? NX / 4 - 1 : NX / 4;  // full input chunks
+  // W1 rows 2t, 2t+1 interleaved in the tile, [w_a(2j), w_b(2j), w_a(2j+1), w_b(2j+1)] per
+  // float4, so each input k is ONE packed FMA over the two units into an (a, b) accumulator -- the layer's
+  // output pair needs no horizontal adds / register shuffles before the packed tanh, and the folded bias
+  // column is an add, not a multiply by 1
+  static constexpr bool kPk = kW1Lds && kBiasCol;
+  static constexpr int kPkPairs = (NIN + 2) / 2;  // float4 pairs of inputs 0 .. NIN (the bias column)
   struct L1Rows {
-    float4 wa[kW1Lds ? NX / 4 : 1], wb[kW1Lds ? NX / 4 : 1], m[NX / 4];
+    float4 wa[kW1Lds && !kPk ? NQ : 1], wb[kW1Lds && !kPk ? NQ : 1], m[NQ];
+    float2 ta, tb;  // kTail: (w, b) of the last chunk
+    float tm;
+    float4 wp[kPk ? kPkPairs : 1];
   };
   __device__ __forceinline__ void l1_prefetch(L1Rows& r, const float* mrow) const {
     const float4* m4 = reinterpret_cast<const float4*>(mrow);
 #pragma unroll
-    for (int q = 0; q < NX / 4; ++q) {
-      if constexpr (kW1Lds) {
+    for (int q = 0; q < NQ; ++q) {
+      if constexpr (kW1Lds && !kPk) {
         r.wa[q] = tile[q * kWave];
         r.wb[q] = tile[(kW1Chunks + q) * kWave];
       }
       r.m[q] = m4[q];
+    }
+    if constexpr (kPk) {
+#pragma unroll
+      for (int j = 0; j < kPkPairs; ++j) r.wp[j] = tile[j * kWave];
+      if constexpr (kTail) r.tm = mrow[4 * NQ];
+    } else if constexpr (kTail) {
+      r.ta = *reinterpret_cast<const float2*>(&tile[NQ * kWave]);
+      r.tb = *reinterpret_cast<const float2*>(&tile[(kW1Chunks + NQ) * kWave]);
+      r.tm = mrow[4 * NQ];
     }
   }
 
@@ -942,12 +982,54 @@ struct MlpPair {
   __device__ __forceinline__ f2 layer1_env(const float* xs, const float* ss, const L1Rows& rows, float& env) const {
     const float4* x4 = reinterpret_cast<const float4*>(xs);
     const float4* s4 = reinterpret_cast<const float4*>(ss);
+    return layer1_env_q<kSameInput>([&](int q) { return x4[q]; }, [&](int q) { return s4[q]; }, rows, env,
+                                    kTail ? xs[4 * NQ] : 0.f, kTail ? ss[4 * NQ] : 0.f);
+  }
+  template <bool kSameInput, class XQ, class SQ>
+  __device__ __forceinline__ f2 layer1_env_q(XQ&& xq, SQ&& sq, const L1Rows& rows, float& env, float xt,
+                                             float st) const {
     f2 aa0 = {b1a, 0.f}, aa1 = {0.f, 0.f}, ab0 = {b1b, 0.f}, ab1 = {0.f, 0.f};
     f2 am0 = {0.f, 0.f}, am1 = {0.f, 0.f};
+    if constexpr (kPk) {
+      // units (a, b) packed: acc[k & 1] += (w_a(k), w_b(k)) * x_k; the bias column (k = NIN) is added
+      f2 acc[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
 #pragma unroll
-    for (int q = 0; q < NX / 4; ++q) {
-      const float4 xv = x4[q], mv = rows.m[q];
-      const float4 sv = kSameInput ? xv : s4[q];
+      for (int q = 0; q < NQ; ++q) {
+        const float4 xv = xq(q), mv = rows.m[q];
+        const float4 sv = kSameInput ? xv : sq(q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int k = 4 * q + i;
+          if (k < NIN) {
+            const float4 w = rows.wp[k >> 1];
+            const f2 xp = (i < 2) ? f2{xv.x, xv.y} : f2{xv.z, xv.w};
+            acc[k & 1] = (k & 1) ? pk_fma_bhi(f2{w.z, w.w}, xp, acc[1]) : pk_fma_blo(f2{w.x, w.y}, xp, acc[0]);
+          }
+        }
+        am0 = pk_fma(f2{mv.x, mv.y}, f2{sv.x, sv.y}, am0);
+        am1 = pk_fma(f2{mv.z, mv.w}, f2{sv.z, sv.w}, am1);
+      }
+      if constexpr (kTail) {  // input 4 NQ = NIN - 1, then the bias
+        const float4 w = rows.wp[(NIN - 1) >> 1];
+        acc[(NIN - 1) & 1] = pk_fma(((NIN - 1) & 1) ? f2{w.z, w.w} : f2{w.x, w.y}, f2{xt, xt}, acc[(NIN - 1) & 1]);
+        am1.x = fmaf(rows.tm, kSameInput ? xt : st, am1.x);
+      }
+      {
+        const float4 w = rows.wp[NIN >> 1];
+        acc[NIN & 1] = acc[NIN & 1] + ((NIN & 1) ? f2{w.z, w.w} : f2{w.x, w.y});
+      }
+      const f2 am = am0 + am1, h = acc[0] + acc[1];
+      env = am.x + am.y;
+      if constexpr (DISC) {
+        return f2{act1(h.x, a1a, c1a), act1(h.y, a1b, c1b)};
+      } else {
+        return tanh2_fast(h);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const float4 xv = xq(q), mv = rows.m[q];
+      const float4 sv = kSameInput ? xv : sq(q);
       float4 wa, wb;
       if constexpr (kW1Lds) {
         wa = rows.wa[q];
@@ -963,6 +1045,11 @@ struct MlpPair {
       ab1 = pk_fma(f2{wb.z, wb.w}, f2{xv.z, xv.w}, ab1);
       am1 = pk_fma(f2{mv.z, mv.w}, f2{sv.z, sv.w}, am1);
     }
+    if constexpr (kTail) {  // w x + b of the last chunk, and m s
+      aa1 = pk_fma(f2{rows.ta.x, rows.ta.y}, f2{xt, 1.f}, aa1);
+      ab1 = pk_fma(f2{rows.tb.x, rows.tb.y}, f2{xt, 1.f}, ab1);
+      am1.x = fmaf(rows.tm, kSameInput ? xt : st, am1.x);
+    }
     const f2 am = am0 + am1, ha = aa0 + aa1, hb = ab0 + ab1;
     env = am.x + am.y;
     if constexpr (DISC) {
@@ -977,9 +1064,9 @@ struct MlpPair {
   template <class Mark>
   __device__ __forceinline__ float layers23(f2 h1, float* h1s, int t, Mark&& mark) const {
     const int c = t & 7;
+    float x[8];
     reinterpret_cast<f2*>(h1s)[t] = h1;
     wave_lds_sync();
-    float x[8];
     lds_bcast<8>(h1s + 8 * c, x);
     // the head's W3 slice (loop-invariant LDS) requested here, in flight during the 64 packed FMAs
     float w3[32];
@@ -1105,7 +1192,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
   float rbuf = 0.f;
   const int zbase = 4 * (32 * hh + (DISC ? 0 : (o < NA ? o : 0)));
   auto* sc = &scratch[wv];
-  float* xs = sc->x[hh];
+  [[maybe_unused]] float* xs = sc->x[hh];
   float* h1s = sc->h1[hh];
   const float* mrow = envMK + ji * MKS;
   constexpr bool kSame = !DISC && !norm_obs;
@@ -1145,6 +1232,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     if constexpr (!kSame) h1s[t] = t < NIN ? s : 0.f;
     wave_lds_sync();
     const f2 h1 = pl.template layer1_env<kSame>(xs, h1s, l1rows, pre);
+
     mark(0, h1.x);
     const float y = pl.layers23(h1, h1s, t, mark);
     pl.l1_prefetch(l1rows, mrow);  // next step's rows, in flight during the action and env phases

@@ -64,7 +64,9 @@ def launch_seed(random_seed, episodes):
 
 
 def run_trap(n_epochs, batch_size=16, seed=124, noise_std=0.02, lr=0.01, eval_prob=0.05,
-             zeta_size=4, action_seed=777, table_size=2 ** 22, counter_seed=False):
+             zeta_size=4, action_seed=777, table_size=2 ** 22, counter_seed=False, epoch_seconds=None):
+    """epoch_seconds: a list that receives each epoch's wall time (the train loop alone, run_sequential.py:113-179,
+    for bench.py's config-1 CPU baseline)."""
     torch.manual_seed(seed)
     np.random.seed(seed)
     omega = _AdaptiveOmega()
@@ -88,7 +90,9 @@ def run_trap(n_epochs, batch_size=16, seed=124, noise_std=0.02, lr=0.01, eval_pr
         return np.float32(action_rng.uniform())
 
     episodes = 0
+    import time
     for _ in range(n_epochs):
+        t_epoch = time.perf_counter()
         theta = learner.theta
         rets, any_eval = [], False
         if counter_seed:
@@ -144,4 +148,6 @@ def run_trap(n_epochs, batch_size=16, seed=124, noise_std=0.02, lr=0.01, eval_pr
                               policy_reward, omega.omega, omega.min_omega, omega.max_omega)
         log.append(dict(rewards=np.array(rewards), idx=np.array([i for _, i, _ in rets]),
                         policy_reward=policy_reward, update=upd))
+        if epoch_seconds is not None:
+            epoch_seconds.append(time.perf_counter() - t_epoch)
     return dict(theta=learner.theta, log=log, cum_steps=cum_steps, policy_reward=policy_reward)
