@@ -49,6 +49,10 @@ IMPALA_CONV_FLOP = 2 * 9 * (3 * 16 * 64 * 64 + 4 * 16 * 16 * 32 * 32 + 16 * 32 *
                             + 32 * 32 * 16 * 16 + 4 * 32 * 32 * 8 * 8)
 # fc + LSTM + head weights streamed per (lane, step) by the core kernel (f32)
 IMPALA_CORE_BYTES = 4 * (2048 * 256 + 257 * 1024 + 256 * 1024)
+# oracle CPU loop rate / the reference's own loop rate, same machine, one thread (tools/cpu_calibrate.py,
+# profiles/r06_cpu_calibration.txt): the cpu_baseline's reference-equivalent rate = measured / ratio
+CPU_CALIBRATION = {"halfcheetah": 1.06, "cartpole": 0.91, "trap": 1.60}
+SURVEY_REF_PER_CORE = 9.5e3      # the patched reference, HalfCheetah-shaped, env steps/s per process
 
 
 def rollout_kernel_name(kind, n_in, n_act, lanes, dev):
@@ -173,8 +177,10 @@ def bench_trap(args):
                "sample": "%d epochs of oracle/runner.run_trap (SequentialRunner.train restated: 16 returns per epoch, "
                          "per-step torch forward + injected-uniform sampling, learner step; %.1f s incl. setup), "
                          "%d env steps; sec_per_fd_step = median epoch" % (n_ep, wall, out["cum_steps"]),
-               "calibration": "profiles/r06_cpu_calibration.txt: the reference's own SequentialRunner.train on the "
-                              "trap env ran at 0.56x this restatement's rate in the build container (same machine)"}
+               "reference_equivalent": {"value": round(rate / CPU_CALIBRATION["trap"], 1),
+                                        "oracle_over_reference": CPU_CALIBRATION["trap"],
+                                        "note": "the reference's own SequentialRunner.train on the trap env timed beside "
+                                                "run_trap in the build container (profiles/r06_cpu_calibration.txt)"}}
     import torch
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -249,8 +255,15 @@ def main():
         P = oimp.num_params(n_act) if kind == "impala" else opol.num_params(kind, n_in, n_act)
         cores = cpu_cores()
         v, steps, eps, fd_s, learn_s, n_learn = cpu_baseline(args.config, args.cpu_seconds, cores, L * E, P, T)
+        ratio = CPU_CALIBRATION.get(args.config)
         cpu = {"value": round(v, 1), "unit": "env steps/s", "cores": cores, "kind": "port",
-               "sec_per_fd_step": round(fd_s, 3),
+               "sec_per_fd_step": round(fd_s, 3), "per_core": round(v / cores, 1),
+               "reference_equivalent": None if ratio is None else {
+                   "value": round(v / ratio, 1), "per_core": round(v / cores / ratio, 1), "oracle_over_reference": ratio,
+                   "note": "the reference's own Worker.collect_returns timed beside this loop in the build container "
+                           "(tools/cpu_calibrate.py, profiles/r06_cpu_calibration.txt); SURVEY 6's 9.5 k/core was "
+                           "measured on that container's CPU, not this host's"},
+               "whole_episodes": eps,
                "sample": ("%d processes x %.0f s of the oracle's reference-shaped loop (worker/worker.py:20-57 + "
                           "worker/agent.py:20-71: perturb, per-step batch-1 torch forward + torch %s sampling, "
                           "env.step, end-of-episode entropy forward; 1 thread each as run_client.py:15; T=%d): "
