@@ -52,7 +52,6 @@ IMPALA_CORE_BYTES = 4 * (2048 * 256 + 257 * 1024 + 256 * 1024)
 # oracle CPU loop rate / the reference's own loop rate, same machine, one thread (tools/cpu_calibrate.py,
 # profiles/r06_cpu_calibration.txt): the cpu_baseline's reference-equivalent rate = measured / ratio
 CPU_CALIBRATION = {"halfcheetah": 1.06, "cartpole": 0.91, "trap": 1.60}
-SURVEY_REF_PER_CORE = 9.5e3      # the patched reference, HalfCheetah-shaped, env steps/s per process
 
 
 def rollout_kernel_name(kind, n_in, n_act, lanes, dev):
