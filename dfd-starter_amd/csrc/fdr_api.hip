@@ -117,6 +117,8 @@ Context& default_context() {
                                                     : strcmp(e, "pair") == 0 ? FDR_ROLLOUT_PAIR : FDR_ROLLOUT_AUTO;
     const char* m = getenv("FDR_CORE_MFMA");  // A/B switch: "0" selects the VALU fp16 pair core
     c->core_mfma = !(m && strcmp(m, "0") == 0);
+    const char* h2 = getenv("FDR_CONV_H2");  // A/B switch: "1" / "0" selects the fp16 conv kernel
+    if (h2) c->conv_h2 = strcmp(h2, "0") != 0;
     return c;
   }();
   return *d;
@@ -178,6 +180,10 @@ int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on) {
   (ctx ? ctx->c : default_context()).core_mfma = on != 0;
   return FDR_OK;
 }
+int fdr_ctx_set_conv_h2(fdr_ctx* ctx, int32_t on) {
+  (ctx ? ctx->c : default_context()).conv_h2 = on != 0;
+  return FDR_OK;
+}
 int fdr_ctx_impala_profile(fdr_ctx* ctx, int32_t enable) { return impala::set_profile(ctx ? ctx->c : default_context(), enable); }
 int fdr_ctx_impala_profile_read(fdr_ctx* ctx, double* ms) {
   if (!ms) return set_error(FDR_ERR_INVALID, "NULL pointer");
@@ -201,6 +207,7 @@ int fdr_ctx_create(int device, fdr_ctx** out) {
   c->c.cus = cus;
   c->c.rollout_impl = default_context().rollout_impl;  // FDR_ROLLOUT applies to new contexts too
   c->c.core_mfma = default_context().core_mfma;        // and FDR_CORE_MFMA
+  c->c.conv_h2 = default_context().conv_h2;            // and FDR_CONV_H2
   *out = c;
   return FDR_OK;
 }
@@ -533,6 +540,7 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* d, const float* thet
   impala::ForwardCall f{};
   f.layout = &L;
   f.fp16 = d->fp16 != 0;
+  f.conv_h2 = C->conv_h2;
   f.theta = theta;
   f.n_envs = n_envs;
   f.frames = frames;
@@ -570,6 +578,7 @@ int fdr_impala_strategies(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lane
   sc.n_lanes = n_lanes;
   sc.n_states = n_states;
   sc.fp16 = d->fp16 != 0;
+  sc.conv_h2 = C->conv_h2;
   sc.frames = frames;
   sc.reward = reward;
   sc.h = h;

@@ -217,6 +217,7 @@ __global__ void finish_kernel(int n_lanes, int envs, int T, int entropy, int jig
 
 // fp16 mode kernels (fdr_impala_h.hip)
 __global__ void conv_kernel_h(Layout L, StepArgs a);
+__global__ void conv_kernel_h2(Layout L, StepArgs a);  // same features, 4 waves / 80 KiB LDS: 2 workgroups per CU
 template <int E, int MODE>
 __global__ void core_kernel_h(Layout L, StepArgs a);
 template <int E>
@@ -234,7 +235,7 @@ template <int E>
 __global__ void xproj_pair_kernel(Layout L, StepArgs a, int t0, int tc, float* gx);
 // MFMA images (kMImg halves each) of n half packs: grid (kFcKS + 4 kGateKS, n)
 __global__ void mfma_image_kernel(Layout L, const _Float16* src, int64_t src_stride, _Float16* dst);
-constexpr int kHThreads = 512;
+constexpr int kHThreads = 512, kH2Threads = 256;
 
 struct Plan {  // workspace carve-up (byte offsets)
   int64_t pack, hpack, feat, h, c, rprev, ci, gx, n2, zeros, thpack, epack, idxe, n2x, mimg, total;
@@ -263,7 +264,7 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
 
 struct ForwardCall {
   const Layout* layout;
-  int fp16;
+  int fp16, conv_h2;
   const float* theta;
   int n_envs;
   const float* frames;
@@ -282,7 +283,7 @@ int64_t forward_workspace_bytes(const Layout& L, int n_envs, bool fp16 = false);
 struct StrategiesCall {
   const Layout* layout;
   LanesArgs lanes;
-  int n_lanes, n_states, fp16;
+  int n_lanes, n_states, fp16, conv_h2;
   const float* frames;   // [Z][3][64][64] f32 0..255
   const float* reward;   // [Z] or NULL
   float* h;              // [n_lanes][256] in/out initial state, or NULL (zero state)

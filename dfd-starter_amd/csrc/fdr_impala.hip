@@ -1344,6 +1344,14 @@ __global__ void pair_offsets_kernel(const int64_t* __restrict__ idx, int n_pairs
   if (p < n_pairs) idxe[p] = idx[2 * p];
 }
 
+// the fp16 conv stack over grid workgroups (one per env, XCD-interleaved lanes): either kernel, same features
+static void launch_conv_h(int h2, int grid, const Layout& L, const StepArgs& a, hipStream_t stream) {
+  if (h2)
+    hipLaunchKernelGGL(conv_kernel_h2, dim3(grid), dim3(kH2Threads), 0, stream, L, a);
+  else
+    hipLaunchKernelGGL(conv_kernel_h, dim3(grid), dim3(kHThreads), 0, stream, L, a);
+}
+
 template <int E>
 static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int entropy, hipStream_t stream) {
   const int conv_grid = (a.n_lanes + 7) / 8 * 8 * a.envs;
@@ -1358,7 +1366,7 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
   for (int t = 0; t < a.T; ++t) {
     a.t = t;
     if (h)
-      hipLaunchKernelGGL(conv_kernel_h, dim3(conv_grid), dim3(kHThreads), 0, stream, L, a);
+      launch_conv_h(ctx.conv_h2, conv_grid, L, a, stream);
     else
       hipLaunchKernelGGL(conv_kernel, dim3(conv_grid), dim3(kConvThreads), 0, stream, L, a);
     mark(prof, stream);
@@ -1569,7 +1577,7 @@ int launch_forward(const ForwardCall& c, void* ws, int64_t ws_bytes, hipStream_t
     launch_pack<_Float16>(L, lanes, a.hpack, reinterpret_cast<double*>(w + p.n2), 1, 1, stream);
   }
   if (c.fp16) {
-    hipLaunchKernelGGL(conv_kernel_h, dim3((c.n_envs + 7) / 8 * 8), dim3(kHThreads), 0, stream, L, a);
+    launch_conv_h(c.conv_h2, (c.n_envs + 7) / 8 * 8, L, a, stream);
     hipLaunchKernelGGL((core_kernel_h<1, kForward>), dim3(c.n_envs), dim3(kCoreThreads), 0, stream, L, a);
   } else {
     hipLaunchKernelGGL(conv_kernel, dim3((c.n_envs + 7) / 8 * 8), dim3(kConvThreads), 0, stream, L, a);
@@ -1731,7 +1739,7 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
     a.frames = c.frames + (int64_t)z0 * kFramePix;
     const int conv_grid = (c.n_lanes + 7) / 8 * 8 * zc;
     if (half)
-      hipLaunchKernelGGL(conv_kernel_h, dim3(conv_grid), dim3(kHThreads), 0, stream, L, a);
+      launch_conv_h(c.conv_h2, conv_grid, L, a, stream);
     else
       hipLaunchKernelGGL(conv_kernel, dim3(conv_grid), dim3(kConvThreads), 0, stream, L, a);
     const dim3 grid(c.n_lanes, (zc + 63) / 64);

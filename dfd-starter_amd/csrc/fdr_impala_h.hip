@@ -131,28 +131,30 @@ constexpr int kBlockHalves = KSteps<CIN>::N * NT * 64 * 8;
 // work: issue() starts the loads (16-B chunks, chunk c by thread c mod 512), commit() stores them to
 // WB.  WB protocol (every phase ends in a barrier): read WB -> af in phase k, commit the next block
 // in phase k+1 or later, read it in a phase after the commit.
-struct WStage {
-  u32x4 r[(kWB / 8 + kHThreads - 1) / kHThreads];
+template <int NTH>
+struct WStageT {
+  u32x4 r[(kWB / 8 + NTH - 1) / NTH];
   template <int NH>
   __device__ __forceinline__ void issue(const _Float16* __restrict__ src) {
-    constexpr int NC = NH / 8, PER = (NC + kHThreads - 1) / kHThreads;
+    constexpr int NC = NH / 8, PER = (NC + NTH - 1) / NTH;
     static_assert(NH % 8 == 0 && NH <= kWB, "weight block");
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const int c = threadIdx.x + k * kHThreads;  // past the block: reload its last chunk (not stored)
-      r[k] = reinterpret_cast<const u32x4*>(src)[NC % kHThreads == 0 || c < NC ? c : NC - 1];
+      const int c = threadIdx.x + k * NTH;  // past the block: reload its last chunk (not stored)
+      r[k] = reinterpret_cast<const u32x4*>(src)[NC % NTH == 0 || c < NC ? c : NC - 1];
     }
   }
   template <int NH>
   __device__ __forceinline__ void commit(_Float16* wb) const {
-    constexpr int NC = NH / 8, PER = (NC + kHThreads - 1) / kHThreads;
+    constexpr int NC = NH / 8, PER = (NC + NTH - 1) / NTH;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
-      const int c = threadIdx.x + k * kHThreads;
-      if (NC % kHThreads == 0 || c < NC) reinterpret_cast<u32x4*>(wb)[c] = r[k];
+      const int c = threadIdx.x + k * NTH;
+      if (NC % NTH == 0 || c < NC) reinterpret_cast<u32x4*>(wb)[c] = r[k];
     }
   }
 };
+using WStage = WStageT<kHThreads>;
 
 // offset (halves) of this lane's 8 K-elements of k-step s inside the receptive field of a pixel
 template <int CIN, int CS, int WP>
@@ -175,7 +177,7 @@ __device__ __forceinline__ int k_offset(int s, int g, int part) {
 // pixels (row-major, width W).
 // qoff: padded-pixel index of Tin within its image (band offset of an entry conv; the swizzle is a
 // function of the image's own pixel index).
-template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT>
+template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT, int NW = 8>
 __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KSteps<CIN>::N][NT],
                                        f32x4 (&acc)[TPW][NT], int wave, int lane, int qoff = 0) {
   constexpr int KS = KSteps<CIN>::N;
@@ -183,11 +185,11 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
   // tile i of this wave exists (wave-uniform): only the last i of a conv whose MT is not a multiple of 8
   // can be past the end -- skipped, not recomputed (the clamped duplicate cost 21 % of the executed MFMA
   // FLOP: stage-3 residual convs have 4 tiles for 8 waves, r05 PMC)
-  auto live = [&](int i) { return TPW * 8 == MT || i < TPW - 1 || wave + 8 * i < MT; };
+  auto live = [&](int i) { return TPW * NW == MT || i < TPW - 1 || wave + NW * i < MT; };
   int base[TPW];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
-    int mt = wave + 8 * i;
+    int mt = wave + NW * i;
     mt = mt < MT ? mt : MT - 1;
     const int m = mt * 16 + (lane & 15);
     base[i] = (m / W) * WP + (m % W);  // padded pixel of tap 0
@@ -246,11 +248,11 @@ __device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KStep
 }
 
 // Visit the outputs: f(ch0, m, v4) -- channels ch0 .. ch0+3 of output pixel m
-template <int NT, int TPW, int MT, typename F>
+template <int NT, int TPW, int MT, int NW = 8, typename F>
 __device__ __forceinline__ void conv_out_h(const f32x4 (&acc)[TPW][NT], int wave, int lane, F f) {
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
-    const int mt = wave + 8 * i;
+    const int mt = wave + NW * i;
     if (mt >= MT) continue;
     const int m = mt * 16 + (lane & 15);
 #pragma unroll
@@ -263,11 +265,11 @@ __device__ __forceinline__ h4 to_h4(float a, float b, float c, float d) {
 }
 
 // T <- BN(X) (optionally ReLU): X [H][H][C] f16 -> padded image [H+2][H+2][CS]; BORDER: zero border.
-template <int C, int H, bool RELU, bool BORDER>
+template <int C, int H, bool RELU, bool BORDER, int NTH = kHThreads>
 __device__ __forceinline__ void to_padded_h(const _Float16* X, _Float16* T, const float* sc, const float* sh) {
   constexpr int CS = Pix<C>::CS, WP = H + 2, G = C / 8;
-  static_assert(kHThreads % G == 0, "a thread keeps one 8-channel group");
-  constexpr int PPI = kHThreads / G, NP = H * H, IT = (NP + PPI - 1) / PPI;
+  static_assert(NTH % G == 0, "a thread keeps one 8-channel group");
+  constexpr int PPI = NTH / G, NP = H * H, IT = (NP + PPI - 1) / PPI;
   const int cg = threadIdx.x % G;
   float scv[8], shv[8];  // this thread's channels: loaded once, not per pixel
 #pragma unroll
@@ -292,7 +294,7 @@ __device__ __forceinline__ void to_padded_h(const _Float16* X, _Float16* T, cons
   }
   if (BORDER) {
     const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = threadIdx.x; i < 4 * (H + 1) * G; i += kHThreads) {
+    for (int i = threadIdx.x; i < 4 * (H + 1) * G; i += NTH) {
       const int cg = i % G, r = i / G, side = r / (H + 1), k = r - side * (H + 1);
       const int pix = side == 0 ? k : side == 1 ? (H + 1) * WP + 1 + k : side == 2 ? (k + 1) * WP : k * WP + WP - 1;
       *reinterpret_cast<h8*>(T + pix * CS + 8 * cg) = z;
@@ -638,6 +640,420 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
                               nullptr);
   }
   FDR_STAMP(a, 32);
+}
+
+// =====================================================================================================
+// conv_kernel_h2: the same conv stack as conv_kernel_h in TWO workgroups per CU.
+// conv_kernel_h's 145 KiB LDS admits one 8-wave workgroup per CU, so its ~45 barrier-separated phases per env
+// step -- entry convs, pools, BN passes, epilogues -- run one after the other with the MFMA pipe idle between
+// them (busy 0.20).  Here a workgroup is 4 waves (1 per SIMD, <= 256 VGPRs) in <= 80 KiB, and two of them (two
+// envs) share a CU: one's pool / epilogue / barrier phases overlap the other's MFMA phases.  What changes to fit:
+//   * the stage-1 frame is generated per entry band (11 padded rows, double-buffered: band b+1's rows are made
+//     during band b's pool phase) instead of as a whole 66 x 66 image;
+//   * entry bands of 9 conv rows (4 pooled rows): 8 bands at stage 1, 4 at stage 2, 1 (17 rows) at stage 3;
+//   * residual convs are single-buffered: conv -> accumulators -> barrier -> in-place epilogue;
+//   * the stage-2 entry writes its pooled rows into the dead rows of its own input image;
+//   * WB is placed per stage (2,560 halves beside X1 in stage 1, 9,216 after X1 dies).
+// LDS map (halves, R = arena after the BN / bias tables; every buffer below R + 38,080):
+//   stage 1 entry : S1 [0, 9216) | FB0 [9216, 12120) | FB1 [12120, 15024) | X1 [18496, 34880) | WB_A [34880, 37440)
+//   stage 1 res   : T1 [0, 18496) | X1 | WB_A
+//   stage 2 entry : T1 (X2 into [0, 8192) band by band) | S2 [18496, 27712) | WB_B [27712, 36928)
+//   stage 2 res   : X2 [0, 8192) | T2 [8192, 18560) | WB_B
+//   stage 3 entry : X3 [0, 2048) | T2 | S3 [18560, 27264) | WB_B
+//   stage 3 res   : X3 | T3 [2048, 5248) | WB_B
+// Arithmetic per output is conv_kernel_h's (same fragments, same K order, same f32 epilogues), so the two
+// kernels' features are identical.
+// =====================================================================================================
+constexpr int kH2Waves = kH2Threads / 64;
+constexpr int kH2BR = 9;                                  // entry band: conv rows (4 pooled rows)
+constexpr int kH2FBRows = kH2BR + 2;                      // padded frame rows per band
+constexpr int kH2FB = kH2FBRows * 66 * 4;                 // halves
+constexpr int kH2Arena = 38080;                           // halves
+constexpr int kH2S1 = 0, kH2FB0 = 9216, kH2FB1 = kH2FB0 + kH2FB, kH2X1 = 18496, kH2WBA = 34880;
+constexpr int kH2S2 = 18496, kH2WBB = 27712, kH2T2 = 8192, kH2S3 = 18560, kH2T3 = 2048;
+constexpr int kH2LdsBytes = 3 * kBnTab * 4 + kH2Arena * 2;
+static_assert(kH2LdsBytes <= 80 * 1024, "two conv_kernel_h2 workgroups per CU");
+static_assert(kH2FB1 + kH2FB <= kH2X1 && kH2X1 + 32 * 32 * 16 == kH2WBA && kH2WBA + 2560 <= kH2Arena, "stage 1 map");
+static_assert(34 * 34 * 16 <= kH2X1 && kH2S2 + kH2BR * 32 * 32 <= kH2WBB && kH2WBB + kWB <= kH2Arena, "stage 2 map");
+static_assert(16 * 16 * 32 <= kH2T2 && kH2T2 + 18 * 18 * 32 <= kH2S3 && kH2S3 + 17 * 16 * 32 <= kH2WBB, "stage 3 map");
+static_assert(8 * 8 * 32 <= kH2T3 && kH2T3 + 10 * 10 * 32 <= kH2T2, "stage 3 res map");
+static_assert(kH2BR * 64 * 16 <= kH2FB0 && 3 * kBnTab * 2 >= 34 * 16, "band scratch / row -1 guard");
+
+// conv_h's arithmetic in tile-outer order (every K-step of tile i, then tile i + 1): per output the same K
+// order and the same separate tap-8 product, so the sums are conv_h's bit for bit.  With 4 waves a wave owns
+// up to 16 tiles; K-outer order keeps 5 pixel addresses per tile live at once (80 VGPRs in the stage-1
+// residual convs, which spilled), tile-outer order keeps one tile's.  Dependent MFMAs on one accumulator
+// issue back to back (SrcC forwarding of the same opcode), and the other workgroup's waves fill the SIMD.
+template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT>
+__device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSteps<CIN>::N][NT],
+                                        f32x4 (&acc)[TPW][NT], int wave, int lane, int qoff = 0) {
+  constexpr int KS = KSteps<CIN>::N, NF = KSteps<CIN>::NF, NW = kH2Waves;
+  // A wave's tiles are wave + NW i: tile i's pixels are tile 0's shifted by DQ i padded pixels (whole rows),
+  // so every read is one of NF per-lane addresses plus an immediate.  The chunk swizzle of q + DQ i is the
+  // swizzle of q XOR flip(i) when DQ keeps the swizzle bits carry-free (asserted).
+  constexpr int DQ = W >= 16 ? (NW / (W / 16)) * WP : NW * (16 / W) * WP;
+  static_assert(W >= 16 ? NW % (W / 16) == 0 : 16 % W == 0, "tile rows");
+  static_assert(CIN == 3 || (CIN == 16 && DQ % 4 == 0) || (CIN == 32 && DQ % 8 == 0), "swizzle step");
+  auto flip = [](int i) { return CIN == 16 ? ((DQ * i) >> 2) & 1 : (CIN == 32 ? ((DQ * i) >> 1) & 3 : 0); };
+  const int g = lane >> 4, m0 = wave * 16 + (lane & 15);
+  const int base = (m0 / W) * WP + (m0 % W);  // padded pixel of tap 0, tile 0
+  int off[NF], sw[NF];
+#pragma unroll
+  for (int s = 0; s < NF; ++s) {
+    if constexpr (CIN == 3) {
+      off[s] = base * CS;
+      sw[s] = 0;
+    } else {
+      constexpr int cpg = CIN / 8, tpk = 32 / CIN;
+      const int tap = s * tpk + g / cpg, q = base + (tap / 3) * WP + tap % 3;
+      off[s] = q * CS;
+      sw[s] = (g % cpg) ^ tsw<CIN>(q + qoff);
+    }
+  }
+  const int qr = base + 2 * WP + 2;  // tap 8
+  const int offr = CIN == 3 ? qr * CS : qr * CS + 4 * (g & 1);
+  const int swr = CIN == 3 ? 0 : (g >> 1) ^ tsw<CIN>(qr + qoff);
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[i][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (TPW * NW == MT || i < TPW - 1 || wave + NW * i < MT) {  // wave-uniform
+      const _Float16* Ti = Tin + DQ * i * CS;
+#pragma unroll
+      for (int s = 0; s < NF; ++s) {
+        h8 b;
+        if constexpr (CIN == 3) {
+          const h4 lo = *reinterpret_cast<const h4*>(Ti + off[s] + k_offset<CIN, CS, WP>(s, g, 0));
+          const h4 hi = *reinterpret_cast<const h4*>(Ti + off[s] + k_offset<CIN, CS, WP>(s, g, 1));
+          b = h8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        } else {
+          b = *reinterpret_cast<const h8*>(Ti + off[s] + ((sw[s] ^ flip(i)) << 3));
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b, acc[i][nt], 0, 0, 0);
+      }
+      if constexpr (KSteps<CIN>::kRem) {  // tap 8 on K = 16, added by VALU (conv_h's note)
+        const h4 b = *reinterpret_cast<const h4*>(Ti + offr + (CIN == 3 ? 0 : (swr ^ flip(i)) << 3));
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const h8 w = af[KS - 1][nt];
+          acc[i][nt] += __builtin_amdgcn_mfma_f32_16x16x16f16(h4{w[0], w[1], w[2], w[3]}, b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        }
+      }
+    }
+    // ordering point: tile i-1's accumulators are final before tile i+1's reads are issued (without it the DAG
+    // linearisation issues every tile's reads up front and sinks the MFMAs to the epilogue: spills)
+    if (i > 0) {
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(acc[i - 1][nt]));
+    }
+  }
+}
+
+// padded frame rows [p0, p0 + kH2FBRows) of this env (policies/impala.py:147 frame / 255, then BN2d(3)) into FB
+// [rows][66][4] f16 -- zero outside the 64 x 64 image and in the 4th channel slot; conv_kernel_h's values.
+__device__ __forceinline__ void frame_band_h2(_Float16* FB, int p0, const StepArgs& a, int64_t env, int e,
+                                              const float* bsc, const float* bsh) {
+  for (int i = threadIdx.x; i < kH2FBRows * 8; i += kH2Threads) {
+    const int r = i >> 3, w = i & 7, y = p0 + r - 1;  // image row of padded row p0 + r
+    float fv[3][8];
+    const bool in = y >= 0 && y < 64;
+    if (in && a.frames) {
+      const float* fr = a.frames + (a.shared_frames ? (int64_t)e : env) * kFramePix;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fv[c][j] = fr[c * 4096 + y * 64 + w * 8 + j];
+    } else if (in) {
+      const uint64_t gid = (uint64_t)(a.lane_offset * a.envs + env);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const uint64_t word = (uint64_t)(c * 512 + y * 8 + w);
+        const uint64_t hb = mix64(a.fkey + ((gid << 32) | ((uint64_t)a.t << 11) | word) * kGolden);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) fv[c][j] = (float)((uint32_t)(hb >> (8 * j)) & 255u);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      h4 o = {0, 0, 0, 0};
+      if (in) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) o[c] = (_Float16)fmaf(fv[c][j] / 255.0f, bsc[c], bsh[c]);
+      }
+      *reinterpret_cast<h4*>(FB + (r * 66 + 1 + w * 8 + j) * 4) = o;
+    }
+  }
+  for (int i = threadIdx.x; i < kH2FBRows * 2; i += kH2Threads)  // the two pad columns of every row
+    *reinterpret_cast<h4*>(FB + ((i >> 1) * 66 + (i & 1) * 65) * 4) = h4{0, 0, 0, 0};
+}
+
+// One entry band: conv rows [(BR-1) b - 1, +BR) of the padded input Tin (its row 0 = padded row (BR-1) b - 1,
+// qoff its padded-pixel index) + bias -> S (conv row -1 as -inf), barrier, then the 3x3 / stride-2 max pool of
+// the band's PRB pooled rows -> X rows [PRB b, +PRB).  between(): work for the pool phase (frame rows of the next
+// band, a weight commit) -- it must not touch S, Tin or X.
+template <int CIN, int COUT, int H, int BR, class Between>
+__device__ __forceinline__ void entry_band_h2(const _Float16* Tin, int qoff, _Float16* S, _Float16* X,
+                                              const h8 (&af)[KSteps<CIN>::N][COUT / 16], const float (&bz)[COUT / 16][4],
+                                              int b, int wave, int lane, Between&& between) {
+  constexpr int CS = Pix<CIN>::CS, WP = H + 2, NT = COUT / 16, MT = BR * H / 16;
+  constexpr int TPW = (MT + kH2Waves - 1) / kH2Waves, HO = H / 2, PRB = (BR - 1) / 2, G = COUT / 8;
+  f32x4 acc[TPW][NT];
+  conv_h2<CIN, CS, NT, TPW, H, WP, MT>(Tin, af, acc, wave, lane, qoff);
+  conv_out_h<NT, TPW, MT, kH2Waves>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
+    const int nt = ch0 >> 4;
+    const bool neg = b == 0 && m < H;  // conv row -1
+    const float ninf = -INFINITY;
+    *reinterpret_cast<h4*>(S + xidx<COUT>(m, ch0)) =
+        neg ? to_h4(ninf, ninf, ninf, ninf) : to_h4(v[0] + bz[nt][0], v[1] + bz[nt][1], v[2] + bz[nt][2], v[3] + bz[nt][3]);
+  });
+  __syncthreads();
+  between();
+  constexpr int NI = PRB * HO * G, IT = (NI + kH2Threads - 1) / kH2Threads;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int i = threadIdx.x + it * kH2Threads;
+    if (NI % kH2Threads != 0 && i >= NI) break;
+    const int cg = i % G, r = i / G, px = r % HO, pr = r / HO;
+    const int xl = 2 * px > 0 ? 2 * px - 1 : 0;
+    h8 v[9];
+#pragma unroll
+    for (int dr = 0; dr < 3; ++dr) {
+      const int row = (2 * pr + dr) * H;
+      v[3 * dr] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + xl, 8 * cg));
+      v[3 * dr + 1] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + 2 * px, 8 * cg));
+      v[3 * dr + 2] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + 2 * px + 1, 8 * cg));
+    }
+    const h8 m01 = __builtin_elementwise_max(v[0], v[1]), m23 = __builtin_elementwise_max(v[2], v[3]);
+    const h8 m45 = __builtin_elementwise_max(v[4], v[5]), m67 = __builtin_elementwise_max(v[6], v[7]);
+    const h8 mx = __builtin_elementwise_max(
+        __builtin_elementwise_max(__builtin_elementwise_max(m01, m23), __builtin_elementwise_max(m45, m67)), v[8]);
+    *reinterpret_cast<h8*>(X + xidx<COUT>((PRB * b + pr) * HO + px, 8 * cg)) = mx;
+  }
+  __syncthreads();
+}
+
+// Two residual blocks, single-buffered (conv -> accumulators -> barrier -> in-place epilogue); the arithmetic
+// of res_blocks_h.  af holds block 0's conv0 on entry and st the issued copy of its conv1.  WB protocol: a
+// commit only after a barrier that follows every wave's fragment load of the previous block.  On exit T holds
+// the next stage's input (or the features are written, LAST), and st holds the issued next-stage block (NEXTH
+// halves; committed by the caller, whose WB may differ).
+template <int C, int H, int LAST, int NEXTH>
+__device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)[KSteps<C>::N][C / 16],
+                                              const _Float16* __restrict__ hp, const Layout& L, int stage,
+                                              const float* bsc, const float* bsh, const float* bcb, int wave, int lane,
+                                              float* __restrict__ out, WStageT<kH2Threads>& st, _Float16* wb,
+                                              const _Float16* __restrict__ next_w) {
+  constexpr int CS = Pix<C>::CS, WP = H + 2, NT = C / 16, MT = H * H / 16;
+  constexpr int TPW = (MT + kH2Waves - 1) / kH2Waves, WH = kBlockHalves<C, C / 16>;
+  auto tpos = [&](int m, int ch0) { return tidx<C>((m / H + 1) * WP + (m % H) + 1, ch0); };
+  const int cl = 4 * (lane >> 4);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int i0 = stage * 5 + 1 + 2 * r, i1 = i0 + 1;
+    const int inext = r == 0 ? i1 + 1 : (stage + 1) * 5;
+    // epilogue constants are read from the tables after each conv's barrier (not held across the MFMA loop:
+    // 4 waves carry twice conv_kernel_h's tiles per wave, and the registers go to accumulators)
+    float b0[NT][4], s1[NT][4], h1[NT][4], b1[NT][4], s2[NT][4], h2[NT][4];
+    f32x4 acc[TPW][NT];
+    // ---- conv0: T -> T (relu(bn1(. + b0))) ----
+    conv_h2<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
+    __syncthreads();  // every wave has read T
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ch = nt * 16 + cl + k;
+        b0[nt][k] = bcb[i0 * 32 + ch];
+        s1[nt][k] = bsc[i1 * 32 + ch];
+        h1[nt][k] = bsh[i1 * 32 + ch];
+      }
+    conv_out_h<NT, TPW, MT, kH2Waves>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
+      const int nt = ch0 >> 4;
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = relu(fmaf(v[k] + b0[nt][k], s1[nt][k], h1[nt][k]));
+      *reinterpret_cast<h4*>(T + tpos(m, ch0)) = to_h4(o[0], o[1], o[2], o[3]);
+    });
+    st.template commit<WH>(wb);  // conv i1 (every wave loaded conv i0's fragments before the barrier above)
+    __syncthreads();
+    load_af_lds<C, NT>(wb, af, lane);
+    if (r == 0) {
+      st.template issue<WH>(hp + L.conv_h[i1 + 1]);  // block 1 conv0 (committed after the next barrier)
+    } else if constexpr (NEXTH > 0) {
+      st.template issue<NEXTH>(next_w);
+    }
+    // ---- conv1: T -> X += . + b1; T <- bn(X) (relu before a block) ----
+    conv_h2<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
+    __syncthreads();
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int ch = nt * 16 + cl + k;
+        b1[nt][k] = bcb[i1 * 32 + ch];
+        s2[nt][k] = (r == 1 && LAST) ? 0.f : bsc[inext * 32 + ch];
+        h2[nt][k] = (r == 1 && LAST) ? 0.f : bsh[inext * 32 + ch];
+      }
+    conv_out_h<NT, TPW, MT, kH2Waves>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
+      const int nt = ch0 >> 4;
+      const h4 xo = *reinterpret_cast<const h4*>(X + xidx<C>(m, ch0));
+      float xn[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xn[k] = (float)(_Float16)((v[k] + b1[nt][k]) + (float)xo[k]);
+      if (r == 0) {
+        *reinterpret_cast<h4*>(X + xidx<C>(m, ch0)) = to_h4(xn[0], xn[1], xn[2], xn[3]);
+        float t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = relu(fmaf(xn[k], s2[nt][k], h2[nt][k]));
+        *reinterpret_cast<h4*>(T + tpos(m, ch0)) = to_h4(t[0], t[1], t[2], t[3]);
+      } else if (!LAST) {
+        float t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = fmaf(xn[k], s2[nt][k], h2[nt][k]);
+        *reinterpret_cast<h4*>(T + tpos(m, ch0)) = to_h4(t[0], t[1], t[2], t[3]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[(ch0 + k) * H * H + m] = relu(xn[k]);  // flatten (C,H,W)
+      }
+    });
+    if (r == 0) st.template commit<WH>(wb);  // block 1 conv0 (af of conv1 loaded before the barrier above)
+    __syncthreads();
+    if (r == 0) {
+      load_af_lds<C, NT>(wb, af, lane);
+      st.template issue<WH>(hp + L.conv_h[i1 + 2]);  // block 1 conv1 (committed after the next barrier)
+    }
+  }
+}
+
+__global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kH2LdsBytes];
+  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+  const int lane = (slot / a.envs) * 8 + xcd, e = slot % a.envs;
+  if (lane >= a.n_lanes) return;
+  const int wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  const int64_t env = (int64_t)lane * a.envs + e;
+  const float* pk = a.pack + (int64_t)lane * a.pack_stride;
+  const _Float16* hp = a.hpack + (int64_t)lane * a.hpack_stride;
+  float* bsc = reinterpret_cast<float*>(smem);
+  float* bsh = bsc + kBnTab;
+  float* bcb = bsh + kBnTab;  // conv biases [15][32]
+  _Float16* R = reinterpret_cast<_Float16*>(smem + 3 * kBnTab * 4);  // the tables double as row -1's guard
+
+  // BN / bias tables (conv_kernel_h's folding), two entries per thread; the weight block of the first residual
+  // conv is issued now and committed in the first entry band's pool phase
+  h8 af3[KSteps<3>::N][1];
+  load_af<3, 1>(hp + L.conv_h[0], af3, ln);
+  WStageT<kH2Threads> st;
+  st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);
+#pragma unroll
+  for (int k = 0; k < (kBnTab + kH2Threads - 1) / kH2Threads; ++k) {
+    const int bi = threadIdx.x + k * kH2Threads;
+    if (bi >= kBnTab) break;
+    const int bidx = bi >> 5, bch = bi & 31;
+    const bool has_bn = bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
+    const bool has_cb = bch < (bidx < 5 ? 16 : 32);
+    float rm = 0.f, rv = 1.f, bnw = 0.f, bnb = 0.f;
+    if (has_bn) {
+      if (a.bn_mean) rm = a.bn_mean[L.bn_stat[bidx] + bch];
+      if (a.bn_var) rv = a.bn_var[L.bn_stat[bidx] + bch];
+      bnw = pk[L.bn_w[bidx] + bch];
+      bnb = pk[L.bn_b[bidx] + bch];
+    }
+    const float sc = has_bn ? bnw * (1.f / sqrtf(rv + kBnEps)) : 0.f;
+    bsc[bi] = sc;
+    bsh[bi] = has_bn ? bnb - rm * sc : 0.f;
+    bcb[bi] = has_cb ? pk[L.conv_b[bidx] + bch] : 0.f;
+  }
+  __syncthreads();
+  FDR_STAMP(a, 0);
+
+  // ---- stage 1: entry (3 -> 16 at 64 x 64, pooled to 32 x 32) in 8 bands ----
+  {
+    _Float16* FB[2] = {R + kH2FB0, R + kH2FB1};
+    frame_band_h2(FB[0], -1, a, env, e, bsc, bsh);
+    __syncthreads();
+    float bz[1][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bz[0][k] = bcb[0 * 32 + 4 * (ln >> 4) + k];
+    for (int bd = 0; bd < 64 / (kH2BR - 1); ++bd) {
+      entry_band_h2<3, 16, 64, kH2BR>(FB[bd & 1], 0, R + kH2S1, R + kH2X1, af3, bz, bd, wave, ln, [&]() {
+        if (bd == 0) st.commit<kBlockHalves<16, 1>>(R + kH2WBA);
+        if (bd + 1 < 64 / (kH2BR - 1)) frame_band_h2(FB[(bd + 1) & 1], (kH2BR - 1) * (bd + 1) - 1, a, env, e, bsc, bsh);
+      });
+    }
+  }
+  FDR_STAMP(a, 1);
+  // ---- stage 1 residual blocks (16 ch, 32 x 32) ----
+  {
+    h8 af[KSteps<16>::N][1];
+    load_af_lds<16, 1>(R + kH2WBA, af, ln);
+    st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[2]);
+    to_padded_h<16, 32, true, true, kH2Threads>(R + kH2X1, R, bsc + 1 * 32, bsh + 1 * 32);
+    __syncthreads();
+    res_blocks_h2<16, 32, 0, kBlockHalves<16, 2>>(R, R + kH2X1, af, hp, L, 0, bsc, bsh, bcb, wave, ln, nullptr, st,
+                                                  R + kH2WBA, hp + L.conv_h[5]);
+    st.commit<kBlockHalves<16, 2>>(R + kH2WBB);  // X1 is dead: the stage-2 entry block goes to WB_B
+    __syncthreads();
+  }
+  FDR_STAMP(a, 2);
+  // ---- stage 2: entry (16 -> 32 at 32 x 32, pooled to 16 x 16) in 4 bands; X2 into T1's consumed rows ----
+  {
+    h8 af[KSteps<16>::N][2];
+    load_af_lds<16, 2>(R + kH2WBB, af, ln);
+    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
+    float bz[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[5 * 32 + nt * 16 + 4 * (ln >> 4) + k];
+    for (int bd = 0; bd < 32 / (kH2BR - 1); ++bd) {
+      const int q0 = ((kH2BR - 1) * bd - 1) * 34;
+      entry_band_h2<16, 32, 32, kH2BR>(R + q0 * 16, q0, R + kH2S2, R, af, bz, bd, wave, ln, [&]() {
+        if (bd == 0) st.commit<kBlockHalves<32, 2>>(R + kH2WBB);
+      });
+    }
+  }
+  FDR_STAMP(a, 3);
+  // ---- stage 2 residual blocks (32 ch, 16 x 16) ----
+  {
+    h8 af[KSteps<32>::N][2];
+    load_af_lds<32, 2>(R + kH2WBB, af, ln);
+    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[7]);
+    to_padded_h<32, 16, true, true, kH2Threads>(R, R + kH2T2, bsc + 6 * 32, bsh + 6 * 32);
+    __syncthreads();
+    res_blocks_h2<32, 16, 0, kBlockHalves<32, 2>>(R + kH2T2, R, af, hp, L, 1, bsc, bsh, bcb, wave, ln, nullptr, st,
+                                                  R + kH2WBB, hp + L.conv_h[10]);
+    st.commit<kBlockHalves<32, 2>>(R + kH2WBB);
+    __syncthreads();
+  }
+  FDR_STAMP(a, 4);
+  // ---- stage 3: entry (32 -> 32 at 16 x 16, pooled to 8 x 8) in one band of 17 rows ----
+  {
+    h8 af[KSteps<32>::N][2];
+    load_af_lds<32, 2>(R + kH2WBB, af, ln);
+    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
+    float bz[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[10 * 32 + nt * 16 + 4 * (ln >> 4) + k];
+    entry_band_h2<32, 32, 16, 17>(R + kH2T2 - 18 * 32, -18, R + kH2S3, R, af, bz, 0, wave, ln, [&]() {
+      st.commit<kBlockHalves<32, 2>>(R + kH2WBB);
+    });
+  }
+  FDR_STAMP(a, 5);
+  // ---- stage 3 residual blocks (32 ch, 8 x 8) -> features ----
+  {
+    h8 af[KSteps<32>::N][2];
+    load_af_lds<32, 2>(R + kH2WBB, af, ln);
+    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[12]);
+    to_padded_h<32, 8, true, true, kH2Threads>(R, R + kH2T3, bsc + 11 * 32, bsh + 11 * 32);
+    __syncthreads();
+    res_blocks_h2<32, 8, 1, 0>(R + kH2T3, R, af, hp, L, 2, bsc, bsh, bcb, wave, ln, a.feat + env * kFeat, st,
+                               R + kH2WBB, nullptr);
+  }
+  FDR_STAMP(a, 6);
 }
 
 // ---- core (fc + LSTM + head) with f16 weights ------------------------------------------------------

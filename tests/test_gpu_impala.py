@@ -444,6 +444,53 @@ def test_fp16_pair_default_path_whole_episode_vs_f32_oracle(engine, table, core_
     assert amb <= 0.01 * L * E * T
 
 
+def test_conv_h2_bit_identical_to_conv_h(engine, table):
+    """conv_kernel_h2 (4 waves, 80 KiB LDS, two workgroups per CU; banded stage-1 / stage-2
+    entry convs, single-buffered residual blocks) computes every conv output with conv_kernel_h's fragments, K
+    order and f32 epilogues, so the two kernels' outputs are bitwise equal: forward features / probs / LSTM state
+    (13 envs, ragged over the 8 XCD slots), a recorded fp16 pair rollout with the entropy replay, and strategies."""
+    A = 4
+    theta_np = _theta(A)
+    theta = torch.tensor(theta_np, device="cuda")
+    spec = engine.ImpalaSpec(A, fp16=True)
+    g = torch.Generator().manual_seed(3)
+    n = 13
+    frames = (torch.rand(n, 3, 64, 64, generator=g) * 255).floor().cuda()
+    reward = torch.randn(n, generator=g).cuda()
+    nb = oi.num_bn()
+    rm = torch.randn(nb, generator=g).mul(0.1).cuda()
+    rv = torch.rand(nb, generator=g).add(0.5).cuda()
+    idx = np.repeat(np.array([77, 2_000_000, 3_000_000], np.int64), 2)
+    sign = np.tile(np.array([1, -1], np.int8), 3)
+    lanes = engine.lanes_desc(theta, 0, torch.tensor(table, device="cuda"), torch.tensor(idx, device="cuda"),
+                              torch.tensor(sign, device="cuda"), 0.02)
+    rspec = engine.ImpalaSpec(A, 4, 20, entropy=True, env_seed=5, fp16=True, pairs=True)
+    res = {}
+    ctx = engine.context()
+    import os
+    prior = os.environ.get("FDR_CONV_H2", "0") != "0"   # the default context's setting (FDR_CONV_H2)
+    try:
+        for on in (False, True):
+            ctx.set_conv_h2(on)
+            h = torch.zeros(n, 256, device="cuda")
+            c = torch.zeros(n, 256, device="cuda")
+            fw = []
+            for t in range(3):
+                probs, feat = engine.impala_forward(spec, theta, frames.roll(t, 0), h, c, reward=reward, bn_mean=rm,
+                                                    bn_var=rv, feat=True)
+                fw += [probs.clone(), feat.clone(), h.clone(), c.clone()]
+            ro = engine.impala_rollout(rspec, lanes, len(idx), 11, record=True, bn_mean=rm, bn_var=rv)
+            st = engine.impala_strategies(spec, lanes, len(idx), frames[:5], reward=reward[:5], bn_mean=rm, bn_var=rv)
+            torch.cuda.synchronize()
+            res[on] = [x.cpu().numpy() for x in fw] + [getattr(ro, f).cpu().numpy() for f in
+                                                       ("actions", "probs", "reward", "entropy")] + [st.cpu().numpy()]
+    finally:
+        ctx.set_conv_h2(prior)
+    assert np.abs(res[True][1]).max() > 0 and np.all(np.isfinite(res[True][1]))
+    for a, b in zip(res[False], res[True]):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("fp16,pairs", [(False, False), (False, True), (True, False), (True, True)])
 def test_full_size_rollout_properties(engine, fp16, pairs):
     """BASELINE configs 4/5 at full size (1024 lanes x 4 envs x T = 1000, A = 6 / 4): bitwise reproducible (a
