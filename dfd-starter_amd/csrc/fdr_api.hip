@@ -117,8 +117,8 @@ Context& default_context() {
                                                     : strcmp(e, "pair") == 0 ? FDR_ROLLOUT_PAIR : FDR_ROLLOUT_AUTO;
     const char* m = getenv("FDR_CORE_MFMA");  // A/B switch: "0" selects the VALU fp16 pair core
     c->core_mfma = !(m && strcmp(m, "0") == 0);
-    const char* h2 = getenv("FDR_CONV_H2");  // A/B switch: "1" / "0" selects the fp16 conv kernel
-    if (h2) c->conv_h2 = strcmp(h2, "0") != 0;
+    const char* h2 = getenv("FDR_CONV_H2");  // A/B switch: "0" selects conv_kernel_h (one workgroup per CU)
+    c->conv_h2 = !(h2 && strcmp(h2, "0") == 0);
     return c;
   }();
   return *d;

@@ -19,6 +19,7 @@ namespace impala {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // pixel stride (halves) of an MFMA input image: unpadded (the chunk swizzle below spreads the banks); the
@@ -264,6 +265,24 @@ __device__ __forceinline__ h4 to_h4(float a, float b, float c, float d) {
   return h4{(_Float16)a, (_Float16)b, (_Float16)c, (_Float16)d};
 }
 
+// fmaf((float)x.lo / x.hi, s, t) as one v_fma_mix_f32 (the f16 operand is converted inside the instruction, one
+// rounding -- fmaf's value; the compiler picks the same instruction for that pattern when it does not pair the
+// fmas into v_pk_fma_f32, which then needs a separate conversion per element)
+__device__ __forceinline__ float fma_mix_lo(h2 x, float s, float t) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(x), "v"(s), "v"(t));
+  return r;
+}
+__device__ __forceinline__ float fma_mix_hi(h2 x, float s, float t) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(x), "v"(s), "v"(t));
+  return r;
+}
+__device__ __forceinline__ h2 lo2(h4 v) { return __builtin_shufflevector(v, v, 0, 1); }
+__device__ __forceinline__ h2 hi2(h4 v) { return __builtin_shufflevector(v, v, 2, 3); }
+// ReLU after the f16 rounding (two v_pk_max_f16): the value of rounding relu(x) (a negative x gives -0 or +0)
+__device__ __forceinline__ h4 relu_h4(h4 v) { return __builtin_elementwise_max(v, h4{0, 0, 0, 0}); }
+
 // T <- BN(X) (optionally ReLU): X [H][H][C] f16 -> padded image [H+2][H+2][CS]; BORDER: zero border.
 template <int C, int H, bool RELU, bool BORDER, int NTH = kHThreads>
 __device__ __forceinline__ void to_padded_h(const _Float16* X, _Float16* T, const float* sc, const float* sh) {
@@ -283,14 +302,17 @@ __device__ __forceinline__ void to_padded_h(const _Float16* X, _Float16* T, cons
     if (NP % PPI != 0 && pix >= NP) break;
     const int y = pix / H, x = pix % H;
     const h8 v = *reinterpret_cast<const h8*>(X + xidx<C>(pix, 8 * cg));
-    h8 o;
+    const h2 p[4] = {__builtin_shufflevector(v, v, 0, 1), __builtin_shufflevector(v, v, 2, 3),
+                     __builtin_shufflevector(v, v, 4, 5), __builtin_shufflevector(v, v, 6, 7)};
+    h4 o[2];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float f = fmaf((float)v[k], scv[k], shv[k]);
-      if (RELU) f = relu(f);
-      o[k] = (_Float16)f;
+    for (int hq = 0; hq < 2; ++hq) {
+      const int k = 4 * hq;
+      o[hq] = to_h4(fma_mix_lo(p[2 * hq], scv[k], shv[k]), fma_mix_hi(p[2 * hq], scv[k + 1], shv[k + 1]),
+                    fma_mix_lo(p[2 * hq + 1], scv[k + 2], shv[k + 2]), fma_mix_hi(p[2 * hq + 1], scv[k + 3], shv[k + 3]));
+      if (RELU) o[hq] = relu_h4(o[hq]);
     }
-    *reinterpret_cast<h8*>(T + tidx<C>((y + 1) * WP + x + 1, 8 * cg)) = o;
+    *reinterpret_cast<h8*>(T + tidx<C>((y + 1) * WP + x + 1, 8 * cg)) = __builtin_shufflevector(o[0], o[1], 0, 1, 2, 3, 4, 5, 6, 7);
   }
   if (BORDER) {
     const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -750,42 +772,65 @@ __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSte
   }
 }
 
-// padded frame rows [p0, p0 + kH2FBRows) of this env (policies/impala.py:147 frame / 255, then BN2d(3)) into FB
-// [rows][66][4] f16 -- zero outside the 64 x 64 image and in the 4th channel slot; conv_kernel_h's values.
-__device__ __forceinline__ void frame_band_h2(_Float16* FB, int p0, const StepArgs& a, int64_t env, int e,
-                                              const float* bsc, const float* bsh) {
-  for (int i = threadIdx.x; i < kH2FBRows * 8; i += kH2Threads) {
-    const int r = i >> 3, w = i & 7, y = p0 + r - 1;  // image row of padded row p0 + r
-    float fv[3][8];
-    const bool in = y >= 0 && y < 64;
-    if (in && a.frames) {
-      const float* fr = a.frames + (a.shared_frames ? (int64_t)e : env) * kFramePix;
+// x / 255 for an integer-valued x in [0, 255], bit-identical to the IEEE division (checked exhaustively: q = x r,
+// one fma residual correction): the synthetic frame's bytes, without the ~10-instruction division sequence.
+__device__ __forceinline__ float div255_byte(float x) {
+  constexpr float r = 1.0f / 255.0f;
+  const float q = x * r;
+  return fmaf(fmaf(-q, 255.0f, x), r, q);
+}
+
+// padded frame rows [p0 + r0, p0 + kH2FBRows) of this env (policies/impala.py:147 frame / 255, then BN2d(3) with
+// this thread's per-channel scale sc / shift sh) into FB [rows][66][4] f16 -- zero outside the 64 x 64 image and
+// in the 4th channel slot; conv_kernel_h's values.  Work item = (row, 8-pixel chunk, channel): one hash word (or
+// 8 frame floats) -> 8 halves of one channel, spread over all 256 threads.  r0 = 3: the band's first three rows
+// are the previous band's last three (prev), copied.
+struct FrameBn {  // BN2d(3) of the frame: per-channel scale / shift (scalars: the struct is passed by value)
+  float s0, s1, s2, h0, h1, h2;
+};
+__device__ __forceinline__ void frame_band_h2(_Float16* FB, const _Float16* prev, int r0, int p0, const StepArgs& a,
+                                              int64_t env, int e, FrameBn bn) {
+  const int nitem = (kH2FBRows - r0) * 24;
+  for (int i = threadIdx.x; i < nitem; i += kH2Threads) {
+    const int c = i % 3, w = (i / 3) & 7, r = r0 + i / 24, y = p0 + r - 1;  // image row of padded row p0 + r
+    _Float16 o[8];
+    if (y >= 0 && y < 64) {
+      float fv[8];
+      if (a.frames) {
+        const float* fr = a.frames + (a.shared_frames ? (int64_t)e : env) * kFramePix + c * 4096 + y * 64 + w * 8;
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) fv[c][j] = fr[c * 4096 + y * 64 + w * 8 + j];
-    } else if (in) {
-      const uint64_t gid = (uint64_t)(a.lane_offset * a.envs + env);
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
+        for (int j = 0; j < 8; ++j) fv[j] = fr[j] / 255.0f;
+      } else {
+        const uint64_t gid = (uint64_t)(a.lane_offset * a.envs + env);
         const uint64_t word = (uint64_t)(c * 512 + y * 8 + w);
         const uint64_t hb = mix64(a.fkey + ((gid << 32) | ((uint64_t)a.t << 11) | word) * kGolden);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) fv[c][j] = (float)((uint32_t)(hb >> (8 * j)) & 255u);
+        for (int j = 0; j < 8; ++j) fv[j] = div255_byte((float)((uint32_t)(hb >> (8 * j)) & 255u));
       }
+      const float s_ = c == 0 ? bn.s0 : (c == 1 ? bn.s1 : bn.s2), h_ = c == 0 ? bn.h0 : (c == 1 ? bn.h1 : bn.h2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (_Float16)fmaf(fv[j], s_, h_);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (_Float16)0.f;
     }
+    _Float16* d = FB + (r * 66 + 1 + w * 8) * 4 + c;
+    if (c == 2) {  // channel 2 and the zero 4th slot in one 4-byte store
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      h4 o = {0, 0, 0, 0};
-      if (in) {
+      for (int j = 0; j < 8; ++j) *reinterpret_cast<h2*>(d + 4 * j) = h2{o[j], (_Float16)0.f};
+    } else {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) o[c] = (_Float16)fmaf(fv[c][j] / 255.0f, bsc[c], bsh[c]);
-      }
-      *reinterpret_cast<h4*>(FB + (r * 66 + 1 + w * 8 + j) * 4) = o;
+      for (int j = 0; j < 8; ++j) d[4 * j] = o[j];
     }
   }
-  for (int i = threadIdx.x; i < kH2FBRows * 2; i += kH2Threads)  // the two pad columns of every row
-    *reinterpret_cast<h4*>(FB + ((i >> 1) * 66 + (i & 1) * 65) * 4) = h4{0, 0, 0, 0};
+  // the two pad columns of every generated row, and the overlap rows
+  const int npad = (kH2FBRows - r0) * 2, ncopy = r0 * 66 * 4 / 8;
+  for (int i = kH2Threads - 1 - threadIdx.x; i < npad + ncopy; i += kH2Threads) {
+    if (i < npad)
+      *reinterpret_cast<h4*>(FB + ((r0 + (i >> 1)) * 66 + (i & 1) * 65) * 4) = h4{0, 0, 0, 0};
+    else
+      reinterpret_cast<uint4*>(FB)[i - npad] = reinterpret_cast<const uint4*>(prev + (kH2FBRows - r0) * 66 * 4)[i - npad];
+  }
 }
 
 // One entry band: conv rows [(BR-1) b - 1, +BR) of the padded input Tin (its row 0 = padded row (BR-1) b - 1,
@@ -795,7 +840,7 @@ __device__ __forceinline__ void frame_band_h2(_Float16* FB, int p0, const StepAr
 template <int CIN, int COUT, int H, int BR, class Between>
 __device__ __forceinline__ void entry_band_h2(const _Float16* Tin, int qoff, _Float16* S, _Float16* X,
                                               const h8 (&af)[KSteps<CIN>::N][COUT / 16], const float (&bz)[COUT / 16][4],
-                                              int b, int wave, int lane, Between&& between) {
+                                              int b, int wave, int lane, const StepArgs& a, int stamp, Between&& between) {
   constexpr int CS = Pix<CIN>::CS, WP = H + 2, NT = COUT / 16, MT = BR * H / 16;
   constexpr int TPW = (MT + kH2Waves - 1) / kH2Waves, HO = H / 2, PRB = (BR - 1) / 2, G = COUT / 8;
   f32x4 acc[TPW][NT];
@@ -808,6 +853,7 @@ __device__ __forceinline__ void entry_band_h2(const _Float16* Tin, int qoff, _Fl
         neg ? to_h4(ninf, ninf, ninf, ninf) : to_h4(v[0] + bz[nt][0], v[1] + bz[nt][1], v[2] + bz[nt][2], v[3] + bz[nt][3]);
   });
   __syncthreads();
+  FDR_STAMP(a, stamp);
   between();
   constexpr int NI = PRB * HO * G, IT = (NI + kH2Threads - 1) / kH2Threads;
 #pragma unroll
@@ -831,6 +877,7 @@ __device__ __forceinline__ void entry_band_h2(const _Float16* Tin, int qoff, _Fl
     *reinterpret_cast<h8*>(X + xidx<COUT>((PRB * b + pr) * HO + px, 8 * cg)) = mx;
   }
   __syncthreads();
+  FDR_STAMP(a, stamp + 1);
 }
 
 // Two residual blocks, single-buffered (conv -> accumulators -> barrier -> in-place epilogue); the arithmetic
@@ -843,22 +890,46 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
                                               const _Float16* __restrict__ hp, const Layout& L, int stage,
                                               const float* bsc, const float* bsh, const float* bcb, int wave, int lane,
                                               float* __restrict__ out, WStageT<kH2Threads>& st, _Float16* wb,
-                                              const _Float16* __restrict__ next_w) {
-  constexpr int CS = Pix<C>::CS, WP = H + 2, NT = C / 16, MT = H * H / 16;
-  constexpr int TPW = (MT + kH2Waves - 1) / kH2Waves, WH = kBlockHalves<C, C / 16>;
-  auto tpos = [&](int m, int ch0) { return tidx<C>((m / H + 1) * WP + (m % H) + 1, ch0); };
-  const int cl = 4 * (lane >> 4);
+                                              const _Float16* __restrict__ next_w, const StepArgs& a, int stamp) {
+  constexpr int CS = Pix<C>::CS, WP = H + 2, NT = C / 16, MT = H * H / 16, NW = kH2Waves;
+  constexpr int TPW = (MT + NW - 1) / NW, WH = kBlockHalves<C, C / 16>;
+  // Epilogue addresses: tile i's pixels are tile 0's + 16 NW i (X, S: the chunk swizzle is unchanged by that
+  // step) and padded pixel + DQ i (T: the swizzle flips by tflip(i), conv_h2's step) -- per-lane bases + immediates.
+  constexpr int DQ = H >= 16 ? (NW / (H / 16)) * WP : NW * (16 / H) * WP;
+  static_assert((C == 16 && DQ % 4 == 0 && (16 * NW) % 16 == 0) || (C == 32 && DQ % 8 == 0 && (16 * NW) % 16 == 0),
+                "epilogue address steps");
+  auto tflip = [](int i) { return C == 16 ? ((DQ * i) >> 2) & 1 : 0; };
+  const int cl = 4 * (lane >> 4), m0 = wave * 16 + (lane & 15), q0 = (m0 / H + 1) * WP + (m0 % H) + 1;
+  int xb[NT], tb[NT][2];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int ch0 = nt * 16 + cl;
+    xb[nt] = xidx<C>(m0, ch0);
+    tb[nt][0] = tidx<C>(q0, ch0);
+    tb[nt][1] = q0 * CS + ((((ch0 >> 3) ^ tsw<C>(q0)) ^ 1) << 3) + (ch0 & 7);
+  }
+  // f(i, nt, x offset, T offset, m, v) over this wave's live tiles
+  auto epilogue = [&](const f32x4 (&acc)[TPW][NT], auto&& f) {
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) {
+      if (!(TPW * NW == MT || wave + NW * i < MT)) continue;  // wave-uniform
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        f(nt, xb[nt] + 16 * NW * i * C, tb[nt][tflip(i)] + DQ * i * CS, m0 + 16 * NW * i, acc[i][nt]);
+    }
+  };
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int i0 = stage * 5 + 1 + 2 * r, i1 = i0 + 1;
     const int inext = r == 0 ? i1 + 1 : (stage + 1) * 5;
     // epilogue constants are read from the tables after each conv's barrier (not held across the MFMA loop:
     // 4 waves carry twice conv_kernel_h's tiles per wave, and the registers go to accumulators)
-    float b0[NT][4], s1[NT][4], h1[NT][4], b1[NT][4], s2[NT][4], h2[NT][4];
+    float b0[NT][4], s1[NT][4], t1[NT][4], b1[NT][4], s2[NT][4], t2[NT][4];
     f32x4 acc[TPW][NT];
     // ---- conv0: T -> T (relu(bn1(. + b0))) ----
     conv_h2<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
     __syncthreads();  // every wave has read T
+    FDR_STAMP(a, stamp + 4 * r);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -866,17 +937,17 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
         const int ch = nt * 16 + cl + k;
         b0[nt][k] = bcb[i0 * 32 + ch];
         s1[nt][k] = bsc[i1 * 32 + ch];
-        h1[nt][k] = bsh[i1 * 32 + ch];
+        t1[nt][k] = bsh[i1 * 32 + ch];
       }
-    conv_out_h<NT, TPW, MT, kH2Waves>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
-      const int nt = ch0 >> 4;
+    epilogue(acc, [&](int nt, int, int to, int, f32x4 v) {
       float o[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = relu(fmaf(v[k] + b0[nt][k], s1[nt][k], h1[nt][k]));
-      *reinterpret_cast<h4*>(T + tpos(m, ch0)) = to_h4(o[0], o[1], o[2], o[3]);
+      for (int k = 0; k < 4; ++k) o[k] = fmaf(v[k] + b0[nt][k], s1[nt][k], t1[nt][k]);
+      *reinterpret_cast<h4*>(T + to) = relu_h4(to_h4(o[0], o[1], o[2], o[3]));
     });
     st.template commit<WH>(wb);  // conv i1 (every wave loaded conv i0's fragments before the barrier above)
     __syncthreads();
+    FDR_STAMP(a, stamp + 4 * r + 1);
     load_af_lds<C, NT>(wb, af, lane);
     if (r == 0) {
       st.template issue<WH>(hp + L.conv_h[i1 + 1]);  // block 1 conv0 (committed after the next barrier)
@@ -886,6 +957,7 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
     // ---- conv1: T -> X += . + b1; T <- bn(X) (relu before a block) ----
     conv_h2<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
     __syncthreads();
+    FDR_STAMP(a, stamp + 4 * r + 2);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -893,32 +965,28 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
         const int ch = nt * 16 + cl + k;
         b1[nt][k] = bcb[i1 * 32 + ch];
         s2[nt][k] = (r == 1 && LAST) ? 0.f : bsc[inext * 32 + ch];
-        h2[nt][k] = (r == 1 && LAST) ? 0.f : bsh[inext * 32 + ch];
+        t2[nt][k] = (r == 1 && LAST) ? 0.f : bsh[inext * 32 + ch];
       }
-    conv_out_h<NT, TPW, MT, kH2Waves>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
-      const int nt = ch0 >> 4;
-      const h4 xo = *reinterpret_cast<const h4*>(X + xidx<C>(m, ch0));
-      float xn[4];
+    epilogue(acc, [&](int nt, int xo_, int to, int m, f32x4 v) {
+      const h4 xo = *reinterpret_cast<const h4*>(X + xo_);
+      // x' = f16((v + b1) + x) and the next BN of x' on v_fma_mix_f32 (x * 1 + s is the f32 add, exact)
+      const h2 xl = lo2(xo), xh = hi2(xo);
+      const h4 xn = to_h4(fma_mix_lo(xl, 1.f, v[0] + b1[nt][0]), fma_mix_hi(xl, 1.f, v[1] + b1[nt][1]),
+                          fma_mix_lo(xh, 1.f, v[2] + b1[nt][2]), fma_mix_hi(xh, 1.f, v[3] + b1[nt][3]));
+      if (r == 1 && LAST) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) xn[k] = (float)(_Float16)((v[k] + b1[nt][k]) + (float)xo[k]);
-      if (r == 0) {
-        *reinterpret_cast<h4*>(X + xidx<C>(m, ch0)) = to_h4(xn[0], xn[1], xn[2], xn[3]);
-        float t[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) t[k] = relu(fmaf(xn[k], s2[nt][k], h2[nt][k]));
-        *reinterpret_cast<h4*>(T + tpos(m, ch0)) = to_h4(t[0], t[1], t[2], t[3]);
-      } else if (!LAST) {
-        float t[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) t[k] = fmaf(xn[k], s2[nt][k], h2[nt][k]);
-        *reinterpret_cast<h4*>(T + tpos(m, ch0)) = to_h4(t[0], t[1], t[2], t[3]);
+        for (int k = 0; k < 4; ++k) out[(nt * 16 + cl + k) * H * H + m] = relu((float)xn[k]);  // flatten (C,H,W)
       } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) out[(ch0 + k) * H * H + m] = relu(xn[k]);  // flatten (C,H,W)
+        if (r == 0) *reinterpret_cast<h4*>(X + xo_) = xn;
+        const h2 nl = lo2(xn), nh = hi2(xn);
+        const h4 t = to_h4(fma_mix_lo(nl, s2[nt][0], t2[nt][0]), fma_mix_hi(nl, s2[nt][1], t2[nt][1]),
+                           fma_mix_lo(nh, s2[nt][2], t2[nt][2]), fma_mix_hi(nh, s2[nt][3], t2[nt][3]));
+        *reinterpret_cast<h4*>(T + to) = r == 0 ? relu_h4(t) : t;
       }
     });
     if (r == 0) st.template commit<WH>(wb);  // block 1 conv0 (af of conv1 loaded before the barrier above)
     __syncthreads();
+    FDR_STAMP(a, stamp + 4 * r + 3);
     if (r == 0) {
       load_af_lds<C, NT>(wb, af, lane);
       st.template issue<WH>(hp + L.conv_h[i1 + 2]);  // block 1 conv1 (committed after the next barrier)
@@ -931,6 +999,7 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
   const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
   const int lane = (slot / a.envs) * 8 + xcd, e = slot % a.envs;
   if (lane >= a.n_lanes) return;
+  FDR_STAMP(a, 0);
   const int wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int64_t env = (int64_t)lane * a.envs + e;
   const float* pk = a.pack + (int64_t)lane * a.pack_stride;
@@ -940,50 +1009,65 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
   float* bcb = bsh + kBnTab;  // conv biases [15][32]
   _Float16* R = reinterpret_cast<_Float16*>(smem + 3 * kBnTab * 4);  // the tables double as row -1's guard
 
-  // BN / bias tables (conv_kernel_h's folding), two entries per thread; the weight block of the first residual
-  // conv is issued now and committed in the first entry band's pool phase
+  // BN / bias tables (conv_kernel_h's folding), two entries per thread: their inputs are loaded first, the first
+  // frame band (which folds BN2d(3) per thread from the same inputs) covers the latency, then the tables are
+  // written.  The weight block of the first residual conv is issued now and committed in the first pool phase.
+  constexpr int kTabIt = (kBnTab + kH2Threads - 1) / kH2Threads;
+  float rm[kTabIt], rv[kTabIt], bnw[kTabIt], bnb[kTabIt], cbv[kTabIt];
+#pragma unroll
+  for (int k = 0; k < kTabIt; ++k) {
+    const int bi = threadIdx.x + k * kH2Threads, bidx = bi >> 5, bch = bi & 31;
+    const bool has_bn = bi < kBnTab && bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
+    const bool has_cb = bi < kBnTab && bch < (bidx < 5 ? 16 : 32);
+    rm[k] = 0.f, rv[k] = 1.f, bnw[k] = 0.f, bnb[k] = 0.f, cbv[k] = 0.f;
+    if (has_bn) {
+      if (a.bn_mean) rm[k] = a.bn_mean[L.bn_stat[bidx] + bch];
+      if (a.bn_var) rv[k] = a.bn_var[L.bn_stat[bidx] + bch];
+      bnw[k] = pk[L.bn_w[bidx] + bch];
+      bnb[k] = pk[L.bn_b[bidx] + bch];
+    }
+    if (has_cb) cbv[k] = pk[L.conv_b[bidx] + bch];
+  }
   h8 af3[KSteps<3>::N][1];
   load_af<3, 1>(hp + L.conv_h[0], af3, ln);
   WStageT<kH2Threads> st;
   st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);
+  float fsc[3], fsh[3];  // BN2d(3) of the frame, per thread (table entries 0..2)
 #pragma unroll
-  for (int k = 0; k < (kBnTab + kH2Threads - 1) / kH2Threads; ++k) {
-    const int bi = threadIdx.x + k * kH2Threads;
+  for (int c = 0; c < 3; ++c) {
+    const float m = a.bn_mean ? a.bn_mean[L.bn_stat[0] + c] : 0.f, v = a.bn_var ? a.bn_var[L.bn_stat[0] + c] : 1.f;
+    fsc[c] = pk[L.bn_w[0] + c] * (1.f / sqrtf(v + kBnEps));
+    fsh[c] = pk[L.bn_b[0] + c] - m * fsc[c];
+  }
+  const FrameBn fbn{fsc[0], fsc[1], fsc[2], fsh[0], fsh[1], fsh[2]};
+  auto FB = [&](int k) { return R + ((k & 1) ? kH2FB1 : kH2FB0); };  // the two frame-band buffers
+  frame_band_h2(FB(0), nullptr, 0, -1, a, env, e, fbn);
+#pragma unroll
+  for (int k = 0; k < kTabIt; ++k) {
+    const int bi = threadIdx.x + k * kH2Threads, bidx = bi >> 5, bch = bi & 31;
     if (bi >= kBnTab) break;
-    const int bidx = bi >> 5, bch = bi & 31;
     const bool has_bn = bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
-    const bool has_cb = bch < (bidx < 5 ? 16 : 32);
-    float rm = 0.f, rv = 1.f, bnw = 0.f, bnb = 0.f;
-    if (has_bn) {
-      if (a.bn_mean) rm = a.bn_mean[L.bn_stat[bidx] + bch];
-      if (a.bn_var) rv = a.bn_var[L.bn_stat[bidx] + bch];
-      bnw = pk[L.bn_w[bidx] + bch];
-      bnb = pk[L.bn_b[bidx] + bch];
-    }
-    const float sc = has_bn ? bnw * (1.f / sqrtf(rv + kBnEps)) : 0.f;
+    const float sc = has_bn ? bnw[k] * (1.f / sqrtf(rv[k] + kBnEps)) : 0.f;
     bsc[bi] = sc;
-    bsh[bi] = has_bn ? bnb - rm * sc : 0.f;
-    bcb[bi] = has_cb ? pk[L.conv_b[bidx] + bch] : 0.f;
+    bsh[bi] = has_bn ? bnb[k] - rm[k] * sc : 0.f;
+    bcb[bi] = cbv[k];
   }
   __syncthreads();
-  FDR_STAMP(a, 0);
+  FDR_STAMP(a, 1);
 
   // ---- stage 1: entry (3 -> 16 at 64 x 64, pooled to 32 x 32) in 8 bands ----
   {
-    _Float16* FB[2] = {R + kH2FB0, R + kH2FB1};
-    frame_band_h2(FB[0], -1, a, env, e, bsc, bsh);
-    __syncthreads();
     float bz[1][4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) bz[0][k] = bcb[0 * 32 + 4 * (ln >> 4) + k];
     for (int bd = 0; bd < 64 / (kH2BR - 1); ++bd) {
-      entry_band_h2<3, 16, 64, kH2BR>(FB[bd & 1], 0, R + kH2S1, R + kH2X1, af3, bz, bd, wave, ln, [&]() {
+      entry_band_h2<3, 16, 64, kH2BR>(FB(bd), 0, R + kH2S1, R + kH2X1, af3, bz, bd, wave, ln, a, 2 + 2 * bd, [&]() {
         if (bd == 0) st.commit<kBlockHalves<16, 1>>(R + kH2WBA);
-        if (bd + 1 < 64 / (kH2BR - 1)) frame_band_h2(FB[(bd + 1) & 1], (kH2BR - 1) * (bd + 1) - 1, a, env, e, bsc, bsh);
+        if (bd + 1 < 64 / (kH2BR - 1))
+          frame_band_h2(FB(bd + 1), FB(bd), 3, (kH2BR - 1) * (bd + 1) - 1, a, env, e, fbn);
       });
     }
   }
-  FDR_STAMP(a, 1);
   // ---- stage 1 residual blocks (16 ch, 32 x 32) ----
   {
     h8 af[KSteps<16>::N][1];
@@ -991,12 +1075,12 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
     st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[2]);
     to_padded_h<16, 32, true, true, kH2Threads>(R + kH2X1, R, bsc + 1 * 32, bsh + 1 * 32);
     __syncthreads();
+    FDR_STAMP(a, 18);
     res_blocks_h2<16, 32, 0, kBlockHalves<16, 2>>(R, R + kH2X1, af, hp, L, 0, bsc, bsh, bcb, wave, ln, nullptr, st,
-                                                  R + kH2WBA, hp + L.conv_h[5]);
+                                                  R + kH2WBA, hp + L.conv_h[5], a, 19);
     st.commit<kBlockHalves<16, 2>>(R + kH2WBB);  // X1 is dead: the stage-2 entry block goes to WB_B
     __syncthreads();
   }
-  FDR_STAMP(a, 2);
   // ---- stage 2: entry (16 -> 32 at 32 x 32, pooled to 16 x 16) in 4 bands; X2 into T1's consumed rows ----
   {
     h8 af[KSteps<16>::N][2];
@@ -1009,12 +1093,11 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
       for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[5 * 32 + nt * 16 + 4 * (ln >> 4) + k];
     for (int bd = 0; bd < 32 / (kH2BR - 1); ++bd) {
       const int q0 = ((kH2BR - 1) * bd - 1) * 34;
-      entry_band_h2<16, 32, 32, kH2BR>(R + q0 * 16, q0, R + kH2S2, R, af, bz, bd, wave, ln, [&]() {
+      entry_band_h2<16, 32, 32, kH2BR>(R + q0 * 16, q0, R + kH2S2, R, af, bz, bd, wave, ln, a, 28 + 2 * bd, [&]() {
         if (bd == 0) st.commit<kBlockHalves<32, 2>>(R + kH2WBB);
       });
     }
   }
-  FDR_STAMP(a, 3);
   // ---- stage 2 residual blocks (32 ch, 16 x 16) ----
   {
     h8 af[KSteps<32>::N][2];
@@ -1022,12 +1105,12 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
     st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[7]);
     to_padded_h<32, 16, true, true, kH2Threads>(R, R + kH2T2, bsc + 6 * 32, bsh + 6 * 32);
     __syncthreads();
+    FDR_STAMP(a, 36);
     res_blocks_h2<32, 16, 0, kBlockHalves<32, 2>>(R + kH2T2, R, af, hp, L, 1, bsc, bsh, bcb, wave, ln, nullptr, st,
-                                                  R + kH2WBB, hp + L.conv_h[10]);
+                                                  R + kH2WBB, hp + L.conv_h[10], a, 37);
     st.commit<kBlockHalves<32, 2>>(R + kH2WBB);
     __syncthreads();
   }
-  FDR_STAMP(a, 4);
   // ---- stage 3: entry (32 -> 32 at 16 x 16, pooled to 8 x 8) in one band of 17 rows ----
   {
     h8 af[KSteps<32>::N][2];
@@ -1038,11 +1121,10 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[10 * 32 + nt * 16 + 4 * (ln >> 4) + k];
-    entry_band_h2<32, 32, 16, 17>(R + kH2T2 - 18 * 32, -18, R + kH2S3, R, af, bz, 0, wave, ln, [&]() {
+    entry_band_h2<32, 32, 16, 17>(R + kH2T2 - 18 * 32, -18, R + kH2S3, R, af, bz, 0, wave, ln, a, 45, [&]() {
       st.commit<kBlockHalves<32, 2>>(R + kH2WBB);
     });
   }
-  FDR_STAMP(a, 5);
   // ---- stage 3 residual blocks (32 ch, 8 x 8) -> features ----
   {
     h8 af[KSteps<32>::N][2];
@@ -1050,10 +1132,10 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
     st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[12]);
     to_padded_h<32, 8, true, true, kH2Threads>(R, R + kH2T3, bsc + 11 * 32, bsh + 11 * 32);
     __syncthreads();
+    FDR_STAMP(a, 47);
     res_blocks_h2<32, 8, 1, 0>(R + kH2T3, R, af, hp, L, 2, bsc, bsh, bcb, wave, ln, a.feat + env * kFeat, st,
-                               R + kH2WBB, nullptr);
+                               R + kH2WBB, nullptr, a, 48);
   }
-  FDR_STAMP(a, 6);
 }
 
 // ---- core (fc + LSTM + head) with f16 weights ------------------------------------------------------

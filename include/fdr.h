@@ -105,7 +105,8 @@ int fdr_ctx_set_replay_gemm(fdr_ctx* ctx, int32_t on);     /* see fdr_impala_set
    (activations rounded to f16); 0 = the VALU form (w = f16(theta) + s f16(sigma eps) formed per element) */
 int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on);
 /* fp16 Impala conv stack (rollout, forward, strategies): 1 = conv_kernel_h2 (4 waves, 80 KiB LDS, two
-   workgroups per CU), 0 = conv_kernel_h (8 waves, 145 KiB LDS); identical features.  Default: FDR_CONV_H2 */
+   workgroups per CU; the default), 0 = conv_kernel_h (8 waves, 145 KiB LDS); identical features.  Default context:
+   1 unless FDR_CONV_H2=0 */
 int fdr_ctx_set_conv_h2(fdr_ctx* ctx, int32_t on);
 int fdr_ctx_impala_profile(fdr_ctx* ctx, int32_t enable);  /* see fdr_impala_profile */
 int fdr_ctx_impala_profile_read(fdr_ctx* ctx, double* ms);

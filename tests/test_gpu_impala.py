@@ -468,7 +468,7 @@ def test_conv_h2_bit_identical_to_conv_h(engine, table):
     res = {}
     ctx = engine.context()
     import os
-    prior = os.environ.get("FDR_CONV_H2", "0") != "0"   # the default context's setting (FDR_CONV_H2)
+    prior = os.environ.get("FDR_CONV_H2", "1") != "0"   # the default context's setting (FDR_CONV_H2)
     try:
         for on in (False, True):
             ctx.set_conv_h2(on)
