@@ -118,7 +118,7 @@ Context& default_context() {
     const char* m = getenv("FDR_CORE_MFMA");  // A/B switch: "0" selects the VALU fp16 pair core
     c->core_mfma = !(m && strcmp(m, "0") == 0);
     const char* h2 = getenv("FDR_CONV_H2");  // A/B switch: "0" selects conv_kernel_h (one workgroup per CU)
-    c->conv_h2 = !(h2 && strcmp(h2, "0") == 0);
+    c->conv_h2 = !h2 ? 1 : strcmp(h2, "0") == 0 ? 0 : strcmp(h2, "2") == 0 ? 2 : 1;
     return c;
   }();
   return *d;
@@ -181,7 +181,8 @@ int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on) {
   return FDR_OK;
 }
 int fdr_ctx_set_conv_h2(fdr_ctx* ctx, int32_t on) {
-  (ctx ? ctx->c : default_context()).conv_h2 = on != 0;
+  if (on < 0 || on > 2) return set_error(FDR_ERR_INVALID, "conv_h2 must be 0, 1 or 2");
+  (ctx ? ctx->c : default_context()).conv_h2 = on;
   return FDR_OK;
 }
 int fdr_ctx_impala_profile(fdr_ctx* ctx, int32_t enable) { return impala::set_profile(ctx ? ctx->c : default_context(), enable); }

@@ -217,7 +217,9 @@ __global__ void finish_kernel(int n_lanes, int envs, int T, int entropy, int jig
 
 // fp16 mode kernels (fdr_impala_h.hip)
 __global__ void conv_kernel_h(Layout L, StepArgs a);
-__global__ void conv_kernel_h2(Layout L, StepArgs a);  // same features, 4 waves / 80 KiB LDS: 2 workgroups per CU
+// same features as conv_kernel_h, 80 KiB LDS: 2 workgroups per CU; NTH = 256 (4 waves) or 512 (8 waves, 128 VGPRs)
+template <int NTH>
+__global__ void conv_kernel_h2(Layout L, StepArgs a);
 template <int E, int MODE>
 __global__ void core_kernel_h(Layout L, StepArgs a);
 template <int E>
@@ -235,7 +237,7 @@ template <int E>
 __global__ void xproj_pair_kernel(Layout L, StepArgs a, int t0, int tc, float* gx);
 // MFMA images (kMImg halves each) of n half packs: grid (kFcKS + 4 kGateKS, n)
 __global__ void mfma_image_kernel(Layout L, const _Float16* src, int64_t src_stride, _Float16* dst);
-constexpr int kHThreads = 512, kH2Threads = 256;
+constexpr int kHThreads = 512;
 
 struct Plan {  // workspace carve-up (byte offsets)
   int64_t pack, hpack, feat, h, c, rprev, ci, gx, n2, zeros, thpack, epack, idxe, n2x, mimg, total;

@@ -1346,8 +1346,10 @@ __global__ void pair_offsets_kernel(const int64_t* __restrict__ idx, int n_pairs
 
 // the fp16 conv stack over grid workgroups (one per env, XCD-interleaved lanes): either kernel, same features
 static void launch_conv_h(int h2, int grid, const Layout& L, const StepArgs& a, hipStream_t stream) {
-  if (h2)
-    hipLaunchKernelGGL(conv_kernel_h2, dim3(grid), dim3(kH2Threads), 0, stream, L, a);
+  if (h2 == 2)
+    hipLaunchKernelGGL(conv_kernel_h2<512>, dim3(grid), dim3(512), 0, stream, L, a);
+  else if (h2)
+    hipLaunchKernelGGL(conv_kernel_h2<256>, dim3(grid), dim3(256), 0, stream, L, a);
   else
     hipLaunchKernelGGL(conv_kernel_h, dim3(grid), dim3(kHThreads), 0, stream, L, a);
 }

@@ -686,7 +686,6 @@ __global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a)
 // Arithmetic per output is conv_kernel_h's (same fragments, same K order, same f32 epilogues), so the two
 // kernels' features are identical.
 // =====================================================================================================
-constexpr int kH2Waves = kH2Threads / 64;
 constexpr int kH2BR = 9;                                  // entry band: conv rows (4 pooled rows)
 constexpr int kH2FBRows = kH2BR + 2;                      // padded frame rows per band
 constexpr int kH2FB = kH2FBRows * 66 * 4;                 // halves
@@ -706,10 +705,17 @@ static_assert(kH2BR * 64 * 16 <= kH2FB0 && 3 * kBnTab * 2 >= 34 * 16, "band scra
 // up to 16 tiles; K-outer order keeps 5 pixel addresses per tile live at once (80 VGPRs in the stage-1
 // residual convs, which spilled), tile-outer order keeps one tile's.  Dependent MFMAs on one accumulator
 // issue back to back (SrcC forwarding of the same opcode), and the other workgroup's waves fill the SIMD.
-template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT>
+#ifndef FDR_H2_STAGGER
+#define FDR_H2_STAGGER 0
+#endif
+// STREAM (Cin = 32 at 8 waves, where 72 fragment VGPRs do not fit beside the accumulators under 128): the A
+// fragments are read from the LDS weight block ws per K-step (K-outer: both channel tiles' fragments, then every
+// tile's B fragment of that step) instead of af -- the same products in the same K order.
+template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT, int NW, bool STREAM = false>
 __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSteps<CIN>::N][NT],
-                                        f32x4 (&acc)[TPW][NT], int wave, int lane, int qoff = 0) {
-  constexpr int KS = KSteps<CIN>::N, NF = KSteps<CIN>::NF, NW = kH2Waves;
+                                        f32x4 (&acc)[TPW][NT], int wave, int lane, int qoff = 0,
+                                        const _Float16* ws = nullptr) {
+  constexpr int KS = KSteps<CIN>::N, NF = KSteps<CIN>::NF;
   // A wave's tiles are wave + NW i: tile i's pixels are tile 0's shifted by DQ i padded pixels (whole rows),
   // so every read is one of NF per-lane addresses plus an immediate.  The chunk swizzle of q + DQ i is the
   // swizzle of q XOR flip(i) when DQ keeps the swizzle bits carry-free (asserted).
@@ -732,6 +738,38 @@ __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSte
       sw[s] = (g % cpg) ^ tsw<CIN>(q + qoff);
     }
   }
+  auto live = [&](int i) { return TPW * NW == MT || i < TPW - 1 || wave + NW * i < MT; };  // wave-uniform
+  if constexpr (STREAM) {
+    static_assert(CIN == 32 && !KSteps<CIN>::kRem, "streamed fragments: Cin = 32");
+#pragma unroll
+    for (int i = 0; i < TPW; ++i)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[i][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NF; ++s) {
+      h8 a[NT], b[TPW];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) a[nt] = *reinterpret_cast<const h8*>(ws + (((s * NT + nt) * 64) + lane) * 8);
+#pragma unroll
+      for (int i = 0; i < TPW; ++i)
+        if (live(i)) b[i] = *reinterpret_cast<const h8*>(Tin + DQ * i * CS + off[s] + ((sw[s] ^ flip(i)) << 3));
+      // ordering point (as in the tile form): step s's reads are issued before step s-1's products are final,
+      // and step s+1's only after -- one step of reads in flight
+      if (s > 0) {
+#pragma unroll
+        for (int i = 0; i < TPW; ++i)
+#pragma unroll
+          for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(acc[i][nt]));
+      }
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        if (!live(i)) continue;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[nt], b[i], acc[i][nt], 0, 0, 0);
+      }
+    }
+    return;
+  }
   const int qr = base + 2 * WP + 2;  // tap 8
   const int offr = CIN == 3 ? qr * CS : qr * CS + 4 * (g & 1);
   const int swr = CIN == 3 ? 0 : (g >> 1) ^ tsw<CIN>(qr + qoff);
@@ -739,7 +777,7 @@ __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSte
   for (int i = 0; i < TPW; ++i) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[i][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (TPW * NW == MT || i < TPW - 1 || wave + NW * i < MT) {  // wave-uniform
+    if (live(i)) {
       const _Float16* Ti = Tin + DQ * i * CS;
 #pragma unroll
       for (int s = 0; s < NF; ++s) {
@@ -788,10 +826,11 @@ __device__ __forceinline__ float div255_byte(float x) {
 struct FrameBn {  // BN2d(3) of the frame: per-channel scale / shift (scalars: the struct is passed by value)
   float s0, s1, s2, h0, h1, h2;
 };
+template <int NTH>
 __device__ __forceinline__ void frame_band_h2(_Float16* FB, const _Float16* prev, int r0, int p0, const StepArgs& a,
                                               int64_t env, int e, FrameBn bn) {
   const int nitem = (kH2FBRows - r0) * 24;
-  for (int i = threadIdx.x; i < nitem; i += kH2Threads) {
+  for (int i = threadIdx.x; i < nitem; i += NTH) {
     const int c = i % 3, w = (i / 3) & 7, r = r0 + i / 24, y = p0 + r - 1;  // image row of padded row p0 + r
     _Float16 o[8];
     if (y >= 0 && y < 64) {
@@ -825,7 +864,7 @@ __device__ __forceinline__ void frame_band_h2(_Float16* FB, const _Float16* prev
   }
   // the two pad columns of every generated row, and the overlap rows
   const int npad = (kH2FBRows - r0) * 2, ncopy = r0 * 66 * 4 / 8;
-  for (int i = kH2Threads - 1 - threadIdx.x; i < npad + ncopy; i += kH2Threads) {
+  for (int i = NTH - 1 - threadIdx.x; i < npad + ncopy; i += NTH) {
     if (i < npad)
       *reinterpret_cast<h4*>(FB + ((r0 + (i >> 1)) * 66 + (i & 1) * 65) * 4) = h4{0, 0, 0, 0};
     else
@@ -837,15 +876,16 @@ __device__ __forceinline__ void frame_band_h2(_Float16* FB, const _Float16* prev
 // qoff its padded-pixel index) + bias -> S (conv row -1 as -inf), barrier, then the 3x3 / stride-2 max pool of
 // the band's PRB pooled rows -> X rows [PRB b, +PRB).  between(): work for the pool phase (frame rows of the next
 // band, a weight commit) -- it must not touch S, Tin or X.
-template <int CIN, int COUT, int H, int BR, class Between>
+template <int NTH, int CIN, int COUT, int H, int BR, bool STREAM, class Between>
 __device__ __forceinline__ void entry_band_h2(const _Float16* Tin, int qoff, _Float16* S, _Float16* X,
-                                              const h8 (&af)[KSteps<CIN>::N][COUT / 16], const float (&bz)[COUT / 16][4],
-                                              int b, int wave, int lane, const StepArgs& a, int stamp, Between&& between) {
+                                              const h8 (&af)[KSteps<CIN>::N][COUT / 16], const _Float16* ws,
+                                              const float (&bz)[COUT / 16][4], int b, int wave, int lane,
+                                              const StepArgs& a, int stamp, Between&& between) {
   constexpr int CS = Pix<CIN>::CS, WP = H + 2, NT = COUT / 16, MT = BR * H / 16;
-  constexpr int TPW = (MT + kH2Waves - 1) / kH2Waves, HO = H / 2, PRB = (BR - 1) / 2, G = COUT / 8;
+  constexpr int NW = NTH / 64, TPW = (MT + NW - 1) / NW, HO = H / 2, PRB = (BR - 1) / 2, G = COUT / 8;
   f32x4 acc[TPW][NT];
-  conv_h2<CIN, CS, NT, TPW, H, WP, MT>(Tin, af, acc, wave, lane, qoff);
-  conv_out_h<NT, TPW, MT, kH2Waves>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
+  conv_h2<CIN, CS, NT, TPW, H, WP, MT, NW, STREAM>(Tin, af, acc, wave, lane, qoff, ws);
+  conv_out_h<NT, TPW, MT, NW>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
     const int nt = ch0 >> 4;
     const bool neg = b == 0 && m < H;  // conv row -1
     const float ninf = -INFINITY;
@@ -855,11 +895,11 @@ __device__ __forceinline__ void entry_band_h2(const _Float16* Tin, int qoff, _Fl
   __syncthreads();
   FDR_STAMP(a, stamp);
   between();
-  constexpr int NI = PRB * HO * G, IT = (NI + kH2Threads - 1) / kH2Threads;
+  constexpr int NI = PRB * HO * G, IT = (NI + NTH - 1) / NTH;
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int i = threadIdx.x + it * kH2Threads;
-    if (NI % kH2Threads != 0 && i >= NI) break;
+    const int i = threadIdx.x + it * NTH;
+    if (NI % NTH != 0 && i >= NI) break;
     const int cg = i % G, r = i / G, px = r % HO, pr = r / HO;
     const int xl = 2 * px > 0 ? 2 * px - 1 : 0;
     h8 v[9];
@@ -885,13 +925,14 @@ __device__ __forceinline__ void entry_band_h2(const _Float16* Tin, int qoff, _Fl
 // commit only after a barrier that follows every wave's fragment load of the previous block.  On exit T holds
 // the next stage's input (or the features are written, LAST), and st holds the issued next-stage block (NEXTH
 // halves; committed by the caller, whose WB may differ).
-template <int C, int H, int LAST, int NEXTH>
+template <int NTH, int C, int H, int LAST, int NEXTH>
 __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)[KSteps<C>::N][C / 16],
                                               const _Float16* __restrict__ hp, const Layout& L, int stage,
                                               const float* bsc, const float* bsh, const float* bcb, int wave, int lane,
-                                              float* __restrict__ out, WStageT<kH2Threads>& st, _Float16* wb,
+                                              float* __restrict__ out, WStageT<NTH>& st, _Float16* wb,
                                               const _Float16* __restrict__ next_w, const StepArgs& a, int stamp) {
-  constexpr int CS = Pix<C>::CS, WP = H + 2, NT = C / 16, MT = H * H / 16, NW = kH2Waves;
+  constexpr int CS = Pix<C>::CS, WP = H + 2, NT = C / 16, MT = H * H / 16, NW = NTH / 64;
+  constexpr bool ST = NTH >= 512 && C == 32;  // A fragments streamed from wb (conv_h2 STREAM); af unused
   constexpr int TPW = (MT + NW - 1) / NW, WH = kBlockHalves<C, C / 16>;
   // Epilogue addresses: tile i's pixels are tile 0's + 16 NW i (X, S: the chunk swizzle is unchanged by that
   // step) and padded pixel + DQ i (T: the swizzle flips by tflip(i), conv_h2's step) -- per-lane bases + immediates.
@@ -927,7 +968,7 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
     float b0[NT][4], s1[NT][4], t1[NT][4], b1[NT][4], s2[NT][4], t2[NT][4];
     f32x4 acc[TPW][NT];
     // ---- conv0: T -> T (relu(bn1(. + b0))) ----
-    conv_h2<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
+    conv_h2<C, CS, NT, TPW, H, WP, MT, NW, ST>(T, af, acc, wave, lane, 0, wb);
     __syncthreads();  // every wave has read T
     FDR_STAMP(a, stamp + 4 * r);
 #pragma unroll
@@ -948,14 +989,14 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
     st.template commit<WH>(wb);  // conv i1 (every wave loaded conv i0's fragments before the barrier above)
     __syncthreads();
     FDR_STAMP(a, stamp + 4 * r + 1);
-    load_af_lds<C, NT>(wb, af, lane);
+    if constexpr (!ST) load_af_lds<C, NT>(wb, af, lane);
     if (r == 0) {
       st.template issue<WH>(hp + L.conv_h[i1 + 1]);  // block 1 conv0 (committed after the next barrier)
     } else if constexpr (NEXTH > 0) {
       st.template issue<NEXTH>(next_w);
     }
     // ---- conv1: T -> X += . + b1; T <- bn(X) (relu before a block) ----
-    conv_h2<C, CS, NT, TPW, H, WP, MT>(T, af, acc, wave, lane);
+    conv_h2<C, CS, NT, TPW, H, WP, MT, NW, ST>(T, af, acc, wave, lane, 0, wb);
     __syncthreads();
     FDR_STAMP(a, stamp + 4 * r + 2);
 #pragma unroll
@@ -988,17 +1029,26 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
     __syncthreads();
     FDR_STAMP(a, stamp + 4 * r + 3);
     if (r == 0) {
-      load_af_lds<C, NT>(wb, af, lane);
+      if constexpr (!ST) load_af_lds<C, NT>(wb, af, lane);
       st.template issue<WH>(hp + L.conv_h[i1 + 2]);  // block 1 conv1 (committed after the next barrier)
     }
   }
 }
 
-__global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[kH2LdsBytes];
+#ifndef FDR_H2_ONE_PER_CU
+#define FDR_H2_ONE_PER_CU 0
+#endif
+template <int NTH>
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))) void conv_kernel_h2(Layout L, StepArgs a) {
+  // experiment: FDR_H2_ONE_PER_CU pads the LDS past half the CU (one workgroup per CU) -- latency sensitivity
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kH2LdsBytes + (FDR_H2_ONE_PER_CU ? 4096 : 0)];
   const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
   const int lane = (slot / a.envs) * 8 + xcd, e = slot % a.envs;
   if (lane >= a.n_lanes) return;
+#if FDR_H2_STAGGER  // experiment: the second workgroup of each CU in the first dispatch round starts late
+  if (b >= 256 && b < 512)
+    for (int k = 0; k < FDR_H2_STAGGER / 8000; ++k) __builtin_amdgcn_s_sleep(125);
+#endif
   FDR_STAMP(a, 0);
   const int wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int64_t env = (int64_t)lane * a.envs + e;
@@ -1012,11 +1062,11 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
   // BN / bias tables (conv_kernel_h's folding), two entries per thread: their inputs are loaded first, the first
   // frame band (which folds BN2d(3) per thread from the same inputs) covers the latency, then the tables are
   // written.  The weight block of the first residual conv is issued now and committed in the first pool phase.
-  constexpr int kTabIt = (kBnTab + kH2Threads - 1) / kH2Threads;
+  constexpr int kTabIt = (kBnTab + NTH - 1) / NTH;
   float rm[kTabIt], rv[kTabIt], bnw[kTabIt], bnb[kTabIt], cbv[kTabIt];
 #pragma unroll
   for (int k = 0; k < kTabIt; ++k) {
-    const int bi = threadIdx.x + k * kH2Threads, bidx = bi >> 5, bch = bi & 31;
+    const int bi = threadIdx.x + k * NTH, bidx = bi >> 5, bch = bi & 31;
     const bool has_bn = bi < kBnTab && bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
     const bool has_cb = bi < kBnTab && bch < (bidx < 5 ? 16 : 32);
     rm[k] = 0.f, rv[k] = 1.f, bnw[k] = 0.f, bnb[k] = 0.f, cbv[k] = 0.f;
@@ -1030,8 +1080,8 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
   }
   h8 af3[KSteps<3>::N][1];
   load_af<3, 1>(hp + L.conv_h[0], af3, ln);
-  WStageT<kH2Threads> st;
-  st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);
+  WStageT<NTH> st;
+  st.template issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);
   float fsc[3], fsh[3];  // BN2d(3) of the frame, per thread (table entries 0..2)
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
@@ -1041,10 +1091,10 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
   }
   const FrameBn fbn{fsc[0], fsc[1], fsc[2], fsh[0], fsh[1], fsh[2]};
   auto FB = [&](int k) { return R + ((k & 1) ? kH2FB1 : kH2FB0); };  // the two frame-band buffers
-  frame_band_h2(FB(0), nullptr, 0, -1, a, env, e, fbn);
+  frame_band_h2<NTH>(FB(0), nullptr, 0, -1, a, env, e, fbn);
 #pragma unroll
   for (int k = 0; k < kTabIt; ++k) {
-    const int bi = threadIdx.x + k * kH2Threads, bidx = bi >> 5, bch = bi & 31;
+    const int bi = threadIdx.x + k * NTH, bidx = bi >> 5, bch = bi & 31;
     if (bi >= kBnTab) break;
     const bool has_bn = bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
     const float sc = has_bn ? bnw[k] * (1.f / sqrtf(rv[k] + kBnEps)) : 0.f;
@@ -1061,10 +1111,10 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
 #pragma unroll
     for (int k = 0; k < 4; ++k) bz[0][k] = bcb[0 * 32 + 4 * (ln >> 4) + k];
     for (int bd = 0; bd < 64 / (kH2BR - 1); ++bd) {
-      entry_band_h2<3, 16, 64, kH2BR>(FB(bd), 0, R + kH2S1, R + kH2X1, af3, bz, bd, wave, ln, a, 2 + 2 * bd, [&]() {
-        if (bd == 0) st.commit<kBlockHalves<16, 1>>(R + kH2WBA);
+      entry_band_h2<NTH, 3, 16, 64, kH2BR, false>(FB(bd), 0, R + kH2S1, R + kH2X1, af3, nullptr, bz, bd, wave, ln, a, 2 + 2 * bd, [&]() {
+        if (bd == 0) st.template commit<kBlockHalves<16, 1>>(R + kH2WBA);
         if (bd + 1 < 64 / (kH2BR - 1))
-          frame_band_h2(FB(bd + 1), FB(bd), 3, (kH2BR - 1) * (bd + 1) - 1, a, env, e, fbn);
+          frame_band_h2<NTH>(FB(bd + 1), FB(bd), 3, (kH2BR - 1) * (bd + 1) - 1, a, env, e, fbn);
       });
     }
   }
@@ -1072,20 +1122,20 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
   {
     h8 af[KSteps<16>::N][1];
     load_af_lds<16, 1>(R + kH2WBA, af, ln);
-    st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[2]);
-    to_padded_h<16, 32, true, true, kH2Threads>(R + kH2X1, R, bsc + 1 * 32, bsh + 1 * 32);
+    st.template issue<kBlockHalves<16, 1>>(hp + L.conv_h[2]);
+    to_padded_h<16, 32, true, true, NTH>(R + kH2X1, R, bsc + 1 * 32, bsh + 1 * 32);
     __syncthreads();
     FDR_STAMP(a, 18);
-    res_blocks_h2<16, 32, 0, kBlockHalves<16, 2>>(R, R + kH2X1, af, hp, L, 0, bsc, bsh, bcb, wave, ln, nullptr, st,
+    res_blocks_h2<NTH, 16, 32, 0, kBlockHalves<16, 2>>(R, R + kH2X1, af, hp, L, 0, bsc, bsh, bcb, wave, ln, nullptr, st,
                                                   R + kH2WBA, hp + L.conv_h[5], a, 19);
-    st.commit<kBlockHalves<16, 2>>(R + kH2WBB);  // X1 is dead: the stage-2 entry block goes to WB_B
+    st.template commit<kBlockHalves<16, 2>>(R + kH2WBB);  // X1 is dead: the stage-2 entry block goes to WB_B
     __syncthreads();
   }
   // ---- stage 2: entry (16 -> 32 at 32 x 32, pooled to 16 x 16) in 4 bands; X2 into T1's consumed rows ----
   {
     h8 af[KSteps<16>::N][2];
     load_af_lds<16, 2>(R + kH2WBB, af, ln);
-    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
+    st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
     float bz[2][4];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
@@ -1093,50 +1143,59 @@ __global__ __launch_bounds__(kH2Threads, 2) void conv_kernel_h2(Layout L, StepAr
       for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[5 * 32 + nt * 16 + 4 * (ln >> 4) + k];
     for (int bd = 0; bd < 32 / (kH2BR - 1); ++bd) {
       const int q0 = ((kH2BR - 1) * bd - 1) * 34;
-      entry_band_h2<16, 32, 32, kH2BR>(R + q0 * 16, q0, R + kH2S2, R, af, bz, bd, wave, ln, a, 28 + 2 * bd, [&]() {
-        if (bd == 0) st.commit<kBlockHalves<32, 2>>(R + kH2WBB);
+      entry_band_h2<NTH, 16, 32, 32, kH2BR, false>(R + q0 * 16, q0, R + kH2S2, R, af, nullptr, bz, bd, wave, ln, a, 28 + 2 * bd, [&]() {
+        if (bd == 0) st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
       });
     }
   }
   // ---- stage 2 residual blocks (32 ch, 16 x 16) ----
   {
     h8 af[KSteps<32>::N][2];
-    load_af_lds<32, 2>(R + kH2WBB, af, ln);
-    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[7]);
-    to_padded_h<32, 16, true, true, kH2Threads>(R, R + kH2T2, bsc + 6 * 32, bsh + 6 * 32);
+    if constexpr (NTH < 512) load_af_lds<32, 2>(R + kH2WBB, af, ln);
+    st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[7]);
+    to_padded_h<32, 16, true, true, NTH>(R, R + kH2T2, bsc + 6 * 32, bsh + 6 * 32);
     __syncthreads();
     FDR_STAMP(a, 36);
-    res_blocks_h2<32, 16, 0, kBlockHalves<32, 2>>(R + kH2T2, R, af, hp, L, 1, bsc, bsh, bcb, wave, ln, nullptr, st,
+    res_blocks_h2<NTH, 32, 16, 0, kBlockHalves<32, 2>>(R + kH2T2, R, af, hp, L, 1, bsc, bsh, bcb, wave, ln, nullptr, st,
                                                   R + kH2WBB, hp + L.conv_h[10], a, 37);
-    st.commit<kBlockHalves<32, 2>>(R + kH2WBB);
+    st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
     __syncthreads();
   }
-  // ---- stage 3: entry (32 -> 32 at 16 x 16, pooled to 8 x 8) in one band of 17 rows ----
+  // ---- stage 3: entry (32 -> 32 at 16 x 16, pooled to 8 x 8): one band of 17 rows at 4 waves; at 8 waves (128
+  // VGPRs) two bands of 9, so a wave's accumulators stay at 2 tiles x 2 channel tiles beside the 72 fragment VGPRs ----
   {
     h8 af[KSteps<32>::N][2];
-    load_af_lds<32, 2>(R + kH2WBB, af, ln);
-    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
+    constexpr bool ST = NTH >= 512;  // conv 10 streamed from WB_B: conv 11's block is committed after the last band
+    if constexpr (!ST) load_af_lds<32, 2>(R + kH2WBB, af, ln);
+    st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
     float bz[2][4];
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
       for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[10 * 32 + nt * 16 + 4 * (ln >> 4) + k];
-    entry_band_h2<32, 32, 16, 17>(R + kH2T2 - 18 * 32, -18, R + kH2S3, R, af, bz, 0, wave, ln, a, 45, [&]() {
-      st.commit<kBlockHalves<32, 2>>(R + kH2WBB);
-    });
+    constexpr int BR3 = NTH >= 512 ? 9 : 17;
+    for (int bd = 0; bd < 16 / (BR3 - 1); ++bd) {
+      const int q0 = ((BR3 - 1) * bd - 1) * 18;
+      entry_band_h2<NTH, 32, 32, 16, BR3, ST>(R + kH2T2 + q0 * 32, q0, R + kH2S3, R, af, R + kH2WBB, bz, bd, wave, ln, a,
+                                              45 + 2 * bd, [&]() {
+        if (bd == (ST ? 16 / (BR3 - 1) - 1 : 0)) st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
+      });
+    }
   }
   // ---- stage 3 residual blocks (32 ch, 8 x 8) -> features ----
   {
     h8 af[KSteps<32>::N][2];
-    load_af_lds<32, 2>(R + kH2WBB, af, ln);
-    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[12]);
-    to_padded_h<32, 8, true, true, kH2Threads>(R, R + kH2T3, bsc + 11 * 32, bsh + 11 * 32);
+    if constexpr (NTH < 512) load_af_lds<32, 2>(R + kH2WBB, af, ln);
+    st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[12]);
+    to_padded_h<32, 8, true, true, NTH>(R, R + kH2T3, bsc + 11 * 32, bsh + 11 * 32);
     __syncthreads();
-    FDR_STAMP(a, 47);
-    res_blocks_h2<32, 8, 1, 0>(R + kH2T3, R, af, hp, L, 2, bsc, bsh, bcb, wave, ln, a.feat + env * kFeat, st,
-                               R + kH2WBB, nullptr, a, 48);
+    FDR_STAMP(a, 49);
+    res_blocks_h2<NTH, 32, 8, 1, 0>(R + kH2T3, R, af, hp, L, 2, bsc, bsh, bcb, wave, ln, a.feat + env * kFeat, st,
+                               R + kH2WBB, nullptr, a, 50);
   }
 }
+template __global__ void conv_kernel_h2<256>(Layout, StepArgs);
+template __global__ void conv_kernel_h2<512>(Layout, StepArgs);
 
 // ---- core (fc + LSTM + head) with f16 weights ------------------------------------------------------
 template <int E, int MODE>

@@ -46,9 +46,10 @@ class Context(object):
         """fp16 pair-form Impala core step: MFMA (True, default) or the VALU form (False)."""
         check(lib.fdr_ctx_set_core_mfma(self.handle, 1 if on else 0), "fdr_ctx_set_core_mfma")
 
-    def set_conv_h2(self, on):
-        """fp16 Impala conv stack: conv_kernel_h2 (True: two workgroups per CU) or conv_kernel_h (False)."""
-        check(lib.fdr_ctx_set_conv_h2(self.handle, 1 if on else 0), "fdr_ctx_set_conv_h2")
+    def set_conv_h2(self, mode):
+        """fp16 Impala conv stack: 1 / True = conv_kernel_h2<256> (two 4-wave workgroups per CU), 2 =
+        conv_kernel_h2<512> (two 8-wave workgroups per CU), 0 / False = conv_kernel_h (one per CU)."""
+        check(lib.fdr_ctx_set_conv_h2(self.handle, int(mode)), "fdr_ctx_set_conv_h2")
 
     def impala_profile(self, enable):
         check(lib.fdr_ctx_impala_profile(self.handle, 1 if enable else 0), "fdr_ctx_impala_profile")

@@ -445,9 +445,9 @@ def test_fp16_pair_default_path_whole_episode_vs_f32_oracle(engine, table, core_
 
 
 def test_conv_h2_bit_identical_to_conv_h(engine, table):
-    """conv_kernel_h2 (4 waves, 80 KiB LDS, two workgroups per CU; banded stage-1 / stage-2
-    entry convs, single-buffered residual blocks) computes every conv output with conv_kernel_h's fragments, K
-    order and f32 epilogues, so the two kernels' outputs are bitwise equal: forward features / probs / LSTM state
+    """conv_kernel_h2 (80 KiB LDS, two workgroups per CU; banded entry convs, single-buffered
+    residual blocks; 4 waves, or 8 waves with the 32-channel A fragments streamed from LDS) computes every conv
+    output with conv_kernel_h's fragments, K order and f32 epilogues, so all three kernels' outputs are equal: forward features / probs / LSTM state
     (13 envs, ragged over the 8 XCD slots), a recorded fp16 pair rollout with the entropy replay, and strategies."""
     A = 4
     theta_np = _theta(A)
@@ -468,9 +468,10 @@ def test_conv_h2_bit_identical_to_conv_h(engine, table):
     res = {}
     ctx = engine.context()
     import os
-    prior = os.environ.get("FDR_CONV_H2", "1") != "0"   # the default context's setting (FDR_CONV_H2)
+    env = os.environ.get("FDR_CONV_H2", "1")   # the default context's setting
+    prior = 0 if env == "0" else (2 if env == "2" else 1)
     try:
-        for on in (False, True):
+        for on in (0, 1, 2):
             ctx.set_conv_h2(on)
             h = torch.zeros(n, 256, device="cuda")
             c = torch.zeros(n, 256, device="cuda")
@@ -486,9 +487,10 @@ def test_conv_h2_bit_identical_to_conv_h(engine, table):
                                                        ("actions", "probs", "reward", "entropy")] + [st.cpu().numpy()]
     finally:
         ctx.set_conv_h2(prior)
-    assert np.abs(res[True][1]).max() > 0 and np.all(np.isfinite(res[True][1]))
-    for a, b in zip(res[False], res[True]):
-        np.testing.assert_array_equal(a, b)
+    assert np.abs(res[1][1]).max() > 0 and np.all(np.isfinite(res[1][1]))
+    for mode in (1, 2):
+        for a, b in zip(res[0], res[mode]):
+            np.testing.assert_array_equal(a, b)
 
 
 @pytest.mark.parametrize("fp16,pairs", [(False, False), (False, True), (True, False), (True, True)])

@@ -5,6 +5,8 @@
 //   chained_nop  the same with s_nop 7 x 2 pinned between the two MFMAs (sched_barrier)
 //   separate     mfma32(a1, b1, 0) + mfma16(a2, b2, 0) added by VALU (the conv's current form)
 //   chained_rev  acc = mfma32(a1, b1, mfma16(a2, b2, 0))        (the other order)
+//   asm_b2b      the chained pair hand-issued in one asm block with no wait states between
+//   asm_nop      the same with 2 x s_nop 7 between
 // Each form runs over 256 tiles with independent random data; the host reports the max error of each.
 // Build: hipcc --offload-arch=gfx950 -O3 tools/probes/srcc_probe.hip -o tools/probes/srcc_probe
 // ISA:   hipcc --offload-arch=gfx950 -O3 -S --offload-device-only tools/probes/srcc_probe.hip -o /tmp/srcc.s
@@ -36,7 +38,31 @@ __global__ void k(const _Float16* A1, const _Float16* B1, const _Float16* A2, co
   }
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
   f32x4 acc;
-  if constexpr (FORM == 0) {
+  // every operand in registers before the first MFMA: the pair below issues with nothing between (r06's probe let
+  // the K = 16 operands' global loads complete between the two MFMAs -- hundreds of cycles -- so it never
+  // exercised the back-to-back SrcC dependency)
+  asm volatile("" : "+v"(fa1), "+v"(fb1), "+v"(fa2), "+v"(fb2));  // forces every load's wait here
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (FORM == 4) {  // hand-issued back to back, no wait states (hazard recognizer bypassed)
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0\n\tv_mfma_f32_16x16x16_f16 %0, %3, %4, %0\n\ts_nop 7\n\ts_nop 7"
+                 : "=&v"(acc) : "v"(fa1), "v"(fb1), "v"(fa2), "v"(fb2));
+  } else if constexpr (FORM == 5) {  // hand-issued with 2 x s_nop 7 between
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0\n\ts_nop 7\n\ts_nop 7\n\tv_mfma_f32_16x16x16_f16 %0, %3, %4, %0\n\ts_nop 7\n\ts_nop 7"
+                 : "=&v"(acc) : "v"(fa1), "v"(fb1), "v"(fa2), "v"(fb2));
+  } else if constexpr (FORM >= 10) {  // hand-issued with s_nop (FORM - 10) between: FORM - 9 wait states
+#define SRCC_PAIR(N)                                                                                                 \
+  asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, 0\n\ts_nop " #N "\n\tv_mfma_f32_16x16x16_f16 %0, %3, %4, %0\n\ts_nop 7\n\ts_nop 7" \
+               : "=&v"(acc) : "v"(fa1), "v"(fb1), "v"(fa2), "v"(fb2))
+    if constexpr (FORM == 10) SRCC_PAIR(0);
+    if constexpr (FORM == 11) SRCC_PAIR(1);
+    if constexpr (FORM == 12) SRCC_PAIR(2);
+    if constexpr (FORM == 13) SRCC_PAIR(3);
+    if constexpr (FORM == 14) SRCC_PAIR(4);
+    if constexpr (FORM == 15) SRCC_PAIR(5);
+    if constexpr (FORM == 16) SRCC_PAIR(6);
+    if constexpr (FORM == 17) SRCC_PAIR(7);
+#undef SRCC_PAIR
+  } else if constexpr (FORM == 0) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa1, fb1, z, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x16f16(fa2, fb2, acc, 0, 0, 0);
   } else if constexpr (FORM == 1) {
@@ -74,18 +100,31 @@ int main() {
       }
   _Float16 *dA1, *dB1, *dA2, *dB2;
   float* dD;
-  hipMalloc(&dA1, NT * 1024); hipMalloc(&dB1, NT * 1024); hipMalloc(&dA2, NT * 512); hipMalloc(&dB2, NT * 512);
+  (void)hipMalloc(&dA1, NT * 1024); hipMalloc(&dB1, NT * 1024); hipMalloc(&dA2, NT * 512); hipMalloc(&dB2, NT * 512);
   hipMalloc(&dD, NT * 1024);
   hipMemcpy(dA1, hA1, NT * 1024, hipMemcpyHostToDevice); hipMemcpy(dB1, hB1, NT * 1024, hipMemcpyHostToDevice);
   hipMemcpy(dA2, hA2, NT * 512, hipMemcpyHostToDevice); hipMemcpy(dB2, hB2, NT * 512, hipMemcpyHostToDevice);
   float* D = new float[NT * 256];
-  const char* names[4] = {"chained (SrcC, back to back)", "chained + s_nop 7 x2", "separate + VALU add", "chained, K=16 first"};
-  for (int f = 0; f < 4; ++f) {
+  const char* names[14] = {"chained (compiler wait states)", "chained + s_nop 7 x2", "separate + VALU add",
+                           "chained, K=16 first", "asm back to back, 0 nops", "asm + s_nop 7 x2",
+                           "asm + s_nop 0 (1 wait state)", "asm + s_nop 1 (2)", "asm + s_nop 2 (3)", "asm + s_nop 3 (4)",
+                           "asm + s_nop 4 (5)", "asm + s_nop 5 (6)", "asm + s_nop 6 (7)", "asm + s_nop 7 (8)"};
+  for (int f = 0; f < 14; ++f) {
     hipMemset(dD, 0, NT * 1024);
     if (f == 0) hipLaunchKernelGGL(k<0>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
     if (f == 1) hipLaunchKernelGGL(k<1>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
     if (f == 2) hipLaunchKernelGGL(k<2>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
     if (f == 3) hipLaunchKernelGGL(k<3>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
+    if (f == 4) hipLaunchKernelGGL(k<4>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
+    if (f == 5) hipLaunchKernelGGL(k<5>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
+    if (f == 6) hipLaunchKernelGGL(k<10>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
+    if (f == 7) hipLaunchKernelGGL(k<11>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
+    if (f == 8) hipLaunchKernelGGL(k<12>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
+    if (f == 9) hipLaunchKernelGGL(k<13>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
+    if (f == 10) hipLaunchKernelGGL(k<14>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
+    if (f == 11) hipLaunchKernelGGL(k<15>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
+    if (f == 12) hipLaunchKernelGGL(k<16>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
+    if (f == 13) hipLaunchKernelGGL(k<17>, dim3(NT), dim3(64), 0, 0, dA1, dB1, dA2, dB2, dD);
     hipMemcpy(D, dD, NT * 1024, hipMemcpyDeviceToHost);
     double e = 0;
     int bad = 0;
