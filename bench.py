@@ -473,9 +473,10 @@ def main():
         core_prof = None if prof is None else prof.get("core_kernel")
         roofline = {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(achieved_tf / peak, 4), "traffic": traffic,
-                    "kernel": (("impala conv_kernel_h (15 convs, v_mfma_f32_16x16x32_f16; 1 workgroup / CU)"
-                                if os.environ.get("FDR_CONV_H2") == "0" else
-                                "impala conv_kernel_h2 (15 convs, v_mfma_f32_16x16x32_f16; 2 workgroups / CU)")
+                    "kernel": ({"0": "impala conv_kernel_h (15 convs, v_mfma_f32_16x16x32_f16; 1 x 8 waves / CU)",
+                                "1": "impala conv_kernel_h2<256> (15 convs, v_mfma_f32_16x16x32_f16; 2 x 4 waves / CU)"}
+                               .get(os.environ.get("FDR_CONV_H2"),
+                                    "impala conv_kernel_h2<512> (15 convs, v_mfma_f32_16x16x32_f16; 2 x 8 waves / CU)")
                                if fp16 else "impala conv_kernel (15 convs, v_mfma_f32_16x16x4_f32)"),
                     "conv_launch_ms": round(conv_launch_ms, 4), "flop_per_env_step": IMPALA_CONV_FLOP,
                     "envs_per_launch": L * E, "rollout_ms": round(rollout_ms, 3),

@@ -118,7 +118,7 @@ Context& default_context() {
     const char* m = getenv("FDR_CORE_MFMA");  // A/B switch: "0" selects the VALU fp16 pair core
     c->core_mfma = !(m && strcmp(m, "0") == 0);
     const char* h2 = getenv("FDR_CONV_H2");  // A/B switch: "0" selects conv_kernel_h (one workgroup per CU)
-    c->conv_h2 = !h2 ? 1 : strcmp(h2, "0") == 0 ? 0 : strcmp(h2, "2") == 0 ? 2 : 1;
+    c->conv_h2 = !h2 ? 2 : strcmp(h2, "0") == 0 ? 0 : strcmp(h2, "1") == 0 ? 1 : 2;
     return c;
   }();
   return *d;

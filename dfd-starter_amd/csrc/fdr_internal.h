@@ -22,7 +22,7 @@ struct Context {
   int rollout_impl = 2; // FDR_ROLLOUT_AUTO
   int replay_gemm = 1;
   int core_mfma = 1;    // fp16 pair-form core step on MFMA (core_kernel_hpm); 0: the VALU form (core_kernel_hp)
-  int conv_h2 = 1;      // fp16 conv stack in two workgroups per CU (conv_kernel_h2, default); 0: conv_kernel_h
+  int conv_h2 = 2;      // fp16 conv stack, two workgroups per CU: 2 = conv_kernel_h2<512> (default), 1 = <256>; 0: conv_kernel_h
   uint64_t* debug_clock = nullptr;
   impala::Profile* prof = nullptr;  // owned, created on first enable
 };

@@ -104,9 +104,10 @@ int fdr_ctx_set_replay_gemm(fdr_ctx* ctx, int32_t on);     /* see fdr_impala_set
    v_mfma_f32_16x16x32_f16 as theta X + E (S X) over MFMA-fragment images of theta and each pair's sigma-eps
    (activations rounded to f16); 0 = the VALU form (w = f16(theta) + s f16(sigma eps) formed per element) */
 int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on);
-/* fp16 Impala conv stack (rollout, forward, strategies): 1 = conv_kernel_h2 (4 waves, 80 KiB LDS, two
-   workgroups per CU; the default), 0 = conv_kernel_h (8 waves, 145 KiB LDS); identical features.  Default context:
-   1 unless FDR_CONV_H2=0 */
+/* fp16 Impala conv stack (rollout, forward, strategies), identical features in every mode:
+   2 (default) = conv_kernel_h2<512>: 8 waves, 80 KiB LDS, 128 VGPRs, two workgroups per CU;
+   1 = conv_kernel_h2<256>: 4 waves, two workgroups per CU;  0 = conv_kernel_h: 8 waves, 145 KiB LDS, one per CU.
+   Default context: FDR_CONV_H2 (0 / 1 / 2) or 2 */
 int fdr_ctx_set_conv_h2(fdr_ctx* ctx, int32_t on);
 int fdr_ctx_impala_profile(fdr_ctx* ctx, int32_t enable);  /* see fdr_impala_profile */
 int fdr_ctx_impala_profile_read(fdr_ctx* ctx, double* ms);

@@ -468,8 +468,8 @@ def test_conv_h2_bit_identical_to_conv_h(engine, table):
     res = {}
     ctx = engine.context()
     import os
-    env = os.environ.get("FDR_CONV_H2", "1")   # the default context's setting
-    prior = 0 if env == "0" else (2 if env == "2" else 1)
+    env = os.environ.get("FDR_CONV_H2", "2")   # the default context's setting
+    prior = 0 if env == "0" else (1 if env == "1" else 2)
     try:
         for on in (0, 1, 2):
             ctx.set_conv_h2(on)
