@@ -739,8 +739,11 @@ __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSte
     }
   }
   auto live = [&](int i) { return TPW * NW == MT || i < TPW - 1 || wave + NW * i < MT; };  // wave-uniform
+  const int qr = base + 2 * WP + 2;  // tap 8
+  const int offr = CIN == 3 ? qr * CS : qr * CS + 4 * (g & 1);
+  const int swr = CIN == 3 ? 0 : (g >> 1) ^ tsw<CIN>(qr + qoff);
   if constexpr (STREAM) {
-    static_assert(CIN == 32 && !KSteps<CIN>::kRem, "streamed fragments: Cin = 32");
+    static_assert(CIN == 32 || CIN == 16, "streamed fragments: Cin = 16 / 32");
 #pragma unroll
     for (int i = 0; i < TPW; ++i)
 #pragma unroll
@@ -768,11 +771,23 @@ __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSte
         for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[nt], b[i], acc[i][nt], 0, 0, 0);
       }
     }
+    if constexpr (KSteps<CIN>::kRem) {  // tap 8 on K = 16 (rem_fragment's lane map), added by VALU
+      const int src = (lane & 15) + 16 * (g >> 1);
+      h4 a[NT];
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt)
+        a[nt] = *reinterpret_cast<const h4*>(ws + ((((KS - 1) * NT + nt) * 64) + src) * 8 + 4 * (g & 1));
+#pragma unroll
+      for (int i = 0; i < TPW; ++i) {
+        if (!live(i)) continue;
+        const h4 b = *reinterpret_cast<const h4*>(Tin + DQ * i * CS + offr + ((swr ^ flip(i)) << 3));
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[i][nt] += __builtin_amdgcn_mfma_f32_16x16x16f16(a[nt], b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+    }
     return;
   }
-  const int qr = base + 2 * WP + 2;  // tap 8
-  const int offr = CIN == 3 ? qr * CS : qr * CS + 4 * (g & 1);
-  const int swr = CIN == 3 ? 0 : (g >> 1) ^ tsw<CIN>(qr + qoff);
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
 #pragma unroll
@@ -1134,7 +1149,8 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   // ---- stage 2: entry (16 -> 32 at 32 x 32, pooled to 16 x 16) in 4 bands; X2 into T1's consumed rows ----
   {
     h8 af[KSteps<16>::N][2];
-    load_af_lds<16, 2>(R + kH2WBB, af, ln);
+    constexpr bool ST = NTH >= 512;  // conv 5 streamed from WB_B: conv 6's block is committed after the last band
+    if constexpr (!ST) load_af_lds<16, 2>(R + kH2WBB, af, ln);
     st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
     float bz[2][4];
 #pragma unroll
@@ -1143,8 +1159,9 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
       for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[5 * 32 + nt * 16 + 4 * (ln >> 4) + k];
     for (int bd = 0; bd < 32 / (kH2BR - 1); ++bd) {
       const int q0 = ((kH2BR - 1) * bd - 1) * 34;
-      entry_band_h2<NTH, 16, 32, 32, kH2BR, false>(R + q0 * 16, q0, R + kH2S2, R, af, nullptr, bz, bd, wave, ln, a, 28 + 2 * bd, [&]() {
-        if (bd == 0) st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
+      entry_band_h2<NTH, 16, 32, 32, kH2BR, ST>(R + q0 * 16, q0, R + kH2S2, R, af, R + kH2WBB, bz, bd, wave, ln, a,
+                                                28 + 2 * bd, [&]() {
+        if (bd == (ST ? 32 / (kH2BR - 1) - 1 : 0)) st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
       });
     }
   }
