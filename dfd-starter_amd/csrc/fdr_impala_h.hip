@@ -383,7 +383,7 @@ __device__ __forceinline__ void stage_entry_h(const _Float16* T, _Float16* S, _F
 
 // Zero border of a padded image [H+2][H+2][CS] (the interior is written by a conv epilogue).
 template <int C, int H>
-__device__ __forceinline__ void zero_border_h(_Float16* T) {
+__device__ __forceinline__ void zero_border_h(_Float16* T) {  // (kHThreads = conv_kernel_h2<512>'s block too)
   constexpr int CS = Pix<C>::CS, WP = H + 2, G = C / 8;
   const h8 z = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int i = threadIdx.x; i < 4 * (H + 1) * G; i += kHThreads) {
@@ -841,10 +841,10 @@ __device__ __forceinline__ float div255_byte(float x) {
 struct FrameBn {  // BN2d(3) of the frame: per-channel scale / shift (scalars: the struct is passed by value)
   float s0, s1, s2, h0, h1, h2;
 };
-template <int NTH>
+template <int NTH, int FR = kH2FBRows>
 __device__ __forceinline__ void frame_band_h2(_Float16* FB, const _Float16* prev, int r0, int p0, const StepArgs& a,
                                               int64_t env, int e, FrameBn bn) {
-  const int nitem = (kH2FBRows - r0) * 24;
+  const int nitem = (FR - r0) * 24;
   for (int i = threadIdx.x; i < nitem; i += NTH) {
     const int c = i % 3, w = (i / 3) & 7, r = r0 + i / 24, y = p0 + r - 1;  // image row of padded row p0 + r
     _Float16 o[8];
@@ -878,12 +878,12 @@ __device__ __forceinline__ void frame_band_h2(_Float16* FB, const _Float16* prev
     }
   }
   // the two pad columns of every generated row, and the overlap rows
-  const int npad = (kH2FBRows - r0) * 2, ncopy = r0 * 66 * 4 / 8;
+  const int npad = (FR - r0) * 2, ncopy = r0 * 66 * 4 / 8;
   for (int i = NTH - 1 - threadIdx.x; i < npad + ncopy; i += NTH) {
     if (i < npad)
       *reinterpret_cast<h4*>(FB + ((r0 + (i >> 1)) * 66 + (i & 1) * 65) * 4) = h4{0, 0, 0, 0};
     else
-      reinterpret_cast<uint4*>(FB)[i - npad] = reinterpret_cast<const uint4*>(prev + (kH2FBRows - r0) * 66 * 4)[i - npad];
+      reinterpret_cast<uint4*>(FB)[i - npad] = reinterpret_cast<const uint4*>(prev + (FR - r0) * 66 * 4)[i - npad];
   }
 }
 
@@ -933,6 +933,248 @@ __device__ __forceinline__ void entry_band_h2(const _Float16* Tin, int qoff, _Fl
   }
   __syncthreads();
   FDR_STAMP(a, stamp + 1);
+}
+
+// -----------------------------------------------------------------------------------------------------
+// Stage entries with the max pool in registers (conv_kernel_h2<512>, FDR_H3_ENTRY; DESIGN.md 3.4 "r07 entries").
+// A band is 16 conv rows; wave w owns band rows 2w and 2w + 1, all their pixels, all output channels.  The 3 x 3 /
+// stride-2 pool then needs no image of the conv output: horizontally the window's three columns are in
+// neighbouring lanes (DPP), vertically pooled row w is max(row 2w - 1, 2w, 2w + 1) -- rows 2w, 2w + 1 are the
+// wave's own, row 2w - 1 is wave w - 1's second row, handed over through a small exchange slot (EX) across the
+// band's one barrier (wave 0 takes the previous band's wave-7 slot).  Per band: conv, pool, export, barrier,
+// import, X store -- one barrier instead of conv / S store / barrier / pool / barrier, and no S image.
+// Values: max commutes with the monotone f16(f32(v + b)) of the S store, so pooling the f32 sums and adding the
+// bias after is conv_kernel_h's f16 pool output bit for bit.
+// -----------------------------------------------------------------------------------------------------
+constexpr int kH3FR = 18;                              // padded frame rows per stage-1 band (16 conv rows + 2)
+constexpr int kH3FB = kH3FR * 66 * 4;                  // halves
+constexpr int kH3FB0 = 0, kH3FB1 = kH3FB, kH3EX1 = 2 * kH3FB;   // stage 1: FB0 | FB1 | EX (16 slots x 512)
+constexpr int kH3EX2 = 18560, kH3EX3 = 18560;          // stages 2 / 3: EX after T2's extent
+static_assert(kH3EX1 + 16 * 512 <= kH2X1, "stage 1 h3 map");
+static_assert(kH3EX2 + 16 * 512 <= kH2WBB && kH3EX3 + 8 * 256 <= kH2WBB, "stage 2/3 h3 map");
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float old, float src) {  // src from the DPP lane; invalid source: old
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, src),
+                                                               CTRL, 0xF, 0xF, false));
+}
+constexpr int kDppShl1 = 0x101, kDppShr1 = 0x111, kDppRor1 = 0x121;
+
+// Stage-1 band conv (Cin 3 -> 16 at 64 x 64) in even / odd pixel tiles: tile i = (rho = i >> 2, k = (i >> 1) & 1,
+// par = i & 1) holds, in lane l, the 16 channels of pixel x = 2 (16 k + l) + par of band row 2 wave + rho -- so a
+// pooled pixel's three columns 2p - 1, 2p, 2p + 1 are in one lane (even, odd tile) and its left neighbour (odd tile,
+// one lane down).  FBb: the band's padded frame rows [18][66][4].  conv_h's K order: taps 0..7 on K = 32, tap 8 on
+// K = 16 into its own accumulator, added.
+__device__ __forceinline__ void conv_band_s1(const _Float16* FBb, const h8 (&af)[KSteps<3>::N][1], f32x4 (&acc)[8],
+                                             int wave, int lane) {
+  constexpr int WP = 66, CS = 4;
+  const int g = lane >> 4, l = lane & 15;
+  const _Float16* p = FBb + (2 * wave * WP + 2 * l) * CS;
+  const int o0 = k_offset<3, CS, WP>(0, g, 0), o1 = k_offset<3, CS, WP>(0, g, 1);
+  constexpr int orr = (2 * WP + 2) * CS;
+  const h8 w = af[1][0];
+  const h4 wr = h4{w[0], w[1], w[2], w[3]};
+  // two halves of 4 tiles (the second half's reads in flight under the first half's MFMAs, not all 24 up front)
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    h8 b[4];
+    h4 br[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * hf + j, off = ((i >> 2) * WP + 32 * ((i >> 1) & 1) + (i & 1)) * CS;
+      const h4 lo = *reinterpret_cast<const h4*>(p + off + o0);
+      const h4 hi = *reinterpret_cast<const h4*>(p + off + o1);
+      b[j] = h8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      br[j] = *reinterpret_cast<const h4*>(p + off + orr);
+    }
+    if (hf > 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(acc[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[4 * hf + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[0][0], b[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[4 * hf + j] += __builtin_amdgcn_mfma_f32_16x16x16f16(wr, br[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  }
+}
+
+// Band conv of stages 2 / 3 (Cin 16 / 32, Cout 32, H = 32 / 16) in natural tiles: tile i = (rho = i / TR, k = i % TR),
+// lane l = pixel x = 16 k + l of band row 2 wave + rho (TR = H / 16 tiles per row), A fragments streamed from the LDS
+// weight block ws per K-step (conv_h2 STREAM: the same products in the same K order).  Tin: the whole padded input
+// image, r0: the band's first conv row.
+template <int CIN, int H>
+__device__ __forceinline__ void conv_band_nat(const _Float16* Tin, int r0, const _Float16* ws,
+                                              f32x4 (&acc)[2 * (H / 16)][2], int wave, int lane) {
+  constexpr int CS = Pix<CIN>::CS, WP = H + 2, NT = 2, TR = H / 16, NTL = 2 * TR, KS = KSteps<CIN>::N;
+  constexpr int NF = KSteps<CIN>::NF, cpg = CIN / 8, tpk = 32 / CIN;
+  const int g = lane >> 4, l = lane & 15;
+  const int qb = (r0 + 2 * wave) * WP + l;  // padded pixel of tap 0, row rho = 0, k = 0
+#pragma unroll
+  for (int i = 0; i < NTL; ++i)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[i][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // +16 pixels (tile k + 1) leaves the swizzle bits (bit 2 at 16 channels, bits 1-2 at 32) unchanged: one address
+  // per (rho, K-step), k as an immediate
+#pragma unroll
+  for (int s = 0; s < NF; ++s) {
+    const int tap = s * tpk + g / cpg, tq = (tap / 3) * WP + tap % 3;
+    h8 a[NT], b[NTL];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) a[nt] = *reinterpret_cast<const h8*>(ws + (((s * NT + nt) * 64) + lane) * 8);
+#pragma unroll
+    for (int rho = 0; rho < 2; ++rho) {
+      const int q = qb + rho * WP + tq;
+      const _Float16* pa = Tin + q * CS + (((g % cpg) ^ tsw<CIN>(q)) << 3);
+#pragma unroll
+      for (int k = 0; k < TR; ++k) b[rho * TR + k] = *reinterpret_cast<const h8*>(pa + 16 * k * CS);
+    }
+    if (s > 0) {  // one K-step of reads in flight (conv_h2 STREAM's ordering point)
+#pragma unroll
+      for (int i = 0; i < NTL; ++i)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) asm volatile("" : "+v"(acc[i][nt]));
+    }
+#pragma unroll
+    for (int i = 0; i < NTL; ++i)
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[nt], b[i], acc[i][nt], 0, 0, 0);
+  }
+  if constexpr (KSteps<CIN>::kRem) {  // tap 8 on K = 16 (rem_fragment's lane map), added by VALU
+    const int src = l + 16 * (g >> 1);
+    h4 a[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) a[nt] = *reinterpret_cast<const h4*>(ws + ((((KS - 1) * NT + nt) * 64) + src) * 8 + 4 * (g & 1));
+#pragma unroll
+    for (int rho = 0; rho < 2; ++rho) {
+      const int q = qb + rho * WP + 2 * WP + 2;
+      const _Float16* pa = Tin + q * CS + (((g >> 1) ^ tsw<CIN>(q)) << 3) + 4 * (g & 1);
+#pragma unroll
+      for (int k = 0; k < TR; ++k) {
+        const h4 b = *reinterpret_cast<const h4*>(pa + 16 * k * CS);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[rho * TR + k][nt] += __builtin_amdgcn_mfma_f32_16x16x16f16(a[nt], b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      }
+    }
+  }
+}
+
+// Horizontal 3-wide / stride-2 max of one row value v (natural tiles: lane l = pixel 16 k + l): valid in even lanes
+// (pooled pixel 8 k + l / 2); vp = the row's previous tile (k > 0), whose lane 15 is column 16 k - 1.
+__device__ __forceinline__ float hpool_nat(float v, float vp, bool first) {
+  const float r = dpp_f<kDppShl1>(v, v);                     // column + 1 (lane 15: itself)
+  const float l0 = first ? v : dpp_f<kDppRor1>(v, vp);       // lane 0: column - 1 from the previous tile
+  const float lf = dpp_f<kDppShr1>(l0, v);                   // column - 1
+  return fmaxf(fmaxf(v, r), lf);
+}
+
+// Pool, export, barrier, import, X store of one band (both tile forms).  P: this wave's two rows' horizontal pools
+// combined, B: its second row's; both + bias, rounded to f16.  Pooled row = 8 band + wave.
+// relu(BN(x)) of 4 channels into the next conv's padded image T (to_padded_h's arithmetic: v_fma_mix_f32 on the f16
+// value, rounded, ReLU on f16); sc / sh: the BN table row
+template <int C, int HO>
+__device__ __forceinline__ void t_store_h3(_Float16* T, h4 x, int pr, int px, int ch, const float* sc, const float* sh) {
+  const h2 lo = lo2(x), hi = hi2(x);
+  const h4 t = to_h4(fma_mix_lo(lo, sc[ch], sh[ch]), fma_mix_hi(lo, sc[ch + 1], sh[ch + 1]), fma_mix_lo(hi, sc[ch + 2], sh[ch + 2]),
+                     fma_mix_hi(hi, sc[ch + 3], sh[ch + 3]));
+  *reinterpret_cast<h4*>(T + tidx<C>((pr + 1) * (HO + 2) + px + 1, ch)) = relu_h4(t);
+}
+
+// T: also write relu(BN(pooled)) into the next conv's padded image (sc / sh: its BN row), or nullptr
+template <int COUT, int H, bool EO, int NV>
+__device__ __forceinline__ void band_out_h3(const h4 (&P)[NV], const h4 (&Bx)[NV], h4 (&prev)[NV], _Float16* X,
+                                            _Float16* EX, int band, int wave, int lane, _Float16* T = nullptr,
+                                            const float* sc = nullptr, const float* sh = nullptr) {
+  constexpr int SLOT = (H / 2) * COUT, NT = COUT / 16;
+  const int g = lane >> 4, l = lane & 15;
+  const bool st_lane = EO || (l & 1) == 0;
+  // v = (k, nt): pooled pixel p(k) = EO ? 16 k + l : 8 k + l / 2, channels nt * 16 + 4 g
+  auto pix = [&](int v) { return EO ? 16 * (v / NT) + l : 8 * (v / NT) + (l >> 1); };
+  auto chn = [&](int v) { return (v % NT) * 16 + 4 * g; };
+  _Float16* ex = EX + ((band & 1) * 8 + wave) * SLOT;
+  if (st_lane) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) *reinterpret_cast<h4*>(ex + pix(v) * COUT + chn(v)) = Bx[v];
+  }
+  __syncthreads();
+  h4 o[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) o[v] = P[v];
+  if (wave > 0) {
+    const _Float16* ei = EX + ((band & 1) * 8 + wave - 1) * SLOT;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) o[v] = __builtin_elementwise_max(o[v], *reinterpret_cast<const h4*>(ei + pix(v) * COUT + chn(v)));
+  } else if (band > 0) {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) o[v] = __builtin_elementwise_max(o[v], prev[v]);
+  }
+  if (st_lane) {
+    const int m0 = (8 * band + wave) * (H / 2);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) *reinterpret_cast<h4*>(X + xidx<COUT>(m0 + pix(v), chn(v))) = o[v];
+    if (T) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) t_store_h3<COUT, H / 2>(T, o[v], 8 * band + wave, pix(v), chn(v), sc, sh);
+    }
+  }
+}
+
+// wave 0, band > 0: the previous band's wave-7 slot (row 15), read before this band's barrier -- wave 7 rewrites that
+// slot two bands later, after this band's barrier
+template <int COUT, int H, bool EO, int NV>
+__device__ __forceinline__ void band_prev_h3(h4 (&prev)[NV], const _Float16* EX, int band, int wave, int lane) {
+  constexpr int SLOT = (H / 2) * COUT, NT = COUT / 16;
+  if (wave != 0 || band == 0) return;
+  const int g = lane >> 4, l = lane & 15;
+  const _Float16* ei = EX + (((band - 1) & 1) * 8 + 7) * SLOT;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int p = EO ? 16 * (v / NT) + l : 8 * (v / NT) + (l >> 1);
+    prev[v] = *reinterpret_cast<const h4*>(ei + p * COUT + (v % NT) * 16 + 4 * g);
+  }
+}
+
+// Stage-1 pool of a band (even / odd tiles, 16 channels): P, Bx per pooled tile k (2 per row)
+__device__ __forceinline__ void pool_s1(const f32x4 (&acc)[8], const float (&bz)[1][4], h4 (&P)[2], h4 (&Bx)[2]) {
+  float hp[2][2][4];  // [rho][k][channel]
+#pragma unroll
+  for (int rho = 0; rho < 2; ++rho)
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float e = acc[rho * 4 + k * 2][j], o = acc[rho * 4 + k * 2 + 1][j];
+        const float l0 = k == 0 ? e : dpp_f<kDppRor1>(e, acc[rho * 4 + (k - 1) * 2 + 1][j]);  // lane 0: column 32 k - 1
+        hp[rho][k][j] = fmaxf(fmaxf(e, o), dpp_f<kDppShr1>(l0, o));
+      }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    P[k] = to_h4(fmaxf(hp[0][k][0], hp[1][k][0]) + bz[0][0], fmaxf(hp[0][k][1], hp[1][k][1]) + bz[0][1],
+                 fmaxf(hp[0][k][2], hp[1][k][2]) + bz[0][2], fmaxf(hp[0][k][3], hp[1][k][3]) + bz[0][3]);
+    Bx[k] = to_h4(hp[1][k][0] + bz[0][0], hp[1][k][1] + bz[0][1], hp[1][k][2] + bz[0][2], hp[1][k][3] + bz[0][3]);
+  }
+}
+
+// Stage-2 / 3 pool of a band (natural tiles, 32 channels): v = (k, nt)
+template <int H>
+__device__ __forceinline__ void pool_nat(const f32x4 (&acc)[2 * (H / 16)][2], const float (&bz)[2][4],
+                                         h4 (&P)[2 * (H / 16)], h4 (&Bx)[2 * (H / 16)]) {
+  constexpr int TR = H / 16;
+#pragma unroll
+  for (int k = 0; k < TR; ++k)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      float pv[4], bv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float h0 = hpool_nat(acc[k][nt][j], acc[k > 0 ? k - 1 : 0][nt][j], k == 0);
+        const float h1 = hpool_nat(acc[TR + k][nt][j], acc[TR + (k > 0 ? k - 1 : 0)][nt][j], k == 0);
+        pv[j] = fmaxf(h0, h1) + bz[nt][j];
+        bv[j] = h1 + bz[nt][j];
+      }
+      P[k * 2 + nt] = to_h4(pv[0], pv[1], pv[2], pv[3]);
+      Bx[k * 2 + nt] = to_h4(bv[0], bv[1], bv[2], bv[3]);
+    }
 }
 
 // Two residual blocks, single-buffered (conv -> accumulators -> barrier -> in-place epilogue); the arithmetic
@@ -1053,8 +1295,20 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
 #ifndef FDR_H2_ONE_PER_CU
 #define FDR_H2_ONE_PER_CU 0
 #endif
+#ifndef FDR_H3_ENTRY
+#define FDR_H3_ENTRY 1
+#endif
+#ifdef FDR_H3_FINE  // diagnostics build: clocks inside the h3 entry bands (dbg[64..])
+#define FDR_FINE_STAMP(a, k) FDR_STAMP(a, k)
+#else
+#define FDR_FINE_STAMP(a, k) \
+  do {                       \
+  } while (0)
+#endif
 template <int NTH>
 __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))) void conv_kernel_h2(Layout L, StepArgs a) {
+  constexpr bool H3 = NTH >= 512 && FDR_H3_ENTRY;  // stage entries with the pool in registers
+  static_assert(!H3 || NTH == kHThreads, "h3 entries: 8 waves (zero_border_h's thread count)");
   // experiment: FDR_H2_ONE_PER_CU pads the LDS past half the CU (one workgroup per CU) -- latency sensitivity
   __shared__ __attribute__((aligned(16))) unsigned char smem[kH2LdsBytes + (FDR_H2_ONE_PER_CU ? 4096 : 0)];
   const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
@@ -1106,7 +1360,11 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   }
   const FrameBn fbn{fsc[0], fsc[1], fsc[2], fsh[0], fsh[1], fsh[2]};
   auto FB = [&](int k) { return R + ((k & 1) ? kH2FB1 : kH2FB0); };  // the two frame-band buffers
-  frame_band_h2<NTH>(FB(0), nullptr, 0, -1, a, env, e, fbn);
+  auto FB3 = [&](int k) { return R + ((k & 1) ? kH3FB1 : kH3FB0); };
+  if constexpr (H3)
+    frame_band_h2<NTH, kH3FR>(FB3(0), nullptr, 0, 0, a, env, e, fbn);
+  else
+    frame_band_h2<NTH>(FB(0), nullptr, 0, -1, a, env, e, fbn);
 #pragma unroll
   for (int k = 0; k < kTabIt; ++k) {
     const int bi = threadIdx.x + k * NTH, bidx = bi >> 5, bch = bi & 31;
@@ -1120,8 +1378,28 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   __syncthreads();
   FDR_STAMP(a, 1);
 
-  // ---- stage 1: entry (3 -> 16 at 64 x 64, pooled to 32 x 32) in 8 bands ----
-  {
+  // ---- stage 1: entry (3 -> 16 at 64 x 64, pooled to 32 x 32) in 8 bands (h3: 4 bands, pool in registers) ----
+  if constexpr (H3) {
+    for (int bd = 0; bd < 4; ++bd) {
+      h4 prev[2], P[2], Bx[2];
+      f32x4 acc[8];
+      conv_band_s1(FB3(bd), af3, acc, wave, ln);
+      FDR_FINE_STAMP(a, 64 + 4 * bd);
+      if (bd + 1 < 4) frame_band_h2<NTH, kH3FR>(FB3(bd + 1), FB3(bd), 2, 16 * (bd + 1), a, env, e, fbn);
+      FDR_FINE_STAMP(a, 65 + 4 * bd);
+      float bz[1][4];  // (from the LDS table here, not held across the conv)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) bz[0][k] = bcb[0 * 32 + 4 * (ln >> 4) + k];
+      pool_s1(acc, bz, P, Bx);
+      FDR_FINE_STAMP(a, 66 + 4 * bd);
+      band_prev_h3<16, 64, true>(prev, R + kH3EX1, bd, wave, ln);
+      if (bd == 0) st.template commit<kBlockHalves<16, 1>>(R + kH2WBA);
+      band_out_h3<16, 64, true>(P, Bx, prev, R + kH2X1, R + kH3EX1, bd, wave, ln);
+      FDR_STAMP(a, 2 + bd);
+    }
+    __syncthreads();
+    FDR_STAMP(a, 6);
+  } else {
     float bz[1][4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) bz[0][k] = bcb[0 * 32 + 4 * (ln >> 4) + k];
@@ -1146,8 +1424,43 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     st.template commit<kBlockHalves<16, 2>>(R + kH2WBB);  // X1 is dead: the stage-2 entry block goes to WB_B
     __syncthreads();
   }
-  // ---- stage 2: entry (16 -> 32 at 32 x 32, pooled to 16 x 16) in 4 bands; X2 into T1's consumed rows ----
-  {
+  // ---- stage 2: entry (16 -> 32 at 32 x 32, pooled to 16 x 16) in 4 bands; X2 into T1's consumed rows (h3: 2
+  // bands of 16 rows, pool in registers; band 1 reads padded rows 16..33, past X2's first half) ----
+  if constexpr (H3) {
+    st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
+    for (int bd = 0; bd < 2; ++bd) {
+      h4 prev[4], P[4], Bx[4];
+      f32x4 acc[4][2];
+      conv_band_nat<16, 32>(R, 16 * bd, R + kH2WBB, acc, wave, ln);
+      FDR_FINE_STAMP(a, 80 + 4 * bd);
+      float bz[2][4];
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[5 * 32 + nt * 16 + 4 * (ln >> 4) + k];
+      pool_nat<32>(acc, bz, P, Bx);
+      FDR_FINE_STAMP(a, 81 + 4 * bd);
+      band_prev_h3<32, 32, false>(prev, R + kH3EX2, bd, wave, ln);
+      // (barrier inside).  Band 1 also writes T2 = relu(BN(X2)) of its rows: T2 lies over T1's rows 15.., which band
+      // 1's conv read before that barrier
+      band_out_h3<32, 32, false>(P, Bx, prev, R, R + kH3EX2, bd, wave, ln, bd == 1 ? R + kH2T2 : nullptr,
+                                 bsc + 6 * 32, bsh + 6 * 32);
+      if (bd == 1) st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);   // every wave is past conv 5's reads
+      FDR_STAMP(a, 28 + bd);
+    }
+    // band 0's rows of T2 from the wave's own X2 row (its own stores: no barrier), and T2's zero border
+    if ((ln & 1) == 0) {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int px = 8 * (v >> 1) + ((ln & 15) >> 1), ch = (v & 1) * 16 + 4 * (ln >> 4);
+        t_store_h3<32, 16>(R + kH2T2, *reinterpret_cast<const h4*>(R + xidx<32>(wave * 16 + px, ch)), wave, px, ch,
+                           bsc + 6 * 32, bsh + 6 * 32);
+      }
+    }
+    zero_border_h<32, 16>(R + kH2T2);
+    __syncthreads();  // X2, T2 complete
+    FDR_STAMP(a, 30);
+  } else {
     h8 af[KSteps<16>::N][2];
     constexpr bool ST = NTH >= 512;  // conv 5 streamed from WB_B: conv 6's block is committed after the last band
     if constexpr (!ST) load_af_lds<16, 2>(R + kH2WBB, af, ln);
@@ -1170,17 +1483,37 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     h8 af[KSteps<32>::N][2];
     if constexpr (NTH < 512) load_af_lds<32, 2>(R + kH2WBB, af, ln);
     st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[7]);
-    to_padded_h<32, 16, true, true, NTH>(R, R + kH2T2, bsc + 6 * 32, bsh + 6 * 32);
-    __syncthreads();
-    FDR_STAMP(a, 36);
+    if constexpr (!H3) {  // (h3: T2 written by the entry)
+      to_padded_h<32, 16, true, true, NTH>(R, R + kH2T2, bsc + 6 * 32, bsh + 6 * 32);
+      __syncthreads();
+      FDR_STAMP(a, 36);
+    }
     res_blocks_h2<NTH, 32, 16, 0, kBlockHalves<32, 2>>(R + kH2T2, R, af, hp, L, 1, bsc, bsh, bcb, wave, ln, nullptr, st,
                                                   R + kH2WBB, hp + L.conv_h[10], a, 37);
     st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
     __syncthreads();
   }
   // ---- stage 3: entry (32 -> 32 at 16 x 16, pooled to 8 x 8): one band of 17 rows at 4 waves; at 8 waves (128
-  // VGPRs) two bands of 9, so a wave's accumulators stay at 2 tiles x 2 channel tiles beside the 72 fragment VGPRs ----
-  {
+  // VGPRs) two bands of 9, so a wave's accumulators stay at 2 tiles x 2 channel tiles beside the 72 fragment VGPRs
+  // (h3: one band of 16 rows, pool in registers) ----
+  if constexpr (H3) {
+    st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
+    h4 prev[2], P[2], Bx[2];
+    f32x4 acc[2][2];
+    conv_band_nat<32, 16>(R + kH2T2, 0, R + kH2WBB, acc, wave, ln);
+    float bz[2][4];
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[10 * 32 + nt * 16 + 4 * (ln >> 4) + k];
+    pool_nat<16>(acc, bz, P, Bx);
+    band_out_h3<32, 16, false>(P, Bx, prev, R, R + kH3EX3, 0, wave, ln, R + kH2T3, bsc + 11 * 32, bsh + 11 * 32);
+    zero_border_h<32, 8>(R + kH2T3);
+    st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
+    FDR_STAMP(a, 45);
+    __syncthreads();  // X3, T3 complete
+    FDR_STAMP(a, 46);
+  } else {
     h8 af[KSteps<32>::N][2];
     constexpr bool ST = NTH >= 512;  // conv 10 streamed from WB_B: conv 11's block is committed after the last band
     if constexpr (!ST) load_af_lds<32, 2>(R + kH2WBB, af, ln);
@@ -1204,9 +1537,11 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     h8 af[KSteps<32>::N][2];
     if constexpr (NTH < 512) load_af_lds<32, 2>(R + kH2WBB, af, ln);
     st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[12]);
-    to_padded_h<32, 8, true, true, NTH>(R, R + kH2T3, bsc + 11 * 32, bsh + 11 * 32);
-    __syncthreads();
-    FDR_STAMP(a, 49);
+    if constexpr (!H3) {  // (h3: T3 written by the entry)
+      to_padded_h<32, 8, true, true, NTH>(R, R + kH2T3, bsc + 11 * 32, bsh + 11 * 32);
+      __syncthreads();
+      FDR_STAMP(a, 49);
+    }
     res_blocks_h2<NTH, 32, 8, 1, 0>(R + kH2T3, R, af, hp, L, 2, bsc, bsh, bcb, wave, ln, a.feat + env * kFeat, st,
                                R + kH2WBB, nullptr, a, 50);
   }

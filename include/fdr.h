@@ -428,8 +428,8 @@ int fdr_impala_env_frames(uint64_t env_seed, int32_t n_act, int64_t env_id, int3
 int fdr_impala_profile(int32_t enable);
 int fdr_impala_profile_read(double* ms);
 /* Diagnostics: subsequent fdr_impala_rollout launches write s_memtime clocks of conv workgroup 0 at
- * its phase boundaries into the DEVICE buffer buf (u64[64]: 33 stage/block boundaries, then the
- * fp16 entry-conv band boundaries at 40..63; overwritten each step); NULL = off. */
+ * its phase boundaries into the DEVICE buffer buf (u64[128]: stage / block / entry-band boundaries at
+ * 0..63, diagnostics builds also 64..127; overwritten each step); NULL = off. */
 int fdr_impala_debug_clock(uint64_t* buf);
 /* Entropy replay of fdr_impala_rollout (process-wide, default on): 1 = the x W_ih^T half of the
  * replayed LSTM gates is one MFMA GEMM per lane over 64-step chunks (bit-identical gates; the replay

@@ -15,12 +15,18 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from fdr import engine  # noqa: E402
 
 
-def names():
+def names(h3=False):
     n = {1: "bn table", 18: "stage1 bn -> padded", 36: "stage2 bn -> padded", 49: "stage3 bn -> padded"}
-    for st, base, nb in ((1, 2, 8), (2, 28, 4), (3, 45, 2)):
-        for b in range(nb):
-            n[base + 2 * b] = "stage%d band%d conv" % (st, b)
-            n[base + 2 * b + 1] = "stage%d band%d pool" % (st, b)
+    if h3:  # in-register pool entries: one stamp per band (conv + pool + exchange + X store), one after the stage
+        for st, base, nb in ((1, 2, 4), (2, 28, 2), (3, 45, 1)):
+            for b in range(nb):
+                n[base + b] = "stage%d band%d conv+pool" % (st, b)
+            n[base + nb] = "stage%d entry end" % st
+    else:
+        for st, base, nb in ((1, 2, 8), (2, 28, 4), (3, 45, 2)):
+            for b in range(nb):
+                n[base + 2 * b] = "stage%d band%d conv" % (st, b)
+                n[base + 2 * b + 1] = "stage%d band%d pool" % (st, b)
     for st, base in ((1, 19), (2, 37), (3, 50)):
         for r in range(2):
             for k, what in enumerate(("conv0", "epilogue0", "conv1", "epilogue1")):
@@ -33,6 +39,7 @@ def main():
     ap.add_argument("--lanes", type=int, default=1024)
     ap.add_argument("--envs", type=int, default=4)
     ap.add_argument("--mode", type=int, default=1, help="1: conv_kernel_h2<256>, 2: conv_kernel_h2<512>")
+    ap.add_argument("--old-entry", action="store_true", help="mode 2 built with FDR_H3_ENTRY=0 (banded S image entries)")
     args = ap.parse_args()
     A = 4
     P = engine.impala_num_params(A)
@@ -42,7 +49,7 @@ def main():
     idx = torch.randint(0, 4096, (args.lanes,), dtype=torch.int64).cuda()
     sign = torch.ones(args.lanes, dtype=torch.int8).cuda()
     lanes = engine.lanes_desc(theta, 0, table, idx, sign, 0.02)
-    dbg = torch.zeros(64, dtype=torch.int64).cuda()
+    dbg = torch.zeros(128, dtype=torch.int64).cuda()
     ctx = engine.context()
     ctx.set_conv_h2(args.mode)
     ctx.impala_debug_clock(dbg)
@@ -51,7 +58,7 @@ def main():
     torch.cuda.synchronize()
     ctx.impala_debug_clock(None)
     c = dbg.cpu().numpy().astype(np.int64)
-    n = names()
+    n = names(h3=args.mode == 2 and not args.old_entry)
     order = [0] + sorted(k for k in n if c[k] != 0)  # the 4-wave kernel has one stage-3 band
     tot = c[order[-1]] - c[0]
     print("conv_kernel_h2 (mode %d) workgroup 0: %d clocks total" % (args.mode, tot))
@@ -62,6 +69,15 @@ def main():
         key = " ".join(w for w in n[b].split() if not w.startswith(("band", "res")) or True)
         kind = n[b].split()[-1]
         groups[kind] = groups.get(kind, 0) + d
+    if c[64:].any():  # FDR_H3_FINE build: inside the entry bands (relative to the band's start)
+        for b in range(4):
+            t0 = c[1] if b == 0 else c[1 + b]
+            print("stage1 band%d: conv issued %d, frame %d, pool %d, exchange+barrier+X %d" % (
+                b, c[64 + 4 * b] - t0, c[65 + 4 * b] - c[64 + 4 * b], c[66 + 4 * b] - c[65 + 4 * b], c[2 + b] - c[66 + 4 * b]))
+        for b in range(2):
+            t0 = c[28 + b - 1] if b > 0 else max(c[k] for k in range(19, 27))
+            print("stage2 band%d: conv %d, pool %d, exchange+barrier+X %d" % (
+                b, c[80 + 4 * b] - t0, c[81 + 4 * b] - c[80 + 4 * b], c[28 + b] - c[81 + 4 * b]))
     print("by kind:", ", ".join("%s %d (%.1f%%)" % (k, v, 100.0 * v / tot) for k, v in sorted(groups.items(), key=lambda x: -x[1])))
 
 
