@@ -711,10 +711,11 @@ static_assert(kH2BR * 64 * 16 <= kH2FB0 && 3 * kBnTab * 2 >= 34 * 16, "band scra
 // STREAM (Cin = 32 at 8 waves, where 72 fragment VGPRs do not fit beside the accumulators under 128): the A
 // fragments are read from the LDS weight block ws per K-step (K-outer: both channel tiles' fragments, then every
 // tile's B fragment of that step) instead of af -- the same products in the same K order.
-template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT, int NW, bool STREAM = false>
+// NTA / nt0 (streamed form): the block holds NTA channel tiles, this wave computes tiles nt0 .. nt0 + NT - 1.
+template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT, int NW, bool STREAM = false, int NTA = NT>
 __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSteps<CIN>::N][NT],
                                         f32x4 (&acc)[TPW][NT], int wave, int lane, int qoff = 0,
-                                        const _Float16* ws = nullptr) {
+                                        const _Float16* ws = nullptr, int nt0 = 0) {
   constexpr int KS = KSteps<CIN>::N, NF = KSteps<CIN>::NF;
   // A wave's tiles are wave + NW i: tile i's pixels are tile 0's shifted by DQ i padded pixels (whole rows),
   // so every read is one of NF per-lane addresses plus an immediate.  The chunk swizzle of q + DQ i is the
@@ -752,7 +753,7 @@ __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSte
     for (int s = 0; s < NF; ++s) {
       h8 a[NT], b[TPW];
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) a[nt] = *reinterpret_cast<const h8*>(ws + (((s * NT + nt) * 64) + lane) * 8);
+      for (int nt = 0; nt < NT; ++nt) a[nt] = *reinterpret_cast<const h8*>(ws + (((s * NTA + nt0 + nt) * 64) + lane) * 8);
 #pragma unroll
       for (int i = 0; i < TPW; ++i)
         if (live(i)) b[i] = *reinterpret_cast<const h8*>(Tin + DQ * i * CS + off[s] + ((sw[s] ^ flip(i)) << 3));
@@ -776,7 +777,7 @@ __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSte
       h4 a[NT];
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt)
-        a[nt] = *reinterpret_cast<const h4*>(ws + ((((KS - 1) * NT + nt) * 64) + src) * 8 + 4 * (g & 1));
+        a[nt] = *reinterpret_cast<const h4*>(ws + ((((KS - 1) * NTA + nt0 + nt) * 64) + src) * 8 + 4 * (g & 1));
 #pragma unroll
       for (int i = 0; i < TPW; ++i) {
         if (!live(i)) continue;
@@ -1182,15 +1183,28 @@ __device__ __forceinline__ void pool_nat(const f32x4 (&acc)[2 * (H / 16)][2], co
 // commit only after a barrier that follows every wave's fragment load of the previous block.  On exit T holds
 // the next stage's input (or the features are written, LAST), and st holds the issued next-stage block (NEXTH
 // halves; committed by the caller, whose WB may differ).
+#ifndef FDR_H2_SPLIT
+#define FDR_H2_SPLIT 1
+#endif
 template <int NTH, int C, int H, int LAST, int NEXTH>
 __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)[KSteps<C>::N][C / 16],
                                               const _Float16* __restrict__ hp, const Layout& L, int stage,
                                               const float* bsc, const float* bsh, const float* bcb, int wave, int lane,
                                               float* __restrict__ out, WStageT<NTH>& st, _Float16* wb,
                                               const _Float16* __restrict__ next_w, const StepArgs& a, int stamp) {
-  constexpr int CS = Pix<C>::CS, WP = H + 2, NT = C / 16, MT = H * H / 16, NW = NTH / 64;
+  constexpr int CS = Pix<C>::CS, WP = H + 2, NTA = C / 16, MT = H * H / 16, NWA = NTH / 64;
   constexpr bool ST = NTH >= 512 && C == 32;  // A fragments streamed from wb (conv_h2 STREAM); af unused
+  // SPLIT (8 x 8 stage at 8 waves: 4 pixel tiles x 2 channel tiles): wave = (pixel tile w % 4, channel tile w / 4), so
+  // every wave runs one MFMA per K-step and streams only its own channel tile's A fragments (without it waves 4-7
+  // had no tile but still read both channel tiles' fragments)
+  constexpr int SPLIT = FDR_H2_SPLIT && ST && MT * NTA == NWA ? NTA : 1;
+  static_assert(SPLIT == 1 || (MT == 4 && NTA == 2), "split map");
+  constexpr int NT = NTA / SPLIT, NW = NWA / SPLIT;
+  const int nt0 = SPLIT > 1 ? (wave / NW) * NT : 0;
+  wave = SPLIT > 1 ? wave % NW : wave;
   constexpr int TPW = (MT + NW - 1) / NW, WH = kBlockHalves<C, C / 16>;
+  // conv_h2's fragment argument (unread in the streamed form, which every SPLIT > 1 instance is)
+  auto& afw = reinterpret_cast<h8 (&)[KSteps<C>::N][NT]>(af);
   // Epilogue addresses: tile i's pixels are tile 0's + 16 NW i (X, S: the chunk swizzle is unchanged by that
   // step) and padded pixel + DQ i (T: the swizzle flips by tflip(i), conv_h2's step) -- per-lane bases + immediates.
   constexpr int DQ = H >= 16 ? (NW / (H / 16)) * WP : NW * (16 / H) * WP;
@@ -1201,7 +1215,7 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
   int xb[NT], tb[NT][2];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) {
-    const int ch0 = nt * 16 + cl;
+    const int ch0 = (nt0 + nt) * 16 + cl;
     xb[nt] = xidx<C>(m0, ch0);
     tb[nt][0] = tidx<C>(q0, ch0);
     tb[nt][1] = q0 * CS + ((((ch0 >> 3) ^ tsw<C>(q0)) ^ 1) << 3) + (ch0 & 7);
@@ -1225,14 +1239,14 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
     float b0[NT][4], s1[NT][4], t1[NT][4], b1[NT][4], s2[NT][4], t2[NT][4];
     f32x4 acc[TPW][NT];
     // ---- conv0: T -> T (relu(bn1(. + b0))) ----
-    conv_h2<C, CS, NT, TPW, H, WP, MT, NW, ST>(T, af, acc, wave, lane, 0, wb);
+    conv_h2<C, CS, NT, TPW, H, WP, MT, NW, ST, NTA>(T, afw, acc, wave, lane, 0, wb, nt0);
     __syncthreads();  // every wave has read T
     FDR_STAMP(a, stamp + 4 * r);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int ch = nt * 16 + cl + k;
+        const int ch = (nt0 + nt) * 16 + cl + k;
         b0[nt][k] = bcb[i0 * 32 + ch];
         s1[nt][k] = bsc[i1 * 32 + ch];
         t1[nt][k] = bsh[i1 * 32 + ch];
@@ -1253,14 +1267,14 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
       st.template issue<NEXTH>(next_w);
     }
     // ---- conv1: T -> X += . + b1; T <- bn(X) (relu before a block) ----
-    conv_h2<C, CS, NT, TPW, H, WP, MT, NW, ST>(T, af, acc, wave, lane, 0, wb);
+    conv_h2<C, CS, NT, TPW, H, WP, MT, NW, ST, NTA>(T, afw, acc, wave, lane, 0, wb, nt0);
     __syncthreads();
     FDR_STAMP(a, stamp + 4 * r + 2);
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int ch = nt * 16 + cl + k;
+        const int ch = (nt0 + nt) * 16 + cl + k;
         b1[nt][k] = bcb[i1 * 32 + ch];
         s2[nt][k] = (r == 1 && LAST) ? 0.f : bsc[inext * 32 + ch];
         t2[nt][k] = (r == 1 && LAST) ? 0.f : bsh[inext * 32 + ch];
@@ -1273,7 +1287,7 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
                           fma_mix_lo(xh, 1.f, v[2] + b1[nt][2]), fma_mix_hi(xh, 1.f, v[3] + b1[nt][3]));
       if (r == 1 && LAST) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) out[(nt * 16 + cl + k) * H * H + m] = relu((float)xn[k]);  // flatten (C,H,W)
+        for (int k = 0; k < 4; ++k) out[((nt0 + nt) * 16 + cl + k) * H * H + m] = relu((float)xn[k]);  // flatten (C,H,W)
       } else {
         if (r == 0) *reinterpret_cast<h4*>(X + xo_) = xn;
         const h2 nl = lo2(xn), nh = hi2(xn);
