@@ -12,9 +12,7 @@ step() {  # step <name> <timeout> <cmd...>
   if grep -qE "$FAULT" "gpurun_out/$name.log"; then echo "GPU FAULT in $name -- stopping"; exit 3; fi
   [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ] || exit "$rc"   # 1 = test failures, not a fault
 }
-step dist_single 300 python tools/dist_check.py single
-step dist_multi 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 tools/dist_check.py multi
-step dist_compare 60 python tools/dist_check.py compare
+# (N-rank == 1-rank: tests/test_gpu_dist_equivalence.py drives tools/dist_check.py inside the suite)
 step pytest_gpu 900 python -m pytest tests -m gpu -q -rf
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py "$@"
