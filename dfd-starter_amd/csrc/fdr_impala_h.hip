@@ -116,14 +116,15 @@ __device__ __forceinline__ void load_af(const _Float16* __restrict__ wf, h8 (&af
   rem_fragment<CIN, NT>(wf, af, lane);
 }
 
-// The same fragments from the workgroup's LDS copy of the block (layout identical to the pack's).
-template <int CIN, int NT>
+// The same fragments from the workgroup's LDS copy of the block (layout identical to the pack's).  R32: the last
+// fragment stays in the pack's K = 32 layout (tap 8 + zeros; conv_h2 R32).
+template <int CIN, int NT, bool R32 = false>
 __device__ __forceinline__ void load_af_lds(const _Float16* wb, h8 (&af)[KSteps<CIN>::N][NT], int lane) {
 #pragma unroll
   for (int s = 0; s < KSteps<CIN>::N; ++s)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) af[s][nt] = *reinterpret_cast<const h8*>(wb + (((s * NT + nt) * 64) + lane) * 8);
-  rem_fragment<CIN, NT>(wb, af, lane);
+  if constexpr (!R32) rem_fragment<CIN, NT>(wb, af, lane);
 }
 template <int CIN, int NT>
 constexpr int kBlockHalves = KSteps<CIN>::N * NT * 64 * 8;
@@ -712,7 +713,15 @@ static_assert(kH2BR * 64 * 16 <= kH2FB0 && 3 * kBnTab * 2 >= 34 * 16, "band scra
 // fragments are read from the LDS weight block ws per K-step (K-outer: both channel tiles' fragments, then every
 // tile's B fragment of that step) instead of af -- the same products in the same K order.
 // NTA / nt0 (streamed form): the block holds NTA channel tiles, this wave computes tiles nt0 .. nt0 + NT - 1.
-template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT, int NW, bool STREAM = false, int NTA = NT>
+#ifndef FDR_R32
+#define FDR_R32 1
+#endif
+// R32 (conv_kernel_h2<512>, FDR_R32): the tap-8 remainder runs as one more v_mfma_f32_16x16x32_f16 on the pack's K = 32
+// fragment (tap 8 + zeros) chained onto the accumulator -- a K = 16 MFMA takes the same 16-clock slot
+// (profiles/r08a_mfma_rate_probe.txt), and the separate accumulator's VALU add (the K = 16 product cannot be chained:
+// DESIGN.md 3.4 SrcC) and its registers go.  The sums differ from conv_h's in rounding only.
+template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT, int NW, bool STREAM = false, int NTA = NT,
+          bool R32 = false>
 __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSteps<CIN>::N][NT],
                                         f32x4 (&acc)[TPW][NT], int wave, int lane, int qoff = 0,
                                         const _Float16* ws = nullptr, int nt0 = 0) {
@@ -743,6 +752,8 @@ __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSte
   const int qr = base + 2 * WP + 2;  // tap 8
   const int offr = CIN == 3 ? qr * CS : qr * CS + 4 * (g & 1);
   const int swr = CIN == 3 ? 0 : (g >> 1) ^ tsw<CIN>(qr + qoff);
+  const int offr32 = qr * CS, swr32 = CIN == 3 ? 0 : (g & 1) ^ tsw<CIN>(qr + qoff);
+  (void)offr32, (void)swr32;
   if constexpr (STREAM) {
     static_assert(CIN == 32 || CIN == 16, "streamed fragments: Cin = 16 / 32");
 #pragma unroll
@@ -808,7 +819,13 @@ __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSte
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b, acc[i][nt], 0, 0, 0);
       }
-      if constexpr (KSteps<CIN>::kRem) {  // tap 8 on K = 16, added by VALU (conv_h's note)
+      if constexpr (KSteps<CIN>::kRem && R32) {  // tap 8 + zeros on K = 32, chained
+        static_assert(CIN == 16, "R32: the 16-channel residual convs");
+        // lane group g: tap 8's chunk g & 1 (groups 2, 3 meet the fragment's zeros)
+        const h8 b = *reinterpret_cast<const h8*>(Ti + offr32 + ((swr32 ^ flip(i)) << 3));
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[KS - 1][nt], b, acc[i][nt], 0, 0, 0);
+      } else if constexpr (KSteps<CIN>::kRem) {  // tap 8 on K = 16, added by VALU (conv_h's note)
         const h4 b = *reinterpret_cast<const h4*>(Ti + offr + (CIN == 3 ? 0 : (swr ^ flip(i)) << 3));
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
@@ -994,8 +1011,15 @@ __device__ __forceinline__ void conv_band_s1(const _Float16* FBb, const h8 (&af)
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[4 * hf + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[0][0], b[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    if constexpr (FDR_R32) {  // tap 8 on the K = 32 fragment (lane group 0's halves 0..3; zeros elsewhere), chained
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[4 * hf + j] += __builtin_amdgcn_mfma_f32_16x16x16f16(wr, br[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      for (int j = 0; j < 4; ++j)
+        acc[4 * hf + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[1][0], h8{br[j][0], br[j][1], br[j][2], br[j][3], br[j][0], br[j][1], br[j][2], br[j][3]},
+                                                                 acc[4 * hf + j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[4 * hf + j] += __builtin_amdgcn_mfma_f32_16x16x16f16(wr, br[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    }
   }
 }
 
@@ -1040,7 +1064,23 @@ __device__ __forceinline__ void conv_band_nat(const _Float16* Tin, int r0, const
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[nt], b[i], acc[i][nt], 0, 0, 0);
   }
-  if constexpr (KSteps<CIN>::kRem) {  // tap 8 on K = 16 (rem_fragment's lane map), added by VALU
+  if constexpr (KSteps<CIN>::kRem && FDR_R32) {  // tap 8 + zeros on K = 32 (the pack's fragment), chained
+    h8 a[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) a[nt] = *reinterpret_cast<const h8*>(ws + ((((KS - 1) * NT + nt) * 64) + lane) * 8);
+#pragma unroll
+    for (int rho = 0; rho < 2; ++rho) {
+      const int q = qb + rho * WP + 2 * WP + 2;
+      const _Float16* pa = Tin + q * CS + (((g & 1) ^ tsw<CIN>(q)) << 3);
+#pragma unroll
+      for (int k = 0; k < TR; ++k) {
+        const h8 b = *reinterpret_cast<const h8*>(pa + 16 * k * CS);
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+          acc[rho * TR + k][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[nt], b, acc[rho * TR + k][nt], 0, 0, 0);
+      }
+    }
+  } else if constexpr (KSteps<CIN>::kRem) {  // tap 8 on K = 16 (rem_fragment's lane map), added by VALU
     const int src = l + 16 * (g >> 1);
     h4 a[NT];
 #pragma unroll
@@ -1081,6 +1121,16 @@ __device__ __forceinline__ void t_store_h3(_Float16* T, h4 x, int pr, int px, in
   *reinterpret_cast<h4*>(T + tidx<C>((pr + 1) * (HO + 2) + px + 1, ch)) = relu_h4(t);
 }
 
+// Exchange-slot entry (halves) of 4 channels ch .. ch + 3 of pooled pixel p (PX pooled pixels per row): channel-group-
+// major, so a 16-lane group's b64 stores (one channel group, 16 consecutive pixels) are contiguous; with 32 pixels the
+// odd groups flip pixel bit 4, so the b64 reads' 32-lane groups (channel groups 2j, 2j + 1) use disjoint banks
+// (tools/lds_model/h3_model.py: pixel-major slots were 4-way on the stores).
+template <int PX>
+__device__ __forceinline__ int ex_idx(int p, int ch) {
+  const int cg = ch >> 2;
+  return (cg * PX + (PX >= 32 ? p ^ ((cg & 1) << 4) : p)) * 4;
+}
+
 // T: also write relu(BN(pooled)) into the next conv's padded image (sc / sh: its BN row), or nullptr
 template <int COUT, int H, bool EO, int NV>
 __device__ __forceinline__ void band_out_h3(const h4 (&P)[NV], const h4 (&Bx)[NV], h4 (&prev)[NV], _Float16* X,
@@ -1095,7 +1145,7 @@ __device__ __forceinline__ void band_out_h3(const h4 (&P)[NV], const h4 (&Bx)[NV
   _Float16* ex = EX + ((band & 1) * 8 + wave) * SLOT;
   if (st_lane) {
 #pragma unroll
-    for (int v = 0; v < NV; ++v) *reinterpret_cast<h4*>(ex + pix(v) * COUT + chn(v)) = Bx[v];
+    for (int v = 0; v < NV; ++v) *reinterpret_cast<h4*>(ex + ex_idx<H / 2>(pix(v), chn(v))) = Bx[v];
   }
   __syncthreads();
   h4 o[NV];
@@ -1104,7 +1154,7 @@ __device__ __forceinline__ void band_out_h3(const h4 (&P)[NV], const h4 (&Bx)[NV
   if (wave > 0) {
     const _Float16* ei = EX + ((band & 1) * 8 + wave - 1) * SLOT;
 #pragma unroll
-    for (int v = 0; v < NV; ++v) o[v] = __builtin_elementwise_max(o[v], *reinterpret_cast<const h4*>(ei + pix(v) * COUT + chn(v)));
+    for (int v = 0; v < NV; ++v) o[v] = __builtin_elementwise_max(o[v], *reinterpret_cast<const h4*>(ei + ex_idx<H / 2>(pix(v), chn(v))));
   } else if (band > 0) {
 #pragma unroll
     for (int v = 0; v < NV; ++v) o[v] = __builtin_elementwise_max(o[v], prev[v]);
@@ -1131,7 +1181,7 @@ __device__ __forceinline__ void band_prev_h3(h4 (&prev)[NV], const _Float16* EX,
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int p = EO ? 16 * (v / NT) + l : 8 * (v / NT) + (l >> 1);
-    prev[v] = *reinterpret_cast<const h4*>(ei + p * COUT + (v % NT) * 16 + 4 * g);
+    prev[v] = *reinterpret_cast<const h4*>(ei + ex_idx<H / 2>(p, (v % NT) * 16 + 4 * g));
   }
 }
 
@@ -1186,6 +1236,7 @@ __device__ __forceinline__ void pool_nat(const f32x4 (&acc)[2 * (H / 16)][2], co
 #ifndef FDR_H2_SPLIT
 #define FDR_H2_SPLIT 1
 #endif
+
 template <int NTH, int C, int H, int LAST, int NEXTH>
 __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)[KSteps<C>::N][C / 16],
                                               const _Float16* __restrict__ hp, const Layout& L, int stage,
@@ -1194,6 +1245,7 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
                                               const _Float16* __restrict__ next_w, const StepArgs& a, int stamp) {
   constexpr int CS = Pix<C>::CS, WP = H + 2, NTA = C / 16, MT = H * H / 16, NWA = NTH / 64;
   constexpr bool ST = NTH >= 512 && C == 32;  // A fragments streamed from wb (conv_h2 STREAM); af unused
+  constexpr bool R32 = NTH >= 512 && C == 16 && FDR_R32;  // tap 8 as a chained K = 32 MFMA (conv_h2 R32)
   // SPLIT (8 x 8 stage at 8 waves: 4 pixel tiles x 2 channel tiles): wave = (pixel tile w % 4, channel tile w / 4), so
   // every wave runs one MFMA per K-step and streams only its own channel tile's A fragments (without it waves 4-7
   // had no tile but still read both channel tiles' fragments)
@@ -1239,7 +1291,7 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
     float b0[NT][4], s1[NT][4], t1[NT][4], b1[NT][4], s2[NT][4], t2[NT][4];
     f32x4 acc[TPW][NT];
     // ---- conv0: T -> T (relu(bn1(. + b0))) ----
-    conv_h2<C, CS, NT, TPW, H, WP, MT, NW, ST, NTA>(T, afw, acc, wave, lane, 0, wb, nt0);
+    conv_h2<C, CS, NT, TPW, H, WP, MT, NW, ST, NTA, R32>(T, afw, acc, wave, lane, 0, wb, nt0);
     __syncthreads();  // every wave has read T
     FDR_STAMP(a, stamp + 4 * r);
 #pragma unroll
@@ -1260,14 +1312,14 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
     st.template commit<WH>(wb);  // conv i1 (every wave loaded conv i0's fragments before the barrier above)
     __syncthreads();
     FDR_STAMP(a, stamp + 4 * r + 1);
-    if constexpr (!ST) load_af_lds<C, NT>(wb, af, lane);
+    if constexpr (!ST) load_af_lds<C, NT, R32>(wb, af, lane);
     if (r == 0) {
       st.template issue<WH>(hp + L.conv_h[i1 + 1]);  // block 1 conv0 (committed after the next barrier)
     } else if constexpr (NEXTH > 0) {
       st.template issue<NEXTH>(next_w);
     }
     // ---- conv1: T -> X += . + b1; T <- bn(X) (relu before a block) ----
-    conv_h2<C, CS, NT, TPW, H, WP, MT, NW, ST, NTA>(T, afw, acc, wave, lane, 0, wb, nt0);
+    conv_h2<C, CS, NT, TPW, H, WP, MT, NW, ST, NTA, R32>(T, afw, acc, wave, lane, 0, wb, nt0);
     __syncthreads();
     FDR_STAMP(a, stamp + 4 * r + 2);
 #pragma unroll
@@ -1300,7 +1352,7 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
     __syncthreads();
     FDR_STAMP(a, stamp + 4 * r + 3);
     if (r == 0) {
-      if constexpr (!ST) load_af_lds<C, NT>(wb, af, lane);
+      if constexpr (!ST) load_af_lds<C, NT, R32>(wb, af, lane);
       st.template issue<WH>(hp + L.conv_h[i1 + 2]);  // block 1 conv1 (committed after the next barrier)
     }
   }
@@ -1333,6 +1385,13 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     for (int k = 0; k < FDR_H2_STAGGER / 8000; ++k) __builtin_amdgcn_s_sleep(125);
 #endif
   FDR_STAMP(a, 0);
+#ifdef FDR_WG_TIMELINE  // diagnostics build: every workgroup's start / end (s_memrealtime, 100 MHz) and HW_ID / XCC_ID
+  if (a.dbg && threadIdx.x == 0) {
+    a.dbg[256 + 4 * b] = wall_clock64();
+    a.dbg[256 + 4 * b + 2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    a.dbg[256 + 4 * b + 3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+  }
+#endif
   const int wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
   const int64_t env = (int64_t)lane * a.envs + e;
   const float* pk = a.pack + (int64_t)lane * a.pack_stride;
@@ -1428,7 +1487,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   // ---- stage 1 residual blocks (16 ch, 32 x 32) ----
   {
     h8 af[KSteps<16>::N][1];
-    load_af_lds<16, 1>(R + kH2WBA, af, ln);
+    load_af_lds<16, 1, NTH >= 512 && FDR_R32>(R + kH2WBA, af, ln);
     st.template issue<kBlockHalves<16, 1>>(hp + L.conv_h[2]);
     to_padded_h<16, 32, true, true, NTH>(R + kH2X1, R, bsc + 1 * 32, bsh + 1 * 32);
     __syncthreads();
@@ -1559,6 +1618,10 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     res_blocks_h2<NTH, 32, 8, 1, 0>(R + kH2T3, R, af, hp, L, 2, bsc, bsh, bcb, wave, ln, a.feat + env * kFeat, st,
                                R + kH2WBB, nullptr, a, 50);
   }
+#ifdef FDR_WG_TIMELINE
+  __syncthreads();
+  if (a.dbg && threadIdx.x == 0) a.dbg[256 + 4 * b + 1] = wall_clock64();
+#endif
 }
 template __global__ void conv_kernel_h2<256>(Layout, StepArgs);
 template __global__ void conv_kernel_h2<512>(Layout, StepArgs);

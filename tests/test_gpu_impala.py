@@ -488,9 +488,16 @@ def test_conv_h2_bit_identical_to_conv_h(engine, table):
     finally:
         ctx.set_conv_h2(prior)
     assert np.abs(res[1][1]).max() > 0 and np.all(np.isfinite(res[1][1]))
-    for mode in (1, 2):
-        for a, b in zip(res[0], res[mode]):
-            np.testing.assert_array_equal(a, b)
+    for a, b in zip(res[0], res[1]):
+        np.testing.assert_array_equal(a, b)
+    # conv_kernel_h2<512> runs the tap-8 remainder as a chained K = 32 MFMA (FDR_R32): the same products, summed in
+    # another order -- forward probabilities / features / LSTM state and strategies within rounding of conv_kernel_h
+    # (the recorded rollout's sampled actions may then differ; its parity is the oracle tests' subject)
+    nfw = 12
+    for i, (a, b) in enumerate(zip(res[0][:nfw] + res[0][-1:], res[2][:nfw] + res[2][-1:])):
+        scale = max(1.0, float(np.abs(a).max()))
+        err = float(np.abs(a - b).max()) / scale
+        assert err < 2e-3, (i, err)
 
 
 @pytest.mark.parametrize("fp16,pairs", [(False, False), (False, True), (True, False), (True, True)])
@@ -549,3 +556,4 @@ def test_full_size_rollout_properties(engine, fp16, pairs):
     print("full size fp16=%s pairs=%s: max |dp| %.3g, max rel d(ent) %.3g, %d / %d explained action flips"
           % (fp16, pairs, dp, de, amb, len(sample) * E * T))
     assert amb <= (0.01 if fp16 else 0.001) * len(sample) * E * T
+
