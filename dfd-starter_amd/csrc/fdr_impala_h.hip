@@ -135,24 +135,35 @@ constexpr int kBlockHalves = KSteps<CIN>::N * NT * 64 * 8;
 // in phase k+1 or later, read it in a phase after the commit.
 template <int NTH>
 struct WStageT {
-  u32x4 r[(kWB / 8 + NTH - 1) / NTH];
+  // a block = NC 16-B chunks: NC / NTH full rounds of one chunk per thread in r[], and the remainder REM = NC % NTH
+  // either as one more chunk for threads < REM (rq) or, when it fits, as one dword per thread (rd): the 32 -> 32
+  // blocks' 1,152 chunks over 512 threads then take 2 chunks + 1 dword = 9 VGPRs, not 12 (the 12th..9th were
+  // spilled right behind their global load, which stalled the issuing wave on the load)
+  static constexpr int kMaxFull = (kWB / 8) / NTH;
+  u32x4 r[kMaxFull > 0 ? kMaxFull : 1];
+  u32x4 rq;
+  uint32_t rd;
   template <int NH>
   __device__ __forceinline__ void issue(const _Float16* __restrict__ src) {
-    constexpr int NC = NH / 8, PER = (NC + NTH - 1) / NTH;
-    static_assert(NH % 8 == 0 && NH <= kWB, "weight block");
+    constexpr int NC = NH / 8, PERF = NC / NTH, REM = NC % NTH;
+    static_assert(NH % 8 == 0 && NH <= kWB && PERF <= kMaxFull, "weight block");
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int c = threadIdx.x + k * NTH;  // past the block: reload its last chunk (not stored)
-      r[k] = reinterpret_cast<const u32x4*>(src)[NC % NTH == 0 || c < NC ? c : NC - 1];
+    for (int k = 0; k < PERF; ++k) r[k] = reinterpret_cast<const u32x4*>(src)[threadIdx.x + k * NTH];
+    if constexpr (REM > 0 && REM * 4 <= NTH) {  // (branch-free: the clamped re-read is not stored)
+      rd = reinterpret_cast<const uint32_t*>(src + PERF * NTH * 8)[min((int)threadIdx.x, REM * 4 - 1)];
+    } else if constexpr (REM > 0) {
+      rq = reinterpret_cast<const u32x4*>(src)[PERF * NTH + min((int)threadIdx.x, REM - 1)];
     }
   }
   template <int NH>
   __device__ __forceinline__ void commit(_Float16* wb) const {
-    constexpr int NC = NH / 8, PER = (NC + NTH - 1) / NTH;
+    constexpr int NC = NH / 8, PERF = NC / NTH, REM = NC % NTH;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int c = threadIdx.x + k * NTH;
-      if (NC % NTH == 0 || c < NC) reinterpret_cast<u32x4*>(wb)[c] = r[k];
+    for (int k = 0; k < PERF; ++k) reinterpret_cast<u32x4*>(wb)[threadIdx.x + k * NTH] = r[k];
+    if constexpr (REM > 0 && REM * 4 <= NTH) {
+      if ((int)threadIdx.x < REM * 4) reinterpret_cast<uint32_t*>(wb + PERF * NTH * 8)[threadIdx.x] = rd;
+    } else if constexpr (REM > 0) {
+      if ((int)threadIdx.x < REM) reinterpret_cast<u32x4*>(wb)[PERF * NTH + threadIdx.x] = rq;
     }
   }
 };
@@ -1392,7 +1403,8 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     a.dbg[256 + 4 * b + 3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);
   }
 #endif
-  const int wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
+  // wave index in an SGPR: every wave-uniform tile / address term derived from it stays scalar (VGPR pressure)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
   const int64_t env = (int64_t)lane * a.envs + e;
   const float* pk = a.pack + (int64_t)lane * a.pack_stride;
   const _Float16* hp = a.hpack + (int64_t)lane * a.hpack_stride;
