@@ -24,5 +24,5 @@ if "SQ_LDS_IDX_ACTIVE" in m:
           "LDS wave-instructions per env %.0f" % (
               m["SQ_LDS_IDX_ACTIVE"] / 256 / clk, m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"],
               m["SQ_LDS_IDX_ACTIVE"] / envs, m["SQ_LDS_BANK_CONFLICT"] / envs, m.get("SQ_INSTS_LDS", 0) / envs))
-if "SQ_ACTIVE_INST_VALU" in m:
-    print("VALU active per SIMD %.3f" % (m["SQ_ACTIVE_INST_VALU"] / 1024 / clk))
+if "SQ_ACTIVE_INST_VALU" in m:  # SQ wave counters count quad-cycles
+    print("VALU active per SIMD %.3f" % (4 * m["SQ_ACTIVE_INST_VALU"] / 1024 / clk))
