@@ -977,7 +977,9 @@ __device__ __forceinline__ void entry_band_h2(const _Float16* Tin, int qoff, _Fl
 // -----------------------------------------------------------------------------------------------------
 constexpr int kH3FR = 18;                              // padded frame rows per stage-1 band (16 conv rows + 2)
 constexpr int kH3FB = kH3FR * 66 * 4;                  // halves
-constexpr int kH3FB0 = 0, kH3FB1 = kH3FB, kH3EX1 = 2 * kH3FB;   // stage 1: FB0 | FB1 | EX (16 slots x 512)
+// stage 1: FB0 | pad pixel | FB1 | pad pixel | EX (16 slots x 512).  The pad pixels (zeroed per env) are what the
+// last buffer row's column-66 read of conv_band_s1's tap pairs (kx 2, 3 = zero weight) meets: finite zeros
+constexpr int kH3FB0 = 0, kH3FB1 = kH3FB + 8, kH3EX1 = 2 * kH3FB + 16;
 constexpr int kH3EX2 = 18560, kH3EX3 = 18560;          // stages 2 / 3: EX after T2's extent
 static_assert(kH3EX1 + 16 * 512 <= kH2X1, "stage 1 h3 map");
 static_assert(kH3EX2 + 16 * 512 <= kH2WBB && kH3EX3 + 8 * 256 <= kH2WBB, "stage 2/3 h3 map");
@@ -992,45 +994,74 @@ constexpr int kDppShl1 = 0x101, kDppShr1 = 0x111, kDppRor1 = 0x121;
 // Stage-1 band conv (Cin 3 -> 16 at 64 x 64) in even / odd pixel tiles: tile i = (rho = i >> 2, k = (i >> 1) & 1,
 // par = i & 1) holds, in lane l, the 16 channels of pixel x = 2 (16 k + l) + par of band row 2 wave + rho -- so a
 // pooled pixel's three columns 2p - 1, 2p, 2p + 1 are in one lane (even, odd tile) and its left neighbour (odd tile,
-// one lane down).  FBb: the band's padded frame rows [18][66][4].  conv_h's K order: taps 0..7 on K = 32, tap 8 on
-// K = 16 into its own accumulator, added.
-__device__ __forceinline__ void conv_band_s1(const _Float16* FBb, const h8 (&af)[KSteps<3>::N][1], f32x4 (&acc)[8],
-                                             int wave, int lane) {
+// one lane down).  FBb: the band's padded frame rows [18][66][4].
+// K order (s1_frag): every lane group's two taps of a K-step are horizontally adjacent, (ky, kx0) and (ky, kx0 + 1),
+// so a lane's B fragment is 16 contiguous bytes (one ds_read2_b64 into the operand registers, no assembly moves):
+// K-step 0 = groups (0,0)(0,1) | (1,0)(1,1) | (2,0)(2,1) | (0,2)(0,3); K-step 1 = (1,2)(1,3) | (2,2)(2,3) | - | -.
+// Column-3 taps and the empty groups carry zero weights (their B reads are finite pixels: pads and the buffers' pad
+// pixel).  Both K-steps chain on one accumulator (same opcode).
+__device__ __forceinline__ void s1_tap(int s, int g, int& ky, int& kx0) {
+  if (s == 0) {
+    ky = g < 3 ? g : 0;
+    kx0 = g < 3 ? 0 : 2;
+  } else {
+    ky = g == 1 ? 2 : 1;
+    kx0 = 2;
+  }
+}
+// A fragments in that order, gathered per lane from the pack's K order (conv_h's: group g holds taps 2g, 2g + 1 of
+// K-step t / 8; tap 8 in K-step 1, group 0)
+__device__ __forceinline__ void s1_frag(const _Float16* __restrict__ w, h8 (&af)[2], int lane) {
+  const int g = lane >> 4, m = lane & 15;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    int ky, kx0;
+    s1_tap(s, g, ky, kx0);
+    h4 part[2];
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const int kx = kx0 + pp, t = 3 * ky + kx;
+      const bool valid = kx <= 2 && (s == 0 || g < 2);
+      const int tt = valid ? t : 0;
+      const h4 v = *reinterpret_cast<const h4*>(w + (((tt >> 3) * 64) + m + 16 * ((tt & 7) >> 1)) * 8 + 4 * (tt & 1));
+      part[pp] = valid ? v : h4{0, 0, 0, 0};
+    }
+    af[s] = h8{part[0][0], part[0][1], part[0][2], part[0][3], part[1][0], part[1][1], part[1][2], part[1][3]};
+  }
+}
+__device__ __forceinline__ void conv_band_s1(const _Float16* FBb, const h8 (&af)[2], f32x4 (&acc)[8], int wave, int lane) {
   constexpr int WP = 66, CS = 4;
   const int g = lane >> 4, l = lane & 15;
   const _Float16* p = FBb + (2 * wave * WP + 2 * l) * CS;
-  const int o0 = k_offset<3, CS, WP>(0, g, 0), o1 = k_offset<3, CS, WP>(0, g, 1);
-  constexpr int orr = (2 * WP + 2) * CS;
-  const h8 w = af[1][0];
-  const h4 wr = h4{w[0], w[1], w[2], w[3]};
-  // two halves of 4 tiles (the second half's reads in flight under the first half's MFMAs, not all 24 up front)
+  int o[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    int ky, kx0;
+    s1_tap(s, g, ky, kx0);
+    o[s] = (ky * WP + kx0) * CS;
+  }
+  // two halves of 4 tiles (the second half's reads in flight under the first half's MFMAs, not all 16 up front)
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
-    h8 b[4];
-    h4 br[4];
+    h8 b[4][2];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int i = 4 * hf + j, off = ((i >> 2) * WP + 32 * ((i >> 1) & 1) + (i & 1)) * CS;
-      const h4 lo = *reinterpret_cast<const h4*>(p + off + o0);
-      const h4 hi = *reinterpret_cast<const h4*>(p + off + o1);
-      b[j] = h8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      br[j] = *reinterpret_cast<const h4*>(p + off + orr);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {  // 16 contiguous bytes at 8-byte alignment: two b64 halves
+        const h4 lo = *reinterpret_cast<const h4*>(p + off + o[s]);
+        const h4 hi = *reinterpret_cast<const h4*>(p + off + o[s] + 4);
+        b[j][s] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
     }
     if (hf > 0) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) asm volatile("" : "+v"(acc[j]));
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[4 * hf + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[0][0], b[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-    if constexpr (FDR_R32) {  // tap 8 on the K = 32 fragment (lane group 0's halves 0..3; zeros elsewhere), chained
+    for (int j = 0; j < 4; ++j) acc[4 * hf + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[0], b[j][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[4 * hf + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[1][0], h8{br[j][0], br[j][1], br[j][2], br[j][3], br[j][0], br[j][1], br[j][2], br[j][3]},
-                                                                 acc[4 * hf + j], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[4 * hf + j] += __builtin_amdgcn_mfma_f32_16x16x16f16(wr, br[j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-    }
+    for (int j = 0; j < 4; ++j) acc[4 * hf + j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[1], b[j][1], acc[4 * hf + j], 0, 0, 0);
   }
 }
 
@@ -1433,7 +1464,11 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     if (has_cb) cbv[k] = pk[L.conv_b[bidx] + bch];
   }
   h8 af3[KSteps<3>::N][1];
-  load_af<3, 1>(hp + L.conv_h[0], af3, ln);
+  h8 af3n[2];  // (h3 entries: conv_band_s1's K order)
+  if constexpr (H3)
+    s1_frag(hp + L.conv_h[0], af3n, ln);
+  else
+    load_af<3, 1>(hp + L.conv_h[0], af3, ln);
   WStageT<NTH> st;
   st.template issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);
   float fsc[3], fsh[3];  // BN2d(3) of the frame, per thread (table entries 0..2)
@@ -1446,8 +1481,11 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   const FrameBn fbn{fsc[0], fsc[1], fsc[2], fsh[0], fsh[1], fsh[2]};
   auto FB = [&](int k) { return R + ((k & 1) ? kH2FB1 : kH2FB0); };  // the two frame-band buffers
   auto FB3 = [&](int k) { return R + ((k & 1) ? kH3FB1 : kH3FB0); };
-  if constexpr (H3)
+  if constexpr (H3) {
     frame_band_h2<NTH, kH3FR>(FB3(0), nullptr, 0, 0, a, env, e, fbn);
+    if (threadIdx.x < 2)  // the frame buffers' pad pixels (conv_band_s1)
+      *reinterpret_cast<h4*>(R + (threadIdx.x ? kH3FB1 : kH3FB0) + kH3FB) = h4{0, 0, 0, 0};
+  }
   else
     frame_band_h2<NTH>(FB(0), nullptr, 0, -1, a, env, e, fbn);
 #pragma unroll
@@ -1468,7 +1506,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     for (int bd = 0; bd < 4; ++bd) {
       h4 prev[2], P[2], Bx[2];
       f32x4 acc[8];
-      conv_band_s1(FB3(bd), af3, acc, wave, ln);
+      conv_band_s1(FB3(bd), af3n, acc, wave, ln);
       FDR_FINE_STAMP(a, 64 + 4 * bd);
       if (bd + 1 < 4) frame_band_h2<NTH, kH3FR>(FB3(bd + 1), FB3(bd), 2, 16 * (bd + 1), a, env, e, fbn);
       FDR_FINE_STAMP(a, 65 + 4 * bd);
