@@ -73,6 +73,7 @@ struct LanesArgs {
 struct RolloutArgs {
   LanesArgs lanes;
   int n_lanes;
+  int lane_base;  // first lane of this launch (rollout_pair_kernel launches lanes in rounds, launch_pair)
   int T;
   uint64_t key;
   int jiggle;

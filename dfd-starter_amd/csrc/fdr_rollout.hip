@@ -1155,7 +1155,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
   __syncthreads();
 
   const int tid = threadIdx.x & 63, wv = threadIdx.x >> 6, hh = tid >> 5, t = tid & 31;
-  const int lane0 = (blockIdx.x * kPairWaves + wv) * 2;
+  const int lane0 = a.lane_base + (blockIdx.x * kPairWaves + wv) * 2;
   if (lane0 >= a.n_lanes) return;  // whole wave idle
   const bool active = lane0 + hh < a.n_lanes;
   const int lane = active ? lane0 + hh : lane0;  // an idle half shadows its partner, writes nothing
@@ -1369,16 +1369,34 @@ static void launch_feat(const RolloutArgs& args, dim3 grid, dim3 block, hipStrea
 #undef FDR_FEAT_CASE
 }
 
+// More lanes than one resident round (2 waves per SIMD = 16 lanes per CU) go out as consecutive launches of
+// equal rounds: one launch of two rounds lets early-finishing CUs start second-round workgroups while slow
+// ones still run their first, and the last CUs' second round then runs alone at the end.
 template <int NIN, int NA, bool DISC>
-static void launch_pair(const RolloutArgs& args, hipStream_t stream) {
-  const dim3 grid((args.n_lanes + 2 * kPairWaves - 1) / (2 * kPairWaves)), block(64 * kPairWaves);
+static void launch_pair(const RolloutArgs& args, int round_lanes, hipStream_t stream) {
+  const int quantum = 2 * kPairWaves;
+  const int n_rounds = round_lanes > 0 ? (args.n_lanes + round_lanes - 1) / round_lanes : 1;
+  const int per = ((args.n_lanes + n_rounds - 1) / n_rounds + quantum - 1) / quantum * quantum;
   const int feat = (args.states ? 1 : 0) | (args.obs_mean ? 4 : 0);
-  switch (feat) {
-    case 0: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 0>), grid, block, 0, stream, args); break;
-    case 1: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 1>), grid, block, 0, stream, args); break;
-    case 4: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 4>), grid, block, 0, stream, args); break;
-    default: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 5>), grid, block, 0, stream, args); break;
+  RolloutArgs r = args;
+  for (int base = 0; base < args.n_lanes; base += per) {
+    r.lane_base = base;
+    const dim3 grid((std::min(per, args.n_lanes - base) + quantum - 1) / quantum), block(64 * kPairWaves);
+    switch (feat) {
+      case 0: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 0>), grid, block, 0, stream, r); break;
+      case 1: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 1>), grid, block, 0, stream, r); break;
+      case 4: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 4>), grid, block, 0, stream, r); break;
+      default: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 5>), grid, block, 0, stream, r); break;
+    }
   }
+}
+
+static int pair_round_lanes(const Context& ctx) {
+  static const int env = [] {
+    const char* e = std::getenv("FDR_PAIR_ROUNDS");  // A/B switch: "0" = one launch for all lanes
+    return e ? std::atoi(e) : 1;
+  }();
+  return env ? 16 * context_cus(ctx) : 0;
 }
 
 // Synthetic-env rollouts: rollout_pair_kernel (two lanes per wave) or rollout_kernel (one lane per
@@ -1406,7 +1424,7 @@ int launch_rollout(const Context& ctx, const PolicyKey& k, int env_kind, const R
       return set_error(FDR_ERR_INVALID, "n_params does not match the policy layout");           \
     if (env_kind == FDR_ENV_SYNTH) {                                                            \
       if (use_pair_kernel(ctx, args.n_lanes) && !args.os_mean) {                                            \
-        launch_pair<NIN, NA, DISC>(args, stream);                                               \
+        launch_pair<NIN, NA, DISC>(args, pair_round_lanes(ctx), stream);                        \
         return check_launch("rollout_pair_kernel<synth>");                                      \
       }                                                                                         \
       if (use_wide_kernel(ctx, args.n_lanes)) {                                                 \

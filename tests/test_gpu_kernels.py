@@ -382,6 +382,46 @@ def test_full_size_properties(eng):
     np.testing.assert_allclose(n2, res1.norm2.cpu().numpy(), rtol=1e-12)
 
 
+def test_pair_kernel_multi_round_launch(eng):
+    """More lanes than one resident round of rollout_pair_kernel (16 lanes per CU): the lanes go out as
+    consecutive launches (lane_base) -- here 2 x 16 x CUs + 10 lanes, three rounds with a ragged last one,
+    odd L (an idle half wave at the end).  Every lane against the one-lane kernel, sampled lanes incl. each
+    round's first and last lane against the oracle (bench.py's 4096-pair variant takes this path)."""
+    name = "cheetah"
+    kind, n_in, n_act = SHAPES[name]
+    torch.manual_seed(124)
+    pol = opol.TorchPolicy(kind, n_in, n_act, seed=124)
+    theta = pol.get_flat()
+    P = theta.size
+    t, tab = table(P, size=25_000_000)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    L, T = 2 * 16 * cus + 11, 60
+    idx = np.random.RandomState(3).randint(0, t.max_idx, size=L).astype(np.int64)
+    sign = np.where(np.arange(L) % 2 == 0, 1, -1).astype(np.int8)
+    from envs import SyntheticEnv
+    env = SyntheticEnv(n_in, n_act, False, T)
+    spec = eng.PolicySpec(kind, n_in, n_act, P)
+    lanes = eng.lanes_desc(dev(theta), 0, tab, dev(idx, torch.int64), dev(sign), 0.02)
+    try:
+        eng.context().set_rollout_impl("pair")
+        res = eng.rollout(spec, env, lanes, L, 9)
+        eng.context().set_rollout_impl("single")
+        res1 = eng.rollout(spec, env, lanes, L, 9)
+        torch.cuda.synchronize()
+    finally:
+        eng.context().set_rollout_impl("auto")
+    ret = res.reward.cpu().numpy()
+    assert (res.timesteps.cpu().numpy() == T).all()
+    np.testing.assert_allclose(ret, res1.reward.cpu().numpy(), rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(res.entropy.cpu().numpy(), res1.entropy.cpu().numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(res.norm2.cpu().numpy(), res1.norm2.cpu().numpy(), rtol=1e-12)
+    per = ((L + 2) // 3 + 3) // 4 * 4     # launch_pair: equal rounds in whole workgroups (4 lanes)
+    pick = np.unique(np.array([0, 1, per - 1, per, per + 1, 2 * per - 1, 2 * per, L - 2, L - 1]))
+    oenv = oenvs.BatchedSyntheticEnv(n_in, n_act, False, T, len(pick), env_seed=0)
+    ref = _oracle_lanes_with_ids(kind, n_in, n_act, theta, t.table, idx[pick], sign[pick], oenv, 9, pick)
+    np.testing.assert_allclose(ret[pick], ref, rtol=1e-4, atol=1e-4)
+
+
 def test_full_size_properties_config2(eng):
     """BASELINE config 2 size (1024 lanes x T=500, CartPole-shaped, discrete): the auto-selected WIDE one-lane
     kernel is reproducible, antithetic norms are symmetric, sampled lanes match the oracle over the full
