@@ -781,7 +781,10 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
 //   head       thread (rho = t/16, o = t%16) sums W3[o][.] over the 32 units its own DPP row
 //              holds (32 row_newbcast FMAs), then the two rows of the half (one permlane16 swap).
 // ---------------------------------------------------------------------------------------------
-constexpr int kPairWaves = 2;  // waves per workgroup (4 lanes): 4 workgroups, 8 waves per CU
+#ifndef FDR_PAIR_WAVES
+#define FDR_PAIR_WAVES 2
+#endif
+constexpr int kPairWaves = FDR_PAIR_WAVES;  // waves per workgroup (4 lanes): 4 workgroups, 8 waves per CU
 
 // 16-slot reduce-scatter over the 8 threads of a half-row: v[i] += partner(c ^ 7).v[i + 8] (i < 8),
 // v[i] += partner(c ^ 2).v[i + 4] (i < 4), v[i] += partner(c ^ 1).v[i + 2] (i < 2).  s_nop: a DPP read
