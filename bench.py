@@ -9,6 +9,11 @@ Per-GPU work is fixed as N grows ("weak" scaling): the global batch is 4096 * N 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+`--gpus N > 1` without an external launcher (no WORLD_SIZE in the environment) starts the N ranks itself: the
+parent never touches the GPU, runs `torch.distributed.run --nproc-per-node N` as a child, relays its output and
+checks that rank 0's line reports N GPUs.  Under an external launcher `--gpus` must equal WORLD_SIZE, and N must
+not exceed the visible devices: either mismatch exits non-zero before any GPU work.
+
 Prints ONE JSON line on rank 0.  The cpu_baseline leg (rank 0, N = 1) times the oracle's
 reference-shaped per-lane CPU loop (torch CPU forward per step, as worker/agent.py does) on a
 bounded sample, BEFORE the GPU is initialised.
@@ -211,9 +216,57 @@ def bench_trap(args):
 
 
 # ------------------------------------------------------------------------------------------------
+def check_devices(n):
+    """Exit non-zero unless n GPUs are visible.  torch.cuda.device_count() counts devices without starting the
+    HIP runtime on this image, so the self-launching parent stays GPU-free."""
+    import torch
+    have = torch.cuda.device_count()
+    if n > have:
+        sys.exit("bench.py: %d GPU(s) requested but %d visible" % (n, have))
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n, rehearse):
+    """`bench.py --gpus N` with no external launcher: one fresh process per GPU through torch.distributed.run
+    (the replacement for the reference's N worker clients, run_client.py:46-53 / run_server.py:135-167).  This
+    process never touches the GPU (no exec from a GPU-initialised process); it relays the children's output and
+    exits with their status, non-zero also when rank 0's line is missing or does not report N GPUs."""
+    import subprocess
+    if not rehearse:
+        check_devices(n)
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", port, os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, cwd=REPO)
+    lines = []
+    for line in p.stdout:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+        if line.startswith("{"):
+            lines.append(line)
+    rc = p.wait()
+    if rc != 0:
+        sys.exit(rc)
+    if len(lines) != 1:
+        sys.exit("bench.py: expected ONE JSON line from rank 0, got %d" % len(lines))
+    got = json.loads(lines[0]).get("n_gpus")
+    if got != n:
+        sys.exit("bench.py: rank 0 reports n_gpus=%s, %d were requested" % (got, n))
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of the run; default 1, or WORLD_SIZE under an external launcher")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="halfcheetah", choices=list(CONFIGS) + ["trap"])
@@ -235,12 +288,27 @@ def main():
     ap.add_argument("--no-novelty", action="store_true", help="config 5 without the novelty archive / omega "
                     "(rocprof passes: the archive's conv launches would mix into the rollout conv's average)")
     args = ap.parse_args()
+    rehearse = os.environ.get("FDR_BENCH_REHEARSE") == "1"
+    ext_world = os.environ.get("WORLD_SIZE")
+    if ext_world is None:
+        n = 1 if args.gpus is None else args.gpus
+        if n < 1:
+            sys.exit("bench.py: --gpus must be >= 1 (got %d)" % n)
+        if n > 1:
+            if args.config == "trap":
+                sys.exit("bench.py: --config trap is BASELINE config 1, a single-process run (--gpus 1)")
+            return self_launch(n, rehearse)
+    else:
+        if args.gpus is not None and args.gpus != int(ext_world):
+            sys.exit("bench.py: --gpus %d disagrees with WORLD_SIZE=%s set by the launcher" % (args.gpus, ext_world))
     if args.config == "trap":
         return bench_trap(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if not rehearse:
+        check_devices(max(world, local_rank + 1))
     kind, n_in, n_act, env_name, T = CONFIGS[args.config]
     if args.episode_len:
         T = args.episode_len
@@ -278,7 +346,6 @@ def main():
 
     # FDR_BENCH_REHEARSE=1: rehearse the N-rank path on a one-GPU box (every rank on cuda:0, gloo) -- the
     # exchange protocol, the collective settle and the max-over-ranks timing; not a scaling measurement
-    rehearse = os.environ.get("FDR_BENCH_REHEARSE") == "1"
     dev_index = 0 if rehearse else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)

@@ -161,7 +161,7 @@ static int resolve(fdr_ctx* ctx, Context** out) {
 
 extern "C" {
 
-const char* fdr_version(void) { return "fdr 0.2 gfx950"; }
+const char* fdr_version(void) { return "fdr 0.3 gfx950"; }
 const char* fdr_last_error(void) { return g_err.c_str(); }
 
 static int set_impl(Context& c, int32_t impl) {
@@ -405,6 +405,13 @@ int64_t fdr_fd_grad_fused_counter_bytes(int32_t n_dirs, int64_t n_params) {
   return n_params > 0 ? fused_counter_bytes(n_dirs, n_params) : -1;
 }
 
+int64_t fdr_fd_grad_fused_out_len(int32_t mode, int64_t n_params, int32_t n_all) {
+  if (n_params <= 0) return -1;
+  if (mode == FDR_WEIGHT_ZSCORE || mode == FDR_WEIGHT_CENTERED_RANK) return n_params;
+  if (mode == FDR_WEIGHT_MOMENTS) return n_all > 0 ? 2 * n_params + 1 + n_all : -1;
+  return -1;
+}
+
 static int fd_grad_fused_impl(const float* table, int64_t table_size, const int64_t* idx_local, int32_t n_dirs,
                               int64_t n_params, const double* rewards_all, int32_t n_all, double policy_reward,
                               int32_t lane_lo, const int8_t* sign_local, const double* norm2_local, int32_t lanes_per_dir,
@@ -428,8 +435,11 @@ static int fd_grad_fused_impl(const float* table, int64_t table_size, const int6
 int fdr_fd_grad_fused(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx_local, int32_t n_dirs,
                       int64_t n_params, const double* rewards_all, int32_t n_all, double policy_reward, int32_t lane_lo,
                       const int8_t* sign_local, const double* norm2_local, int32_t lanes_per_dir, float sigma,
-                      int32_t mode, double* out, void* workspace, int64_t workspace_bytes, fdr_stream stream) {
+                      int32_t mode, double* out, int64_t out_len, void* workspace, int64_t workspace_bytes,
+                      fdr_stream stream) {
   FDR_CTX(ctx, C);
+  const int64_t need = fdr_fd_grad_fused_out_len(mode, n_params, n_all);
+  if (need > 0 && out_len < need) return set_error(FDR_ERR_INVALID, "out_len below fdr_fd_grad_fused_out_len");
   return fd_grad_fused_impl(table, table_size, idx_local, n_dirs, n_params, rewards_all, n_all, policy_reward, lane_lo,
                             sign_local, norm2_local, lanes_per_dir, sigma, mode, out, nullptr, 0.0, 0.0, nullptr,
                             nullptr, workspace, workspace_bytes, stream);

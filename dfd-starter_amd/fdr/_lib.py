@@ -28,6 +28,7 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_atari_forward_workspace_bytes", "fdr_atari_forward", "fdr_rollout_set_impl",
            "fdr_impala_set_replay_gemm", "fdr_impala_strategies_workspace_bytes", "fdr_impala_strategies",
            "fdr_impala_env_frames", "fdr_fd_grad_fused_workspace_bytes", "fdr_fd_grad_fused_counter_bytes",
+           "fdr_fd_grad_fused_out_len",
            "fdr_fd_grad_fused", "fdr_rank_weights", "fdr_dsgd_step_ex", "fdr_fd_step",
            "fdr_ctx_set_rollout_impl", "fdr_ctx_set_replay_gemm", "fdr_ctx_set_core_mfma", "fdr_ctx_set_conv_h2", "fdr_ctx_impala_profile",
            "fdr_ctx_impala_profile_read", "fdr_ctx_impala_debug_clock")
@@ -123,8 +124,9 @@ def _load():
         "fdr_dsgd_workspace_bytes": (I64, [I64]),
         "fdr_fd_grad_fused_workspace_bytes": (I64, [I32, I32, I64, I32]),
         "fdr_fd_grad_fused_counter_bytes": (I64, [I32, I64]),
-        "fdr_fd_grad_fused": (ctypes.c_int, [P, P, I64, P, I32, I64, P, I32, F64, I32, P, P, I32, F32, I32, P, P, I64,
-                                             P]),
+        "fdr_fd_grad_fused_out_len": (I64, [I32, I64, I32]),
+        "fdr_fd_grad_fused": (ctypes.c_int, [P, P, I64, P, I32, I64, P, I32, F64, I32, P, P, I32, F32, I32, P, I64, P,
+                                             I64, P]),
         "fdr_rank_weights": (ctypes.c_int, [P, P, I32, I32, I32, P, P]),
         "fdr_fd_step": (ctypes.c_int, [P, P, I64, P, I32, I64, P, I32, F64, P, P, I32, F32, I32, P, F64, F64, P, P, P,
                                        P, I64, P]),

@@ -270,7 +270,9 @@ def fd_grad_fused(table, idx_local, rewards_all, policy_reward, lane_lo, sign_lo
     m = WEIGHT_MODES[mode]
     if n_all is None:
         n_all = rewards_all.numel() + (int(lane_lo) if mode == "moments" else 0)
-    n_out = 2 * n_params + 1 + int(n_all) if mode == "moments" else n_params
+    n_out = int(lib.fdr_fd_grad_fused_out_len(m, n_params, int(n_all)))
+    if n_out <= 0:
+        raise ValueError("fd_grad_fused: bad mode / P / n_all")
     if out is None:
         out = torch.empty(n_out, dtype=torch.float64, device=dev)
     elif out.numel() < n_out:
@@ -278,7 +280,8 @@ def fd_grad_fused(table, idx_local, rewards_all, policy_reward, lane_lo, sign_lo
     ws = _fused_workspace(m, n_dirs, lanes_per_dir, n_params, dev)
     check(lib.fdr_fd_grad_fused(_c(dev), _p(table), table.numel(), _p(idx_local), n_dirs, n_params, _p(rewards_all),
                                 int(n_all), float(policy_reward), int(lane_lo), _p(sign_local), _p(norm2_local),
-                                int(lanes_per_dir), float(sigma), m, _p(out), _p(ws), ws.numel(), _stream(dev)),
+                                int(lanes_per_dir), float(sigma), m, _p(out), out.numel(), _p(ws), ws.numel(),
+                                _stream(dev)),
           "fdr_fd_grad_fused")
     return out
 

@@ -107,7 +107,11 @@ class FiniteDifferences(object):
             # the split is known on every rank (Worker.evaluate's lane_range): [A | B | n | r' slots], ONE all-reduce.
             # Antithetic only: there B = 0 exactly, so A - m B carries no cancellation; one-sided batches with
             # near-constant returns (|m| >> sd) would lose digits in it, and take the exact gather path below.
-            _, rank = fdist.world_rank(self.process_group)
+            ws, rank = fdist.world_rank(self.process_group)
+            if len(sizes) != ws or int(sizes[rank]) != b.reward.numel():
+                # the slots of [A | B | n | r'] would overlap or leave gaps: m, sd and g silently wrong
+                raise ValueError("FDBatch.rank_lanes %s does not match the learner's process group (world %d, rank "
+                                 "%d, %d local lanes)" % (list(sizes), ws, rank, b.reward.numel()))
             mom = engine.fd_grad_fused(table, b.idx, b.reward, policy_reward, int(sum(sizes[:rank])), b.sign, b.norm2,
                                        b.lanes_per_dir, self.noise_std, P, mode="moments", n_all=int(sum(sizes)))
             fdist.allreduce_grad(mom, self.process_group)            # the step's one collective

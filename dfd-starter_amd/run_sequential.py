@@ -61,6 +61,15 @@ def make_env(env_id, device=None, episode_len=None, env_seed=0, n_act=None, envs
     return SyntheticEnv.named(name, device=device, env_seed=env_seed, **kw)
 
 
+def eval_lane_means(values, n_train, E):
+    """Per-(lane, env) values of a launch -> one value per EVAL lane: the mean over its E envs (lanes past n_train
+    are eval lanes, lane-major).  Deliberate divergence: the reference's single env makes one eval
+    return per episode and moves the 0.9 / 0.1 EMAs and zeta once per eval return (run_sequential.py:136-143); an
+    eval lane with E frame envs is that one evaluation, so its E envs are averaged first and the EMAs / zeta draw
+    count do not depend on E.  E == 1 is the reference's update exactly."""
+    return [np.asarray(a[n_train:], dtype=np.float64).reshape(-1, E).mean(1) for a in values]
+
+
 class SequentialRunner(object):
     def __init__(self, opt_fn=DSGD, env_id="Walker2d-v2", normalize_obs=False, learning_rate=0.01,
                  noise_std=0.02, batch_size=40, ent_coef=0.0, random_seed=123, max_delayed_return=10,
@@ -222,8 +231,7 @@ class SequentialRunner(object):
             # run_sequential.py:142-151 runs once per eval EPISODE of the reference's single env; an eval lane with
             # E envs is one such evaluation, so its E returns are averaged and the EMAs / zeta move once per lane
             # (per-env updates would make the 0.9 time constants and the zeta churn depend on E)
-            ev = [a[n_train:].reshape(-1, E).mean(1) for a in (rew, ent, nov)]
-            for r, e, nv in zip(*ev):
+            for r, e, nv in zip(*eval_lane_means((rew, ent, nov), n_train, E)):
                 self.policy_reward = self.policy_reward * 0.9 + r * 0.1
                 self.policy_entropy = self.policy_entropy * 0.9 + e * 0.1
                 self.policy_novelty = self.policy_novelty * 0.9 + nv * 0.1

@@ -236,10 +236,14 @@ int fdr_fd_grad(fdr_ctx* ctx, const float* table, int64_t table_size, const int6
 #define FDR_WEIGHT_MOMENTS 2
 int64_t fdr_fd_grad_fused_workspace_bytes(int32_t n_dirs, int32_t lanes_per_dir, int64_t n_params, int32_t mode);
 int64_t fdr_fd_grad_fused_counter_bytes(int32_t n_dirs, int64_t n_params);
+/* Doubles `out` must hold: P (ZSCORE / CENTERED_RANK) or 2P + 1 + n_all (MOMENTS); -1 for bad arguments.
+ * fdr 0.3: out_len (doubles) is checked against it -- the MOMENTS layout was 2P + 3 before 0.3. */
+int64_t fdr_fd_grad_fused_out_len(int32_t mode, int64_t n_params, int32_t n_all);
 int fdr_fd_grad_fused(fdr_ctx* ctx, const float* table, int64_t table_size, const int64_t* idx_local, int32_t n_dirs,
                       int64_t n_params, const double* rewards_all, int32_t n_all, double policy_reward, int32_t lane_lo,
                       const int8_t* sign_local, const double* norm2_local, int32_t lanes_per_dir, float sigma,
-                      int32_t mode, double* out, void* workspace, int64_t workspace_bytes, fdr_stream stream);
+                      int32_t mode, double* out, int64_t out_len, void* workspace, int64_t workspace_bytes,
+                      fdr_stream stream);
 /* The whole single-process FD step (FiniteDifferences.step, learner/finite_differences.py:24-64, with DSGD
  * dynamic_sgd.py:19-39) in two launches: fdr_fd_grad_fused (mode ZSCORE or CENTERED_RANK over all n_all =
  * n_dirs * lanes_per_dir lanes) writing g [P] and each column block's sum fl32(-g)^2, then the DSGD update of

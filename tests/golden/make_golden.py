@@ -596,7 +596,7 @@ def g12_history():
     save("g12_history.npz", **out)
 
 
-def g12_impala():
+def g12_impala(patched=True):
     """G12 for ImpalaPolicy (config 5's archive): the reference StrategyHandler / SparseHistoryManager
     (strategy/strategy_handler.py:6-31, sparse_history_manager.py:17-148) over a reference ImpalaPolicy
     (policies/impala.py:8-45) with categorical_tvd -- 6 points added, zeta set (8 obs dicts), 14 more
@@ -604,7 +604,9 @@ def g12_impala():
     documented zero-state rule (StrategyPoint.evaluate_strategy would otherwise start
     each point from the state the previous call left in the shared policy object, policies/impala.py:24-27).
     The parameter vectors are not committed (4.6 MB each): theta = 0.1 * table[1000:], point k =
-    theta + scale_k * table[off_k:] with table = RandomState(7).randn(2^22) f32; BN running stats as G8."""
+    theta + scale_k * table[off_k:] with table = RandomState(7).randn(2^22) f32; BN running stats as G8.
+    patched=False (g12_impala_unpatched.npz): the same run with the reference's get_strategy as it is, so the
+    size of the zero-state rule's divergence from the reference's carried-over LSTM state is recorded."""
     from policies.impala import ImpalaPolicy
     A, H, N, Z = 4, 6, 20, 8
     orig = ImpalaPolicy.get_strategy
@@ -613,7 +615,8 @@ def g12_impala():
         self.reset()
         return orig(self, x)
 
-    ImpalaPolicy.get_strategy = get_strategy_from_reset
+    if patched:
+        ImpalaPolicy.get_strategy = get_strategy_from_reset
     try:
         torch.manual_seed(124)
         pol = ImpalaPolicy((64, 64, 3), A, seed=124)
@@ -662,7 +665,7 @@ def g12_impala():
             nov.append(handler.compute_novelty(pol))
     finally:
         ImpalaPolicy.get_strategy = orig
-    save("g12_impala.npz", A=np.array(A), H=np.array(H), P=np.array(P), table_seed=np.array(7),
+    save("g12_impala.npz" if patched else "g12_impala_unpatched.npz", A=np.array(A), H=np.array(H), P=np.array(P), table_seed=np.array(7),
          param_offset=np.array(1000), rm=rm, rv=rv, scales=scales, offs=offs, zeta_frames=frames, zeta_rewards=zrew,
          returns=np.array(rets), worst=np.array(worst), strategies=np.asarray(mgr.strategy_tensor, np.float32),
          dists=D, novelty=np.array(nov))
@@ -671,7 +674,7 @@ def g12_impala():
 GENERATORS = {"g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
               "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g8": g8_impala,
               "g9": g9_novelty, "g10": g10_welford, "g11": g11_atari, "g12": g12_history,
-              "g12i": g12_impala}
+              "g12i": g12_impala, "g12iu": lambda: g12_impala(patched=False)}
 
 if __name__ == "__main__":
     torch.set_num_threads(1)

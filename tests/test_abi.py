@@ -36,6 +36,12 @@ def test_version_and_workspace_queries():
     assert "gfx950" in _lib.version()
     assert _lib.lib.fdr_fd_grad_workspace_bytes(2048, 6092) >= 6092 * 8
     assert _lib.lib.fdr_dsgd_workspace_bytes(6092) > 0
+    # the MOMENTS output length is queryable and checked (fdr 0.3; it was 2P + 3 before)
+    assert _lib.version().startswith("fdr 0.3")
+    assert _lib.lib.fdr_fd_grad_fused_out_len(_lib.FDR_WEIGHT_ZSCORE, 6092, 4096) == 6092
+    assert _lib.lib.fdr_fd_grad_fused_out_len(_lib.FDR_WEIGHT_MOMENTS, 6092, 4096) == 2 * 6092 + 1 + 4096
+    assert _lib.lib.fdr_fd_grad_fused_out_len(_lib.FDR_WEIGHT_MOMENTS, 6092, 0) == -1
+    assert _lib.lib.fdr_fd_grad_fused_out_len(7, 6092, 4096) == -1
 
 
 def test_argument_validation_without_gpu():

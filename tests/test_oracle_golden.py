@@ -269,3 +269,47 @@ def test_impala_history_replacement_matches_reference(golden):
     for k, want in zip((0, len(flats) - 1), z["novelty"]):
         f = (theta - z["scales"][k] * table[z["offs"][k]:z["offs"][k] + P]).astype(np.float32)
         assert abs(onov.novelty(strat(f), np.stack(hist.strategies), "tvd") - want) <= 1e-5 * max(1.0, want)
+
+
+def test_impala_history_unpatched_reference_carried_state(golden):
+    """G12-impala-unpatched: the same archive run with the reference's get_strategy as it is, where
+    every StrategyPoint.evaluate_strategy continues the LSTM state the previous call left in the shared policy
+    object (policies/impala.py:24-27; strategy_point.py:17-25).  The oracle reproduces it by carrying (h, c) through
+    the reference's call order -- set_zeta evaluates points 0..H-1, every _replace_point one candidate,
+    compute_novelty one policy -- which pins the reference's behaviour and the size of the build's documented
+    divergence (the zero-state rule): the two fixtures' archives differ by up to ~0.65 in a probability."""
+    from oracle import history
+    from oracle import impala as oi
+    from oracle import novelty as onov
+    z = golden("g12_impala_unpatched.npz")
+    zp = golden("g12_impala.npz")
+    A, H = int(z["A"]), int(z["H"])
+    _, _, flats = _g12i_flats(z)
+    bn = oi.split_bn(z["rm"], z["rv"])
+    fr = z["zeta_frames"].astype(np.float32)
+    state = [None, None]
+
+    def strat(f):
+        pr, h, c = oi.strategy(oi.unflatten(f, A), bn, fr, z["zeta_rewards"], state[0], state[1])
+        state[0], state[1] = h, c
+        return pr
+    hist = history.History("tvd", H)
+    for k in range(H):
+        hist.submit(None, False)
+    hist.evaluate([strat(f) for f in flats[:H]])
+    worst, rets = [hist.worst_point_idx], []
+    for k in range(H, len(flats)):
+        r = hist.submit(strat(flats[k]), True)
+        rets.append(-2 if r is None else r)
+        worst.append(hist.worst_point_idx)
+    np.testing.assert_array_equal(rets, z["returns"])
+    np.testing.assert_array_equal(worst, z["worst"])
+    np.testing.assert_allclose(np.stack(hist.strategies), z["strategies"], rtol=0, atol=1e-5)
+    theta, table, _ = _g12i_flats(z)
+    P = int(z["P"])
+    for k, want in zip((0, len(flats) - 1), z["novelty"]):
+        f = (theta - z["scales"][k] * table[z["offs"][k]:z["offs"][k] + P]).astype(np.float32)
+        assert abs(onov.novelty(strat(f), np.stack(hist.strategies), "tvd") - want) <= 1e-5 * max(1.0, want)
+    # the recorded divergence of the zero-state rule from the unpatched reference
+    d = float(np.abs(zp["strategies"] - z["strategies"]).max())
+    assert 0.1 < d < 1.0, d

@@ -1,4 +1,4 @@
-"""LDS / VALU utilisation of one kernel from a rocprofv3 --pmc pass (tools/round_r08*.sh LDS counter set).
+"""LDS / VALU utilisation of one kernel from a rocprofv3 --pmc pass (the SQ_LDS_* counter set of a separate --pmc pass).
     python tools/pmc_lds.py <run_counter_collection.csv> [kernel-substring] [envs per launch]"""
 import collections
 import csv
