@@ -338,6 +338,9 @@ int fdr_rollout_ex(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_de
       a.os_count = extras->obs_count;
       a.os_chance = extras->obs_chance;
     }
+    a.u_inject = extras->u_inject;
+    if (a.u_inject && a.os_mean)
+      return set_error(FDR_ERR_UNSUPPORTED, "u_inject is not combined with the obs statistics");
   }
   return launch_rollout(*C, k, env->kind, a, (hipStream_t)stream);
 }

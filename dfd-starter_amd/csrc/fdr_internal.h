@@ -99,6 +99,8 @@ struct RolloutArgs {
   float* os_m2;
   int32_t* os_count;
   float os_chance;
+  // NULL, or [n_lanes, T, k] host-injected draws replacing the counter stream (fdr_rollout_extras.u_inject)
+  const float* u_inject;
 };
 
 int launch_policy_forward(const PolicyKey& k, const LanesArgs& lanes, int n_lanes,

@@ -470,7 +470,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock) void policy_forward_kernel(
 // Whole-episode rollout: fdr_rollout
 // ---------------------------------------------------------------------------------------------
 // FEAT bit 0: record visited observations (fdr_rollout_states); bit 1: Welford obs statistics;
-// bit 2: observation normalisation (obs_mean / obs_std given)
+// bit 2: observation normalisation (obs_mean / obs_std given); bit 3: host-injected draws (u_inject)
 // WIDE (synthetic env, few lanes: <= 2 waves per SIMD): a 256-VGPR budget instead of 128, so the
 // step's loop invariants (M / K rows, the head's W3 slice) stay in registers; the policy input and env
 // state cross lanes by v_readlane instead of an LDS round trip (NIN <= 8); a discrete env's candidate
@@ -563,8 +563,13 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
   // Draw batch starting at step t (lane-parallel), and the normal of step t for action dim o.
   auto draw = [&](int t) {
     const int ds = j / kDrawsPerStep, dk = j % kDrawsPerStep;
-    const uint64_t h = hash_ctr(key, ulane, (uint64_t)(t + ds), (uint64_t)dk);
-    rbuf = DISC ? uniform24(h) : normal_bm(h);
+    if constexpr ((FEAT & 8) != 0) {  // host-injected draws (u_inject), same batch layout
+      const int tt = t + ds;
+      rbuf = tt < T ? a.u_inject[((int64_t)lane * T + tt) * kDrawsPerStep + dk] : 0.f;
+    } else {
+      const uint64_t h = hash_ctr(key, ulane, (uint64_t)(t + ds), (uint64_t)dk);
+      rbuf = DISC ? uniform24(h) : normal_bm(h);
+    }
   };
   // WIDE: loop invariants in registers (M row ji, K row ji, the head's W3 slice)
   float mreg[kRegIn ? NX : 1], kreg[WIDE ? NA : 1], w3reg[WIDE ? 16 : 1];
@@ -1365,6 +1370,12 @@ static void launch_feat(const RolloutArgs& args, dim3 grid, dim3 block, hipStrea
   const int feat = (args.states ? 1 : 0) | (args.os_mean ? 2 : 0) | (args.obs_mean ? 4 : 0);
 #define FDR_FEAT_CASE(F) \
   case F: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, F, WIDE>), grid, block, 0, stream, args); break;
+  if constexpr (!WIDE) {
+    if (args.u_inject) {  // injected draws (never with the Welford statistics: fdr_rollout_ex refuses it)
+      switch (feat) { FDR_FEAT_CASE(8) FDR_FEAT_CASE(9) FDR_FEAT_CASE(12) FDR_FEAT_CASE(13) }
+      return;
+    }
+  }
   switch (feat) {
     FDR_FEAT_CASE(0) FDR_FEAT_CASE(1) FDR_FEAT_CASE(2) FDR_FEAT_CASE(3)
     FDR_FEAT_CASE(4) FDR_FEAT_CASE(5) FDR_FEAT_CASE(6) FDR_FEAT_CASE(7)
@@ -1426,11 +1437,11 @@ int launch_rollout(const Context& ctx, const PolicyKey& k, int env_kind, const R
     if (Layout<NIN, NA, DISC>::P != k.n_params)                                                 \
       return set_error(FDR_ERR_INVALID, "n_params does not match the policy layout");           \
     if (env_kind == FDR_ENV_SYNTH) {                                                            \
-      if (use_pair_kernel(ctx, args.n_lanes) && !args.os_mean) {                                            \
+      if (use_pair_kernel(ctx, args.n_lanes) && !args.os_mean && !args.u_inject) {                         \
         launch_pair<NIN, NA, DISC>(args, pair_round_lanes(ctx), stream);                        \
         return check_launch("rollout_pair_kernel<synth>");                                      \
       }                                                                                         \
-      if (use_wide_kernel(ctx, args.n_lanes)) {                                                 \
+      if (use_wide_kernel(ctx, args.n_lanes) && !args.u_inject) {                               \
         launch_feat<NIN, NA, DISC, FDR_ENV_SYNTH, true>(args, grid, block, stream);             \
         return check_launch("rollout_kernel<synth, wide>");                                     \
       }                                                                                         \

@@ -59,7 +59,7 @@ class LanesDesc(ctypes.Structure):
 
 class RolloutExtras(ctypes.Structure):
     _fields_ = [("states", ctypes.c_void_p), ("obs_mean", ctypes.c_void_p), ("obs_m2", ctypes.c_void_p),
-                ("obs_count", ctypes.c_void_p), ("obs_chance", ctypes.c_float)]
+                ("obs_count", ctypes.c_void_p), ("obs_chance", ctypes.c_float), ("u_inject", ctypes.c_void_p)]
 
 
 class AtariDesc(ctypes.Structure):

@@ -164,9 +164,12 @@ class RolloutResult(object):
 
 
 def rollout(spec, env, lanes, n_lanes, seed, jiggle=True, obs_mean=None, obs_std=None,
-            bn_mean=None, bn_var=None, out=None, device=None, states=None, obs_stats=None, ctx=None):
-    """fdr_rollout; fdr_rollout_ex when states (f32 [n_lanes, T, n_in] device tensor) is given or
-    obs_stats = the per-step sampling chance (-> out.obs_mean / obs_m2 / obs_count per lane)."""
+            bn_mean=None, bn_var=None, out=None, device=None, states=None, obs_stats=None, ctx=None,
+            u_inject=None):
+    """fdr_rollout; fdr_rollout_ex when states (f32 [n_lanes, T, n_in] device tensor) is given,
+    obs_stats = the per-step sampling chance (-> out.obs_mean / obs_m2 / obs_count per lane), or u_inject =
+    host-injected draws (f32 [n_lanes, T, k] device tensor: k = 1 uniform per step for a discrete policy, n_act
+    normals for a continuous one) replacing the counter stream."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     _check_dev(obs_mean, obs_std, bn_mean, bn_var)
     if out is None:
@@ -176,8 +179,15 @@ def rollout(spec, env, lanes, n_lanes, seed, jiggle=True, obs_mean=None, obs_std
                             torch.empty(n_lanes, dtype=torch.float64, device=dev))
     pd = spec.desc(bn_mean, bn_var)
     ed = env.desc()
-    if states is not None or obs_stats is not None:
-        x = _lib.RolloutExtras(None, None, None, None, 0.0)
+    if states is not None or obs_stats is not None or u_inject is not None:
+        x = _lib.RolloutExtras(None, None, None, None, 0.0, None)
+        if u_inject is not None:
+            _check_dev(u_inject)
+            k = 1 if spec.kind == "discrete" else spec.n_act
+            if u_inject.dtype != torch.float32 or not u_inject.is_contiguous() or \
+                    u_inject.numel() != n_lanes * env.episode_len * k:
+                raise ValueError("u_inject must be contiguous float32 [n_lanes, T, %d]" % k)
+            x.u_inject = u_inject.data_ptr()
         if states is not None:
             _check_dev(states)
             if states.dtype != torch.float32 or not states.is_contiguous() or \

@@ -156,10 +156,11 @@ class Worker(object):
         prefetch=True: after launching this rollout, the NEXT call's indices are drawn ahead
         (SharedNoiseTable.peek_batch: the index stream is unchanged) and uploaded on the copy stream, so the
         next rollout does not wait for its host-to-device copy; a next call with other arguments ignores it."""
-        key = (int(n_dirs), bool(antithetic), None if lane_range is None else tuple(lane_range))
         pre, self._next = self._next, None
         idx = self.noise_source.sample_batch(n_dirs)
         lidx, sign, det, lane_range, rank_lanes = self._lanes_of(idx, n_dirs, antithetic, lane_range)
+        # the key holds the RESOLVED lane range ("auto" -> this rank's (lo, hi))
+        key = (int(n_dirs), bool(antithetic), None if lane_range is None else tuple(lane_range))
         lanes_dev = None
         if pre is not None and pre[0] == key and np.array_equal(pre[1], lidx):
             lanes_dev, ev = pre[2]

@@ -170,13 +170,20 @@ int fdr_rollout_states(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_en
  *   obs_mean/obs_m2 [n_lanes, n_in] f32, obs_count [n_lanes] i32: each lane's WelfordRunningStat
  *                 (utils/math_helpers.py:29-38) of the raw observations sampled with probability
  *                 obs_chance per step (worker/agent.py:37-39; coin = counter stream, k = 14);
- *                 merge them with fdr_obs_stats_merge. */
+ *                 merge them with fdr_obs_stats_merge.
+ *   u_inject      [n_lanes, T, k] f32 (nullable; fdr 0.3): host-injected draws replacing the counter stream
+ *                 (SURVEY 8b), k = 1 uniform in [0, 1) per step for a DiscretePolicy (inverse CDF,
+ *                 policies/discrete.py:16-24) or k = n_act standard normals per step for a MujocoPolicy
+ *                 (mean + std * z, policies/mujoco.py:15-22); lane l's step t reads u_inject[(l T + t) k ..];
+ *                 deterministic lanes read nothing.  Replays episodes whose torch multinomial / Normal draws
+ *                 were recorded (worker/agent.py:43).  Runs the one-lane kernel; not with obs statistics. */
 typedef struct fdr_rollout_extras {
   float* states;
   float* obs_mean;
   float* obs_m2;
   int32_t* obs_count;
   float obs_chance;
+  const float* u_inject;
 } fdr_rollout_extras;
 int fdr_rollout_ex(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_desc* env,
                    const fdr_lanes_desc* lanes, int32_t n_lanes, uint64_t seed, int32_t jiggle,

@@ -19,16 +19,20 @@ SCRIPT = os.path.join(ROOT, "tools", "dist_check.py")
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("weighting,port", [("zscore", 29541), ("centred_rank", 29542)])
-def test_two_rank_fd_steps_equal_one_rank(tmp_path, weighting, port):
+@pytest.mark.parametrize("weighting,port,preset", [("zscore", 29541, "small"), ("centred_rank", 29542, "small"),
+                                                   ("zscore", 29543, "bench")])
+def test_two_rank_fd_steps_equal_one_rank(tmp_path, weighting, port, preset):
+    """preset "bench" (VERDICT r3 item 6): bench.py's step at config 3 size -- 2 ranks x 2048 directions per rank
+    x T = 1000, 2 FD steps, z-score through the one-collective [A | B | n | r' slots] all-reduce at its real size
+    (2P + 1 + 8192 doubles), prefetched indices and step_async as in bench.py."""
     out = str(tmp_path)
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    p = subprocess.run([sys.executable, SCRIPT, "single", weighting, out], cwd=ROOT, env=env, capture_output=True,
-                       text=True, timeout=180)
+    p = subprocess.run([sys.executable, SCRIPT, "single", weighting, out, preset], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=180)
     assert p.returncode == 0, p.stderr[-2000:]
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", str(port), SCRIPT, "multi", weighting, out],
-                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), SCRIPT, "multi", weighting, out,
+                        preset], cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
     assert p.returncode == 0, p.stderr[-2000:]
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     try:

@@ -4,12 +4,15 @@
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
         tools/dist_check.py multi <weighting> <out_dir>            # 2 ranks  -> <out_dir>/theta_rank{r}.npy
     python tools/dist_check.py compare <weighting> <out_dir>
+    ... <mode> <weighting> <out_dir> bench                         # BASELINE config 3 size (below)
 
 weighting: "zscore" (the default one-collective moments form) or "centred_rank" (all-gather + all-reduce).
 The product path end to end: every rank draws the full index stream (SharedNoiseTable), Worker.evaluate runs its
 lane slice (lane_range="auto", lanes keyed by their GLOBAL index), FiniteDifferences.step exchanges and applies
 the replicated DSGD step -- for STEPS FD steps.  All ranks must end bit-identical, and equal to the
 single-process run up to the collective's summation order.  tests/test_gpu_dist_equivalence.py drives it.
+Preset "bench": bench.py's step at BASELINE config 3 size -- 2048 directions (4096 lanes) PER RANK, T = 1000, the
+25 M-entry table, 2 FD steps through Worker.evaluate(prefetch=True) + FiniteDifferences.step_async.
 """
 import os
 import sys
@@ -19,7 +22,11 @@ sys.path[:0] = [REPO, os.path.join(REPO, "dfd-starter_amd")]
 STEPS = 3
 
 
-def run(mode, weighting, out):
+PRESETS = {"small": dict(dirs_per_rank=48, T=200, table=1 << 22, steps=STEPS, bench=False),
+           "bench": dict(dirs_per_rank=2048, T=1000, table=25_000_000, steps=2, bench=True)}
+
+
+def run(mode, weighting, out, preset="small"):
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -36,19 +43,25 @@ def run(mode, weighting, out):
     from worker import Agent, Worker
     torch.manual_seed(124)
     policy = MujocoPolicy(17, 6, seed=124, device=dev)
-    env = SyntheticEnv(17, 6, False, 200, device=dev)
-    table = SharedNoiseTable(1 << 22, policy.num_params, random_seed=124)
+    cfg = PRESETS[preset]
+    env = SyntheticEnv(17, 6, False, cfg["T"], device=dev)
+    table = SharedNoiseTable(cfg["table"], policy.num_params, random_seed=124)
     agent = Agent(policy, env, random_seed=7)
     worker = Worker(policy, agent, table, None, sigma=0.02, random_seed=124)
     learner = FiniteDifferences(policy, DSGD(policy.parameters(), lr=0.01), AdaptiveOmega(), table, noise_std=0.02,
                                 weighting=weighting)
-    n_dirs = 96
+    # the global direction count is the 2-rank job's, whichever mode runs it
+    n_dirs = 2 * cfg["dirs_per_rank"]
     upd = []
-    for step in range(STEPS):
+    for step in range(cfg["steps"]):
         # the same counter-stream key for a lane whatever rank evaluates it: seed by step only,
         # and lanes are keyed by their GLOBAL index through lane_offset
-        batch = worker.evaluate(n_dirs, antithetic=True, lane_range="auto", seed=1000 + step)
-        upd.append(learner.step(batch, 0.25, 0.0, 0.0))
+        if cfg["bench"]:    # bench.py's fd_step: prefetched indices, the learner's no-sync step
+            batch = worker.evaluate(n_dirs, antithetic=True, lane_range="auto", seed=1000 + step, prefetch=True)
+            upd.append(learner.step_async(batch, 0.0, 0.0, 0.0).tolist()[0])
+        else:
+            batch = worker.evaluate(n_dirs, antithetic=True, lane_range="auto", seed=1000 + step)
+            upd.append(learner.step(batch, 0.25, 0.0, 0.0))
     os.makedirs(out, exist_ok=True)
     name = "single" if mode == "single" else "rank%d" % rank
     np.save(os.path.join(out, "theta_%s.npy" % name), policy.get_trainable_flat())
@@ -75,4 +88,4 @@ if __name__ == "__main__":
         assert compare(out) <= 1e-6
         print("dist_check ok")
     else:
-        run(mode, weighting, out)
+        run(mode, weighting, out, sys.argv[4] if len(sys.argv) > 4 else "small")
