@@ -20,6 +20,7 @@ int launch_rollout(int n_act, int envs, int T, uint64_t env_seed, const LanesArg
                    double* norm2, int32_t* actions, float* probs, void* ws, int64_t ws_bytes, hipStream_t stream);
 int launch_forward(int n_act, const float* theta, int n, const float* frames, const float* bn_mean,
                    const float* bn_var, float* probs, float* feat, void* ws, int64_t ws_bytes, hipStream_t stream);
+int launch_env_frames(uint64_t env_seed, uint64_t env_id, int t0, int n, float* frames, hipStream_t stream);
 }  // namespace atari
 }  // namespace fdr
 
@@ -706,6 +707,13 @@ int fdr_atari_rollout(fdr_ctx* ctx, const fdr_atari_desc* d, const fdr_lanes_des
 
 int64_t fdr_atari_forward_workspace_bytes(int32_t n_act, int32_t n) {
   return n < 0 ? -1 : atari::forward_workspace_bytes(n_act, n);
+}
+
+int fdr_atari_env_frames(uint64_t env_seed, int64_t env_id, int32_t t0, int32_t n, float* frames, fdr_stream stream) {
+  if (n < 0 || t0 < 0 || t0 + (int64_t)n >= (1 << 20) || env_id < 0 || env_id >= (1ll << 31))
+    return set_error(FDR_ERR_INVALID, "bad range");
+  if (n > 0 && !frames) return set_error(FDR_ERR_INVALID, "NULL frames");
+  return atari::launch_env_frames(env_seed, (uint64_t)env_id, t0, n, frames, (hipStream_t)stream);
 }
 
 int fdr_atari_forward(fdr_ctx* ctx, const fdr_atari_desc* d, const float* theta, int32_t n, const float* frames,

@@ -379,5 +379,25 @@ int launch_forward(int n_act, const float* theta, int n, const float* frames, co
   return check_launch("atari forward");
 }
 
+// The env's frames at steps t0 .. t0 + n - 1 of global env env_id (the atari_conv_kernel hash; they do not depend
+// on the actions): one workgroup per step, 8 pixels (one hash word) per thread and iteration, two float4 stores.
+__global__ __launch_bounds__(256) void env_frames_kernel(uint64_t fkey, uint64_t env_id, int t0, float* frames) {
+  const int t = t0 + blockIdx.x;
+  float4* fr = reinterpret_cast<float4*>(frames + (int64_t)blockIdx.x * kFramePix);
+  for (int w = threadIdx.x; w < kFramePix / 8; w += 256) {
+    const uint64_t hb = mix64(fkey + ((env_id << 32) | ((uint64_t)t << 11) | (uint64_t)w) * impala::kGolden);
+    const uint32_t lo = (uint32_t)hb, hi = (uint32_t)(hb >> 32);
+    fr[2 * w] = float4{(float)(lo & 255u), (float)((lo >> 8) & 255u), (float)((lo >> 16) & 255u), (float)(lo >> 24)};
+    fr[2 * w + 1] = float4{(float)(hi & 255u), (float)((hi >> 8) & 255u), (float)((hi >> 16) & 255u), (float)(hi >> 24)};
+  }
+}
+
+int launch_env_frames(uint64_t env_seed, uint64_t env_id, int t0, int n, float* frames, hipStream_t stream) {
+  static_assert(kFramePix % 8 == 0, "whole hash words per frame");
+  if (n == 0) return FDR_OK;
+  hipLaunchKernelGGL(env_frames_kernel, dim3(n), dim3(256), 0, stream, mix64(env_seed ^ kFrameSalt), env_id, t0, frames);
+  return check_launch("atari env_frames_kernel");
+}
+
 }  // namespace atari
 }  // namespace fdr

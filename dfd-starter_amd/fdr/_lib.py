@@ -25,7 +25,7 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_strategy_distances", "fdr_rollout_states", "fdr_rollout_ex", "fdr_obs_stats_merge",
            "fdr_fd_lambda_norms", "fdr_fd_grad_lambda", "fdr_bn_refresh_workspace_bytes", "fdr_bn_refresh",
            "fdr_atari_num_params", "fdr_atari_workspace_bytes", "fdr_atari_rollout",
-           "fdr_atari_forward_workspace_bytes", "fdr_atari_forward", "fdr_rollout_set_impl",
+           "fdr_atari_forward_workspace_bytes", "fdr_atari_forward", "fdr_atari_env_frames", "fdr_rollout_set_impl",
            "fdr_impala_set_replay_gemm", "fdr_impala_strategies_workspace_bytes", "fdr_impala_strategies",
            "fdr_impala_env_frames", "fdr_fd_grad_fused_workspace_bytes", "fdr_fd_grad_fused_counter_bytes",
            "fdr_fd_grad_fused_out_len",
@@ -132,6 +132,7 @@ def _load():
                                        P, I64, P]),
         "fdr_dsgd_step_ex": (ctypes.c_int, [P, P, P, I32, I64, F64, F64, P, P, P, I64, P]),
         "fdr_dsgd_step": (ctypes.c_int, [P, P, P, I64, F64, F64, P, P, I64, P]),
+        "fdr_atari_env_frames": (ctypes.c_int, [ctypes.c_uint64, I64, I32, I32, P, P]),
         "fdr_impala_num_params": (I64, [I32]),
         "fdr_impala_num_bn_stats": (I64, []),
         "fdr_impala_workspace_bytes": (I64, [ctypes.POINTER(ImpalaDesc), I32]),

@@ -33,6 +33,17 @@ def lane_range(n_dirs, lanes_per_dir, world, rank):
     return d_lo * lanes_per_dir, d_hi * lanes_per_dir
 
 
+def exchange_counts(n, device, group=None):
+    """Every rank's local count (one all-gather of an int64; a host sync) -> list of ints in rank order."""
+    ws, _ = world_rank(group)
+    if ws == 1:
+        return [int(n)]
+    t = torch.tensor([int(n)], dtype=torch.int64, device=device)
+    counts = torch.empty(ws, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(counts, t, group=group)
+    return [int(c) for c in counts.tolist()]
+
+
 def gather_rewards(local, group=None, sizes=None):
     """All-gather per-lane rewards -> (all rewards in rank order, this rank's offset).
 

@@ -631,6 +631,16 @@ def atari_rollout(spec, lanes, n_lanes, seed, jiggle=True, bn_mean=None, bn_var=
     return out
 
 
+def atari_env_frames(env_seed, env_id, t0, n, device=None):
+    """The stacked-frame env's observations [n, 4, 84, 84] f32 of global env env_id at steps t0 .. t0 + n - 1
+    (fdr_atari_env_frames; independent of the actions)."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    out = torch.empty((int(n), 4, 84, 84), dtype=torch.float32, device=dev)
+    check(lib.fdr_atari_env_frames(ctypes.c_uint64(int(env_seed) & ((1 << 64) - 1)), int(env_id), int(t0), int(n),
+                                   _p(out), _stream(dev)), "fdr_atari_env_frames")
+    return out
+
+
 def atari_forward(spec, theta, frames, bn_mean=None, bn_var=None, feat=False):
     _check_dev(theta, frames)
     frames = frames.to(torch.float32).reshape(-1, 4 * 84 * 84).contiguous()

@@ -19,7 +19,8 @@ z-score) ranks all returns, so it keeps the all-gather of the per-lane returns +
 
 Returns carry a current epoch in the synchronous engine; returns from an older epoch (the
 reference's async server mode) add the parameter drift theta_epoch - theta_now to lambda
-(finite_differences.py:66-92) -- that rare path runs as plain torch device ops (not a hot path).
+(finite_differences.py:66-92) -- fdr_fd_lambda_norms / fdr_fd_grad_lambda, single-process or sharded
+(a list of FDReturn on every rank: counts + rewards all-gathered, one all-reduce of g).
 """
 import numpy as np
 import torch
@@ -171,36 +172,19 @@ class FiniteDifferences(object):
                 self.discarded_returns += 1
                 continue
             keep.append(r)
+        if self._distributed():
+            # every rank joins the exchange, even with no (kept) returns of its own
+            return self._step_returns_lambda(keep, policy_reward)
         if not keep:
             return None
         dev = self.policy.flat.device
         table = self.noise_source.device_table(dev)
         P = self.policy.num_params
-        sigma32 = np.float32(self.noise_std)
         current = [r for r in keep if self.dist_map[r.epoch] is None]
         stale = [r for r in keep if self.dist_map[r.epoch] is not None]
-        if stale and self._distributed():
-            raise NotImplementedError("stale (delayed) returns are a single-process path; the sharded "
-                                      "engine is synchronous and never produces them")
         if stale:
-            # finite_differences.py:88-114 on the device: lambda_i = sigma * eps_i + dist_map[epoch_i],
-            # v_i = lambda_i / ||lambda_i||^2, z-score over all kept returns, g = z . V
-            epochs = sorted({r.epoch for r in stale})
-            drift = torch.stack([self.dist_map[e] for e in epochs]).contiguous()
-            slot_of = {e: k for k, e in enumerate(epochs)}
-            idx = np.array([int(r.encoded_noise) for r in keep], dtype=np.int64)
-            sign = np.array([int(getattr(r, "sign", 1) or 1) for r in keep], dtype=np.int8)
-            slot = np.array([slot_of.get(r.epoch, -1) if self.dist_map[r.epoch] is not None else -1 for r in keep],
-                            dtype=np.int32)
-            idx_d, sign_d, slot_d = (torch.as_tensor(a, device=dev) for a in (idx, sign, slot))
-            rewards = torch.as_tensor([r.reward for r in keep], dtype=torch.float64, device=dev)
-            n2 = engine.fd_lambda_norms(table, idx_d, sign_d, slot_d, self.noise_std, drift, P)
-            ones = torch.ones(len(keep), dtype=torch.int8, device=dev)
-            coef = engine.fd_weights(rewards, policy_reward, 0, ones, n2, 1, 1.0)
-            g = engine.fd_grad_lambda(table, idx_d, sign_d, slot_d, coef, self.noise_std, drift, P,
-                                      self.gradient_memory)
-            fdist.allreduce_grad(g, self.process_group)
-            return self._apply(g)
+            # finite_differences.py:88-114: lambda_i = sigma * eps_i + dist_map[epoch_i], v_i = lambda_i / ||lambda_i||^2
+            return self._step_returns_lambda(keep, policy_reward)
         rewards = torch.as_tensor([r.reward for r in current], dtype=torch.float64, device=dev)
         idx = np.array([int(r.encoded_noise) for r in current], dtype=np.int64)
         sign = np.array([int(getattr(r, "sign", 1) or 1) for r in current], dtype=np.int8)
@@ -212,6 +196,44 @@ class FiniteDifferences(object):
             n2 = engine.fd_lambda_norms(table, idx_d, sign_d, None, self.noise_std, None, P)
         b = FDBatch(rewards, None, None, n2, idx_d, sign_d, idx, sign, self.epoch)
         return self._step_batch(b, policy_reward)
+
+
+    def _step_returns_lambda(self, keep, policy_reward):
+        """list[FDReturn] with the lambda kernels: delayed returns single-process, and every sharded list step (finite_differences.py:24-64, 80-114; the
+        reference's server accepts returns up to max_delayed_return epochs old, networking/server.py:83-89).
+        Sharded, each rank holds its own returns; the policy history -- hence dist_map -- is replicated (every rank applies
+        the same DSGD step), so each rank forms its lambda_i = sign_i fl32(sigma eps_i) + dist_map[epoch_i] alone.
+        Exchange: the per-rank return counts + an all-gather of the rewards (the z-score is global), then ONE
+        all-reduce of g.  Every rank takes this path for every list step, stale returns or not, so the ranks'
+        collectives always match."""
+        dev = self.policy.flat.device
+        table = self.noise_source.device_table(dev)
+        P = self.policy.num_params
+        n = len(keep)
+        sizes = fdist.exchange_counts(n, dev, self.process_group)
+        if sum(sizes) == 0:
+            return None
+        epochs = sorted({r.epoch for r in keep if self.dist_map[r.epoch] is not None})
+        drift = torch.stack([self.dist_map[e] for e in epochs]).contiguous() if epochs else None
+        slot_of = {e: k for k, e in enumerate(epochs)}
+        rewards = torch.as_tensor([r.reward for r in keep], dtype=torch.float64, device=dev)
+        rewards_all, lane_lo = fdist.gather_rewards(rewards, self.process_group, sizes)
+        g = self.gradient_memory
+        if n:
+            idx_d = torch.as_tensor(np.array([int(r.encoded_noise) for r in keep], np.int64), device=dev)
+            sign_d = torch.as_tensor(np.array([int(getattr(r, "sign", 1) or 1) for r in keep], np.int8), device=dev)
+            slot_d = torch.as_tensor(np.array([slot_of.get(r.epoch, -1) for r in keep], np.int32), device=dev)
+            n2 = engine.fd_lambda_norms(table, idx_d, sign_d, slot_d, self.noise_std, drift, P)
+            if self.weighting == "centred_rank":   # ranks over all returns, v_i = lambda_i / ||lambda_i||^2
+                coef = engine.rank_weights(rewards_all, lane_lo, n) / n2
+            else:
+                ones = torch.ones(n, dtype=torch.int8, device=dev)
+                coef = engine.fd_weights(rewards_all, policy_reward, lane_lo, ones, n2, 1, 1.0)
+            g = engine.fd_grad_lambda(table, idx_d, sign_d, slot_d, coef, self.noise_std, drift, P, g)
+        else:
+            g.zero_()
+        fdist.allreduce_grad(g, self.process_group)
+        return self._apply(g)
 
 
 class _LazyDistMap(object):

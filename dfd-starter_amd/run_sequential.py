@@ -139,6 +139,15 @@ class SequentialRunner(object):
             self.zeta_idxs = list(range(len(self.zeta["frame"])))
             if vbn_buffer_size > 0:
                 self.vbn_buffer = {k: v[:vbn_buffer_size] for k, v in obs.items()}
+        elif self.frames:
+            # AtariPolicy: the stacked-frame env's observations do not depend on the actions, so the random-action
+            # steps of run_sequential.py:198-213 are env 0's first frames (host f32 [n, 4, 84, 84])
+            n = max(vbn_buffer_size, zeta_size)
+            obs = engine.atari_env_frames(self.env.env_seed, 0, 0, n, device=self.device).cpu().numpy()
+            self.zeta = obs[:zeta_size].copy()
+            self.zeta_idxs = list(range(len(self.zeta)))
+            if vbn_buffer_size > 0:
+                self.vbn_buffer = obs[:vbn_buffer_size]
         elif vbn_buffer_size > 0 and not self.frames:
             # run_sequential.py:198-213 samples the buffer from env steps; the GPU envs expose no host
             # stepping, so the buffer is drawn around the reset state (documented deviation)

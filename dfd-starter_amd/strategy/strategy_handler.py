@@ -10,6 +10,7 @@ sequence) started from the reset state -- the state Worker._build_ret scores nov
 (worker/agent.py:66 resets the policy before worker.py:53).  Distances and novelty come from
 ``fdr_strategy_distances`` (the reference's
 ``l2_dist`` / ``categorical_tvd`` / ``gaussian_wasserstein_dist_from_strategies``, f64 accumulation).
+AtariPolicy (stateless) strategies are its forward over the zeta frames, one fdr_atari_forward per vector.
 ``lane_novelty`` scores every perturbed lane of a batch in two launches -- the batched form of
 ``Worker._build_ret``'s per-return ``compute_novelty`` (worker/worker.py:53), which the reference
 evaluates on the perturbed policy.  Replacement when full follows ``_replace_point`` /
@@ -56,13 +57,21 @@ class StrategyHandler(object):
             spec = engine.ImpalaSpec(p.output_shape, fp16=self.fp16)
             return engine.impala_strategies(spec, lanes_fn(1), n, frames, reward, bn_mean=bm, bn_var=bv)
         if p.KIND != "discrete" and p.KIND != "mujoco":
-            raise NotImplementedError("strategies of a %s policy are not built (novelty needs get_strategy over "
-                                      "zeta: policies/atari.py:31-32)" % p.KIND)
+            raise NotImplementedError("strategies of a %s policy" % p.KIND)
         return engine.lane_strategies(p.spec, lanes_fn, n, self.zeta, bm, bv)
+
+    def _atari_strategies(self, thetas):
+        """AtariPolicy.get_strategy (policies/atari.py:31-32: forward(zeta) probs, stateless) of each parameter
+        vector in thetas (device f32 [k, P]) -> [k, Z, A]: fdr_atari_forward over the zeta frames per vector."""
+        p = self.policy
+        bm, bv = p.bn_stats()
+        return torch.stack([engine.atari_forward(p.spec, th, self.zeta, bm, bv) for th in thetas])
 
     def _strategies_of_flat(self, flat):
         """get_strategy(zeta) of one parameter vector -> [1, Z, D]."""
         base = torch.as_tensor(np.asarray(flat, np.float32), device=self._dev()).contiguous()
+        if self.policy.KIND == "atari":
+            return self._atari_strategies(base.view(1, -1))
         return self._strategies(lambda Z: engine.lanes_desc(base, 0), 1)
 
     def _strategies_of_flats(self, flats):
@@ -76,6 +85,11 @@ class StrategyHandler(object):
     def lane_strategies(self, table, idx, sign, sigma):
         """Strategies of the perturbed lanes theta + sign * sigma * table[idx:] -> [n, Z, D]."""
         p = self.policy
+        if p.KIND == "atari":   # theta' materialised per chunk of lanes (fdr_perturb), then one forward each
+            out = [self._atari_strategies(engine.perturb(p.flat, table, idx[c:c + 64].contiguous(),
+                                                         sign[c:c + 64].contiguous(), sigma))
+                   for c in range(0, idx.numel(), 64)]
+            return torch.cat(out)
 
         def lanes(Z):
             return engine.lanes_desc(p.flat, 0, table, idx.repeat_interleave(Z), sign.repeat_interleave(Z), sigma)

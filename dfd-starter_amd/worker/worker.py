@@ -236,7 +236,8 @@ class Worker(object):
           MLP policies: raw observations, host f32 [T, n_in] (fdr_rollout_states).
           ImpalaPolicy: the obs dicts stacked (impala.py:35-45) -- {frame [n, 3, 64, 64], reward [n] (the
           reward each obs carries: that of the previous step), done [n]} device tensors, n = min(T,
-          max_states) -- of env instance 0 (fdr_impala_env_frames over the recorded actions)."""
+          max_states) -- of env instance 0 (fdr_impala_env_frames over the recorded actions).
+          AtariPolicy: frames [n, 4, 84, 84] (host f32) of env instance 0 (fdr_atari_env_frames)."""
         p = self.policy
         dev = p.flat.device
         T = self.agent.env.episode_len
@@ -251,6 +252,10 @@ class Worker(object):
             frames, r = engine.impala_env_frames(env.env_seed, p.output_shape, 0, 0, n, res.actions[0, :n], device=dev)
             carried = torch.cat([torch.zeros(1, dtype=torch.float32, device=dev), r[:-1]])
             return {"frame": frames, "reward": carried, "done": torch.zeros(n, dtype=torch.bool, device=dev)}
+        if p.KIND == "atari":
+            # the stacked-frame env's frames do not depend on the actions: env 0's first n observations
+            n = T if max_states is None else min(T, int(max_states))
+            return engine.atari_env_frames(self.agent.env.env_seed, 0, 0, n, device=dev).cpu().numpy()
         if p.KIND != "discrete" and p.KIND != "mujoco":
             return None
         states = torch.empty((1, T, p.input_shape), dtype=torch.float32, device=dev)

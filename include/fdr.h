@@ -395,6 +395,10 @@ int fdr_atari_rollout(fdr_ctx* ctx, const fdr_atari_desc* desc, const fdr_lanes_
                       int32_t* actions, float* probs, void* workspace, int64_t workspace_bytes, fdr_stream stream);
 /* AtariPolicy.forward for n frames [n, 4, 84, 84] (f32, raw 0..255 as the reference feeds them):
  * probs [n, A]; feat [n, 2592] optional.  workspace: fdr_atari_forward_workspace_bytes(n_act, n). */
+/* The synthetic stacked-frame env's observations [n, 4, 84, 84] f32 (0..255) of global env env_id (= lane_offset * E
+ * + lane * E + e of a rollout) at steps t0 .. t0+n-1 -- the frames do not depend on the actions.  The eval states
+ * (worker/agent.py:36,58-59) that become zeta for AtariPolicy novelty (run_sequential.py:142-143). */
+int fdr_atari_env_frames(uint64_t env_seed, int64_t env_id, int32_t t0, int32_t n, float* frames, fdr_stream stream);
 int64_t fdr_atari_forward_workspace_bytes(int32_t n_act, int32_t n);
 int fdr_atari_forward(fdr_ctx* ctx, const fdr_atari_desc* desc, const float* theta, int32_t n, const float* frames,
                       float* probs, float* feat, void* workspace, int64_t workspace_bytes, fdr_stream stream);

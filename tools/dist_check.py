@@ -11,6 +11,8 @@ The product path end to end: every rank draws the full index stream (SharedNoise
 lane slice (lane_range="auto", lanes keyed by their GLOBAL index), FiniteDifferences.step exchanges and applies
 the replicated DSGD step -- for STEPS FD steps.  All ranks must end bit-identical, and equal to the
 single-process run up to the collective's summation order.  tests/test_gpu_dist_equivalence.py drives it.
+Preset "stale": from step 1 on, lists of FDReturn with the previous step's returns again as one-epoch-old
+(delayed) returns -- the sharded drift path of FiniteDifferences.
 Preset "bench": bench.py's step at BASELINE config 3 size -- 2048 directions (4096 lanes) PER RANK, T = 1000, the
 25 M-entry table, 2 FD steps through Worker.evaluate(prefetch=True) + FiniteDifferences.step_async.
 """
@@ -23,7 +25,8 @@ STEPS = 3
 
 
 PRESETS = {"small": dict(dirs_per_rank=48, T=200, table=1 << 22, steps=STEPS, bench=False),
-           "bench": dict(dirs_per_rank=2048, T=1000, table=25_000_000, steps=2, bench=True)}
+           "bench": dict(dirs_per_rank=2048, T=1000, table=25_000_000, steps=2, bench=True),
+           "stale": dict(dirs_per_rank=24, T=100, table=1 << 22, steps=STEPS, bench=False, stale=True)}
 
 
 def run(mode, weighting, out, preset="small"):
@@ -56,6 +59,23 @@ def run(mode, weighting, out, preset="small"):
     for step in range(cfg["steps"]):
         # the same counter-stream key for a lane whatever rank evaluates it: seed by step only,
         # and lanes are keyed by their GLOBAL index through lane_offset
+        if cfg.get("stale"):
+            # delayed returns (the reference's async server, learner/finite_differences.py:66-92): from step 1 on,
+            # the learner gets a list of FDReturn -- this step's returns (current epoch) + the previous step's
+            # returns again (one epoch old: lambda carries the drift theta_prev - theta_now); each rank holds its
+            # own lanes of both
+            batch = worker.evaluate(n_dirs, antithetic=True, lane_range="auto", seed=1000 + step)
+            if step == 0:
+                upd.append(learner.step(batch, 0.25, 0.0, 0.0))
+            else:
+                cur = batch.to_returns()
+                for r in cur:
+                    r.epoch = learner.epoch
+                for r in prev:
+                    r.epoch = learner.epoch - 1
+                upd.append(learner.step(cur + prev, 0.25, 0.0, 0.0))
+            prev = batch.to_returns()
+            continue
         if cfg["bench"]:    # bench.py's fd_step: prefetched indices, the learner's no-sync step
             batch = worker.evaluate(n_dirs, antithetic=True, lane_range="auto", seed=1000 + step, prefetch=True)
             upd.append(learner.step_async(batch, 0.0, 0.0, 0.0).tolist()[0])
