@@ -26,6 +26,10 @@
 #include "fdr_internal.h"
 #include "fdr_wave.h"
 
+#ifndef FDR_FAST_SOFTMAX  // sampled discrete lanes: approximate exp / reciprocal softmax (MlpLane::softmax)
+#define FDR_FAST_SOFTMAX 1
+#endif
+
 namespace fdr {
 
 constexpr int kLanesPerBlock = 4;
@@ -419,14 +423,23 @@ struct MlpLane {
   }
 
   // Discrete: softmax across the row (o = j & 15 < NA); returns p_o, 0 for o >= NA.  kAll: every lane
-  // holds a logit (head2: output j & 1).
-  template <bool kAll = false>
+  // holds a logit (head2: output j & 1).  kFast (sampled lanes, FDR_FAST_SOFTMAX): exp as v_exp_f32 of x log2 e and
+  // the normalisation as a v_rcp_f32 product -- 4 VALU instead of libm expf (13) + the IEEE division (11); the
+  // probabilities move by ~1e-7 relative (inside the 1e-5 forward tolerance), so a sampled action can differ
+  // from the exact form's only where u * sum p lies within that of a partition boundary.  Deterministic lanes
+  // (argmax, the trap env's integer-exact episodes) keep the exact form.
+  template <bool kAll = false, bool kFast = false>
   __device__ __forceinline__ float softmax(float logit, int j) const {
     const bool valid = kAll || (j & 15) < NOUT;
     const float v = valid ? logit : -FLT_MAX;
     const float mx = row16_max_n<NOUT>(v);
-    const float e = valid ? expf(v - mx) : 0.f;
-    return e / row16_sum_n<NOUT>(e);
+    if constexpr (kFast) {
+      const float e = valid ? __builtin_amdgcn_exp2f((v - mx) * 1.44269504088896341f) : 0.f;
+      return e * __builtin_amdgcn_rcpf(row16_sum_n<NOUT>(e));
+    } else {
+      const float e = valid ? expf(v - mx) : 0.f;
+      return e / row16_sum_n<NOUT>(e);
+    }
   }
 };
 
@@ -678,7 +691,11 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
     int act_d = 0;
     float act_c = 0.f;
     if constexpr (DISC) {
-      const float p = pl.template softmax<kHead2>(y, j);
+      float p;
+      if (det || !FDR_FAST_SOFTMAX)  // wave-uniform: a scalar branch
+        p = pl.template softmax<kHead2, false>(y, j);
+      else
+        p = pl.template softmax<kHead2, (FDR_FAST_SOFTMAX != 0)>(y, j);
       float pv[NA];
 #pragma unroll
       for (int i = 0; i < NA; ++i) pv[i] = readlane_f(p, i);
@@ -1120,12 +1137,18 @@ struct MlpPair {
     return out;
   }
 
+  template <bool kAll = false, bool kFast = false>  // as MlpLane::softmax
   __device__ __forceinline__ float softmax(float logit, int t) const {
     const bool valid = (t & 15) < NOUT;
     const float v = valid ? logit : -FLT_MAX;
     const float mx = row16_max_n<NOUT>(v);
-    const float e = valid ? expf(v - mx) : 0.f;
-    return e / row16_sum_n<NOUT>(e);
+    if constexpr (kFast) {
+      const float e = valid ? __builtin_amdgcn_exp2f((v - mx) * 1.44269504088896341f) : 0.f;
+      return e * __builtin_amdgcn_rcpf(row16_sum_n<NOUT>(e));
+    } else {
+      const float e = valid ? expf(v - mx) : 0.f;
+      return e / row16_sum_n<NOUT>(e);
+    }
   }
 };
 
@@ -1245,7 +1268,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     const float y = pl.layers23(h1, h1s, t, mark);
     pl.l1_prefetch(l1rows, mrow);  // next step's rows, in flight during the action and env phases
     if constexpr (DISC) {
-      const float p = pl.softmax(y, t);
+      const float p = det || !FDR_FAST_SOFTMAX ? pl.softmax(y, t) : pl.template softmax<false, (FDR_FAST_SOFTMAX != 0)>(y, t);
       float pv[NA];
       row_bcast_all(p, pv, std::make_integer_sequence<int, NA>{});  // pv[i] = p of output i
       float tot = 0.f;
