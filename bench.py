@@ -417,11 +417,9 @@ def main():
         # 1-GPU run bit-identically, whatever the shard (include/fdr.h lane_offset)
         seed = 1000 + step_no[0]
         step_no[0] += 1
-        if timed:
-            cur[0][0].record()
-        batch = worker.evaluate(n_dirs, antithetic=True, lane_range=rng, seed=seed, novelty=novelty, prefetch=True)
-        if timed:
-            cur[0][1].record()
+        # the events bracket the rollout launch alone (Worker.launch), not the host index draw before it
+        batch = worker.evaluate(n_dirs, antithetic=True, lane_range=rng, seed=seed, novelty=novelty, prefetch=True,
+                                timing=cur[0] if timed else None)
         out = learner.step_async(batch, 0.0, 0.0, 0.0)
         if novelty:
             # run_sequential.py:149-151 (the noisy mean reward; one host read per FD step) and :160

@@ -90,11 +90,13 @@ class Worker(object):
         arrs = (d[:8 * n].view(torch.int64), d[8 * n:9 * n].view(torch.int8), d[9 * n:].view(torch.int8))
         return (arrs, ev) if defer_wait else arrs
 
-    def launch(self, idx, sign, det, seed=None, out=None, jiggle=True, lane_offset=0, lanes_dev=None, pairs=False):
+    def launch(self, idx, sign, det, seed=None, out=None, jiggle=True, lane_offset=0, lanes_dev=None, pairs=False,
+               timing=None):
         """Run one rollout over explicit lanes (host arrays) -> FDBatch (asynchronous).  lanes_dev: the same lanes
         already on the device (idx, sign, det), e.g. uploaded ahead by evaluate(prefetch=True).  pairs: lanes 2p,
         2p+1 are antithetic pairs (checked here) -- an Impala rollout then streams each pair's sigma-eps once
-        (fdr_impala_desc.pairs)."""
+        (fdr_impala_desc.pairs).  timing: a (start, end) pair of torch.cuda.Event recorded on the stream right
+        around the rollout launch(es), nothing else inside (bench.py's kernel-time pass)."""
         p = self.policy
         n = len(idx)
         idx_d, sign_d, det_d = lanes_dev if lanes_dev is not None else self._lanes_to_device(idx, sign, det)
@@ -114,7 +116,11 @@ class Worker(object):
                 # the pair's sign from its first lane and would perturb an eval lane
                 spec.pairs = bool(n % 2 == 0 and np.array_equal(ii[0::2], ii[1::2]) and np.all(ss[0::2] == 1)
                                   and np.all(ss[1::2] == -1) and not np.any(dd))
+            if timing is not None:
+                timing[0].record()
             res = roll(spec, lanes, n, seed, jiggle=jiggle, bn_mean=bm, bn_var=bv, device=p.flat.device)
+            if timing is not None:
+                timing[1].record()
             if E > 1:
                 res.norm2 = res.norm2.repeat_interleave(E)
                 idx_d, sign_d = idx_d.repeat_interleave(E), sign_d.repeat_interleave(E)
@@ -122,8 +128,12 @@ class Worker(object):
         om, osd = self.agent.obs_norm_tensors(self.fixed_obs_stats.mean, self.fixed_obs_stats.std)
         # agent.py:37-39: with normalize_obs every episode also samples raw obs into its Welford stats
         chance = self.agent.obs_stats_update_chance if self.agent.normalize_obs else None
+        if timing is not None:
+            timing[0].record()
         res = engine.rollout(p.spec, self.agent.env, lanes, n, seed, jiggle=jiggle, obs_mean=om, obs_std=osd,
                              bn_mean=bm, bn_var=bv, out=out, device=p.flat.device, obs_stats=chance)
+        if timing is not None:
+            timing[1].record()
         return res, idx_d, sign_d
 
     def _lanes_of(self, idx, n_dirs, antithetic, lane_range):
@@ -147,7 +157,8 @@ class Worker(object):
             lidx, sign = lidx[lo:hi], sign[lo:hi]
         return lidx, sign, np.zeros(len(lidx), np.int8), lane_range, rank_lanes
 
-    def evaluate(self, n_dirs, antithetic=True, seed=None, lane_range=None, out=None, novelty=False, prefetch=False):
+    def evaluate(self, n_dirs, antithetic=True, seed=None, lane_range=None, out=None, novelty=False, prefetch=False,
+                 timing=None):
         """n_dirs perturbation directions (x2 lanes if antithetic) -> FDBatch on the device.
         novelty=True also scores every lane against the strategy archive (FDBatch.novelty, device f64).
 
@@ -155,7 +166,8 @@ class Worker(object):
         draws the full index list, in order, and keeps its contiguous share).
         prefetch=True: after launching this rollout, the NEXT call's indices are drawn ahead
         (SharedNoiseTable.peek_batch: the index stream is unchanged) and uploaded on the copy stream, so the
-        next rollout does not wait for its host-to-device copy; a next call with other arguments ignores it."""
+        next rollout does not wait for its host-to-device copy; a next call with other arguments ignores it.
+        timing: (start, end) events around the rollout launch (Worker.launch)."""
         pre, self._next = self._next, None
         idx = self.noise_source.sample_batch(n_dirs)
         lidx, sign, det, lane_range, rank_lanes = self._lanes_of(idx, n_dirs, antithetic, lane_range)
@@ -168,7 +180,7 @@ class Worker(object):
         lpd = 2 if antithetic else 1
         lo = 0 if lane_range is None else lane_range[0]
         res, idx_d, sign_d = self.launch(lidx, sign, det, seed=seed, out=out, lane_offset=lo, lanes_dev=lanes_dev,
-                                         pairs=antithetic)
+                                         pairs=antithetic, timing=timing)
         if prefetch and hasattr(self.noise_source, "peek_batch"):
             nidx = self.noise_source.peek_batch(n_dirs)
             nl, ns, nd, _, _ = self._lanes_of(nidx, n_dirs, antithetic, key[2])
