@@ -1395,7 +1395,7 @@ static void launch_feat(const RolloutArgs& args, dim3 grid, dim3 block, hipStrea
   case F: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, F, WIDE>), grid, block, 0, stream, args); break;
   if constexpr (!WIDE) {
     if (args.u_inject) {  // injected draws (never with the Welford statistics: fdr_rollout_ex refuses it)
-      switch (feat) { FDR_FEAT_CASE(8) FDR_FEAT_CASE(9) FDR_FEAT_CASE(12) FDR_FEAT_CASE(13) }
+      switch (feat | 8) { FDR_FEAT_CASE(8) FDR_FEAT_CASE(9) FDR_FEAT_CASE(12) FDR_FEAT_CASE(13) }
       return;
     }
   }
