@@ -43,8 +43,9 @@ class DiscretePolicy(Policy):
         off = 0
         for m in bns:
             n = m.num_features
-            m.running_mean.copy_(bm[off:off + n])
-            m.running_var.copy_(bv[off:off + n])
+            if m.running_mean.data_ptr() != bm[off:off + n].data_ptr():   # (no-op when they alias, Policy._bn_flat)
+                m.running_mean.copy_(bm[off:off + n])
+                m.running_var.copy_(bv[off:off + n])
             m.num_batches_tracked += 1
             off += n
 

@@ -46,6 +46,25 @@ class Policy(nn.Module):
                 p.data = flat[off:off + n].view_as(p)
                 off += n
         self.flat = flat
+        # the BN running statistics as views into two flat buffers too (the [n_in | 64 | 64] order the kernels
+        # read): bn_stats() hands them out without a concatenation kernel per launch; torch's train-mode update
+        # and load_state_dict write the buffers in place
+        self._bn_flat = None
+        bns = [m for m in self.model if isinstance(m, nn.BatchNorm1d)]
+        if bns:
+            n = sum(m.num_features for m in bns)
+            fm = torch.empty(n, dtype=torch.float32, device=self._device)
+            fv = torch.empty(n, dtype=torch.float32, device=self._device)
+            off = 0
+            with torch.no_grad():
+                for m in bns:
+                    k = m.num_features
+                    fm[off:off + k].copy_(m.running_mean)
+                    fv[off:off + k].copy_(m.running_var)
+                    m.running_mean = fm[off:off + k]
+                    m.running_var = fv[off:off + k]
+                    off += k
+            self._bn_flat = (fm, fv)
         if self.KIND in ("discrete", "mujoco"):
             self.spec = engine.PolicySpec(self.KIND, self.input_shape, self.output_shape, self.num_params)
 
@@ -81,8 +100,22 @@ class Policy(nn.Module):
         bns = [m for m in self.model if isinstance(m, nn.BatchNorm1d)]
         if not bns:
             return None, None
+        fl = getattr(self, "_bn_flat", None)
+        if fl is not None and self._bn_views_intact(bns):
+            return fl
         return (torch.cat([m.running_mean for m in bns]).float().contiguous(),
                 torch.cat([m.running_var for m in bns]).float().contiguous())
+
+    def _bn_views_intact(self, bns):
+        """The modules' running stats still alias the flat buffers (a user may have reassigned one)."""
+        fm, fv = self._bn_flat
+        off = 0
+        for m in bns:
+            k = m.num_features
+            if m.running_mean.data_ptr() != fm.data_ptr() + 4 * off or m.running_var.data_ptr() != fv.data_ptr() + 4 * off:
+                return False
+            off += k
+        return True
 
     def _forward_lanes(self, x, lanes=None, n_lanes=None):
         x = torch.as_tensor(x, dtype=torch.float32)
