@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <utility>
 
 #include "fdr_common.h"
@@ -613,155 +614,167 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
     const int addr = zbase + 4 * NA * (t % kStepsPerBatch);
     return __builtin_bit_cast(float, __builtin_amdgcn_ds_bpermute(addr, __builtin_bit_cast(int, rbuf)));
   };
-  for (int t = 0; t < T; ++t) {
-    // The W1 / M / K rows are loop-invariant LDS data; hoisting their loads out of the loop would
-    // pin ~46 more VGPRs (and spill W2).  Keep them per-step reads.
-    asm volatile("" ::: "memory");
-    mark(-1, s);
-    const int tb = t % kStepsPerBatch;
-    if (!det && tb == 0) draw(t);
-    const float zt = fetch_z(t);  // this step's normal for action dim o (continuous)
-    if constexpr (FEAT & 1) {  // visited (raw) observations, worker/agent.py:36 / 58-59 (save_states)
-      if (j < NIN) a.states[((int64_t)lane * T + t) * NIN + j] = s;
-    }
-    if constexpr (FEAT & 2) {
-      // worker/agent.py:37-39: with probability obs_stats_update_chance the raw obs enters the lane's
-      // WelfordRunningStat (utils/math_helpers.py:29-38, f32, same operation order, no contraction).
-      // Coins come 64 steps at a time: lane i draws step t + i (counter k = 14), one ballot.
-      if ((t & 63) == 0) {
-        const float u = uniform24(hash_ctr(key, ulane, (uint64_t)(t + j), 14));
-        os_mask = __ballot(u < a.os_chance);
-      }
-      if ((os_mask >> (t & 63)) & 1ull) {
-#pragma clang fp contract(off)
-        const int cc = os_n;
-        os_n += 1;
-        const float delta = s - os_mean;
-        const float delta_n = delta / (float)os_n;
-        os_mean += delta_n;
-        os_m2 += (delta * delta_n) * (float)cc;
-      }
-    }
-    auto* sc = &scratch[wv];
-    constexpr bool kSame = !DISC && !norm_obs;  // mujoco: policy input == env state
-    const float* mrow = envMK + ji * MKS;
-    float pre = 0.f;
-    float h1;
-    float cand[kCand ? NA : 1];  // discrete WIDE: next state for each action
-    if constexpr (kRegIn) {
-      // policy input and env state of lanes 0 .. NIN-1, wave-uniform through v_readlane
-      const float xin = j < NIN ? policy_input(s) : 0.f;
-      float xv[NX], sv[NX];
-#pragma unroll
-      for (int k = 0; k < NX; ++k) {
-        xv[k] = k < NIN ? readlane_f(xin, k) : (k == NIN ? 1.f : 0.f);
-        sv[k] = k < NIN ? (kSame ? xv[k] : readlane_f(s, k)) : 0.f;
-      }
-      h1 = pl.layer1_env_reg(xv, sv, mreg, pre);
-      if constexpr (kCand) {
-#pragma unroll
-        for (int i = 0; i < NA; ++i) cand[i] = tanh_fast(pre + kreg[i]);
-      }
-    } else {
-    // policy input (and env state) broadcast through the wave's LDS scratch, then packed FMAs
-    // against the lane's W1 row and M row (two MACs per instruction instead of one DPP FMA)
-    sc->x[j] = j < NIN ? policy_input(s) : (j == NIN ? 1.f : 0.f);
-    if constexpr (ENV == FDR_ENV_SYNTH && !kSame) sc->h1[j] = j < NIN ? s : 0.f;
-    wave_lds_sync();
-    if constexpr (ENV == FDR_ENV_SYNTH) {
-      // one pass over the input chunks: W1 row j against x, M row j against s (M's padding
-      // columns are 0, so the bias column's 1 drops out of M s)
-      h1 = pl.template layer1_env_pk<kSame>(sc->x, sc->h1, mrow, pre);
-    } else {
-      float xb[NX];
-      lds_bcast<NX>(sc->x, xb);
-      h1 = pl.layer1(xb);
-    }
-    }
-    mark(0, h1);
-    float y;
-    if constexpr (kHead2) {
-      const float h2 = pl.layer2(h1, sc, j);
-      mark(1, h2);
-      y = pl.head2(h2, w3c, b3p, j);
-      mark(2, y);
-    } else {
-      y = pl.layers23(h1, sc, j, mark, WIDE ? w3reg : nullptr);
-    }
-    int act_d = 0;
-    float act_c = 0.f;
-    if constexpr (DISC) {
-      float p;
-      if (det || !FDR_FAST_SOFTMAX)  // wave-uniform: a scalar branch
-        p = pl.template softmax<kHead2, false>(y, j);
-      else
-        p = pl.template softmax<kHead2, (FDR_FAST_SOFTMAX != 0)>(y, j);
-      float pv[NA];
-#pragma unroll
-      for (int i = 0; i < NA; ++i) pv[i] = readlane_f(p, i);
-      float tot = 0.f;  // sequential f32 cumsum, the oracle's order
-#pragma unroll
-      for (int i = 0; i < NA; ++i) tot += pv[i];
-      // Branch-free selection (selects, no data-dependent control flow):
-      //   argmax = first maximal index; inverse CDF = first i with cumsum_i > target, i.e. the
-      //   number of (monotone) partial sums <= target, capped at NA - 1.
-      if (det) {
-        float best = pv[0];
-#pragma unroll
-        for (int i = 1; i < NA; ++i) {
-          act_d = pv[i] > best ? i : act_d;
-          best = fmaxf(best, pv[i]);
+  // The deterministic / sampled choice is fixed for the episode (wave-uniform): one specialised loop each, and the
+  // draw batches as an outer loop, so the per-step body carries neither branch.
+  auto episode = [&](auto det_tag) {
+    constexpr bool kDet = decltype(det_tag)::value;
+    for (int t0 = 0; t0 < T; t0 += kStepsPerBatch) {
+      if constexpr (!kDet) draw(t0);
+      const int nb = T - t0 < kStepsPerBatch ? T - t0 : kStepsPerBatch;
+      for (int tb = 0; tb < nb; ++tb) {
+        const int t = t0 + tb;
+        // The W1 / M / K rows are loop-invariant LDS data; hoisting their loads out of the loop would
+        // pin ~46 more VGPRs (and spill W2).  Keep them per-step reads.
+        asm volatile("" ::: "memory");
+        mark(-1, s);
+        const float zt = fetch_z(t);  // this step's normal for action dim o (continuous)
+        if constexpr (FEAT & 1) {  // visited (raw) observations, worker/agent.py:36 / 58-59 (save_states)
+          if (j < NIN) a.states[((int64_t)lane * T + t) * NIN + j] = s;
         }
-      } else {
-        const float target = readlane_f(rbuf, tb) * tot;
-        float c = 0.f;
-#pragma unroll
-        for (int i = 0; i < NA - 1; ++i) {
-          c += pv[i];
-          act_d += c <= target ? 1 : 0;
+        if constexpr (FEAT & 2) {
+          // worker/agent.py:37-39: with probability obs_stats_update_chance the raw obs enters the lane's
+          // WelfordRunningStat (utils/math_helpers.py:29-38, f32, same operation order, no contraction).
+          // Coins come 64 steps at a time: lane i draws step t + i (counter k = 14), one ballot.
+          if ((t & 63) == 0) {
+            const float u = uniform24(hash_ctr(key, ulane, (uint64_t)(t + j), 14));
+            os_mask = __ballot(u < a.os_chance);
+          }
+          if ((os_mask >> (t & 63)) & 1ull) {
+    #pragma clang fp contract(off)
+            const int cc = os_n;
+            os_n += 1;
+            const float delta = s - os_mean;
+            const float delta_n = delta / (float)os_n;
+            os_mean += delta_n;
+            os_m2 += (delta * delta_n) * (float)cc;
+          }
         }
-      }
-      // Categorical(probs) entropy: probs normalised, log clamped (torch semantics)
-      eacc -= (j < NA) ? disc_entropy_term(p, tot) : 0.f;
-    } else {
-      const float th = tanh_fast(y);
-      const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
-      eacc += __builtin_amdgcn_logf(sd);  // log2; lanes >= NA and the ln 2 scale: epilogue
-      act_c = det ? th : gauss_action(th, sd, zt);
-    }
-
-    mark(3, DISC ? (float)act_d : act_c);
-    // ---- env step ----
-    if constexpr (ENV == FDR_ENV_SYNTH) {
-      if constexpr (kCand) {
-        s = cand[0];
-#pragma unroll
-        for (int i = 1; i < NA; ++i) s = act_d == i ? cand[i] : s;
-      } else {
-        if constexpr (DISC) {
-          pre += mrow[NX + act_d];
+        auto* sc = &scratch[wv];
+        constexpr bool kSame = !DISC && !norm_obs;  // mujoco: policy input == env state
+        const float* mrow = envMK + ji * MKS;
+        float pre = 0.f;
+        float h1;
+        float cand[kCand ? NA : 1];  // discrete WIDE: next state for each action
+        if constexpr (kRegIn) {
+          // policy input and env state of lanes 0 .. NIN-1, wave-uniform through v_readlane
+          const float xin = j < NIN ? policy_input(s) : 0.f;
+          float xv[NX], sv[NX];
+    #pragma unroll
+          for (int k = 0; k < NX; ++k) {
+            xv[k] = k < NIN ? readlane_f(xin, k) : (k == NIN ? 1.f : 0.f);
+            sv[k] = k < NIN ? (kSame ? xv[k] : readlane_f(s, k)) : 0.f;
+          }
+          h1 = pl.layer1_env_reg(xv, sv, mreg, pre);
+          if constexpr (kCand) {
+    #pragma unroll
+            for (int i = 0; i < NA; ++i) cand[i] = tanh_fast(pre + kreg[i]);
+          }
         } else {
-          float kr[NA];
-#pragma unroll
-          for (int m = 0; m < NA; ++m) kr[m] = WIDE ? kreg[m] : mrow[NX + m];
-          dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in lane m of every row
+        // policy input (and env state) broadcast through the wave's LDS scratch, then packed FMAs
+        // against the lane's W1 row and M row (two MACs per instruction instead of one DPP FMA)
+        sc->x[j] = j < NIN ? policy_input(s) : (j == NIN ? 1.f : 0.f);
+        if constexpr (ENV == FDR_ENV_SYNTH && !kSame) sc->h1[j] = j < NIN ? s : 0.f;
+        wave_lds_sync();
+        if constexpr (ENV == FDR_ENV_SYNTH) {
+          // one pass over the input chunks: W1 row j against x, M row j against s (M's padding
+          // columns are 0, so the bias column's 1 drops out of M s)
+          h1 = pl.template layer1_env_pk<kSame>(sc->x, sc->h1, mrow, pre);
+        } else {
+          float xb[NX];
+          lds_bcast<NX>(sc->x, xb);
+          h1 = pl.layer1(xb);
         }
-        s = tanh_fast(pre);
+        }
+        mark(0, h1);
+        float y;
+        if constexpr (kHead2) {
+          const float h2 = pl.layer2(h1, sc, j);
+          mark(1, h2);
+          y = pl.head2(h2, w3c, b3p, j);
+          mark(2, y);
+        } else {
+          y = pl.layers23(h1, sc, j, mark, WIDE ? w3reg : nullptr);
+        }
+        int act_d = 0;
+        float act_c = 0.f;
+        if constexpr (DISC) {
+          float p;
+          if constexpr (kDet || !FDR_FAST_SOFTMAX)
+            p = pl.template softmax<kHead2, false>(y, j);
+          else
+            p = pl.template softmax<kHead2, (FDR_FAST_SOFTMAX != 0)>(y, j);
+          float pv[NA];
+    #pragma unroll
+          for (int i = 0; i < NA; ++i) pv[i] = readlane_f(p, i);
+          float tot = 0.f;  // sequential f32 cumsum, the oracle's order
+    #pragma unroll
+          for (int i = 0; i < NA; ++i) tot += pv[i];
+          // Branch-free selection (selects, no data-dependent control flow):
+          //   argmax = first maximal index; inverse CDF = first i with cumsum_i > target, i.e. the
+          //   number of (monotone) partial sums <= target, capped at NA - 1.
+          if constexpr (kDet) {
+            float best = pv[0];
+    #pragma unroll
+            for (int i = 1; i < NA; ++i) {
+              act_d = pv[i] > best ? i : act_d;
+              best = fmaxf(best, pv[i]);
+            }
+          } else {
+            const float target = readlane_f(rbuf, tb) * tot;
+            float c = 0.f;
+    #pragma unroll
+            for (int i = 0; i < NA - 1; ++i) {
+              c += pv[i];
+              act_d += c <= target ? 1 : 0;
+            }
+          }
+          // Categorical(probs) entropy: probs normalised, log clamped (torch semantics)
+          eacc -= (j < NA) ? disc_entropy_term(p, tot) : 0.f;
+        } else {
+          const float th = tanh_fast(y);
+          const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
+          eacc += __builtin_amdgcn_logf(sd);  // log2; lanes >= NA and the ln 2 scale: epilogue
+          act_c = kDet ? th : gauss_action(th, sd, zt);
+        }
+
+        mark(3, DISC ? (float)act_d : act_c);
+        // ---- env step ----
+        if constexpr (ENV == FDR_ENV_SYNTH) {
+          if constexpr (kCand) {
+            s = cand[0];
+    #pragma unroll
+            for (int i = 1; i < NA; ++i) s = act_d == i ? cand[i] : s;
+          } else {
+            if constexpr (DISC) {
+              pre += mrow[NX + act_d];
+            } else {
+              float kr[NA];
+    #pragma unroll
+              for (int m = 0; m < NA; ++m) kr[m] = WIDE ? kreg[m] : mrow[NX + m];
+              dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in lane m of every row
+            }
+            s = tanh_fast(pre);
+          }
+          racc += (double)s;  // lane 0 holds the reward s'[0]; other lanes' sums are discarded
+        } else {
+          // custom_envs/simple_trap_env: node.py:9-14, tile_map.py:11-23, environment.py:33-48
+          const int prev_x = col * 7;
+          const int tc = col + act_d / 3 - 1, tr = row + act_d % 3 - 1;
+          if (tc >= 0 && tc < a.map_w && tr >= 0 && tr < a.map_h && a.walkable[tr * a.map_w + tc]) {
+            col = tc;
+            row = tr;
+          }
+          racc += (double)(col * 7 - prev_x);
+          s = trap_obs(j, col, row);
+        }
+        mark(4, s);
       }
-      racc += (double)s;  // lane 0 holds the reward s'[0]; other lanes' sums are discarded
-    } else {
-      // custom_envs/simple_trap_env: node.py:9-14, tile_map.py:11-23, environment.py:33-48
-      const int prev_x = col * 7;
-      const int tc = col + act_d / 3 - 1, tr = row + act_d % 3 - 1;
-      if (tc >= 0 && tc < a.map_w && tr >= 0 && tr < a.map_h && a.walkable[tr * a.map_w + tc]) {
-        col = tc;
-        row = tr;
-      }
-      racc += (double)(col * 7 - prev_x);
-      s = trap_obs(j, col, row);
     }
-    mark(4, s);
-  }
+  };
+  if (det)
+    episode(std::true_type{});
+  else
+    episode(std::false_type{});
 #ifdef FDR_PHASE_STAMPS
   if (blockIdx.x == 0 && threadIdx.x == 0)
     for (int k = 0; k < 5; ++k) g_phase_stamps[k] = ph_acc[k];

@@ -50,8 +50,8 @@ class Policy(nn.Module):
         # read): bn_stats() hands them out without a concatenation kernel per launch; torch's train-mode update
         # and load_state_dict write the buffers in place
         self._bn_flat = None
-        bns = [m for m in self.model if isinstance(m, nn.BatchNorm1d)]
-        if bns:
+        bns = [m for m in self.model if isinstance(m, nn.BatchNorm1d)] if isinstance(self.model, nn.Sequential) else []
+        if bns and self.KIND == "discrete":
             n = sum(m.num_features for m in bns)
             fm = torch.empty(n, dtype=torch.float32, device=self._device)
             fv = torch.empty(n, dtype=torch.float32, device=self._device)
