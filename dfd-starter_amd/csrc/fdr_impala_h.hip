@@ -1406,6 +1406,9 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
 #ifndef FDR_H3_ENTRY
 #define FDR_H3_ENTRY 1
 #endif
+#ifndef FDR_S2_ISSUE
+#define FDR_S2_ISSUE 1
+#endif
 #ifdef FDR_H3_FINE  // diagnostics build: clocks inside the h3 entry bands (dbg[64..])
 #define FDR_FINE_STAMP(a, k) FDR_STAMP(a, k)
 #else
@@ -1550,7 +1553,11 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   // ---- stage 2: entry (16 -> 32 at 32 x 32, pooled to 16 x 16) in 4 bands; X2 into T1's consumed rows (h3: 2
   // bands of 16 rows, pool in registers; band 1 reads padded rows 16..33, past X2's first half) ----
   if constexpr (H3) {
-    st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
+    // FDR_S2_ISSUE (r10): where conv 6's weight block is requested.  0: before the two bands (its 9 staging VGPRs live
+    // across both bands' convs -- one 16-B chunk was spilled, the store waiting on its own global load, and the
+    // reload read back at the commit: the kernel's only scratch traffic, 33.5 MB written + read per launch);
+    // 1: after band 1's conv, once the accumulators are pooled (the lane's other envs have it in L2 by then)
+    if constexpr (FDR_S2_ISSUE == 0) st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
     for (int bd = 0; bd < 2; ++bd) {
       h4 prev[4], P[4], Bx[4];
       f32x4 acc[4][2];
@@ -1562,6 +1569,9 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
 #pragma unroll
         for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[5 * 32 + nt * 16 + 4 * (ln >> 4) + k];
       pool_nat<32>(acc, bz, P, Bx);
+      if constexpr (FDR_S2_ISSUE == 1) {
+        if (bd == 1) st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
+      }
       FDR_FINE_STAMP(a, 81 + 4 * bd);
       band_prev_h3<32, 32, false>(prev, R + kH3EX2, bd, wave, ln);
       // (barrier inside).  Band 1 also writes T2 = relu(BN(X2)) of its rows: T2 lies over T1's rows 15.., which band
