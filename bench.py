@@ -349,7 +349,9 @@ def main():
     dev_index = 0 if rehearse else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    if world > 1:
+    # FDR_FORCE_COLLECTIVES=1 under a one-rank launcher: the N > 1 exchange on a process group of one (RCCL path check)
+    from fdr import dist as fdist
+    if world > 1 or (fdist.FORCE and "WORLD_SIZE" in os.environ):
         if rehearse:
             dist.init_process_group("gloo")
         else:
@@ -615,9 +617,11 @@ def main():
     }
     if novelty:
         line["config"]["novelty"] = {"archive": len(handler.points), "zeta": ZETA_SIZE, "omega": omega.omega}
+    if fdist.FORCE and world == 1:
+        line["config"]["collectives"] = "forced on a one-rank process group (FDR_FORCE_COLLECTIVES=1)"
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -11,12 +11,20 @@ One process per GPU; the perturbation set is split into contiguous lane slices, 
     (P * 8 bytes).  DSGD then runs replicated and bit-identically on every rank.
 Backend "nccl" is RCCL on ROCm (xGMI); the same helpers run on gloo for CPU tests.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
+# FDR_FORCE_COLLECTIVES=1: a process group of ONE rank still takes the sharded exchange (count / reward all-gathers,
+# the moments or gradient all-reduce) -- runs the RCCL code path on a one-GPU box (tests/test_gpu_dist_equivalence.py)
+FORCE = os.environ.get("FDR_FORCE_COLLECTIVES") == "1"
+
 
 def active(group=None):
-    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size(group) > 1 or FORCE
 
 
 def world_rank(group=None):
@@ -36,7 +44,7 @@ def lane_range(n_dirs, lanes_per_dir, world, rank):
 def exchange_counts(n, device, group=None):
     """Every rank's local count (one all-gather of an int64; a host sync) -> list of ints in rank order."""
     ws, _ = world_rank(group)
-    if ws == 1:
+    if not active(group):
         return [int(n)]
     t = torch.tensor([int(n)], dtype=torch.int64, device=device)
     counts = torch.empty(ws, dtype=torch.int64, device=device)
@@ -51,7 +59,7 @@ def gather_rewards(local, group=None, sizes=None):
     lane_range split sets FDBatch.rank_lanes): then the exchange is ONE all-gather issued on the
     stream with no host synchronisation.  Without it the counts are exchanged first (a host sync)."""
     ws, rank = world_rank(group)
-    if ws == 1:
+    if not active(group):
         return local, 0
     if sizes is None:
         n = torch.tensor([local.numel()], dtype=torch.int64, device=local.device)

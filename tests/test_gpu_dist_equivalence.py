@@ -49,3 +49,26 @@ def test_two_rank_fd_steps_equal_one_rank(tmp_path, weighting, port, preset):
     np.testing.assert_array_equal(u0, np.load(os.path.join(out, "upd_rank1.npy")))
     np.testing.assert_allclose(u0, u1, rtol=1e-6)
     assert np.all(u0 > 0)
+
+
+@pytest.mark.parametrize("weighting,port", [("zscore", 29551), ("centred_rank", 29552)])
+def test_rccl_one_rank_exchange_equals_single_process(tmp_path, weighting, port):
+    """The exchange on RCCL (backend "nccl"): a one-rank process group with FDR_FORCE_COLLECTIVES=1 runs the
+    sharded path -- count exchange and reward all-gathers, the one-collective moments all-reduce (z-score) or the
+    gradient all-reduce (centred rank) -- through RCCL on the box's GPU, and must land where the single-process
+    learner does (the moments form vs the direct z-score: rounding only)."""
+    out = str(tmp_path)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.run([sys.executable, SCRIPT, "single", weighting, out], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-2000:]
+    env["FDR_FORCE_COLLECTIVES"] = "1"
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), SCRIPT, "nccl1", weighting, out],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert p.returncode == 0, p.stderr[-2000:]
+    single = np.load(os.path.join(out, "theta_single.npy"))
+    r0 = np.load(os.path.join(out, "theta_rank0.npy"))
+    assert float(np.abs(r0 - single).max()) <= 1e-6
+    np.testing.assert_allclose(np.load(os.path.join(out, "upd_rank0.npy")), np.load(os.path.join(out, "upd_single.npy")),
+                               rtol=1e-6)

@@ -4,6 +4,8 @@
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
         tools/dist_check.py multi <weighting> <out_dir>            # 2 ranks  -> <out_dir>/theta_rank{r}.npy
     python tools/dist_check.py compare <weighting> <out_dir>
+    FDR_FORCE_COLLECTIVES=1 python -m torch.distributed.run --nproc-per-node 1 ... tools/dist_check.py nccl1 <w> <out>
+                                                                   # RCCL, one rank, the sharded exchange forced on
     ... <mode> <weighting> <out_dir> bench                         # BASELINE config 3 size (below)
 
 weighting: "zscore" (the default one-collective moments form) or "centred_rank" (all-gather + all-reduce).
@@ -34,10 +36,12 @@ def run(mode, weighting, out, preset="small"):
     import torch
     import torch.distributed as dist
     rank = int(os.environ.get("RANK", "0"))
-    if mode == "multi":
-        dist.init_process_group("gloo")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if mode == "multi":
+        dist.init_process_group("gloo")
+    elif mode == "nccl1":   # RCCL with ONE rank; FDR_FORCE_COLLECTIVES=1 keeps the sharded exchange on
+        dist.init_process_group("nccl", device_id=dev)
     from dsgd import DSGD
     from envs import SyntheticEnv
     from learner import FiniteDifferences
@@ -86,7 +90,7 @@ def run(mode, weighting, out, preset="small"):
     name = "single" if mode == "single" else "rank%d" % rank
     np.save(os.path.join(out, "theta_%s.npy" % name), policy.get_trainable_flat())
     np.save(os.path.join(out, "upd_%s.npy" % name), np.asarray(upd))
-    if mode == "multi":
+    if mode in ("multi", "nccl1"):
         dist.destroy_process_group()
 
 
