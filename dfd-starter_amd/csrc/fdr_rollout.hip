@@ -27,6 +27,9 @@
 #include "fdr_internal.h"
 #include "fdr_wave.h"
 
+#ifndef FDR_PAIR_HEAD  // pair kernel head: 0 = DPP-broadcast dot (32 DPP FMAs), 1 = packed FMAs + reduce-scatter
+#define FDR_PAIR_HEAD 0
+#endif
 #ifndef FDR_FAST_SOFTMAX  // sampled discrete lanes: approximate exp / reciprocal softmax (MlpLane::softmax)
 #define FDR_FAST_SOFTMAX 1
 #endif
@@ -847,6 +850,34 @@ __device__ __forceinline__ void reduce_scatter16(float (&v)[16]) {
       : "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
 }
 
+// Reduce-scatter of 16 slots over the 16 threads of a DPP row (packed head, FDR_PAIR_HEAD = 1): register i of
+// thread t holds slot i ^ (t & 15); levels with partners t ^ 15 (row_mirror), t ^ 7 (row_half_mirror), t ^ 2, t ^ 1
+// (quad perms) each add the partner's register i ^ mask, leaving the row sum of slot t & 15 in v[0].
+__device__ __forceinline__ void reduce_scatter16_row(float (&v)[16]) {
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %15, %0 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %14, %1 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %2, %13, %2 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %3, %12, %3 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %4, %11, %4 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %5, %10, %5 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %6, %9, %6 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %7, %8, %7 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %7, %0 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %6, %1 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %2, %5, %2 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %3, %4, %3 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %2, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %3, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+      : "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
+}
+
 // tanh_fast on a register pair: packed mul / add / fma around the two exp and two rcp
 __device__ __forceinline__ f2 tanh2_fast(f2 x) {
   const f2 t = x * f2{2.88539008177792681f, 2.88539008177792681f};
@@ -923,7 +954,21 @@ struct MlpPair {
     const int u2a = 16 * r + c, u2b = 16 * r + 8 + c;  // this thread's layer-2 units
     b2a = src.get(L::L2B + u2a);
     b2b = src.get(L::L2B + u2b);
-    if (o < NOUT) {
+    if constexpr (FDR_PAIR_HEAD == 1) {
+      // packed head: chunk m = (W3[(2m)^o][u2a], W3[(2m+1)^o][u2a], W3[(2m)^o][u2b], W3[(2m+1)^o][u2b]) -- register
+      // slot i of this thread holds output i ^ o (the reduce-scatter's thread-dependent order); every W3 element is
+      // loaded by exactly one thread of the half (its unit's), so norm2 counts it once
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int s0 = (2 * m) ^ o, s1 = (2 * m + 1) ^ o;
+        const float e0 = s0 < NOUT ? src.get(L::L3W + (int64_t)s0 * kHidden + u2a) : 0.f;
+        const float e1 = s1 < NOUT ? src.get(L::L3W + (int64_t)s1 * kHidden + u2a) : 0.f;
+        const float e2 = s0 < NOUT ? src.get(L::L3W + (int64_t)s0 * kHidden + u2b) : 0.f;
+        const float e3 = s1 < NOUT ? src.get(L::L3W + (int64_t)s1 * kHidden + u2b) : 0.f;
+        my[(2 * kW1Chunks + m) * kWave] = float4{e0, e1, e2, e3};
+      }
+      b3 = o < NOUT ? (rho == 0 ? src.get(L::L3B + o) : src.get_nocount(L::L3B + o)) : 0.f;
+    } else if (o < NOUT) {
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         float e[4];
@@ -1141,9 +1186,26 @@ struct MlpPair {
       h2a = h2.x;
       h2b = h2.y;
     }
-    float s0, s1, s2, s3;  // four independent chains of 8 (first product a v_mul: no zeroing)
-    dpp_dot_32x4(s0, s1, s2, s3, h2a, h2b, w3);
-    float u = (s0 + s2) + (s1 + s3), v = u;
+    float u;
+    if constexpr (FDR_PAIR_HEAD == 1) {
+      // packed head: 8 output pairs x this thread's two units (16 packed MACs), then a 4-level reduce-scatter over
+      // the 16-thread row (partners t^15, t^7, t^2, t^1) leaves output o = t & 15 in this thread
+      float hs[16];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const f2 a = pk_fma(f2{w3[4 * m + 2], w3[4 * m + 3]}, f2{h2b, h2b},
+                            f2{w3[4 * m], w3[4 * m + 1]} * f2{h2a, h2a});
+        hs[2 * m] = a.x;
+        hs[2 * m + 1] = a.y;
+      }
+      reduce_scatter16_row(hs);
+      u = hs[0];
+    } else {
+      float s0, s1, s2, s3;  // four independent chains of 8 (first product a v_mul: no zeroing)
+      dpp_dot_32x4(s0, s1, s2, s3, h2a, h2b, w3);
+      u = (s0 + s2) + (s1 + s3);
+    }
+    float v = u;
     permlane16_swap(u, v);  // u = row 2h's partial, v = row 2h+1's, in both rows of half h
     const float out = (u + v) + b3;
     mark(2, out);
