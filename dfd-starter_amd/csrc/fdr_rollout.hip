@@ -30,6 +30,9 @@
 #ifndef FDR_PAIR_HEAD  // pair kernel head: 0 = DPP-broadcast dot (32 DPP FMAs), 1 = packed FMAs + reduce-scatter
 #define FDR_PAIR_HEAD 0
 #endif
+#ifndef FDR_PAIR_CHAINS  // pair kernel: layer 1 on 4 accumulator chains, the env's K a on 2 (r10 A/B switch)
+#define FDR_PAIR_CHAINS 0
+#endif
 #ifndef FDR_FAST_SOFTMAX  // sampled discrete lanes: approximate exp / reciprocal softmax (MlpLane::softmax)
 #define FDR_FAST_SOFTMAX 1
 #endif
@@ -878,6 +881,23 @@ __device__ __forceinline__ void reduce_scatter16_row(float (&v)[16]) {
       : "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
 }
 
+// acc += sum_{m<6} w[m] * X(row lane m) as two chains of three DPP FMAs + one add (FDR_PAIR_CHAINS): the env's
+// K a after the action, 4 dependent steps instead of 6
+__device__ __forceinline__ void dpp_tail6_2chains(float& acc, float X, const float* w) {
+  float b;
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_fmac_f32_dpp %0, %2, %3 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
+      "v_mul_f32_dpp %1, %2, %6 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %4 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %7 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %2, %5 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %2, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
+      : "+v"(acc), "=&v"(b)
+      : "v"(X), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]));
+  acc += b;
+}
+
 // tanh_fast on a register pair: packed mul / add / fma around the two exp and two rcp
 __device__ __forceinline__ f2 tanh2_fast(f2 x) {
   const f2 t = x * f2{2.88539008177792681f, 2.88539008177792681f};
@@ -1074,8 +1094,12 @@ struct MlpPair {
     f2 aa0 = {b1a, 0.f}, aa1 = {0.f, 0.f}, ab0 = {b1b, 0.f}, ab1 = {0.f, 0.f};
     f2 am0 = {0.f, 0.f}, am1 = {0.f, 0.f};
     if constexpr (kPk) {
-      // units (a, b) packed: acc[k & 1] += (w_a(k), w_b(k)) * x_k; the bias column (k = NIN) is added
-      f2 acc[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
+      // units (a, b) packed: acc[k % NC] += (w_a(k), w_b(k)) * x_k; the bias column (k = NIN) is added.
+      // NC = 2 chains of ~9 dependent packed FMAs, or 4 of ~5 (FDR_PAIR_CHAINS) + two packed adds
+      constexpr int NC = FDR_PAIR_CHAINS ? 4 : 2;
+      f2 acc[NC];
+#pragma unroll
+      for (int q = 0; q < NC; ++q) acc[q] = f2{0.f, 0.f};
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         const float4 xv = xq(q), mv = rows.m[q];
@@ -1086,7 +1110,7 @@ struct MlpPair {
           if (k < NIN) {
             const float4 w = rows.wp[k >> 1];
             const f2 xp = (i < 2) ? f2{xv.x, xv.y} : f2{xv.z, xv.w};
-            acc[k & 1] = (k & 1) ? pk_fma_bhi(f2{w.z, w.w}, xp, acc[1]) : pk_fma_blo(f2{w.x, w.y}, xp, acc[0]);
+            acc[k % NC] = (k & 1) ? pk_fma_bhi(f2{w.z, w.w}, xp, acc[k % NC]) : pk_fma_blo(f2{w.x, w.y}, xp, acc[k % NC]);
           }
         }
         am0 = pk_fma(f2{mv.x, mv.y}, f2{sv.x, sv.y}, am0);
@@ -1094,14 +1118,19 @@ struct MlpPair {
       }
       if constexpr (kTail) {  // input 4 NQ = NIN - 1, then the bias
         const float4 w = rows.wp[(NIN - 1) >> 1];
-        acc[(NIN - 1) & 1] = pk_fma(((NIN - 1) & 1) ? f2{w.z, w.w} : f2{w.x, w.y}, f2{xt, xt}, acc[(NIN - 1) & 1]);
+        acc[(NIN - 1) % NC] = pk_fma(((NIN - 1) & 1) ? f2{w.z, w.w} : f2{w.x, w.y}, f2{xt, xt}, acc[(NIN - 1) % NC]);
         am1.x = fmaf(rows.tm, kSameInput ? xt : st, am1.x);
       }
       {
         const float4 w = rows.wp[NIN >> 1];
-        acc[NIN & 1] = acc[NIN & 1] + ((NIN & 1) ? f2{w.z, w.w} : f2{w.x, w.y});
+        acc[NIN % NC] = acc[NIN % NC] + ((NIN & 1) ? f2{w.z, w.w} : f2{w.x, w.y});
       }
-      const f2 am = am0 + am1, h = acc[0] + acc[1];
+      f2 h;
+      if constexpr (NC == 4)
+        h = (acc[0] + acc[2]) + (acc[1] + acc[3]);
+      else
+        h = acc[0] + acc[1];
+      const f2 am = am0 + am1;
       env = am.x + am.y;
       if constexpr (DISC) {
         return f2{act1(h.x, a1a, c1a), act1(h.y, a1b, c1b)};
@@ -1200,6 +1229,10 @@ struct MlpPair {
       }
       reduce_scatter16_row(hs);
       u = hs[0];
+    } else if constexpr (FDR_PAIR_CHAINS >= 2) {
+      float s0, s1, s2, s3, s4, s5, s6, s7;  // eight chains of 4
+      dpp_dot_32x8(s0, s1, s2, s3, s4, s5, s6, s7, h2a, h2b, w3);
+      u = ((s0 + s4) + (s2 + s6)) + ((s1 + s5) + (s3 + s7));
     } else {
       float s0, s1, s2, s3;  // four independent chains of 8 (first product a v_mul: no zeroing)
       dpp_dot_32x4(s0, s1, s2, s3, h2a, h2b, w3);
@@ -1374,7 +1407,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
       eacc += __builtin_amdgcn_logf(sd);
       const float act_c = det ? th : gauss_action(th, sd, zt);
       mark(3, act_c);
-      dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in thread m of both rows of the half
+      if constexpr (FDR_PAIR_CHAINS && NA == 6)
+        dpp_tail6_2chains(pre, act_c, kr);   // a[m] sits in thread m of both rows of the half
+      else
+        dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in thread m of both rows of the half
     }
     s = tanh_fast(pre);
     racc += (double)s;  // thread 0 of the half holds the reward s'[0]
