@@ -30,6 +30,9 @@
 #ifndef FDR_PAIR_HEAD  // pair kernel head: 0 = DPP-broadcast dot (32 DPP FMAs), 1 = packed FMAs + reduce-scatter
 #define FDR_PAIR_HEAD 0
 #endif
+#ifndef FDR_PAIR_NOMOV  // pair kernel: op_sel broadcasts in L2, packed multiplies start the L1 chains (r10 A/B)
+#define FDR_PAIR_NOMOV 1
+#endif
 #ifndef FDR_PAIR_CHAINS  // pair kernel: layer 1 on 4 accumulator chains, the env's K a on 2 (r10 A/B switch)
 #define FDR_PAIR_CHAINS 0
 #endif
@@ -138,6 +141,18 @@ __device__ __forceinline__ f2 pk_fma_blo(f2 a, f2 b, f2 c) {
 }
 __device__ __forceinline__ f2 pk_fma_bhi(f2 a, f2 b, f2 c) {
   asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[1,1,1]" : "+v"(c) : "v"(a), "v"(b));
+  return c;
+}
+
+// a * (b.x, b.x) / a * (b.y, b.y): the first term of an op_sel chain (no zeroed accumulator to move in)
+__device__ __forceinline__ f2 pk_mul_blo(f2 a, f2 b) {
+  f2 c;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(c) : "v"(a), "v"(b));
+  return c;
+}
+__device__ __forceinline__ f2 pk_mul_bhi(f2 a, f2 b) {
+  f2 c;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(c) : "v"(a), "v"(b));
   return c;
 }
 
@@ -1110,7 +1125,10 @@ struct MlpPair {
           if (k < NIN) {
             const float4 w = rows.wp[k >> 1];
             const f2 xp = (i < 2) ? f2{xv.x, xv.y} : f2{xv.z, xv.w};
-            acc[k % NC] = (k & 1) ? pk_fma_bhi(f2{w.z, w.w}, xp, acc[k % NC]) : pk_fma_blo(f2{w.x, w.y}, xp, acc[k % NC]);
+            if (FDR_PAIR_NOMOV && k < NC)
+              acc[k % NC] = (k & 1) ? pk_mul_bhi(f2{w.z, w.w}, xp) : pk_mul_blo(f2{w.x, w.y}, xp);
+            else
+              acc[k % NC] = (k & 1) ? pk_fma_bhi(f2{w.z, w.w}, xp, acc[k % NC]) : pk_fma_blo(f2{w.x, w.y}, xp, acc[k % NC]);
           }
         }
         am0 = pk_fma(f2{mv.x, mv.y}, f2{sv.x, sv.y}, am0);
@@ -1196,7 +1214,86 @@ struct MlpPair {
 #pragma unroll
     for (int k = 0; k < 8; ++k)
 #pragma unroll
-      for (int p = 0; p < 8; ++p) acc[p] = pk_fma(w2[p * 8 + k], f2{x[k], x[k]}, acc[p]);
+      for (int p = 0; p < 8; ++p)
+        if (!FDR_PAIR_NOMOV || k == 0) acc[p] = pk_fma(w2[p * 8 + k], f2{x[k], x[k]}, acc[p]);
+#if FDR_PAIR_NOMOV
+    // k >= 1 as op_sel broadcasts of the b128 pairs (x[k - 1], x[k]) / (x[k], x[k + 1]) in ONE asm statement: the
+    // compiler follows every asm statement with an s_nop, and would move each odd x[k] to an even register
+    // (operands: %0-%7 acc, %(8 + 8 (k - 1) + p) = w2[8 p + k], %64-%67 the x pairs)
+    {
+      const f2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]}, x45 = {x[4], x[5]}, x67 = {x[6], x[7]};
+#define FDR_L2_HI "op_sel:[0,1,0] op_sel_hi:[1,1,1]"
+#define FDR_L2_LO "op_sel_hi:[1,0,1]"
+      asm(
+          "v_pk_fma_f32 %0, %8, %64, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %9, %64, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %10, %64, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %11, %64, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %4, %12, %64, %4 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %5, %13, %64, %5 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %6, %14, %64, %6 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %7, %15, %64, %7 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %16, %65, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %17, %65, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %18, %65, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %19, %65, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %4, %20, %65, %4 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %5, %21, %65, %5 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %6, %22, %65, %6 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %7, %23, %65, %7 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %24, %65, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %25, %65, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %26, %65, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %27, %65, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %4, %28, %65, %4 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %5, %29, %65, %5 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %6, %30, %65, %6 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %7, %31, %65, %7 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %32, %66, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %33, %66, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %34, %66, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %35, %66, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %4, %36, %66, %4 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %5, %37, %66, %5 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %6, %38, %66, %6 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %7, %39, %66, %7 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %40, %66, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %41, %66, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %42, %66, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %43, %66, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %4, %44, %66, %4 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %5, %45, %66, %5 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %6, %46, %66, %6 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %7, %47, %66, %7 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %48, %67, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %49, %67, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %50, %67, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %51, %67, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %4, %52, %67, %4 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %5, %53, %67, %5 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %6, %54, %67, %6 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %7, %55, %67, %7 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %56, %67, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %57, %67, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %58, %67, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %59, %67, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %4, %60, %67, %4 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %5, %61, %67, %5 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %6, %62, %67, %6 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %7, %63, %67, %7 " FDR_L2_HI "\n"
+          : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]), "+v"(acc[7])
+          : "v"(w2[1]), "v"(w2[9]), "v"(w2[17]), "v"(w2[25]), "v"(w2[33]), "v"(w2[41]), "v"(w2[49]), "v"(w2[57]),
+            "v"(w2[2]), "v"(w2[10]), "v"(w2[18]), "v"(w2[26]), "v"(w2[34]), "v"(w2[42]), "v"(w2[50]), "v"(w2[58]),
+            "v"(w2[3]), "v"(w2[11]), "v"(w2[19]), "v"(w2[27]), "v"(w2[35]), "v"(w2[43]), "v"(w2[51]), "v"(w2[59]),
+            "v"(w2[4]), "v"(w2[12]), "v"(w2[20]), "v"(w2[28]), "v"(w2[36]), "v"(w2[44]), "v"(w2[52]), "v"(w2[60]),
+            "v"(w2[5]), "v"(w2[13]), "v"(w2[21]), "v"(w2[29]), "v"(w2[37]), "v"(w2[45]), "v"(w2[53]), "v"(w2[61]),
+            "v"(w2[6]), "v"(w2[14]), "v"(w2[22]), "v"(w2[30]), "v"(w2[38]), "v"(w2[46]), "v"(w2[54]), "v"(w2[62]),
+            "v"(w2[7]), "v"(w2[15]), "v"(w2[23]), "v"(w2[31]), "v"(w2[39]), "v"(w2[47]), "v"(w2[55]), "v"(w2[63]),
+            "v"(x01), "v"(x23), "v"(x45), "v"(x67));
+#undef FDR_L2_LO
+#undef FDR_L2_HI
+    }
+#endif
     // reduce-scatter over the 8 threads of the half-row: slot i = acc[i / 2][i % 2], output of
     // slot i = 16r + 8 (i % 2) + (c ^ sigma(i / 2)); partners c ^ 7, c ^ 2, c ^ 1
     float sl[16];
