@@ -33,6 +33,9 @@
 #ifndef FDR_PAIR_NOMOV  // pair kernel: op_sel broadcasts in L2, packed multiplies start the L1 chains (r10 A/B)
 #define FDR_PAIR_NOMOV 1
 #endif
+#ifndef FDR_RS_OUT  // pair kernel: L2 reduce-scatter with untied outputs (r10 A/B)
+#define FDR_RS_OUT 1
+#endif
 #ifndef FDR_PAIR_CHAINS  // pair kernel: layer 1 on 4 accumulator chains, the env's K a on 2 (r10 A/B switch)
 #define FDR_PAIR_CHAINS 0
 #endif
@@ -868,6 +871,34 @@ __device__ __forceinline__ void reduce_scatter16(float (&v)[16]) {
       : "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
 }
 
+// reduce_scatter16 with untied outputs (FDR_PAIR_NOMOV): level 1 writes fresh registers, so the compiler does not
+// copy the low halves of the packed accumulators into separate tied registers; returns the two kept slots
+__device__ __forceinline__ f2 reduce_scatter16_out(const float (&v)[16]) {
+  float o[8];
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %16, %8 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %17, %9 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %2, %18, %10 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %3, %19, %11 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %4, %20, %12 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %5, %21, %13 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %6, %22, %14 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %7, %23, %15 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %4, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %5, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %2, %6, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %3, %7, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "s_nop 1\n\t"
+      "v_add_f32_dpp %0, %2, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %3, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7])
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]), "v"(v[9]),
+        "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
+  return f2{o[0], o[1]};
+}
+
 // Reduce-scatter of 16 slots over the 16 threads of a DPP row (packed head, FDR_PAIR_HEAD = 1): register i of
 // thread t holds slot i ^ (t & 15); levels with partners t ^ 15 (row_mirror), t ^ 7 (row_half_mirror), t ^ 2, t ^ 1
 // (quad perms) each add the partner's register i ^ mask, leaving the row sum of slot t & 15 in v[0].
@@ -1299,9 +1330,15 @@ struct MlpPair {
     float sl[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) sl[i] = (i & 1) ? acc[i >> 1].y : acc[i >> 1].x;
+#if FDR_RS_OUT
+    const f2 zs = reduce_scatter16_out(sl);
+    const float za = zs.x + b2a;  // unit 16r + c
+    const float zb = zs.y + b2b;  // unit 16r + 8 + c
+#else
     reduce_scatter16(sl);  // one asm block: the SLP vectoriser would split the DPP adds into movs
     const float za = sl[0] + b2a;  // unit 16r + c
     const float zb = sl[1] + b2b;  // unit 16r + 8 + c
+#endif
     mark(1, za);
     float h2a, h2b;
     if constexpr (DISC) {
