@@ -37,10 +37,12 @@ __device__ __forceinline__ float normal_bm(uint64_t h) {
 }
 
 // tanh(x) = 1 - 2 / (1 + e^{2x}) on v_exp_f32 / v_rcp_f32 (abs error ~3e-7; saturates to +-1)
-__device__ __forceinline__ float tanh_fast(float x) {
-  const float e = __builtin_amdgcn_exp2f(x * 2.88539008177792681f);  // 2 * log2(e)
+constexpr float kTanhScale = 2.88539008177792681f;  // 2 * log2(e)
+__device__ __forceinline__ float tanh_pre(float t) {  // tanh(x) for t = kTanhScale * x
+  const float e = __builtin_amdgcn_exp2f(t);
   return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
 }
+__device__ __forceinline__ float tanh_fast(float x) { return tanh_pre(x * kTanhScale); }
 
 // ---------------------------------------------------------------------------------------------
 // Wave-scope LDS ordering: LDS ops of one wave complete in order, so a wave that only talks to

@@ -39,6 +39,9 @@
 #ifndef FDR_PAIR_CHAINS  // pair kernel: layer 1 on 4 accumulator chains, the env's K a on 2 (r10 A/B switch)
 #define FDR_PAIR_CHAINS 0
 #endif
+#ifndef FDR_PAIR_PRESCALE  // pair kernel: tanh pre-activations scaled by 2 log2(e) in the weights, biases in the chains
+#define FDR_PAIR_PRESCALE 1
+#endif
 #ifndef FDR_FAST_SOFTMAX  // sampled discrete lanes: approximate exp / reciprocal softmax (MlpLane::softmax)
 #define FDR_FAST_SOFTMAX 1
 #endif
@@ -945,10 +948,25 @@ __device__ __forceinline__ void dpp_tail6_2chains(float& acc, float X, const flo
 }
 
 // tanh_fast on a register pair: packed mul / add / fma around the two exp and two rcp
-__device__ __forceinline__ f2 tanh2_fast(f2 x) {
-  const f2 t = x * f2{2.88539008177792681f, 2.88539008177792681f};
+__device__ __forceinline__ f2 tanh2_pre(f2 t) {  // t = 2 log2(e) x
   const f2 d = f2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + f2{1.f, 1.f};
   return pk_fma(f2{-2.f, -2.f}, f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)}, f2{1.f, 1.f});
+}
+__device__ __forceinline__ f2 tanh2_fast(f2 x) {
+  return tanh2_pre(x * f2{kTanhScale, kTanhScale});
+}
+// FDR_PAIR_PRESCALE: every weight and bias feeding a tanh is stored times kTanhScale (after its norm2 count), so
+// the activation starts at the exp2 -- one multiply fewer per tanh (L1, L2, head, env: 4 per step)
+constexpr float kPreScale = FDR_PAIR_PRESCALE ? kTanhScale : 1.f;
+template <bool kPre>
+__device__ __forceinline__ float tanh_act(float z) {
+  if constexpr (kPre) return tanh_pre(z);
+  else return tanh_fast(z);
+}
+template <bool kPre>
+__device__ __forceinline__ f2 tanh2_act(f2 z) {
+  if constexpr (kPre) return tanh2_pre(z);
+  else return tanh2_fast(z);
 }
 
 template <int NIN, int NA, bool DISC>
@@ -959,6 +977,8 @@ struct MlpPair {
   static_assert(NX <= 32, "pair kernel: policy input wider than 32");
   static constexpr bool kBiasCol = NIN < NX;
   static constexpr bool kW1Lds = NIN > 8;
+  static constexpr bool kPre = !DISC && FDR_PAIR_PRESCALE;  // tanh layers' weights stored x kTanhScale
+  static constexpr float kWS = kPre ? kTanhScale : 1.f;
   static constexpr int kW1Chunks = kW1Lds ? NX / 4 : 0;     // per W1 row
   static constexpr int kTileF4 = (2 * kW1Chunks + 8) * kWave;  // float4 per wave: W1 rows, W3 slice
   f2 w1a[kW1Lds ? 1 : NX / 2], w1b[kW1Lds ? 1 : NX / 2];
@@ -980,7 +1000,7 @@ struct MlpPair {
     float4* my = wave_tile + tid;
     tile = my;
     auto w1v = [&](int u, int k) {
-      return k < NIN ? src.get(L::L1W + (int64_t)u * NIN + k) : (k == NIN ? src.get(L::L1B + u) : 0.f);
+      return kWS * (k < NIN ? src.get(L::L1W + (int64_t)u * NIN + k) : (k == NIN ? src.get(L::L1B + u) : 0.f));
     };
     if constexpr (kPk) {
 #pragma unroll
@@ -1005,8 +1025,8 @@ struct MlpPair {
         w1b[p] = f2{f0, f1};
       }
     }
-    b1a = kBiasCol ? 0.f : src.get(L::L1B + ua);
-    b1b = kBiasCol ? 0.f : src.get(L::L1B + ub);
+    b1a = kBiasCol ? 0.f : kWS * src.get(L::L1B + ua);
+    b1b = kBiasCol ? 0.f : kWS * src.get(L::L1B + ub);
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
       const int row0 = 16 * r + (c ^ l2_sigma(p)), row1 = row0 + 8;
@@ -1014,12 +1034,12 @@ struct MlpPair {
       for (int k = 0; k < 8; ++k) {
         const float e0 = src.get(L::L2W + (int64_t)row0 * kHidden + 8 * c + k);
         const float e1 = src.get(L::L2W + (int64_t)row1 * kHidden + 8 * c + k);
-        w2[p * 8 + k] = f2{e0, e1};
+        w2[p * 8 + k] = f2{kWS * e0, kWS * e1};
       }
     }
     const int u2a = 16 * r + c, u2b = 16 * r + 8 + c;  // this thread's layer-2 units
-    b2a = src.get(L::L2B + u2a);
-    b2b = src.get(L::L2B + u2b);
+    b2a = kWS * src.get(L::L2B + u2a);
+    b2b = kWS * src.get(L::L2B + u2b);
     if constexpr (FDR_PAIR_HEAD == 1) {
       // packed head: chunk m = (W3[(2m)^o][u2a], W3[(2m+1)^o][u2a], W3[(2m)^o][u2b], W3[(2m+1)^o][u2b]) -- register
       // slot i of this thread holds output i ^ o (the reduce-scatter's thread-dependent order); every W3 element is
@@ -1031,9 +1051,9 @@ struct MlpPair {
         const float e1 = s1 < NOUT ? src.get(L::L3W + (int64_t)s1 * kHidden + u2a) : 0.f;
         const float e2 = s0 < NOUT ? src.get(L::L3W + (int64_t)s0 * kHidden + u2b) : 0.f;
         const float e3 = s1 < NOUT ? src.get(L::L3W + (int64_t)s1 * kHidden + u2b) : 0.f;
-        my[(2 * kW1Chunks + m) * kWave] = float4{e0, e1, e2, e3};
+        my[(2 * kW1Chunks + m) * kWave] = float4{kWS * e0, kWS * e1, kWS * e2, kWS * e3};
       }
-      b3 = o < NOUT ? (rho == 0 ? src.get(L::L3B + o) : src.get_nocount(L::L3B + o)) : 0.f;
+      b3 = kWS * (o < NOUT ? (rho == 0 ? src.get(L::L3B + o) : src.get_nocount(L::L3B + o)) : 0.f);
     } else if (o < NOUT) {
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
@@ -1044,9 +1064,9 @@ struct MlpPair {
           // w < 16: value z.x of row-thread w; else z.y of row-thread w - 16
           e[i] = src.get(L::L3W + (int64_t)o * kHidden + head_unit(rho, w & 15, w >> 4));
         }
-        my[(2 * kW1Chunks + m) * kWave] = float4{e[0], e[1], e[2], e[3]};
+        my[(2 * kW1Chunks + m) * kWave] = float4{kWS * e[0], kWS * e[1], kWS * e[2], kWS * e[3]};
       }
-      b3 = rho == 0 ? src.get(L::L3B + o) : src.get_nocount(L::L3B + o);
+      b3 = kWS * (rho == 0 ? src.get(L::L3B + o) : src.get_nocount(L::L3B + o));
     } else {
 #pragma unroll
       for (int m = 0; m < 8; ++m) my[(2 * kW1Chunks + m) * kWave] = float4{0.f, 0.f, 0.f, 0.f};
@@ -1082,7 +1102,7 @@ struct MlpPair {
     if constexpr (DISC) {
       return fmaf(fmaxf(z, 0.f), av, cv);
     } else {
-      return tanh_fast(z);
+      return tanh_act<kPre>(z);
     }
   }
 
@@ -1156,7 +1176,11 @@ struct MlpPair {
           if (k < NIN) {
             const float4 w = rows.wp[k >> 1];
             const f2 xp = (i < 2) ? f2{xv.x, xv.y} : f2{xv.z, xv.w};
-            if (FDR_PAIR_NOMOV && k < NC)
+            if (kPre && k == NIN % NC) {  // the chain that takes the bias column starts from it
+              const float4 wb = rows.wp[NIN >> 1];
+              const f2 bias = (NIN & 1) ? f2{wb.z, wb.w} : f2{wb.x, wb.y};
+              acc[k % NC] = (k & 1) ? pk_fma_bhi(f2{w.z, w.w}, xp, bias) : pk_fma_blo(f2{w.x, w.y}, xp, bias);
+            } else if (FDR_PAIR_NOMOV && k < NC)
               acc[k % NC] = (k & 1) ? pk_mul_bhi(f2{w.z, w.w}, xp) : pk_mul_blo(f2{w.x, w.y}, xp);
             else
               acc[k % NC] = (k & 1) ? pk_fma_bhi(f2{w.z, w.w}, xp, acc[k % NC]) : pk_fma_blo(f2{w.x, w.y}, xp, acc[k % NC]);
@@ -1170,7 +1194,7 @@ struct MlpPair {
         acc[(NIN - 1) % NC] = pk_fma(((NIN - 1) & 1) ? f2{w.z, w.w} : f2{w.x, w.y}, f2{xt, xt}, acc[(NIN - 1) % NC]);
         am1.x = fmaf(rows.tm, kSameInput ? xt : st, am1.x);
       }
-      {
+      if constexpr (!kPre || NIN % NC >= NIN) {
         const float4 w = rows.wp[NIN >> 1];
         acc[NIN % NC] = acc[NIN % NC] + ((NIN & 1) ? f2{w.z, w.w} : f2{w.x, w.y});
       }
@@ -1184,7 +1208,7 @@ struct MlpPair {
       if constexpr (DISC) {
         return f2{act1(h.x, a1a, c1a), act1(h.y, a1b, c1b)};
       } else {
-        return tanh2_fast(h);
+        return tanh2_act<kPre>(h);
       }
     }
 #pragma unroll
@@ -1216,7 +1240,7 @@ struct MlpPair {
     if constexpr (DISC) {
       return f2{act1(ha.x + ha.y, a1a, c1a), act1(hb.x + hb.y, a1b, c1b)};
     } else {
-      return tanh2_fast(f2{ha.x + ha.y, hb.x + hb.y});
+      return tanh2_act<kPre>(f2{ha.x + ha.y, hb.x + hb.y});
     }
   }
 
@@ -1246,7 +1270,9 @@ struct MlpPair {
     for (int k = 0; k < 8; ++k)
 #pragma unroll
       for (int p = 0; p < 8; ++p)
-        if (!FDR_PAIR_NOMOV || k == 0) acc[p] = pk_fma(w2[p * 8 + k], f2{x[k], x[k]}, acc[p]);
+        if (!FDR_PAIR_NOMOV || k == 0)
+          // kPre: the thread's own slots (acc[0]) start from its biases -- each output's sum takes them once
+          acc[p] = pk_fma(w2[p * 8 + k], f2{x[k], x[k]}, (kPre && k == 0 && p == 0) ? f2{b2a, b2b} : acc[p]);
 #if FDR_PAIR_NOMOV
     // k >= 1 as op_sel broadcasts of the b128 pairs (x[k - 1], x[k]) / (x[k], x[k + 1]) in ONE asm statement: the
     // compiler follows every asm statement with an s_nop, and would move each odd x[k] to an even register
@@ -1332,8 +1358,8 @@ struct MlpPair {
     for (int i = 0; i < 16; ++i) sl[i] = (i & 1) ? acc[i >> 1].y : acc[i >> 1].x;
 #if FDR_RS_OUT
     const f2 zs = reduce_scatter16_out(sl);
-    const float za = zs.x + b2a;  // unit 16r + c
-    const float zb = zs.y + b2b;  // unit 16r + 8 + c
+    const float za = kPre ? zs.x : zs.x + b2a;  // unit 16r + c
+    const float zb = kPre ? zs.y : zs.y + b2b;  // unit 16r + 8 + c
 #else
     reduce_scatter16(sl);  // one asm block: the SLP vectoriser would split the DPP adds into movs
     const float za = sl[0] + b2a;  // unit 16r + c
@@ -1345,7 +1371,7 @@ struct MlpPair {
       h2a = fmaf(fmaxf(za, 0.f), a2a, c2a);
       h2b = fmaf(fmaxf(zb, 0.f), a2b, c2b);
     } else {
-      const f2 h2 = tanh2_fast(f2{za, zb});
+      const f2 h2 = tanh2_act<kPre>(f2{za, zb});
       h2a = h2.x;
       h2b = h2.y;
     }
@@ -1423,7 +1449,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
   float* envMK = reinterpret_cast<float*>(env4);
   for (int e = threadIdx.x; e < NIN * MKS; e += blockDim.x) {
     const int i = e / MKS, k = e % MKS;
-    envMK[e] = k < NIN ? a.M[i * NIN + k] : (k >= NX && k < NX + NA ? a.K[i * NA + k - NX] : 0.f);
+    envMK[e] = kPreScale * (k < NIN ? a.M[i * NIN + k] : (k >= NX && k < NX + NA ? a.K[i * NA + k - NX] : 0.f));
   }
   __syncthreads();
 
@@ -1536,7 +1562,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
       eacc -= (o < NA) ? disc_entropy_term(p, tot) : 0.f;
       pre += mrow[NX + act_d];
     } else {
-      const float th = tanh_fast(y);
+      const float th = tanh_act<Lane::kPre>(y);
       const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
       eacc += __builtin_amdgcn_logf(sd);
       const float act_c = det ? th : gauss_action(th, sd, zt);
@@ -1546,7 +1572,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
       else
         dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in thread m of both rows of the half
     }
-    s = tanh_fast(pre);
+    s = tanh_act<(FDR_PAIR_PRESCALE != 0)>(pre);
     racc += (double)s;  // thread 0 of the half holds the reward s'[0]
     mark(4, s);
   };
