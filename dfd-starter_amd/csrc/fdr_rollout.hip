@@ -33,6 +33,9 @@
 #ifndef FDR_PAIR_NOMOV  // pair kernel: op_sel broadcasts in L2, packed multiplies start the L1 chains (r10 A/B)
 #define FDR_PAIR_NOMOV 1
 #endif
+#ifndef FDR_RS_SCHED  // pair kernel: reduce-scatter DPP adds ordered to need no s_nop (r10 A/B)
+#define FDR_RS_SCHED 1
+#endif
 #ifndef FDR_RS_OUT  // pair kernel: L2 reduce-scatter with untied outputs (r10 A/B)
 #define FDR_RS_OUT 1
 #endif
@@ -878,6 +881,29 @@ __device__ __forceinline__ void reduce_scatter16(float (&v)[16]) {
 // copy the low halves of the packed accumulators into separate tied registers; returns the two kept slots
 __device__ __forceinline__ f2 reduce_scatter16_out(const float (&v)[16]) {
   float o[8];
+#if FDR_RS_SCHED
+  // ordered so that every DPP source was written >= 3 instructions earlier (2 wait states): level 1 produces
+  // o6, o7, o4 first, level 2 o2, o3 first -- no s_nop inside; the caller's layer-2 block writes v[8..15] early
+  asm volatile(
+      "v_add_f32_dpp %6, %22, %14 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %7, %23, %15 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %4, %20, %12 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %5, %21, %13 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %2, %18, %10 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %3, %19, %11 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %0, %16, %8 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %17, %9 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %2, %6, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %3, %7, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %0, %4, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %5, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %0, %2, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_add_f32_dpp %1, %3, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7])
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]), "v"(v[9]),
+        "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
+#else
+
   asm volatile(
       "s_nop 1\n\t"
       "v_add_f32_dpp %0, %16, %8 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
@@ -899,6 +925,7 @@ __device__ __forceinline__ f2 reduce_scatter16_out(const float (&v)[16]) {
       : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7])
       : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]), "v"(v[9]),
         "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
+#endif
   return f2{o[0], o[1]};
 }
 
@@ -1276,7 +1303,8 @@ struct MlpPair {
 #if FDR_PAIR_NOMOV
     // k >= 1 as op_sel broadcasts of the b128 pairs (x[k - 1], x[k]) / (x[k], x[k + 1]) in ONE asm statement: the
     // compiler follows every asm statement with an s_nop, and would move each odd x[k] to an even register
-    // (operands: %0-%7 acc, %(8 + 8 (k - 1) + p) = w2[8 p + k], %64-%67 the x pairs)
+    // (operands: %0-%7 acc, %(8 + 8 (k - 1) + p) = w2[8 p + k], %64-%67 the x pairs).  k = 7 writes acc[4..7] first:
+    // they are the reduce-scatter's DPP sources, which need 2 wait states after their VALU write
     {
       const f2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]}, x45 = {x[4], x[5]}, x67 = {x[6], x[7]};
 #define FDR_L2_HI "op_sel:[0,1,0] op_sel_hi:[1,1,1]"
@@ -1330,14 +1358,14 @@ struct MlpPair {
           "v_pk_fma_f32 %5, %53, %67, %5 " FDR_L2_LO "\n"
           "v_pk_fma_f32 %6, %54, %67, %6 " FDR_L2_LO "\n"
           "v_pk_fma_f32 %7, %55, %67, %7 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %0, %56, %67, %0 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %1, %57, %67, %1 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %2, %58, %67, %2 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %3, %59, %67, %3 " FDR_L2_HI "\n"
           "v_pk_fma_f32 %4, %60, %67, %4 " FDR_L2_HI "\n"
           "v_pk_fma_f32 %5, %61, %67, %5 " FDR_L2_HI "\n"
           "v_pk_fma_f32 %6, %62, %67, %6 " FDR_L2_HI "\n"
           "v_pk_fma_f32 %7, %63, %67, %7 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %56, %67, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %57, %67, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %58, %67, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %59, %67, %3 " FDR_L2_HI "\n"
           : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]), "+v"(acc[7])
           : "v"(w2[1]), "v"(w2[9]), "v"(w2[17]), "v"(w2[25]), "v"(w2[33]), "v"(w2[41]), "v"(w2[49]), "v"(w2[57]),
             "v"(w2[2]), "v"(w2[10]), "v"(w2[18]), "v"(w2[26]), "v"(w2[34]), "v"(w2[42]), "v"(w2[50]), "v"(w2[58]),
