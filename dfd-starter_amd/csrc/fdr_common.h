@@ -43,6 +43,11 @@ __device__ __forceinline__ float tanh_pre(float t) {  // tanh(x) for t = kTanhSc
   return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + e);
 }
 __device__ __forceinline__ float tanh_fast(float x) { return tanh_pre(x * kTanhScale); }
+template <bool kPre>  // kPre: the argument is already x kTanhScale
+__device__ __forceinline__ float tanh_act(float z) {
+  if constexpr (kPre) return tanh_pre(z);
+  else return tanh_fast(z);
+}
 
 // ---------------------------------------------------------------------------------------------
 // Wave-scope LDS ordering: LDS ops of one wave complete in order, so a wave that only talks to

@@ -33,6 +33,15 @@
 #ifndef FDR_PAIR_NOMOV  // pair kernel: op_sel broadcasts in L2, packed multiplies start the L1 chains (r10 A/B)
 #define FDR_PAIR_NOMOV 1
 #endif
+#ifndef FDR_LANE_ENV_PRESCALE  // rollout_kernel: the synthetic env's M, K stored x 2 log2(e) (r10 A/B)
+#define FDR_LANE_ENV_PRESCALE 0
+#endif
+#ifndef FDR_L1_ONECHAIN  // pair kernel: layer 1 and the env's M s as one packed chain each (r10 A/B)
+#define FDR_L1_ONECHAIN 0
+#endif
+#ifndef FDR_L2_QUAD  // pair kernel: layer 2 as 8 x 16 blocks reduced over a quad (r10 A/B)
+#define FDR_L2_QUAD 0
+#endif
 #ifndef FDR_RS_SCHED  // pair kernel: reduce-scatter DPP adds ordered to need no s_nop (r10 A/B)
 #define FDR_RS_SCHED 1
 #endif
@@ -542,7 +551,9 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
   if constexpr (ENV == FDR_ENV_SYNTH) {
     for (int e = threadIdx.x; e < NIN * MKS; e += blockDim.x) {  // padding columns zero (b128 row reads)
       const int i = e / MKS, k = e % MKS;
-      envMK[e] = k < NIN ? a.M[i * NIN + k] : (k >= NX && k < NX + NA ? a.K[i * NA + k - NX] : 0.f);
+      // FDR_LANE_ENV_PRESCALE: x kTanhScale, so the env's tanh starts at its exp2
+      envMK[e] = (FDR_LANE_ENV_PRESCALE ? kTanhScale : 1.f) *
+                 (k < NIN ? a.M[i * NIN + k] : (k >= NX && k < NX + NA ? a.K[i * NA + k - NX] : 0.f));
     }
     __syncthreads();  // the only cross-wave hand-off: shared env matrices
   }
@@ -697,7 +708,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
           h1 = pl.layer1_env_reg(xv, sv, mreg, pre);
           if constexpr (kCand) {
     #pragma unroll
-            for (int i = 0; i < NA; ++i) cand[i] = tanh_fast(pre + kreg[i]);
+            for (int i = 0; i < NA; ++i) cand[i] = tanh_act<(FDR_LANE_ENV_PRESCALE != 0)>(pre + kreg[i]);
           }
         } else {
         // policy input (and env state) broadcast through the wave's LDS scratch, then packed FMAs
@@ -783,7 +794,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
               for (int m = 0; m < NA; ++m) kr[m] = WIDE ? kreg[m] : mrow[NX + m];
               dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in lane m of every row
             }
-            s = tanh_fast(pre);
+            s = tanh_act<(FDR_LANE_ENV_PRESCALE != 0)>(pre);
           }
           racc += (double)s;  // lane 0 holds the reward s'[0]; other lanes' sums are discarded
         } else {
@@ -986,11 +997,6 @@ __device__ __forceinline__ f2 tanh2_fast(f2 x) {
 // the activation starts at the exp2 -- one multiply fewer per tanh (L1, L2, head, env: 4 per step)
 constexpr float kPreScale = FDR_PAIR_PRESCALE ? kTanhScale : 1.f;
 template <bool kPre>
-__device__ __forceinline__ float tanh_act(float z) {
-  if constexpr (kPre) return tanh_pre(z);
-  else return tanh_fast(z);
-}
-template <bool kPre>
 __device__ __forceinline__ f2 tanh2_act(f2 z) {
   if constexpr (kPre) return tanh2_pre(z);
   else return tanh2_fast(z);
@@ -1017,12 +1023,17 @@ struct MlpPair {
 
   // unit of layer 2 that row-thread k's value e (0: z.x, 1: z.y) holds, within the row's 32 units
   __host__ __device__ static constexpr int head_unit(int rho, int k, int e) {
+#if FDR_L2_QUAD
+    return 32 * rho + 8 * (k >> 2) + 4 * e + (k & 3);  // thread 4q + c holds units 8q + c, 8q + 4 + c
+#else
     return 32 * rho + 16 * (k >> 3) + 8 * e + (k & 7);
+#endif
   }
 
   __device__ __forceinline__ void load(ParamSrc& src, int t, int tid, const float* bn_mean, const float* bn_var,
                                        float4* wave_tile) {
-    const int r = t >> 3, c = t & 7, rho = t >> 4, o = t & 15;
+    [[maybe_unused]] const int r = t >> 3, c = t & 7;
+    const int rho = t >> 4, o = t & 15;
     const int ua = 2 * t, ub = 2 * t + 1;
     float4* my = wave_tile + tid;
     tile = my;
@@ -1054,6 +1065,22 @@ struct MlpPair {
     }
     b1a = kBiasCol ? 0.f : kWS * src.get(L::L1B + ua);
     b1b = kBiasCol ? 0.f : kWS * src.get(L::L1B + ub);
+#if FDR_L2_QUAD
+    // quad q = t / 4 owns units 8q .. 8q + 7; thread c = t % 4 of it takes inputs 16c .. 16c + 15 and pair p the
+    // units (8q + (c ^ p), 8q + 4 + (c ^ p)): the quad's reduce-scatter (partners c ^ 2, c ^ 1) leaves pair 0
+    const int q4 = t >> 2, c4 = t & 3;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int row0 = 8 * q4 + (c4 ^ p), row1 = row0 + 4;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float e0 = src.get(L::L2W + (int64_t)row0 * kHidden + 16 * c4 + k);
+        const float e1 = src.get(L::L2W + (int64_t)row1 * kHidden + 16 * c4 + k);
+        w2[p * 16 + k] = f2{kWS * e0, kWS * e1};
+      }
+    }
+    const int u2a = 8 * q4 + c4, u2b = 8 * q4 + 4 + c4;  // this thread's layer-2 units
+#else
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
       const int row0 = 16 * r + (c ^ l2_sigma(p)), row1 = row0 + 8;
@@ -1065,6 +1092,7 @@ struct MlpPair {
       }
     }
     const int u2a = 16 * r + c, u2b = 16 * r + 8 + c;  // this thread's layer-2 units
+#endif
     b2a = kWS * src.get(L::L2B + u2a);
     b2b = kWS * src.get(L::L2B + u2b);
     if constexpr (FDR_PAIR_HEAD == 1) {
@@ -1189,7 +1217,7 @@ struct MlpPair {
     if constexpr (kPk) {
       // units (a, b) packed: acc[k % NC] += (w_a(k), w_b(k)) * x_k; the bias column (k = NIN) is added.
       // NC = 2 chains of ~9 dependent packed FMAs, or 4 of ~5 (FDR_PAIR_CHAINS) + two packed adds
-      constexpr int NC = FDR_PAIR_CHAINS ? 4 : 2;
+      constexpr int NC = FDR_PAIR_CHAINS ? 4 : (FDR_L1_ONECHAIN ? 1 : 2);
       f2 acc[NC];
 #pragma unroll
       for (int q = 0; q < NC; ++q) acc[q] = f2{0.f, 0.f};
@@ -1214,12 +1242,18 @@ struct MlpPair {
           }
         }
         am0 = pk_fma(f2{mv.x, mv.y}, f2{sv.x, sv.y}, am0);
-        am1 = pk_fma(f2{mv.z, mv.w}, f2{sv.z, sv.w}, am1);
+        if constexpr (FDR_L1_ONECHAIN)
+          am0 = pk_fma(f2{mv.z, mv.w}, f2{sv.z, sv.w}, am0);
+        else
+          am1 = pk_fma(f2{mv.z, mv.w}, f2{sv.z, sv.w}, am1);
       }
       if constexpr (kTail) {  // input 4 NQ = NIN - 1, then the bias
         const float4 w = rows.wp[(NIN - 1) >> 1];
         acc[(NIN - 1) % NC] = pk_fma(((NIN - 1) & 1) ? f2{w.z, w.w} : f2{w.x, w.y}, f2{xt, xt}, acc[(NIN - 1) % NC]);
-        am1.x = fmaf(rows.tm, kSameInput ? xt : st, am1.x);
+        if constexpr (FDR_L1_ONECHAIN)
+          am0.x = fmaf(rows.tm, kSameInput ? xt : st, am0.x);
+        else
+          am1.x = fmaf(rows.tm, kSameInput ? xt : st, am1.x);
       }
       if constexpr (!kPre || NIN % NC >= NIN) {
         const float4 w = rows.wp[NIN >> 1];
@@ -1228,9 +1262,11 @@ struct MlpPair {
       f2 h;
       if constexpr (NC == 4)
         h = (acc[0] + acc[2]) + (acc[1] + acc[3]);
-      else
+      else if constexpr (NC == 2)
         h = acc[0] + acc[1];
-      const f2 am = am0 + am1;
+      else
+        h = acc[0];
+      const f2 am = FDR_L1_ONECHAIN ? am0 : am0 + am1;
       env = am.x + am.y;
       if constexpr (DISC) {
         return f2{act1(h.x, a1a, c1a), act1(h.y, a1b, c1b)};
@@ -1275,6 +1311,136 @@ struct MlpPair {
   // Returns the head pre-activation for output o = t & 15 (identical in both rows of the half).
   template <class Mark>
   __device__ __forceinline__ float layers23(f2 h1, float* h1s, int t, Mark&& mark) const {
+#if FDR_L2_QUAD
+    static_assert(FDR_PAIR_NOMOV && FDR_RS_OUT, "FDR_L2_QUAD needs the op_sel layer-2 block");
+    const int c4 = t & 3;
+    float x[16];
+    reinterpret_cast<f2*>(h1s)[t] = h1;
+    wave_lds_sync();
+    lds_bcast<16>(h1s + 16 * c4, x);
+    float w3[32];
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const float4 w = tile[(2 * kW1Chunks + m) * kWave];
+      w3[4 * m] = w.x;
+      w3[4 * m + 1] = w.y;
+      w3[4 * m + 2] = w.z;
+      w3[4 * m + 3] = w.w;
+    }
+    f2 acc[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)  // k = 0; kPre: the own pair (p = 0) starts from the biases
+      acc[p] = pk_fma(w2[p * 16], f2{x[0], x[0]}, (kPre && p == 0) ? f2{b2a, b2b} : f2{0.f, 0.f});
+    {
+      // k = 1 .. 15 by op_sel broadcasts of the pairs xp[j] = (x[2j], x[2j + 1]) in one asm statement (operands:
+      // %0-%3 acc, %(4 + 4 (k - 1) + p) = w2[16 p + k], %64-%71 the pairs); k = 15 writes acc[3], acc[2] first,
+      // the reduce-scatter's first DPP sources
+      f2 xp[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xp[j] = f2{x[2 * j], x[2 * j + 1]};
+#define FDR_L2_HI "op_sel:[0,1,0] op_sel_hi:[1,1,1]"
+#define FDR_L2_LO "op_sel_hi:[1,0,1]"
+      asm(
+          "v_pk_fma_f32 %0, %4, %64, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %5, %64, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %6, %64, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %7, %64, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %8, %65, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %9, %65, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %10, %65, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %11, %65, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %12, %65, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %13, %65, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %14, %65, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %15, %65, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %16, %66, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %17, %66, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %18, %66, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %19, %66, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %20, %66, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %21, %66, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %22, %66, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %23, %66, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %24, %67, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %25, %67, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %26, %67, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %27, %67, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %28, %67, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %29, %67, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %30, %67, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %31, %67, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %32, %68, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %33, %68, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %34, %68, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %35, %68, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %36, %68, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %37, %68, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %38, %68, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %39, %68, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %40, %69, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %41, %69, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %42, %69, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %43, %69, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %44, %69, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %45, %69, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %46, %69, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %47, %69, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %48, %70, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %49, %70, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %50, %70, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %51, %70, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %52, %70, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %53, %70, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %54, %70, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %55, %70, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %56, %71, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %57, %71, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %58, %71, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %59, %71, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %63, %71, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %62, %71, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %60, %71, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %61, %71, %1 " FDR_L2_HI "\n"
+          : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+          : "v"(w2[1]), "v"(w2[17]), "v"(w2[33]), "v"(w2[49]),
+            "v"(w2[2]), "v"(w2[18]), "v"(w2[34]), "v"(w2[50]),
+            "v"(w2[3]), "v"(w2[19]), "v"(w2[35]), "v"(w2[51]),
+            "v"(w2[4]), "v"(w2[20]), "v"(w2[36]), "v"(w2[52]),
+            "v"(w2[5]), "v"(w2[21]), "v"(w2[37]), "v"(w2[53]),
+            "v"(w2[6]), "v"(w2[22]), "v"(w2[38]), "v"(w2[54]),
+            "v"(w2[7]), "v"(w2[23]), "v"(w2[39]), "v"(w2[55]),
+            "v"(w2[8]), "v"(w2[24]), "v"(w2[40]), "v"(w2[56]),
+            "v"(w2[9]), "v"(w2[25]), "v"(w2[41]), "v"(w2[57]),
+            "v"(w2[10]), "v"(w2[26]), "v"(w2[42]), "v"(w2[58]),
+            "v"(w2[11]), "v"(w2[27]), "v"(w2[43]), "v"(w2[59]),
+            "v"(w2[12]), "v"(w2[28]), "v"(w2[44]), "v"(w2[60]),
+            "v"(w2[13]), "v"(w2[29]), "v"(w2[45]), "v"(w2[61]),
+            "v"(w2[14]), "v"(w2[30]), "v"(w2[46]), "v"(w2[62]),
+            "v"(w2[15]), "v"(w2[31]), "v"(w2[47]), "v"(w2[63]),
+            "v"(xp[0]), "v"(xp[1]), "v"(xp[2]), "v"(xp[3]), "v"(xp[4]), "v"(xp[5]), "v"(xp[6]), "v"(xp[7]));
+#undef FDR_L2_LO
+#undef FDR_L2_HI
+    }
+    // reduce-scatter over the quad: slot i = acc[i / 2][i % 2]; level 1 o_i = v_i + partner(c ^ 2).v_{i + 4} in
+    // the order o2, o3, o0, o1, level 2 o_i += partner(c ^ 1).o_{i + 2} -- every DPP source >= 3 instructions old
+    f2 zs;
+    {
+      float o0, o1, o2, o3;
+      asm volatile(
+          "v_add_f32_dpp %2, %10, %6 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+          "v_add_f32_dpp %3, %11, %7 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+          "v_add_f32_dpp %0, %8, %4 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+          "v_add_f32_dpp %1, %9, %5 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+          "v_add_f32_dpp %0, %2, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+          "v_add_f32_dpp %1, %3, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+          : "=&v"(o0), "=&v"(o1), "=&v"(o2), "=&v"(o3)
+          : "v"(acc[0].x), "v"(acc[0].y), "v"(acc[1].x), "v"(acc[1].y), "v"(acc[2].x), "v"(acc[2].y), "v"(acc[3].x),
+            "v"(acc[3].y));
+      zs = f2{o0, o1};
+    }
+    const float za = kPre ? zs.x : zs.x + b2a;  // unit 8q + c
+    const float zb = kPre ? zs.y : zs.y + b2b;  // unit 8q + 4 + c
+#else
     const int c = t & 7;
     float x[8];
     reinterpret_cast<f2*>(h1s)[t] = h1;
@@ -1392,6 +1558,7 @@ struct MlpPair {
     reduce_scatter16(sl);  // one asm block: the SLP vectoriser would split the DPP adds into movs
     const float za = sl[0] + b2a;  // unit 16r + c
     const float zb = sl[1] + b2b;  // unit 16r + 8 + c
+#endif
 #endif
     mark(1, za);
     float h2a, h2b;
