@@ -33,6 +33,9 @@
 #ifndef FDR_PAIR_NOMOV  // pair kernel: op_sel broadcasts in L2, packed multiplies start the L1 chains (r10 A/B)
 #define FDR_PAIR_NOMOV 1
 #endif
+#ifndef FDR_HEAD_CHAINS  // pair kernel head: accumulator chains of the 32-term DPP dot (4 or 2; r10 A/B)
+#define FDR_HEAD_CHAINS 4
+#endif
 #ifndef FDR_LANE_ENV_PRESCALE  // rollout_kernel: the synthetic env's M, K stored x 2 log2(e) (r10 A/B)
 #define FDR_LANE_ENV_PRESCALE 0
 #endif
@@ -1588,6 +1591,10 @@ struct MlpPair {
       float s0, s1, s2, s3, s4, s5, s6, s7;  // eight chains of 4
       dpp_dot_32x8(s0, s1, s2, s3, s4, s5, s6, s7, h2a, h2b, w3);
       u = ((s0 + s4) + (s2 + s6)) + ((s1 + s5) + (s3 + s7));
+    } else if constexpr (FDR_HEAD_CHAINS == 2) {
+      float s0, s1;  // two chains of 16
+      dpp_dot_32x2(s0, s1, h2a, h2b, w3);
+      u = s0 + s1;
     } else {
       float s0, s1, s2, s3;  // four independent chains of 8 (first product a v_mul: no zeroing)
       dpp_dot_32x4(s0, s1, s2, s3, h2a, h2b, w3);
