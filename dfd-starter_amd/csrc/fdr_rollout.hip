@@ -34,7 +34,7 @@
 #define FDR_PAIR_NOMOV 1
 #endif
 #ifndef FDR_HEAD_CHAINS  // pair kernel head: accumulator chains of the 32-term DPP dot (4 or 2; r10 A/B)
-#define FDR_HEAD_CHAINS 4
+#define FDR_HEAD_CHAINS 2
 #endif
 #ifndef FDR_LANE_ENV_PRESCALE  // rollout_kernel: the synthetic env's M, K stored x 2 log2(e) (r10 A/B)
 #define FDR_LANE_ENV_PRESCALE 0
@@ -43,7 +43,7 @@
 #define FDR_L1_ONECHAIN 0
 #endif
 #ifndef FDR_L2_QUAD  // pair kernel: layer 2 as 8 x 16 blocks reduced over a quad (r10 A/B)
-#define FDR_L2_QUAD 0
+#define FDR_L2_QUAD 1
 #endif
 #ifndef FDR_RS_SCHED  // pair kernel: reduce-scatter DPP adds ordered to need no s_nop (r10 A/B)
 #define FDR_RS_SCHED 1
