@@ -33,8 +33,11 @@
 #ifndef FDR_PAIR_NOMOV  // pair kernel: op_sel broadcasts in L2, packed multiplies start the L1 chains (r10 A/B)
 #define FDR_PAIR_NOMOV 1
 #endif
-#ifndef FDR_HEAD_CHAINS  // pair kernel head: accumulator chains of the 32-term DPP dot (4 or 2; r10 A/B)
-#define FDR_HEAD_CHAINS 2
+#ifndef FDR_PAIR_DETSPLIT  // pair kernel: a select-free episode loop for waves without deterministic lanes (r10 A/B)
+#define FDR_PAIR_DETSPLIT 0
+#endif
+#ifndef FDR_HEAD_CHAINS  // pair kernel head: accumulator chains of the 32-term DPP dot (4, 2 or 1; r10 A/B)
+#define FDR_HEAD_CHAINS 1
 #endif
 #ifndef FDR_LANE_ENV_PRESCALE  // rollout_kernel: the synthetic env's M, K stored x 2 log2(e) (r10 A/B)
 #define FDR_LANE_ENV_PRESCALE 0
@@ -1591,6 +1594,8 @@ struct MlpPair {
       float s0, s1, s2, s3, s4, s5, s6, s7;  // eight chains of 4
       dpp_dot_32x8(s0, s1, s2, s3, s4, s5, s6, s7, h2a, h2b, w3);
       u = ((s0 + s4) + (s2 + s6)) + ((s1 + s5) + (s3 + s7));
+    } else if constexpr (FDR_HEAD_CHAINS == 1) {
+      dpp_dot_32x1(u, h2a, h2b, w3);  // one chain of 32 (the accumulator is no DPP source: no wait states)
     } else if constexpr (FDR_HEAD_CHAINS == 2) {
       float s0, s1;  // two chains of 16
       dpp_dot_32x2(s0, s1, h2a, h2b, w3);
@@ -1721,7 +1726,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     const uint64_t hsh = hash_ctr(key, ulane, (uint64_t)(st + ds), (uint64_t)dk);
     rbuf = DISC ? uniform24(hsh) : normal_bm(hsh);
   };
-  auto step = [&](int st, int tb) {
+  // sampled_tag: std::true_type when no lane of the wave is deterministic (FDR_PAIR_DETSPLIT), so the action
+  // needs no select
+  auto step = [&](int st, int tb, auto sampled_tag) {
+    constexpr bool kSampled = decltype(sampled_tag)::value;
     // this step's draw: the uniform (discrete) or the normal of action dim o (continuous)
     const float zt = __builtin_bit_cast(
         float, __builtin_amdgcn_ds_bpermute(zbase + 4 * kDrawsPerStep * tb, __builtin_bit_cast(int, rbuf)));
@@ -1767,7 +1775,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
       const float th = tanh_act<Lane::kPre>(y);
       const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
       eacc += __builtin_amdgcn_logf(sd);
-      const float act_c = det ? th : gauss_action(th, sd, zt);
+      const float act_c = (!kSampled && det) ? th : gauss_action(th, sd, zt);
       mark(3, act_c);
       if constexpr (FDR_PAIR_CHAINS && NA == 6)
         dpp_tail6_2chains(pre, act_c, kr);   // a[m] sits in thread m of both rows of the half
@@ -1779,37 +1787,44 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     mark(4, s);
   };
   if constexpr (!DISC) {
-    // continuous: the loop unrolled by the draw batch (5 steps for 6 dims); the draw is issued
-    // unconditionally at the top of the unrolled body (det lanes ignore it), so it schedules into the
-    // first step's waits instead of sitting behind a branch
-    int st = 0;
-    for (; st + kStepsPerBatch <= T; st += kStepsPerBatch) {
-      asm volatile("" ::: "memory");
-      mark(-1, s);
-      draw(st);
-#pragma unroll
-      for (int k = 0; k < kStepsPerBatch; ++k) {
-        if (k) {
-          asm volatile("" ::: "memory");
-          mark(-1, s);
-        }
-        step(st + k, k);
-      }
-    }
-    if (st < T) {
-      draw(st);
-      for (int k = 0; st + k < T; ++k) {
+    auto episode = [&](auto sampled_tag) {
+      // continuous: the loop unrolled by the draw batch (5 steps for 6 dims); the draw is issued
+      // unconditionally at the top of the unrolled body (det lanes ignore it), so it schedules into the
+      // first step's waits instead of sitting behind a branch
+      int st = 0;
+      for (; st + kStepsPerBatch <= T; st += kStepsPerBatch) {
         asm volatile("" ::: "memory");
         mark(-1, s);
-        step(st + k, k);
+        draw(st);
+#pragma unroll
+        for (int k = 0; k < kStepsPerBatch; ++k) {
+          if (k) {
+            asm volatile("" ::: "memory");
+            mark(-1, s);
+          }
+          step(st + k, k, sampled_tag);
+        }
       }
-    }
+      if (st < T) {
+        draw(st);
+        for (int k = 0; st + k < T; ++k) {
+          asm volatile("" ::: "memory");
+          mark(-1, s);
+          step(st + k, k, sampled_tag);
+        }
+      }
+    };
+    // one specialised copy for waves without deterministic lanes (the common case), one generic
+    if (FDR_PAIR_DETSPLIT && !__builtin_amdgcn_readfirstlane(__ballot(det) != 0 ? 1 : 0))
+      episode(std::true_type{});
+    else
+      episode(std::false_type{});
   } else {
     for (int st = 0; st < T; ++st) {
       asm volatile("" ::: "memory");
       mark(-1, s);
       if (!det && tb == 0) draw(st);
-      step(st, tb);
+      step(st, tb, std::false_type{});
       tb = tb + 1 == kStepsPerBatch ? 0 : tb + 1;
     }
   }
