@@ -39,6 +39,10 @@
 #ifndef FDR_HEAD_CHAINS  // pair kernel head: accumulator chains of the 32-term DPP dot (4, 2 or 1; r10 A/B)
 #define FDR_HEAD_CHAINS 1
 #endif
+#ifndef FDR_LANE_L2_ASM  // WIDE rollout_kernel: layer 2 as an op_sel asm block with b2 in the own slot, head2 weights
+                         // pre-swapped per lane parity (r10 A/B)
+#define FDR_LANE_L2_ASM 0
+#endif
 #ifndef FDR_LANE_ENV_PRESCALE  // rollout_kernel: the synthetic env's M, K stored x 2 log2(e) (r10 A/B)
 #define FDR_LANE_ENV_PRESCALE 0
 #endif
@@ -430,9 +434,11 @@ struct MlpLane {
   // w3c = (W3[0][j], W3[1][j]), keeps the product of output o = j & 1 and hands the other to its quad
   // partner, then sums over the 32 lanes of its parity (row_ror 4, row_ror 8, quad xor 2, the 4-row
   // permlane all-reduce): output o in every lane of parity o, 9 VALU instead of the 16-DPP-FMA dot.
+  // kKeepFirst: w3c already holds (W3[o][j], W3[1 - o][j]) (FDR_LANE_L2_ASM), so no selects
+  template <bool kKeepFirst = false>
   __device__ __forceinline__ float head2(float h2, f2 w3c, float b3p, int j) const {
     const f2 m = w3c * f2{h2, h2};
-    const bool odd = (j & 1) != 0;
+    const bool odd = !kKeepFirst && (j & 1) != 0;
     const float keep = odd ? m.y : m.x, give = odd ? m.x : m.y;
     float v = keep + dpp_mov<kDppQuadXor1>(give);
     v += dpp_mov<kDppRowRor + 4>(v);
@@ -441,18 +447,78 @@ struct MlpLane {
     return row_allreduce_sum(v) + b3p;
   }
 
-  // second hidden layer: h = layer-1 output of unit j; returns unit j's activation
+  // second hidden layer: h = layer-1 output of unit j; returns unit j's activation.  kAsm (the 256-VGPR WIDE
+  // kernel only: in the 128-VGPR instances the asm block's live range spills): op_sel block, b2 in the own slot
+  template <bool kAsm = false>
   __device__ __forceinline__ float layer2(float h, Scratch* sc, int j) const {
     const int c = j & 7;
     sc->h1[j] = h;
     wave_lds_sync();
     float x[8];
     lds_bcast<8>(sc->h1 + 8 * c, x);
-    f2 acc[4] = {f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}, f2{0.f, 0.f}};
+    f2 acc[4];
+    float kB2;
+    if constexpr (kAsm) {
+    // k = 0 starts the lane's own slot (acc[0].x, the reduce-scatter's non-DPP operand all the way down) from b2;
+    // k = 1 .. 7 as op_sel broadcasts of the pairs (x[2j], x[2j + 1]) in one asm statement (no moves of odd
+    // elements; operands %0-%3 acc, %(4 + 4 (k - 1) + p) = w2[8 p + k], %36-%39 the pairs)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) acc[p] = pk_fma(w2[p * 8], f2{x[0], x[0]}, f2{p == 0 ? b2 : 0.f, 0.f});
+    {
+      const f2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]}, x45 = {x[4], x[5]}, x67 = {x[6], x[7]};
+#define FDR_L2_HI "op_sel:[0,1,0] op_sel_hi:[1,1,1]"
+#define FDR_L2_LO "op_sel_hi:[1,0,1]"
+      asm(
+          "v_pk_fma_f32 %0, %4, %36, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %5, %36, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %6, %36, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %7, %36, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %8, %37, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %9, %37, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %10, %37, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %11, %37, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %12, %37, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %13, %37, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %14, %37, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %15, %37, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %16, %38, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %17, %38, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %18, %38, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %19, %38, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %20, %38, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %21, %38, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %22, %38, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %23, %38, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %24, %39, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %25, %39, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %26, %39, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %27, %39, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %28, %39, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %29, %39, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %30, %39, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %31, %39, %3 " FDR_L2_HI "\n"
+          : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+          : "v"(w2[1]), "v"(w2[9]), "v"(w2[17]), "v"(w2[25]),
+            "v"(w2[2]), "v"(w2[10]), "v"(w2[18]), "v"(w2[26]),
+            "v"(w2[3]), "v"(w2[11]), "v"(w2[19]), "v"(w2[27]),
+            "v"(w2[4]), "v"(w2[12]), "v"(w2[20]), "v"(w2[28]),
+            "v"(w2[5]), "v"(w2[13]), "v"(w2[21]), "v"(w2[29]),
+            "v"(w2[6]), "v"(w2[14]), "v"(w2[22]), "v"(w2[30]),
+            "v"(w2[7]), "v"(w2[15]), "v"(w2[23]), "v"(w2[31]),
+            "v"(x01), "v"(x23), "v"(x45), "v"(x67));
+#undef FDR_L2_LO
+#undef FDR_L2_HI
+    }
+    kB2 = 0.f;
+    } else {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) acc[p] = f2{0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 8; ++k)
 #pragma unroll
       for (int p = 0; p < 4; ++p) acc[p] = pk_fma(w2[p * 8 + k], f2{x[k], x[k]}, acc[p]);
+    kB2 = b2;
+    }
     // reduce-scatter over the 8 lanes of the half-row: slot i = acc[i / 2][i % 2]
     const float q0 = acc[0].x + dpp_mov<kDppHalfMirror>(acc[2].x);
     const float q1 = acc[0].y + dpp_mov<kDppHalfMirror>(acc[2].y);
@@ -460,7 +526,7 @@ struct MlpLane {
     const float q3 = acc[1].y + dpp_mov<kDppHalfMirror>(acc[3].y);
     const float r0 = q0 + dpp_mov<kDppQuadXor2>(q2);
     const float r1 = q1 + dpp_mov<kDppQuadXor2>(q3);
-    const float z = (r0 + dpp_mov<kDppQuadXor1>(r1)) + b2;
+    const float z = kAsm ? r0 + dpp_mov<kDppQuadXor1>(r1) : (r0 + dpp_mov<kDppQuadXor1>(r1)) + kB2;
     if constexpr (DISC) {
       return fmaf(fmaxf(z, 0.f), a2, c2);
     } else {
@@ -652,6 +718,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
     const float* t0 = reinterpret_cast<const float*>(pl.tile - j + (Lane::kW1Chunks + ((j & 15) >> 2)) * kWave +
                                                      (j >> 4) * 16);
     w3c = f2{t0[j & 3], t0[4 + (j & 3)]};
+    if (WIDE && FDR_LANE_L2_ASM && (j & 1)) w3c = f2{w3c.y, w3c.x};  // output j & 1 first (head2<true>)
     const float b30 = readlane_f(pl.b3, 0), b31 = readlane_f(pl.b3, 1);
     b3p = (j & 1) ? b31 : b30;
   }
@@ -735,9 +802,9 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
         mark(0, h1);
         float y;
         if constexpr (kHead2) {
-          const float h2 = pl.layer2(h1, sc, j);
+          const float h2 = pl.template layer2<WIDE && (FDR_LANE_L2_ASM != 0)>(h1, sc, j);
           mark(1, h2);
-          y = pl.head2(h2, w3c, b3p, j);
+          y = pl.template head2<WIDE && (FDR_LANE_L2_ASM != 0)>(h2, w3c, b3p, j);
           mark(2, y);
         } else {
           y = pl.layers23(h1, sc, j, mark, WIDE ? w3reg : nullptr);
