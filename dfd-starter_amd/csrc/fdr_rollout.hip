@@ -461,7 +461,7 @@ struct MlpLane {
     if constexpr (kAsm) {
     // k = 0 starts the lane's own slot (acc[0].x, the reduce-scatter's non-DPP operand all the way down) from b2;
     // k = 1 .. 7 as op_sel broadcasts of the pairs (x[2j], x[2j + 1]) in one asm statement (no moves of odd
-    // elements; operands %0-%3 acc, %(4 + 4 (k - 1) + p) = w2[8 p + k], %36-%39 the pairs)
+    // elements; operands %0-%3 acc, %(4 + 4 (k - 1) + p) = w2[8 p + k], %32-%35 the pairs)
 #pragma unroll
     for (int p = 0; p < 4; ++p) acc[p] = pk_fma(w2[p * 8], f2{x[0], x[0]}, f2{p == 0 ? b2 : 0.f, 0.f});
     {
@@ -469,34 +469,34 @@ struct MlpLane {
 #define FDR_L2_HI "op_sel:[0,1,0] op_sel_hi:[1,1,1]"
 #define FDR_L2_LO "op_sel_hi:[1,0,1]"
       asm(
-          "v_pk_fma_f32 %0, %4, %36, %0 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %1, %5, %36, %1 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %2, %6, %36, %2 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %3, %7, %36, %3 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %0, %8, %37, %0 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %1, %9, %37, %1 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %2, %10, %37, %2 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %3, %11, %37, %3 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %0, %12, %37, %0 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %1, %13, %37, %1 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %2, %14, %37, %2 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %3, %15, %37, %3 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %0, %16, %38, %0 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %1, %17, %38, %1 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %2, %18, %38, %2 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %3, %19, %38, %3 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %0, %20, %38, %0 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %1, %21, %38, %1 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %2, %22, %38, %2 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %3, %23, %38, %3 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %0, %24, %39, %0 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %1, %25, %39, %1 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %2, %26, %39, %2 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %3, %27, %39, %3 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %0, %28, %39, %0 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %1, %29, %39, %1 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %2, %30, %39, %2 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %3, %31, %39, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %4, %32, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %5, %32, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %6, %32, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %7, %32, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %8, %33, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %9, %33, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %10, %33, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %11, %33, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %12, %33, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %13, %33, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %14, %33, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %15, %33, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %16, %34, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %17, %34, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %18, %34, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %19, %34, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %20, %34, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %21, %34, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %22, %34, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %23, %34, %3 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %0, %24, %35, %0 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %1, %25, %35, %1 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %2, %26, %35, %2 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %3, %27, %35, %3 " FDR_L2_LO "\n"
+          "v_pk_fma_f32 %0, %28, %35, %0 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %1, %29, %35, %1 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %2, %30, %35, %2 " FDR_L2_HI "\n"
+          "v_pk_fma_f32 %3, %31, %35, %3 " FDR_L2_HI "\n"
           : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
           : "v"(w2[1]), "v"(w2[9]), "v"(w2[17]), "v"(w2[25]),
             "v"(w2[2]), "v"(w2[10]), "v"(w2[18]), "v"(w2[26]),
