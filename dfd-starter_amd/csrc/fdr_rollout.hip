@@ -39,10 +39,6 @@
 #ifndef FDR_HEAD_CHAINS  // pair kernel head: accumulator chains of the 32-term DPP dot (4, 2 or 1; r10 A/B)
 #define FDR_HEAD_CHAINS 1
 #endif
-#ifndef FDR_LANE_L2_ASM  // WIDE rollout_kernel: layer 2 as an op_sel asm block with b2 in the own slot, head2 weights
-                         // pre-swapped per lane parity (r10 A/B)
-#define FDR_LANE_L2_ASM 0
-#endif
 #ifndef FDR_LANE_ENV_PRESCALE  // rollout_kernel: the synthetic env's M, K stored x 2 log2(e) (r10 A/B)
 #define FDR_LANE_ENV_PRESCALE 0
 #endif
@@ -820,9 +816,9 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
           float pv[NA];
     #pragma unroll
           for (int i = 0; i < NA; ++i) pv[i] = readlane_f(p, i);
-          float tot = 0.f;  // sequential f32 cumsum, the oracle's order
+          float tot = FDR_LANE_L2_ASM ? pv[0] : 0.f;  // sequential f32 cumsum, the oracle's order (0 + p0 == p0)
     #pragma unroll
-          for (int i = 0; i < NA; ++i) tot += pv[i];
+          for (int i = FDR_LANE_L2_ASM ? 1 : 0; i < NA; ++i) tot += pv[i];
           // Branch-free selection (selects, no data-dependent control flow):
           //   argmax = first maximal index; inverse CDF = first i with cumsum_i > target, i.e. the
           //   number of (monotone) partial sums <= target, capped at NA - 1.
