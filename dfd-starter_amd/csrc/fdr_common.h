@@ -42,6 +42,9 @@ __device__ __forceinline__ float normal_bm(uint64_t h) {
 #define FDR_LANE_L2_ASM 1
 #endif
 
+#ifndef FDR_WIDE_SAMPLE_DPP  // WIDE two-output sampling without readlanes (r10 A/B)
+#define FDR_WIDE_SAMPLE_DPP 0
+#endif
 constexpr float kTanhScale = 2.88539008177792681f;  // 2 * log2(e)
 __device__ __forceinline__ float tanh_pre(float t) {  // tanh(x) for t = kTanhScale * x
   const float e = __builtin_amdgcn_exp2f(t);

@@ -813,6 +813,16 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
             p = pl.template softmax<kHead2, false>(y, j);
           else
             p = pl.template softmax<kHead2, (FDR_FAST_SOFTMAX != 0)>(y, j);
+          if constexpr (kHead2 && !kDet && FDR_WIDE_SAMPLE_DPP) {
+            // two outputs, sampled: everything in VALU, no readlane round trip -- lane parity o holds p_o;
+            // tot = p0 + p1 (the oracle's 0 + p0 + p1, exactly), p0 to every lane by one DPP move, and the
+            // inverse CDF of two outputs is (p0 <= u tot); no contraction of p's product into the sum
+    #pragma clang fp contract(off)
+            const float tot = p + dpp_mov<kDppQuadXor1>(p);
+            const float p0 = dpp_mov<0xA0>(p);  // quad_perm [0,0,2,2]
+            act_d = p0 <= readlane_f(rbuf, tb) * tot ? 1 : 0;
+            eacc -= (j < NA) ? disc_entropy_term(p, tot) : 0.f;
+          } else {
           float pv[NA];
     #pragma unroll
           for (int i = 0; i < NA; ++i) pv[i] = readlane_f(p, i);
@@ -840,6 +850,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
           }
           // Categorical(probs) entropy: probs normalised, log clamped (torch semantics)
           eacc -= (j < NA) ? disc_entropy_term(p, tot) : 0.f;
+          }
         } else {
           const float th = tanh_fast(y);
           const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
