@@ -42,6 +42,9 @@ __device__ __forceinline__ float normal_bm(uint64_t h) {
 #define FDR_LANE_L2_ASM 1
 #endif
 
+#ifndef FDR_WIDE_HEAD_FOLD  // WIDE sampled loop: head2 bias and the softmax's log2 e folded into the head (r10 A/B)
+#define FDR_WIDE_HEAD_FOLD 0
+#endif
 #ifndef FDR_WIDE_SAMPLE_DPP  // WIDE two-output sampling without readlanes (r10 A/B)
 #define FDR_WIDE_SAMPLE_DPP 0
 #endif

@@ -430,6 +430,17 @@ struct MlpLane {
   // w3c = (W3[0][j], W3[1][j]), keeps the product of output o = j & 1 and hands the other to its quad
   // partner, then sums over the 32 lanes of its parity (row_ror 4, row_ror 8, quad xor 2, the 4-row
   // permlane all-reduce): output o in every lane of parity o, 9 VALU instead of the 16-DPP-FMA dot.
+  // Sampled WIDE loop (FDR_WIDE_HEAD_FOLD): w3s = w3c x log2 e (keep first), bias pair bp = (b3[o] log2 e, 0) in
+  // lanes 0 / 1 and 0 elsewhere, so the head's sum carries the bias and the logit comes out x log2 e
+  __device__ __forceinline__ float head2_fold(float h2, f2 w3s, f2 bp) const {
+    const f2 m = pk_fma(w3s, f2{h2, h2}, bp);
+    float v = m.x + dpp_mov<kDppQuadXor1>(m.y);
+    v += dpp_mov<kDppRowRor + 4>(v);
+    v += dpp_mov<kDppRowRor + 8>(v);
+    v += dpp_mov<kDppQuadXor2>(v);
+    return row_allreduce_sum(v);
+  }
+
   // kKeepFirst: w3c already holds (W3[o][j], W3[1 - o][j]) (FDR_LANE_L2_ASM), so no selects
   template <bool kKeepFirst = false>
   __device__ __forceinline__ float head2(float h2, f2 w3c, float b3p, int j) const {
@@ -536,13 +547,14 @@ struct MlpLane {
   // probabilities move by ~1e-7 relative (inside the 1e-5 forward tolerance), so a sampled action can differ
   // from the exact form's only where u * sum p lies within that of a partition boundary.  Deterministic lanes
   // (argmax, the trap env's integer-exact episodes) keep the exact form.
-  template <bool kAll = false, bool kFast = false>
+  // kPre2 (with kFast): the logits are already x log2(e) (FDR_WIDE_HEAD_FOLD's sampled loop)
+  template <bool kAll = false, bool kFast = false, bool kPre2 = false>
   __device__ __forceinline__ float softmax(float logit, int j) const {
     const bool valid = kAll || (j & 15) < NOUT;
     const float v = valid ? logit : -FLT_MAX;
     const float mx = row16_max_n<NOUT>(v);
     if constexpr (kFast) {
-      const float e = valid ? __builtin_amdgcn_exp2f((v - mx) * 1.44269504088896341f) : 0.f;
+      const float e = valid ? __builtin_amdgcn_exp2f(kPre2 ? v - mx : (v - mx) * 1.44269504088896341f) : 0.f;
       return e * __builtin_amdgcn_rcpf(row16_sum_n<NOUT>(e));
     } else {
       const float e = valid ? expf(v - mx) : 0.f;
@@ -718,6 +730,9 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
     const float b30 = readlane_f(pl.b3, 0), b31 = readlane_f(pl.b3, 1);
     b3p = (j & 1) ? b31 : b30;
   }
+  constexpr bool kFold = kHead2 && WIDE && FDR_LANE_L2_ASM && FDR_WIDE_HEAD_FOLD;
+  const f2 w3s = w3c * f2{1.44269504088896341f, 1.44269504088896341f};
+  const f2 b3s = f2{j < 2 ? b3p * 1.44269504088896341f : 0.f, 0.f};
   const int zbase = 4 * (o < NA ? o : 0);  // ds_bpermute byte address of dim o in step 0 of a batch
   auto fetch_z = [&](int t) {
     if constexpr (DISC) return 0.f;
@@ -800,7 +815,10 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
         if constexpr (kHead2) {
           const float h2 = pl.template layer2<WIDE && (FDR_LANE_L2_ASM != 0)>(h1, sc, j);
           mark(1, h2);
-          y = pl.template head2<WIDE && (FDR_LANE_L2_ASM != 0)>(h2, w3c, b3p, j);
+          if constexpr (kFold && !kDet)
+            y = pl.head2_fold(h2, w3s, b3s);  // x log2 e
+          else
+            y = pl.template head2<WIDE && (FDR_LANE_L2_ASM != 0)>(h2, w3c, b3p, j);
           mark(2, y);
         } else {
           y = pl.layers23(h1, sc, j, mark, WIDE ? w3reg : nullptr);
@@ -812,7 +830,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
           if constexpr (kDet || !FDR_FAST_SOFTMAX)
             p = pl.template softmax<kHead2, false>(y, j);
           else
-            p = pl.template softmax<kHead2, (FDR_FAST_SOFTMAX != 0)>(y, j);
+            p = pl.template softmax<kHead2, (FDR_FAST_SOFTMAX != 0), kFold && FDR_FAST_SOFTMAX>(y, j);
           if constexpr (kHead2 && !kDet && FDR_WIDE_SAMPLE_DPP) {
             // two outputs, sampled: everything in VALU, no readlane round trip -- lane parity o holds p_o;
             // tot = p0 + p1 (the oracle's 0 + p0 + p1, exactly), p0 to every lane by one DPP move, and the
