@@ -46,7 +46,7 @@ __device__ __forceinline__ float normal_bm(uint64_t h) {
 #define FDR_WIDE_HEAD_FOLD 0
 #endif
 #ifndef FDR_WIDE_SAMPLE_DPP  // WIDE two-output sampling without readlanes (r10 A/B)
-#define FDR_WIDE_SAMPLE_DPP 0
+#define FDR_WIDE_SAMPLE_DPP 1
 #endif
 constexpr float kTanhScale = 2.88539008177792681f;  // 2 * log2(e)
 __device__ __forceinline__ float tanh_pre(float t) {  // tanh(x) for t = kTanhScale * x
