@@ -617,7 +617,7 @@ def main():
     }
     if novelty:
         line["config"]["novelty"] = {"archive": len(handler.points), "zeta": ZETA_SIZE, "omega": omega.omega}
-    if fdist.FORCE and world == 1:
+    if fdist.FORCE and world == 1 and dist.is_initialized():  # only when a group ran
         line["config"]["collectives"] = "forced on a one-rank process group (FDR_FORCE_COLLECTIVES=1)"
     if rank == 0:
         print(json.dumps(line), flush=True)

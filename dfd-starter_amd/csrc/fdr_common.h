@@ -37,17 +37,6 @@ __device__ __forceinline__ float normal_bm(uint64_t h) {
 }
 
 // tanh(x) = 1 - 2 / (1 + e^{2x}) on v_exp_f32 / v_rcp_f32 (abs error ~3e-7; saturates to +-1)
-#ifndef FDR_LANE_L2_ASM  // WIDE rollout_kernel: layer 2 as an op_sel asm block with b2 in the own slot, head2 weights
-                         // pre-swapped per lane parity, the 2-logit softmax max as one v_max_f32_dpp (r10 A/B)
-#define FDR_LANE_L2_ASM 1
-#endif
-
-#ifndef FDR_WIDE_HEAD_FOLD  // WIDE sampled loop: head2 bias and the softmax's log2 e folded into the head (r10 A/B)
-#define FDR_WIDE_HEAD_FOLD 0
-#endif
-#ifndef FDR_WIDE_SAMPLE_DPP  // WIDE two-output sampling without readlanes (r10 A/B)
-#define FDR_WIDE_SAMPLE_DPP 1
-#endif
 constexpr float kTanhScale = 2.88539008177792681f;  // 2 * log2(e)
 __device__ __forceinline__ float tanh_pre(float t) {  // tanh(x) for t = kTanhScale * x
   const float e = __builtin_amdgcn_exp2f(t);

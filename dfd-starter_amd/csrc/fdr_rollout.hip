@@ -27,43 +27,6 @@
 #include "fdr_internal.h"
 #include "fdr_wave.h"
 
-#ifndef FDR_PAIR_HEAD  // pair kernel head: 0 = DPP-broadcast dot (32 DPP FMAs), 1 = packed FMAs + reduce-scatter
-#define FDR_PAIR_HEAD 0
-#endif
-#ifndef FDR_PAIR_NOMOV  // pair kernel: op_sel broadcasts in L2, packed multiplies start the L1 chains (r10 A/B)
-#define FDR_PAIR_NOMOV 1
-#endif
-#ifndef FDR_PAIR_DETSPLIT  // pair kernel: a select-free episode loop for waves without deterministic lanes (r10 A/B)
-#define FDR_PAIR_DETSPLIT 0
-#endif
-#ifndef FDR_HEAD_CHAINS  // pair kernel head: accumulator chains of the 32-term DPP dot (4, 2 or 1; r10 A/B)
-#define FDR_HEAD_CHAINS 1
-#endif
-#ifndef FDR_LANE_ENV_PRESCALE  // rollout_kernel: the synthetic env's M, K stored x 2 log2(e) (r10 A/B)
-#define FDR_LANE_ENV_PRESCALE 0
-#endif
-#ifndef FDR_L1_ONECHAIN  // pair kernel: layer 1 and the env's M s as one packed chain each (r10 A/B)
-#define FDR_L1_ONECHAIN 0
-#endif
-#ifndef FDR_L2_QUAD  // pair kernel: layer 2 as 8 x 16 blocks reduced over a quad (r10 A/B)
-#define FDR_L2_QUAD 1
-#endif
-#ifndef FDR_RS_SCHED  // pair kernel: reduce-scatter DPP adds ordered to need no s_nop (r10 A/B)
-#define FDR_RS_SCHED 1
-#endif
-#ifndef FDR_RS_OUT  // pair kernel: L2 reduce-scatter with untied outputs (r10 A/B)
-#define FDR_RS_OUT 1
-#endif
-#ifndef FDR_PAIR_CHAINS  // pair kernel: layer 1 on 4 accumulator chains, the env's K a on 2 (r10 A/B switch)
-#define FDR_PAIR_CHAINS 0
-#endif
-#ifndef FDR_PAIR_PRESCALE  // pair kernel: tanh pre-activations scaled by 2 log2(e) in the weights, biases in the chains
-#define FDR_PAIR_PRESCALE 1
-#endif
-#ifndef FDR_FAST_SOFTMAX  // sampled discrete lanes: approximate exp / reciprocal softmax (MlpLane::softmax)
-#define FDR_FAST_SOFTMAX 1
-#endif
-
 namespace fdr {
 
 constexpr int kLanesPerBlock = 4;
@@ -430,18 +393,7 @@ struct MlpLane {
   // w3c = (W3[0][j], W3[1][j]), keeps the product of output o = j & 1 and hands the other to its quad
   // partner, then sums over the 32 lanes of its parity (row_ror 4, row_ror 8, quad xor 2, the 4-row
   // permlane all-reduce): output o in every lane of parity o, 9 VALU instead of the 16-DPP-FMA dot.
-  // Sampled WIDE loop (FDR_WIDE_HEAD_FOLD): w3s = w3c x log2 e (keep first), bias pair bp = (b3[o] log2 e, 0) in
-  // lanes 0 / 1 and 0 elsewhere, so the head's sum carries the bias and the logit comes out x log2 e
-  __device__ __forceinline__ float head2_fold(float h2, f2 w3s, f2 bp) const {
-    const f2 m = pk_fma(w3s, f2{h2, h2}, bp);
-    float v = m.x + dpp_mov<kDppQuadXor1>(m.y);
-    v += dpp_mov<kDppRowRor + 4>(v);
-    v += dpp_mov<kDppRowRor + 8>(v);
-    v += dpp_mov<kDppQuadXor2>(v);
-    return row_allreduce_sum(v);
-  }
-
-  // kKeepFirst: w3c already holds (W3[o][j], W3[1 - o][j]) (FDR_LANE_L2_ASM), so no selects
+  // kKeepFirst: w3c already holds (W3[o][j], W3[1 - o][j]) (the WIDE kernel), so no selects
   template <bool kKeepFirst = false>
   __device__ __forceinline__ float head2(float h2, f2 w3c, float b3p, int j) const {
     const f2 m = w3c * f2{h2, h2};
@@ -542,19 +494,18 @@ struct MlpLane {
   }
 
   // Discrete: softmax across the row (o = j & 15 < NA); returns p_o, 0 for o >= NA.  kAll: every lane
-  // holds a logit (head2: output j & 1).  kFast (sampled lanes, FDR_FAST_SOFTMAX): exp as v_exp_f32 of x log2 e and
+  // holds a logit (head2: output j & 1).  kFast (sampled lanes): exp as v_exp_f32 of x log2 e and
   // the normalisation as a v_rcp_f32 product -- 4 VALU instead of libm expf (13) + the IEEE division (11); the
   // probabilities move by ~1e-7 relative (inside the 1e-5 forward tolerance), so a sampled action can differ
   // from the exact form's only where u * sum p lies within that of a partition boundary.  Deterministic lanes
   // (argmax, the trap env's integer-exact episodes) keep the exact form.
-  // kPre2 (with kFast): the logits are already x log2(e) (FDR_WIDE_HEAD_FOLD's sampled loop)
-  template <bool kAll = false, bool kFast = false, bool kPre2 = false>
+  template <bool kAll = false, bool kFast = false>
   __device__ __forceinline__ float softmax(float logit, int j) const {
     const bool valid = kAll || (j & 15) < NOUT;
     const float v = valid ? logit : -FLT_MAX;
     const float mx = row16_max_n<NOUT>(v);
     if constexpr (kFast) {
-      const float e = valid ? __builtin_amdgcn_exp2f(kPre2 ? v - mx : (v - mx) * 1.44269504088896341f) : 0.f;
+      const float e = valid ? __builtin_amdgcn_exp2f((v - mx) * 1.44269504088896341f) : 0.f;
       return e * __builtin_amdgcn_rcpf(row16_sum_n<NOUT>(e));
     } else {
       const float e = valid ? expf(v - mx) : 0.f;
@@ -631,9 +582,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
   if constexpr (ENV == FDR_ENV_SYNTH) {
     for (int e = threadIdx.x; e < NIN * MKS; e += blockDim.x) {  // padding columns zero (b128 row reads)
       const int i = e / MKS, k = e % MKS;
-      // FDR_LANE_ENV_PRESCALE: x kTanhScale, so the env's tanh starts at its exp2
-      envMK[e] = (FDR_LANE_ENV_PRESCALE ? kTanhScale : 1.f) *
-                 (k < NIN ? a.M[i * NIN + k] : (k >= NX && k < NX + NA ? a.K[i * NA + k - NX] : 0.f));
+      envMK[e] = (k < NIN ? a.M[i * NIN + k] : (k >= NX && k < NX + NA ? a.K[i * NA + k - NX] : 0.f));
     }
     __syncthreads();  // the only cross-wave hand-off: shared env matrices
   }
@@ -726,13 +675,10 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
     const float* t0 = reinterpret_cast<const float*>(pl.tile - j + (Lane::kW1Chunks + ((j & 15) >> 2)) * kWave +
                                                      (j >> 4) * 16);
     w3c = f2{t0[j & 3], t0[4 + (j & 3)]};
-    if (WIDE && FDR_LANE_L2_ASM && (j & 1)) w3c = f2{w3c.y, w3c.x};  // output j & 1 first (head2<true>)
+    if (WIDE && (j & 1)) w3c = f2{w3c.y, w3c.x};  // output j & 1 first (head2<true>)
     const float b30 = readlane_f(pl.b3, 0), b31 = readlane_f(pl.b3, 1);
     b3p = (j & 1) ? b31 : b30;
   }
-  constexpr bool kFold = kHead2 && WIDE && FDR_LANE_L2_ASM && FDR_WIDE_HEAD_FOLD;
-  const f2 w3s = w3c * f2{1.44269504088896341f, 1.44269504088896341f};
-  const f2 b3s = f2{j < 2 ? b3p * 1.44269504088896341f : 0.f, 0.f};
   const int zbase = 4 * (o < NA ? o : 0);  // ds_bpermute byte address of dim o in step 0 of a batch
   auto fetch_z = [&](int t) {
     if constexpr (DISC) return 0.f;
@@ -792,7 +738,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
           h1 = pl.layer1_env_reg(xv, sv, mreg, pre);
           if constexpr (kCand) {
     #pragma unroll
-            for (int i = 0; i < NA; ++i) cand[i] = tanh_act<(FDR_LANE_ENV_PRESCALE != 0)>(pre + kreg[i]);
+            for (int i = 0; i < NA; ++i) cand[i] = tanh_fast(pre + kreg[i]);
           }
         } else {
         // policy input (and env state) broadcast through the wave's LDS scratch, then packed FMAs
@@ -813,12 +759,9 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
         mark(0, h1);
         float y;
         if constexpr (kHead2) {
-          const float h2 = pl.template layer2<WIDE && (FDR_LANE_L2_ASM != 0)>(h1, sc, j);
+          const float h2 = pl.template layer2<WIDE>(h1, sc, j);
           mark(1, h2);
-          if constexpr (kFold && !kDet)
-            y = pl.head2_fold(h2, w3s, b3s);  // x log2 e
-          else
-            y = pl.template head2<WIDE && (FDR_LANE_L2_ASM != 0)>(h2, w3c, b3p, j);
+          y = pl.template head2<WIDE>(h2, w3c, b3p, j);
           mark(2, y);
         } else {
           y = pl.layers23(h1, sc, j, mark, WIDE ? w3reg : nullptr);
@@ -827,11 +770,8 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
         float act_c = 0.f;
         if constexpr (DISC) {
           float p;
-          if constexpr (kDet || !FDR_FAST_SOFTMAX)
-            p = pl.template softmax<kHead2, false>(y, j);
-          else
-            p = pl.template softmax<kHead2, (FDR_FAST_SOFTMAX != 0), kFold && FDR_FAST_SOFTMAX>(y, j);
-          if constexpr (kHead2 && !kDet && FDR_WIDE_SAMPLE_DPP) {
+          p = pl.template softmax<kHead2, !kDet>(y, j);
+          if constexpr (kHead2 && !kDet) {
             // two outputs, sampled: everything in VALU, no readlane round trip -- lane parity o holds p_o;
             // tot = p0 + p1 (the oracle's 0 + p0 + p1, exactly), p0 to every lane by one DPP move, and the
             // inverse CDF of two outputs is (p0 <= u tot); no contraction of p's product into the sum
@@ -844,9 +784,9 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
           float pv[NA];
     #pragma unroll
           for (int i = 0; i < NA; ++i) pv[i] = readlane_f(p, i);
-          float tot = FDR_LANE_L2_ASM ? pv[0] : 0.f;  // sequential f32 cumsum, the oracle's order (0 + p0 == p0)
+          float tot = pv[0];  // sequential f32 cumsum, the oracle's order (0 + p0 == p0)
     #pragma unroll
-          for (int i = FDR_LANE_L2_ASM ? 1 : 0; i < NA; ++i) tot += pv[i];
+          for (int i = 1; i < NA; ++i) tot += pv[i];
           // Branch-free selection (selects, no data-dependent control flow):
           //   argmax = first maximal index; inverse CDF = first i with cumsum_i > target, i.e. the
           //   number of (monotone) partial sums <= target, capped at NA - 1.
@@ -892,7 +832,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
               for (int m = 0; m < NA; ++m) kr[m] = WIDE ? kreg[m] : mrow[NX + m];
               dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in lane m of every row
             }
-            s = tanh_act<(FDR_LANE_ENV_PRESCALE != 0)>(pre);
+            s = tanh_fast(pre);
           }
           racc += (double)s;  // lane 0 holds the reward s'[0]; other lanes' sums are discarded
         } else {
@@ -955,133 +895,7 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
 //   head       thread (rho = t/16, o = t%16) sums W3[o][.] over the 32 units its own DPP row
 //              holds (32 row_newbcast FMAs), then the two rows of the half (one permlane16 swap).
 // ---------------------------------------------------------------------------------------------
-#ifndef FDR_PAIR_WAVES
-#define FDR_PAIR_WAVES 2
-#endif
-constexpr int kPairWaves = FDR_PAIR_WAVES;  // waves per workgroup (4 lanes): 4 workgroups, 8 waves per CU
-
-// 16-slot reduce-scatter over the 8 threads of a half-row: v[i] += partner(c ^ 7).v[i + 8] (i < 8),
-// v[i] += partner(c ^ 2).v[i + 4] (i < 4), v[i] += partner(c ^ 1).v[i + 2] (i < 2).  s_nop: a DPP read
-// of a VGPR needs 2 wait states after its VALU write.
-__device__ __forceinline__ void reduce_scatter16(float (&v)[16]) {
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %8, %0 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %9, %1 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %2, %10, %2 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %3, %11, %3 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %4, %12, %4 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %5, %13, %5 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %6, %14, %6 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %7, %15, %7 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %4, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %5, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %2, %6, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %3, %7, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %2, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %3, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
-      : "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
-}
-
-// reduce_scatter16 with untied outputs (FDR_PAIR_NOMOV): level 1 writes fresh registers, so the compiler does not
-// copy the low halves of the packed accumulators into separate tied registers; returns the two kept slots
-__device__ __forceinline__ f2 reduce_scatter16_out(const float (&v)[16]) {
-  float o[8];
-#if FDR_RS_SCHED
-  // ordered so that every DPP source was written >= 3 instructions earlier (2 wait states): level 1 produces
-  // o6, o7, o4 first, level 2 o2, o3 first -- no s_nop inside; the caller's layer-2 block writes v[8..15] early
-  asm volatile(
-      "v_add_f32_dpp %6, %22, %14 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %7, %23, %15 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %4, %20, %12 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %5, %21, %13 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %2, %18, %10 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %3, %19, %11 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %0, %16, %8 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %17, %9 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %2, %6, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %3, %7, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %0, %4, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %5, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %0, %2, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %3, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7])
-      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]), "v"(v[9]),
-        "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
-#else
-
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %16, %8 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %17, %9 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %2, %18, %10 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %3, %19, %11 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %4, %20, %12 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %5, %21, %13 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %6, %22, %14 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %7, %23, %15 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %4, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %5, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %2, %6, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %3, %7, %3 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %2, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %3, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      : "=&v"(o[0]), "=&v"(o[1]), "=&v"(o[2]), "=&v"(o[3]), "=&v"(o[4]), "=&v"(o[5]), "=&v"(o[6]), "=&v"(o[7])
-      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]), "v"(v[8]), "v"(v[9]),
-        "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
-#endif
-  return f2{o[0], o[1]};
-}
-
-// Reduce-scatter of 16 slots over the 16 threads of a DPP row (packed head, FDR_PAIR_HEAD = 1): register i of
-// thread t holds slot i ^ (t & 15); levels with partners t ^ 15 (row_mirror), t ^ 7 (row_half_mirror), t ^ 2, t ^ 1
-// (quad perms) each add the partner's register i ^ mask, leaving the row sum of slot t & 15 in v[0].
-__device__ __forceinline__ void reduce_scatter16_row(float (&v)[16]) {
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %15, %0 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %14, %1 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %2, %13, %2 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %3, %12, %3 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %4, %11, %4 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %5, %10, %5 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %6, %9, %6 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %7, %8, %7 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %7, %0 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %6, %1 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %2, %5, %2 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %3, %4, %3 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %2, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "v_add_f32_dpp %1, %3, %1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      "s_nop 1\n\t"
-      "v_add_f32_dpp %0, %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
-      : "v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]), "v"(v[14]), "v"(v[15]));
-}
-
-// acc += sum_{m<6} w[m] * X(row lane m) as two chains of three DPP FMAs + one add (FDR_PAIR_CHAINS): the env's
-// K a after the action, 4 dependent steps instead of 6
-__device__ __forceinline__ void dpp_tail6_2chains(float& acc, float X, const float* w) {
-  float b;
-  asm volatile(
-      "s_nop 1\n\t"
-      "v_fmac_f32_dpp %0, %2, %3 row_newbcast:0 row_mask:0xf bank_mask:0xf\n\t"
-      "v_mul_f32_dpp %1, %2, %6 row_newbcast:3 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f32_dpp %0, %2, %4 row_newbcast:1 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f32_dpp %1, %2, %7 row_newbcast:4 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f32_dpp %0, %2, %5 row_newbcast:2 row_mask:0xf bank_mask:0xf\n\t"
-      "v_fmac_f32_dpp %1, %2, %8 row_newbcast:5 row_mask:0xf bank_mask:0xf\n\t"
-      : "+v"(acc), "=&v"(b)
-      : "v"(X), "v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]));
-  acc += b;
-}
+constexpr int kPairWaves = 2;  // waves per workgroup (4 lanes): 4 workgroups, 8 waves per CU
 
 // tanh_fast on a register pair: packed mul / add / fma around the two exp and two rcp
 __device__ __forceinline__ f2 tanh2_pre(f2 t) {  // t = 2 log2(e) x
@@ -1091,9 +905,9 @@ __device__ __forceinline__ f2 tanh2_pre(f2 t) {  // t = 2 log2(e) x
 __device__ __forceinline__ f2 tanh2_fast(f2 x) {
   return tanh2_pre(x * f2{kTanhScale, kTanhScale});
 }
-// FDR_PAIR_PRESCALE: every weight and bias feeding a tanh is stored times kTanhScale (after its norm2 count), so
-// the activation starts at the exp2 -- one multiply fewer per tanh (L1, L2, head, env: 4 per step)
-constexpr float kPreScale = FDR_PAIR_PRESCALE ? kTanhScale : 1.f;
+// Every weight and bias feeding a tanh is stored times kTanhScale (after its norm2 count), so the activation
+// starts at the exp2 -- one multiply fewer per tanh (L1, L2, head, env: 4 per step)
+constexpr float kPreScale = kTanhScale;
 template <bool kPre>
 __device__ __forceinline__ f2 tanh2_act(f2 z) {
   if constexpr (kPre) return tanh2_pre(z);
@@ -1108,7 +922,7 @@ struct MlpPair {
   static_assert(NX <= 32, "pair kernel: policy input wider than 32");
   static constexpr bool kBiasCol = NIN < NX;
   static constexpr bool kW1Lds = NIN > 8;
-  static constexpr bool kPre = !DISC && FDR_PAIR_PRESCALE;  // tanh layers' weights stored x kTanhScale
+  static constexpr bool kPre = !DISC;  // tanh layers' weights stored x kTanhScale
   static constexpr float kWS = kPre ? kTanhScale : 1.f;
   static constexpr int kW1Chunks = kW1Lds ? NX / 4 : 0;     // per W1 row
   static constexpr int kTileF4 = (2 * kW1Chunks + 8) * kWave;  // float4 per wave: W1 rows, W3 slice
@@ -1121,16 +935,11 @@ struct MlpPair {
 
   // unit of layer 2 that row-thread k's value e (0: z.x, 1: z.y) holds, within the row's 32 units
   __host__ __device__ static constexpr int head_unit(int rho, int k, int e) {
-#if FDR_L2_QUAD
     return 32 * rho + 8 * (k >> 2) + 4 * e + (k & 3);  // thread 4q + c holds units 8q + c, 8q + 4 + c
-#else
-    return 32 * rho + 16 * (k >> 3) + 8 * e + (k & 7);
-#endif
   }
 
   __device__ __forceinline__ void load(ParamSrc& src, int t, int tid, const float* bn_mean, const float* bn_var,
                                        float4* wave_tile) {
-    [[maybe_unused]] const int r = t >> 3, c = t & 7;
     const int rho = t >> 4, o = t & 15;
     const int ua = 2 * t, ub = 2 * t + 1;
     float4* my = wave_tile + tid;
@@ -1163,7 +972,6 @@ struct MlpPair {
     }
     b1a = kBiasCol ? 0.f : kWS * src.get(L::L1B + ua);
     b1b = kBiasCol ? 0.f : kWS * src.get(L::L1B + ub);
-#if FDR_L2_QUAD
     // quad q = t / 4 owns units 8q .. 8q + 7; thread c = t % 4 of it takes inputs 16c .. 16c + 15 and pair p the
     // units (8q + (c ^ p), 8q + 4 + (c ^ p)): the quad's reduce-scatter (partners c ^ 2, c ^ 1) leaves pair 0
     const int q4 = t >> 2, c4 = t & 3;
@@ -1178,36 +986,9 @@ struct MlpPair {
       }
     }
     const int u2a = 8 * q4 + c4, u2b = 8 * q4 + 4 + c4;  // this thread's layer-2 units
-#else
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int row0 = 16 * r + (c ^ l2_sigma(p)), row1 = row0 + 8;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float e0 = src.get(L::L2W + (int64_t)row0 * kHidden + 8 * c + k);
-        const float e1 = src.get(L::L2W + (int64_t)row1 * kHidden + 8 * c + k);
-        w2[p * 8 + k] = f2{kWS * e0, kWS * e1};
-      }
-    }
-    const int u2a = 16 * r + c, u2b = 16 * r + 8 + c;  // this thread's layer-2 units
-#endif
     b2a = kWS * src.get(L::L2B + u2a);
     b2b = kWS * src.get(L::L2B + u2b);
-    if constexpr (FDR_PAIR_HEAD == 1) {
-      // packed head: chunk m = (W3[(2m)^o][u2a], W3[(2m+1)^o][u2a], W3[(2m)^o][u2b], W3[(2m+1)^o][u2b]) -- register
-      // slot i of this thread holds output i ^ o (the reduce-scatter's thread-dependent order); every W3 element is
-      // loaded by exactly one thread of the half (its unit's), so norm2 counts it once
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const int s0 = (2 * m) ^ o, s1 = (2 * m + 1) ^ o;
-        const float e0 = s0 < NOUT ? src.get(L::L3W + (int64_t)s0 * kHidden + u2a) : 0.f;
-        const float e1 = s1 < NOUT ? src.get(L::L3W + (int64_t)s1 * kHidden + u2a) : 0.f;
-        const float e2 = s0 < NOUT ? src.get(L::L3W + (int64_t)s0 * kHidden + u2b) : 0.f;
-        const float e3 = s1 < NOUT ? src.get(L::L3W + (int64_t)s1 * kHidden + u2b) : 0.f;
-        my[(2 * kW1Chunks + m) * kWave] = float4{kWS * e0, kWS * e1, kWS * e2, kWS * e3};
-      }
-      b3 = kWS * (o < NOUT ? (rho == 0 ? src.get(L::L3B + o) : src.get_nocount(L::L3B + o)) : 0.f);
-    } else if (o < NOUT) {
+    if (o < NOUT) {
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         float e[4];
@@ -1314,8 +1095,8 @@ struct MlpPair {
     f2 am0 = {0.f, 0.f}, am1 = {0.f, 0.f};
     if constexpr (kPk) {
       // units (a, b) packed: acc[k % NC] += (w_a(k), w_b(k)) * x_k; the bias column (k = NIN) is added.
-      // NC = 2 chains of ~9 dependent packed FMAs, or 4 of ~5 (FDR_PAIR_CHAINS) + two packed adds
-      constexpr int NC = FDR_PAIR_CHAINS ? 4 : (FDR_L1_ONECHAIN ? 1 : 2);
+      // NC = 2 chains of ~9 dependent packed FMAs
+      constexpr int NC = 2;
       f2 acc[NC];
 #pragma unroll
       for (int q = 0; q < NC; ++q) acc[q] = f2{0.f, 0.f};
@@ -1333,38 +1114,26 @@ struct MlpPair {
               const float4 wb = rows.wp[NIN >> 1];
               const f2 bias = (NIN & 1) ? f2{wb.z, wb.w} : f2{wb.x, wb.y};
               acc[k % NC] = (k & 1) ? pk_fma_bhi(f2{w.z, w.w}, xp, bias) : pk_fma_blo(f2{w.x, w.y}, xp, bias);
-            } else if (FDR_PAIR_NOMOV && k < NC)
+            } else if (k < NC)
               acc[k % NC] = (k & 1) ? pk_mul_bhi(f2{w.z, w.w}, xp) : pk_mul_blo(f2{w.x, w.y}, xp);
             else
               acc[k % NC] = (k & 1) ? pk_fma_bhi(f2{w.z, w.w}, xp, acc[k % NC]) : pk_fma_blo(f2{w.x, w.y}, xp, acc[k % NC]);
           }
         }
         am0 = pk_fma(f2{mv.x, mv.y}, f2{sv.x, sv.y}, am0);
-        if constexpr (FDR_L1_ONECHAIN)
-          am0 = pk_fma(f2{mv.z, mv.w}, f2{sv.z, sv.w}, am0);
-        else
-          am1 = pk_fma(f2{mv.z, mv.w}, f2{sv.z, sv.w}, am1);
+        am1 = pk_fma(f2{mv.z, mv.w}, f2{sv.z, sv.w}, am1);
       }
       if constexpr (kTail) {  // input 4 NQ = NIN - 1, then the bias
         const float4 w = rows.wp[(NIN - 1) >> 1];
         acc[(NIN - 1) % NC] = pk_fma(((NIN - 1) & 1) ? f2{w.z, w.w} : f2{w.x, w.y}, f2{xt, xt}, acc[(NIN - 1) % NC]);
-        if constexpr (FDR_L1_ONECHAIN)
-          am0.x = fmaf(rows.tm, kSameInput ? xt : st, am0.x);
-        else
-          am1.x = fmaf(rows.tm, kSameInput ? xt : st, am1.x);
+        am1.x = fmaf(rows.tm, kSameInput ? xt : st, am1.x);
       }
       if constexpr (!kPre || NIN % NC >= NIN) {
         const float4 w = rows.wp[NIN >> 1];
         acc[NIN % NC] = acc[NIN % NC] + ((NIN & 1) ? f2{w.z, w.w} : f2{w.x, w.y});
       }
-      f2 h;
-      if constexpr (NC == 4)
-        h = (acc[0] + acc[2]) + (acc[1] + acc[3]);
-      else if constexpr (NC == 2)
-        h = acc[0] + acc[1];
-      else
-        h = acc[0];
-      const f2 am = FDR_L1_ONECHAIN ? am0 : am0 + am1;
+      const f2 h = acc[0] + acc[1];
+      const f2 am = am0 + am1;
       env = am.x + am.y;
       if constexpr (DISC) {
         return f2{act1(h.x, a1a, c1a), act1(h.y, a1b, c1b)};
@@ -1409,8 +1178,6 @@ struct MlpPair {
   // Returns the head pre-activation for output o = t & 15 (identical in both rows of the half).
   template <class Mark>
   __device__ __forceinline__ float layers23(f2 h1, float* h1s, int t, Mark&& mark) const {
-#if FDR_L2_QUAD
-    static_assert(FDR_PAIR_NOMOV && FDR_RS_OUT, "FDR_L2_QUAD needs the op_sel layer-2 block");
     const int c4 = t & 3;
     float x[16];
     reinterpret_cast<f2*>(h1s)[t] = h1;
@@ -1538,126 +1305,6 @@ struct MlpPair {
     }
     const float za = kPre ? zs.x : zs.x + b2a;  // unit 8q + c
     const float zb = kPre ? zs.y : zs.y + b2b;  // unit 8q + 4 + c
-#else
-    const int c = t & 7;
-    float x[8];
-    reinterpret_cast<f2*>(h1s)[t] = h1;
-    wave_lds_sync();
-    lds_bcast<8>(h1s + 8 * c, x);
-    // the head's W3 slice (loop-invariant LDS) requested here, in flight during the 64 packed FMAs
-    float w3[32];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      const float4 w = tile[(2 * kW1Chunks + m) * kWave];
-      w3[4 * m] = w.x;
-      w3[4 * m + 1] = w.y;
-      w3[4 * m + 2] = w.z;
-      w3[4 * m + 3] = w.w;
-    }
-    f2 acc[8];
-#pragma unroll
-    for (int p = 0; p < 8; ++p) acc[p] = f2{0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-#pragma unroll
-      for (int p = 0; p < 8; ++p)
-        if (!FDR_PAIR_NOMOV || k == 0)
-          // kPre: the thread's own slots (acc[0]) start from its biases -- each output's sum takes them once
-          acc[p] = pk_fma(w2[p * 8 + k], f2{x[k], x[k]}, (kPre && k == 0 && p == 0) ? f2{b2a, b2b} : acc[p]);
-#if FDR_PAIR_NOMOV
-    // k >= 1 as op_sel broadcasts of the b128 pairs (x[k - 1], x[k]) / (x[k], x[k + 1]) in ONE asm statement: the
-    // compiler follows every asm statement with an s_nop, and would move each odd x[k] to an even register
-    // (operands: %0-%7 acc, %(8 + 8 (k - 1) + p) = w2[8 p + k], %64-%67 the x pairs).  k = 7 writes acc[4..7] first:
-    // they are the reduce-scatter's DPP sources, which need 2 wait states after their VALU write
-    {
-      const f2 x01 = {x[0], x[1]}, x23 = {x[2], x[3]}, x45 = {x[4], x[5]}, x67 = {x[6], x[7]};
-#define FDR_L2_HI "op_sel:[0,1,0] op_sel_hi:[1,1,1]"
-#define FDR_L2_LO "op_sel_hi:[1,0,1]"
-      asm(
-          "v_pk_fma_f32 %0, %8, %64, %0 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %1, %9, %64, %1 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %2, %10, %64, %2 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %3, %11, %64, %3 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %4, %12, %64, %4 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %5, %13, %64, %5 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %6, %14, %64, %6 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %7, %15, %64, %7 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %0, %16, %65, %0 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %1, %17, %65, %1 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %2, %18, %65, %2 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %3, %19, %65, %3 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %4, %20, %65, %4 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %5, %21, %65, %5 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %6, %22, %65, %6 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %7, %23, %65, %7 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %0, %24, %65, %0 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %1, %25, %65, %1 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %2, %26, %65, %2 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %3, %27, %65, %3 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %4, %28, %65, %4 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %5, %29, %65, %5 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %6, %30, %65, %6 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %7, %31, %65, %7 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %0, %32, %66, %0 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %1, %33, %66, %1 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %2, %34, %66, %2 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %3, %35, %66, %3 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %4, %36, %66, %4 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %5, %37, %66, %5 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %6, %38, %66, %6 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %7, %39, %66, %7 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %0, %40, %66, %0 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %1, %41, %66, %1 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %2, %42, %66, %2 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %3, %43, %66, %3 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %4, %44, %66, %4 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %5, %45, %66, %5 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %6, %46, %66, %6 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %7, %47, %66, %7 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %0, %48, %67, %0 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %1, %49, %67, %1 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %2, %50, %67, %2 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %3, %51, %67, %3 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %4, %52, %67, %4 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %5, %53, %67, %5 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %6, %54, %67, %6 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %7, %55, %67, %7 " FDR_L2_LO "\n"
-          "v_pk_fma_f32 %4, %60, %67, %4 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %5, %61, %67, %5 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %6, %62, %67, %6 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %7, %63, %67, %7 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %0, %56, %67, %0 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %1, %57, %67, %1 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %2, %58, %67, %2 " FDR_L2_HI "\n"
-          "v_pk_fma_f32 %3, %59, %67, %3 " FDR_L2_HI "\n"
-          : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]), "+v"(acc[6]), "+v"(acc[7])
-          : "v"(w2[1]), "v"(w2[9]), "v"(w2[17]), "v"(w2[25]), "v"(w2[33]), "v"(w2[41]), "v"(w2[49]), "v"(w2[57]),
-            "v"(w2[2]), "v"(w2[10]), "v"(w2[18]), "v"(w2[26]), "v"(w2[34]), "v"(w2[42]), "v"(w2[50]), "v"(w2[58]),
-            "v"(w2[3]), "v"(w2[11]), "v"(w2[19]), "v"(w2[27]), "v"(w2[35]), "v"(w2[43]), "v"(w2[51]), "v"(w2[59]),
-            "v"(w2[4]), "v"(w2[12]), "v"(w2[20]), "v"(w2[28]), "v"(w2[36]), "v"(w2[44]), "v"(w2[52]), "v"(w2[60]),
-            "v"(w2[5]), "v"(w2[13]), "v"(w2[21]), "v"(w2[29]), "v"(w2[37]), "v"(w2[45]), "v"(w2[53]), "v"(w2[61]),
-            "v"(w2[6]), "v"(w2[14]), "v"(w2[22]), "v"(w2[30]), "v"(w2[38]), "v"(w2[46]), "v"(w2[54]), "v"(w2[62]),
-            "v"(w2[7]), "v"(w2[15]), "v"(w2[23]), "v"(w2[31]), "v"(w2[39]), "v"(w2[47]), "v"(w2[55]), "v"(w2[63]),
-            "v"(x01), "v"(x23), "v"(x45), "v"(x67));
-#undef FDR_L2_LO
-#undef FDR_L2_HI
-    }
-#endif
-    // reduce-scatter over the 8 threads of the half-row: slot i = acc[i / 2][i % 2], output of
-    // slot i = 16r + 8 (i % 2) + (c ^ sigma(i / 2)); partners c ^ 7, c ^ 2, c ^ 1
-    float sl[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sl[i] = (i & 1) ? acc[i >> 1].y : acc[i >> 1].x;
-#if FDR_RS_OUT
-    const f2 zs = reduce_scatter16_out(sl);
-    const float za = kPre ? zs.x : zs.x + b2a;  // unit 16r + c
-    const float zb = kPre ? zs.y : zs.y + b2b;  // unit 16r + 8 + c
-#else
-    reduce_scatter16(sl);  // one asm block: the SLP vectoriser would split the DPP adds into movs
-    const float za = sl[0] + b2a;  // unit 16r + c
-    const float zb = sl[1] + b2b;  // unit 16r + 8 + c
-#endif
-#endif
     mark(1, za);
     float h2a, h2b;
     if constexpr (DISC) {
@@ -1669,34 +1316,7 @@ struct MlpPair {
       h2b = h2.y;
     }
     float u;
-    if constexpr (FDR_PAIR_HEAD == 1) {
-      // packed head: 8 output pairs x this thread's two units (16 packed MACs), then a 4-level reduce-scatter over
-      // the 16-thread row (partners t^15, t^7, t^2, t^1) leaves output o = t & 15 in this thread
-      float hs[16];
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        const f2 a = pk_fma(f2{w3[4 * m + 2], w3[4 * m + 3]}, f2{h2b, h2b},
-                            f2{w3[4 * m], w3[4 * m + 1]} * f2{h2a, h2a});
-        hs[2 * m] = a.x;
-        hs[2 * m + 1] = a.y;
-      }
-      reduce_scatter16_row(hs);
-      u = hs[0];
-    } else if constexpr (FDR_PAIR_CHAINS >= 2) {
-      float s0, s1, s2, s3, s4, s5, s6, s7;  // eight chains of 4
-      dpp_dot_32x8(s0, s1, s2, s3, s4, s5, s6, s7, h2a, h2b, w3);
-      u = ((s0 + s4) + (s2 + s6)) + ((s1 + s5) + (s3 + s7));
-    } else if constexpr (FDR_HEAD_CHAINS == 1) {
-      dpp_dot_32x1(u, h2a, h2b, w3);  // one chain of 32 (the accumulator is no DPP source: no wait states)
-    } else if constexpr (FDR_HEAD_CHAINS == 2) {
-      float s0, s1;  // two chains of 16
-      dpp_dot_32x2(s0, s1, h2a, h2b, w3);
-      u = s0 + s1;
-    } else {
-      float s0, s1, s2, s3;  // four independent chains of 8 (first product a v_mul: no zeroing)
-      dpp_dot_32x4(s0, s1, s2, s3, h2a, h2b, w3);
-      u = (s0 + s2) + (s1 + s3);
-    }
+    dpp_dot_32x1(u, h2a, h2b, w3);  // one chain of 32 (the accumulator is no DPP source: no wait states)
     float v = u;
     permlane16_swap(u, v);  // u = row 2h's partial, v = row 2h+1's, in both rows of half h
     const float out = (u + v) + b3;
@@ -1818,10 +1438,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     const uint64_t hsh = hash_ctr(key, ulane, (uint64_t)(st + ds), (uint64_t)dk);
     rbuf = DISC ? uniform24(hsh) : normal_bm(hsh);
   };
-  // sampled_tag: std::true_type when no lane of the wave is deterministic (FDR_PAIR_DETSPLIT), so the action
-  // needs no select
-  auto step = [&](int st, int tb, auto sampled_tag) {
-    constexpr bool kSampled = decltype(sampled_tag)::value;
+  auto step = [&](int st, int tb) {
     // this step's draw: the uniform (discrete) or the normal of action dim o (continuous)
     const float zt = __builtin_bit_cast(
         float, __builtin_amdgcn_ds_bpermute(zbase + 4 * kDrawsPerStep * tb, __builtin_bit_cast(int, rbuf)));
@@ -1838,7 +1455,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     const float y = pl.layers23(h1, h1s, t, mark);
     pl.l1_prefetch(l1rows, mrow);  // next step's rows, in flight during the action and env phases
     if constexpr (DISC) {
-      const float p = det || !FDR_FAST_SOFTMAX ? pl.softmax(y, t) : pl.template softmax<false, (FDR_FAST_SOFTMAX != 0)>(y, t);
+      const float p = det ? pl.softmax(y, t) : pl.template softmax<false, true>(y, t);
       float pv[NA];
       row_bcast_all(p, pv, std::make_integer_sequence<int, NA>{});  // pv[i] = p of output i
       float tot = 0.f;
@@ -1867,19 +1484,16 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
       const float th = tanh_act<Lane::kPre>(y);
       const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
       eacc += __builtin_amdgcn_logf(sd);
-      const float act_c = (!kSampled && det) ? th : gauss_action(th, sd, zt);
+      const float act_c = det ? th : gauss_action(th, sd, zt);
       mark(3, act_c);
-      if constexpr (FDR_PAIR_CHAINS && NA == 6)
-        dpp_tail6_2chains(pre, act_c, kr);   // a[m] sits in thread m of both rows of the half
-      else
-        dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in thread m of both rows of the half
+      dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in thread m of both rows of the half
     }
-    s = tanh_act<(FDR_PAIR_PRESCALE != 0)>(pre);
+    s = tanh_pre(pre);  // M, K stored x kPreScale
     racc += (double)s;  // thread 0 of the half holds the reward s'[0]
     mark(4, s);
   };
   if constexpr (!DISC) {
-    auto episode = [&](auto sampled_tag) {
+    {
       // continuous: the loop unrolled by the draw batch (5 steps for 6 dims); the draw is issued
       // unconditionally at the top of the unrolled body (det lanes ignore it), so it schedules into the
       // first step's waits instead of sitting behind a branch
@@ -1894,7 +1508,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
             asm volatile("" ::: "memory");
             mark(-1, s);
           }
-          step(st + k, k, sampled_tag);
+          step(st + k, k);
         }
       }
       if (st < T) {
@@ -1902,21 +1516,16 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
         for (int k = 0; st + k < T; ++k) {
           asm volatile("" ::: "memory");
           mark(-1, s);
-          step(st + k, k, sampled_tag);
+          step(st + k, k);
         }
       }
-    };
-    // one specialised copy for waves without deterministic lanes (the common case), one generic
-    if (FDR_PAIR_DETSPLIT && !__builtin_amdgcn_readfirstlane(__ballot(det) != 0 ? 1 : 0))
-      episode(std::true_type{});
-    else
-      episode(std::false_type{});
+    }
   } else {
     for (int st = 0; st < T; ++st) {
       asm volatile("" ::: "memory");
       mark(-1, s);
       if (!det && tb == 0) draw(st);
-      step(st, tb, std::false_type{});
+      step(st, tb);
       tb = tb + 1 == kStepsPerBatch ? 0 : tb + 1;
     }
   }
@@ -2008,13 +1617,7 @@ static void launch_pair(const RolloutArgs& args, int round_lanes, hipStream_t st
   }
 }
 
-static int pair_round_lanes(const Context& ctx) {
-  static const int env = [] {
-    const char* e = std::getenv("FDR_PAIR_ROUNDS");  // A/B switch: "0" = one launch for all lanes
-    return e ? std::atoi(e) : 1;
-  }();
-  return env ? 16 * context_cus(ctx) : 0;
-}
+static int pair_round_lanes(const Context& ctx) { return 16 * context_cus(ctx); }
 
 // Synthetic-env rollouts: rollout_pair_kernel (two lanes per wave) or rollout_kernel (one lane per
 // wave), by the context's rollout_impl: FDR_ROLLOUT_AUTO (default) takes the pair kernel once it puts

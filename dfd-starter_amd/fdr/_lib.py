@@ -31,7 +31,7 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_fd_grad_fused_out_len",
            "fdr_fd_grad_fused", "fdr_rank_weights", "fdr_dsgd_step_ex", "fdr_fd_step",
            "fdr_ctx_set_rollout_impl", "fdr_ctx_set_replay_gemm", "fdr_ctx_set_core_mfma", "fdr_ctx_set_conv_h2", "fdr_ctx_impala_profile",
-           "fdr_ctx_impala_profile_read", "fdr_ctx_impala_debug_clock")
+           "fdr_ctx_impala_profile_read", "fdr_ctx_impala_debug_clock", "fdr_noise_draw_indices")
 
 
 class FDRError(RuntimeError):
@@ -99,6 +99,7 @@ def _load():
                                           ctypes.POINTER(LanesDesc), I32, U64, I32, P, P, P, P, P, P,
                                           ctypes.POINTER(RolloutExtras), P]),
         "fdr_obs_stats_merge": (ctypes.c_int, [P, P, P, P, I32, I32, P, P, P, P]),
+        "fdr_noise_draw_indices": (ctypes.c_int, [P, ctypes.POINTER(ctypes.c_int32), I64, I32, P]),
         "fdr_fd_lambda_norms": (ctypes.c_int, [P, P, I64, P, P, P, I32, I64, F32, P, I32, P, P]),
         "fdr_fd_grad_lambda": (ctypes.c_int, [P, P, I64, P, P, P, P, I32, I64, F32, P, I32, P, P, I64, P]),
         "fdr_bn_refresh_workspace_bytes": (I64, [I32]),

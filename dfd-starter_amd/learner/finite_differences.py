@@ -29,6 +29,7 @@ from dsgd import DSGD
 from fdr import dist as fdist
 from fdr import engine
 from utils import math_helpers
+from utils.noise_sources import require_device_table
 
 from .fd_return import FDBatch
 
@@ -47,6 +48,7 @@ class FiniteDifferences(object):
         self.noise_std = noise_std
         self.policy = policy
         self.gradient_optimizer = gradient_optimizer
+        require_device_table(noise_source, "FiniteDifferences")
         self.noise_source = noise_source
         self.omega = omega
         self.batch_size = batch_size

@@ -16,6 +16,7 @@ import torch
 from fdr import engine
 from learner.fd_return import FDBatch
 from utils.math_helpers import WelfordRunningStat
+from utils.noise_sources import require_device_table
 
 
 def obs_partials(res):
@@ -28,6 +29,7 @@ class Worker(object):
     def __init__(self, policy, agent, noise_source, strategy_handler, sigma=0.02, eval_prob=0.1, random_seed=123):
         self.policy = policy
         self.agent = agent
+        require_device_table(noise_source, "Worker")
         self.noise_source = noise_source
         self.strategy_handler = strategy_handler
         self.sigma = sigma

@@ -190,6 +190,13 @@ int fdr_rollout_ex(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_de
                    const float* obs_mean, const float* obs_std, double* ret, double* ent, int32_t* steps,
                    double* norm2, const fdr_rollout_extras* extras, fdr_stream stream);
 
+/* ---- noise-table index draw on the HOST (utils/noise_sources.py:44-47) -----------------------------
+ * out[i], i < n: the indices n successive RandomState.randint(0, max_idx) calls return, drawn from the MT19937
+ * state key [624] u32 / *pos (numpy RandomState.get_state()[1:3]) and advanced in place: 32-bit words masked by
+ * the smallest all-ones mask >= max_idx - 1, rejected while > max_idx - 1 (numpy's legacy masked path).  HOST
+ * pointers, no device work; FDR_ERR_UNSUPPORTED when max_idx - 1 needs more than 32 bits. */
+int fdr_noise_draw_indices(uint32_t* key, int32_t* pos, int64_t max_idx, int32_t n, int64_t* out);
+
 /* ---- obs statistics merge (utils/math_helpers.py:68-87, increment_from_obs_stats_update) --------
  * Folds n partial Welford statistics (mean/m2 [n, dim] f32, count [n] i32, e.g. from
  * fdr_rollout_ex) into the accumulator (acc_mean/acc_m2 [dim] f32, acc_count [1] i64, device,

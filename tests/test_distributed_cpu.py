@@ -33,7 +33,12 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, out_dir):
+# (P, directions): the small case, and BASELINE config 3 at N = 8 (8 ranks x 4096 lanes = 16384 directions,
+# 32768 r' slots in the moments payload)
+SIZES = {"small": (1000, 37), "bench8": (6092, 16384)}
+
+
+def _rank_main(rank, world, port, out_dir, size="small"):
     sys.path[:0] = [REPO, PKG]
     import torch.distributed as dist
     from fdr import dist as fdist
@@ -41,7 +46,7 @@ def _rank_main(rank, world, port, out_dir):
     from oracle import noise as onoise
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    P, D, sigma = 1000, 37, 0.02
+    (P, D), sigma = SIZES[size], 0.02
     t = onoise.NoiseTable(1 << 16, P, 5)
     idx = t.sample_indices(D)                        # every rank draws the full stream
     lidx = np.repeat(idx, 2)
@@ -69,13 +74,13 @@ def _rank_main(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
-def test_two_rank_gradient_matches_single_process(tmp_path, world):
+@pytest.mark.parametrize("world,size", [(2, "small"), (8, "small"), (8, "bench8")])
+def test_two_rank_gradient_matches_single_process(tmp_path, world, size):
     port = _free_port()
-    mp.spawn(_rank_main, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_rank_main, args=(world, port, str(tmp_path), size), nprocs=world, join=True)
     from oracle import learner as olearn
     from oracle import noise as onoise
-    P, D = 1000, 37
+    P, D = SIZES[size]
     t = onoise.NoiseTable(1 << 16, P, 5)
     idx = t.sample_indices(D)
     lidx = np.repeat(idx, 2)
@@ -85,9 +90,13 @@ def test_two_rank_gradient_matches_single_process(tmp_path, world):
     for r in range(world):
         g = np.load(os.path.join(str(tmp_path), "g%d.npy" % r))
         assert np.linalg.norm(g - g_ref) / np.linalg.norm(g_ref) < 1e-12
-    # every rank holds the identical reduced gradient -> replicated DSGD stays in lock-step
-    assert np.array_equal(np.load(os.path.join(str(tmp_path), "g0.npy")),
-                          np.load(os.path.join(str(tmp_path), "g1.npy")))
+    # every rank holds the identical reduced gradient -> replicated DSGD stays in lock-step (theta bitwise)
+    g0 = np.load(os.path.join(str(tmp_path), "g0.npy"))
+    theta0 = olearn.dsgd_step(np.zeros(P, np.float32), g0, 0.01)[0]
+    for r in range(1, world):
+        gr = np.load(os.path.join(str(tmp_path), "g%d.npy" % r))
+        assert np.array_equal(g0, gr)
+        assert np.array_equal(olearn.dsgd_step(np.zeros(P, np.float32), gr, 0.01)[0], theta0)
 
 
 def _moment_rewards(kind, n):
@@ -99,7 +108,7 @@ def _moment_rewards(kind, n):
     return 500.0 + rs.choice([-1e-12, 1e-12], n)
 
 
-def _rank_main_moments(rank, world, port, out_dir, kind):
+def _rank_main_moments(rank, world, port, out_dir, kind, size="small"):
     """The one-collective z-score protocol (FiniteDifferences._step_batch, sharded): every rank reduces its lanes
     to [A | B | n_local | r' slots], ONE all-reduce sums them, g = (A - m B) / sd with m, sd over all r'."""
     sys.path[:0] = [REPO, PKG]
@@ -109,7 +118,7 @@ def _rank_main_moments(rank, world, port, out_dir, kind):
     from oracle import noise as onoise
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    P, D, sigma = 1000, 37, 0.02
+    (P, D), sigma = SIZES[size], 0.02
     t = onoise.NoiseTable(1 << 16, P, 5)
     idx = t.sample_indices(D)
     lidx = np.repeat(idx, 2)
@@ -123,13 +132,15 @@ def _rank_main_moments(rank, world, port, out_dir, kind):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,kind", [(2, "spread"), (3, "spread"), (2, "near_constant")])
-def test_one_collective_moments_gradient_matches_two_collective(tmp_path, world, kind):
+@pytest.mark.parametrize("world,kind,size", [(2, "spread", "small"), (3, "spread", "small"),
+                                            (2, "near_constant", "small"), (8, "spread", "bench8"),
+                                            (8, "near_constant", "bench8")])
+def test_one_collective_moments_gradient_matches_two_collective(tmp_path, world, kind, size):
     port = _free_port()
-    mp.spawn(_rank_main_moments, args=(world, port, str(tmp_path), kind), nprocs=world, join=True)
+    mp.spawn(_rank_main_moments, args=(world, port, str(tmp_path), kind, size), nprocs=world, join=True)
     from oracle import learner as olearn
     from oracle import noise as onoise
-    P, D = 1000, 37
+    P, D = SIZES[size]
     t = onoise.NoiseTable(1 << 16, P, 5)
     idx = t.sample_indices(D)
     lidx = np.repeat(idx, 2)

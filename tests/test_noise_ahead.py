@@ -18,3 +18,65 @@ def test_peek_then_sample_is_the_sequential_stream():
     got += list(a.sample_batch(23))
     assert got == seq
     assert list(pk) == seq[:10]
+
+
+def test_host_only_noise_sources_are_refused_at_construction():
+    """the reference's default RNGNoiseSource (run_sequential.py:89) and SimpleNoiseSource have no
+    table for the GPU path to gather from -- a TypeError naming SharedNoiseTable at construction, not an
+    AttributeError mid-step."""
+    import pytest
+    from learner.finite_differences import FiniteDifferences
+    from utils.noise_sources import RNGNoiseSource, SharedNoiseTable, SimpleNoiseSource
+    from worker.worker import Worker
+    for src in (RNGNoiseSource(100, 1), SimpleNoiseSource(100, 1)):
+        with pytest.raises(TypeError, match="SharedNoiseTable"):
+            Worker(object(), object(), src, None)
+        with pytest.raises(TypeError, match="SharedNoiseTable"):
+            FiniteDifferences(object(), None, 0.0, src)
+    from utils.noise_sources import require_device_table
+    require_device_table(SharedNoiseTable(1 << 12, 100, 1), "Worker")   # accepted
+
+
+def test_native_index_draw_is_numpy_randint():
+    """fdr_noise_draw_indices (the product's host draw) == RandomState.randint, the reference's draw
+    (utils/noise_sources.py:45), word for word: the same indices and the same generator state afterwards --
+    including the cached Gaussian of the table's randn, across 624-word refills and for masks of every width."""
+    from utils.noise_sources import SharedNoiseTable
+    for size, P, seed in ((1 << 16, 1000, 7), (25_000_000, 6092, 124), (6093, 6092, 3), (6094, 6092, 9),
+                          ((1 << 20) + 1, 1, 11)):
+        t = SharedNoiseTable(size, P, seed)
+        ref = np.random.RandomState(seed)
+        ref.randn(size)
+        for n in (1, 5, 700, 16384, 3):
+            got = t._draw(n)
+            exp = ref.randint(0, size - P, size=n).astype(np.int64)
+            assert np.array_equal(got, exp), (size, n)
+        a, b = t._rng.get_state(), ref.get_state()
+        assert np.array_equal(a[1], b[1]) and a[2:] == b[2:]
+        assert t._rng.randn() == ref.randn()     # the cached Gaussian survives set_state
+
+
+def test_host_draw_of_an_eight_rank_step_is_short():
+    """at N = 8 every rank draws the whole 16,384-index stream of a config-3 step (2048
+    directions x 8), then builds its lane slice and the packed upload.  It runs under the rollout it overlaps
+    (Worker.evaluate(prefetch=True) draws the next step while this one runs): < 10 % of the ~1 ms step."""
+    import time
+    from utils.noise_sources import SharedNoiseTable
+    from fdr import dist as fdist
+    t = SharedNoiseTable(25_000_000, 6092, 124)
+    ts = []
+    for _ in range(30):
+        t0 = time.perf_counter()
+        idx = t.sample_batch(16384)
+        lo, hi = fdist.lane_range(16384, 2, 8, 3)
+        lidx = np.repeat(idx[lo // 2:hi // 2], 2)
+        sign = np.tile(np.array([1, -1], np.int8), (hi - lo) // 2)
+        m = hi - lo
+        packed = np.empty(10 * m, np.uint8)
+        packed[:8 * m] = lidx.view(np.uint8)
+        packed[8 * m:9 * m] = sign.view(np.uint8)
+        packed[9 * m:] = 0
+        ts.append(time.perf_counter() - t0)
+    med = float(np.median(ts))
+    print("host draw + lane slice + pack, 16384 indices: %.1f us" % (med * 1e6))
+    assert med < 100e-6 * 2   # 2x margin over the < 0.1 ms target for a loaded CI host

@@ -15,6 +15,9 @@ the replicated DSGD step -- for STEPS FD steps.  All ranks must end bit-identica
 single-process run up to the collective's summation order.  tests/test_gpu_dist_equivalence.py drives it.
 Preset "stale": from step 1 on, lists of FDReturn with the previous step's returns again as one-epoch-old
 (delayed) returns -- the sharded drift path of FiniteDifferences.
+Preset "uneven" (ADVICE r4): lists of FDReturn split unevenly over the ranks -- step 0: rank 1 holds none, step 1:
+30 % / 70 %, step 2: rank 0 holds none -- the count exchange, the padded unequal all-gather and the zero-gradient
+branch of a rank without returns, against the single process holding every return.
 Preset "bench": bench.py's step at BASELINE config 3 size -- 2048 directions (4096 lanes) PER RANK, T = 1000, the
 25 M-entry table, 2 FD steps through Worker.evaluate(prefetch=True) + FiniteDifferences.step_async.
 """
@@ -28,7 +31,8 @@ STEPS = 3
 
 PRESETS = {"small": dict(dirs_per_rank=48, T=200, table=1 << 22, steps=STEPS, bench=False),
            "bench": dict(dirs_per_rank=2048, T=1000, table=25_000_000, steps=2, bench=True),
-           "stale": dict(dirs_per_rank=24, T=100, table=1 << 22, steps=STEPS, bench=False, stale=True)}
+           "stale": dict(dirs_per_rank=24, T=100, table=1 << 22, steps=STEPS, bench=False, stale=True),
+           "uneven": dict(dirs_per_rank=24, T=100, table=1 << 22, steps=STEPS, bench=False, uneven=True)}
 
 
 def run(mode, weighting, out, preset="small"):
@@ -79,6 +83,17 @@ def run(mode, weighting, out, preset="small"):
                     r.epoch = learner.epoch - 1
                 upd.append(learner.step(cur + prev, 0.25, 0.0, 0.0))
             prev = batch.to_returns()
+            continue
+        if cfg.get("uneven"):
+            # every process evaluates all lanes (global lane keys: identical returns everywhere), then each rank keeps
+            # its share of the list; the single process keeps all of it
+            rets = worker.evaluate(n_dirs, antithetic=True, seed=1000 + step).to_returns()
+            for r in rets:
+                r.epoch = learner.epoch
+            if mode != "single":
+                cut = [len(rets), (3 * len(rets)) // 10, 0][step % 3]
+                rets = rets[:cut] if rank == 0 else rets[cut:]
+            upd.append(learner.step(rets, 0.25, 0.0, 0.0))
             continue
         if cfg["bench"]:    # bench.py's fd_step: prefetched indices, the learner's no-sync step
             batch = worker.evaluate(n_dirs, antithetic=True, lane_range="auto", seed=1000 + step, prefetch=True)
