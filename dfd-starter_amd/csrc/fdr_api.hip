@@ -733,8 +733,9 @@ int fdr_atari_forward(fdr_ctx* ctx, const fdr_atari_desc* d, const float* theta,
 // (Matsumoto & Nishimura 1998, the generator behind numpy's legacy RandomState) advanced in place from the
 // state numpy reports (key[624], pos), and numpy's masked rejection for ranges that fit 32 bits: each draw takes
 // 32-bit words masked by the smallest all-ones mask >= max_idx - 1 until one is <= max_idx - 1.  numpy makes
-// one indirect generator call per word (~11 ns per index); this loop is ~4x faster, which keeps an 8-rank
-// step's 16,384-index draw (every rank consumes the whole stream) well under the rollout it overlaps.
+// one indirect generator call and one unpredictable branch per word (~11 ns per index on the build host); a block
+// of tempered words with a branch-free compaction takes ~2.5 ns, which keeps an 8-rank step's 16,384-index draw
+// (every rank consumes the whole stream) well under the rollout it overlaps.
 // ---------------------------------------------------------------------------------------------
 namespace {
 constexpr int kMtN = 624, kMtM = 397;
@@ -775,19 +776,33 @@ extern "C" int fdr_noise_draw_indices(uint32_t* key, int32_t* pos, int64_t max_i
   mask |= mask >> 4;
   mask |= mask >> 8;
   mask |= mask >> 16;
+  // a refill block at a time: temper + mask the block's remaining words (vectorised), then a branch-free
+  // compaction keeps the accepted ones; the last block stops at the word that completes the n-th index, as
+  // numpy's loop does (no extra words consumed)
   int p = *pos;
-  for (int32_t i = 0; i < n; ++i) {
-    uint32_t v;
-    do {
-      if (p == kMtN) {
-        mt_refill(key);
-        p = 0;
+  int32_t k = 0;
+  uint32_t buf[kMtN];
+  while (k < n) {
+    if (p == kMtN) {
+      mt_refill(key);
+      p = 0;
+    }
+    const int m = kMtN - p;
+    for (int i = 0; i < m; ++i) buf[i] = mt_temper(key[p + i]) & mask;
+    if (n - k >= m) {  // the whole block fits: k < n at every write
+      for (int i = 0; i < m; ++i) {
+        out[k] = buf[i];
+        k += buf[i] <= (uint32_t)rng;
       }
-      v = mt_temper(key[p++]);
-      if (rng == 0xFFFFFFFFull) break;  // the full 32-bit range: every word
-      v &= mask;
-    } while (v > (uint32_t)rng);
-    out[i] = (int64_t)v;
+      p += m;
+    } else {
+      int i = 0;
+      for (; i < m && k < n; ++i) {
+        out[k] = buf[i];
+        k += buf[i] <= (uint32_t)rng;
+      }
+      p += i;
+    }
   }
   *pos = p;
   return FDR_OK;

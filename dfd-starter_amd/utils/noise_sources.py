@@ -22,12 +22,30 @@ from fdr import _lib
 class SharedNoiseTable(object):
     def __init__(self, size, n_params, random_seed=123):
         assert size > n_params, "!ATTEMPTED TO MAKE NOISE TABLE WITH SIZE {} FOR {} PARAMETERS!".format(size, n_params)
-        self._rng = np.random.RandomState(random_seed)
-        self._table = self._rng.randn(size).astype(np.float32)
+        rng = np.random.RandomState(random_seed)
+        self._table = rng.randn(size).astype(np.float32)
         self._n_params = n_params
         self._max_sample_idx = size - n_params
         self._device_tables = {}
         self._ahead = np.empty(0, np.int64)     # drawn by peek_batch, not yet consumed
+        # the index stream continues the table's MT19937 state (noise_sources.py:45); the draws advance this copy of
+        # it natively (fdr_noise_draw_indices), and rng_state() / _rng hand it back in numpy's format
+        name, key, pos, has_gauss, cached = rng.get_state()
+        self._mt_key = np.array(key, dtype=np.uint32)
+        self._mt_pos = ctypes.c_int32(int(pos))
+        self._mt_extra = (name, has_gauss, cached)
+
+    def rng_state(self):
+        """The index stream's generator state as numpy's RandomState.get_state() tuple."""
+        name, has_gauss, cached = self._mt_extra
+        return (name, self._mt_key.copy(), int(self._mt_pos.value), has_gauss, cached)
+
+    @property
+    def _rng(self):
+        """A RandomState at the index stream's current position (the reference's attribute; a snapshot)."""
+        rs = np.random.RandomState()
+        rs.set_state(self.rng_state())
+        return rs
 
     @property
     def size(self):
@@ -38,21 +56,23 @@ class SharedNoiseTable(object):
         return "{}".format(idx), self._table[idx:idx + self._n_params]
 
     def _draw(self, n):
-        """n randint(0, max_idx) draws from the table's RandomState: fdr_noise_draw_indices advances numpy's own
-        MT19937 state (get_state / set_state keep the RandomState object current, its cached Gaussian included) --
-        bit-identical to RandomState.randint (tests/test_noise_ahead.py), ~4x faster at the sizes one step draws."""
+        """n randint(0, max_idx) draws continuing the table's RandomState stream: fdr_noise_draw_indices advances the
+        MT19937 state natively -- bit-identical to RandomState.randint (tests/test_noise_ahead.py), ~4x faster
+        than numpy's per-word loop at the sizes one step draws (16,384 indices per rank at N = 8)."""
         n = int(n)
         out = np.empty(n, np.int64)
         if n == 0:
             return out
-        name, key, pos, has_gauss, cached = self._rng.get_state()
-        key = np.array(key, dtype=np.uint32)
-        p = ctypes.c_int32(int(pos))
-        rc = _lib.lib.fdr_noise_draw_indices(key.ctypes.data, ctypes.byref(p), self._max_sample_idx, n, out.ctypes.data)
+        rc = _lib.lib.fdr_noise_draw_indices(self._mt_key.ctypes.data, ctypes.byref(self._mt_pos), self._max_sample_idx,
+                                             n, out.ctypes.data)
         if rc == _lib.FDR_ERR_UNSUPPORTED:      # a table wider than 2^32 entries: numpy's own 64-bit path
-            return self._rng.randint(0, self._max_sample_idx, size=n).astype(np.int64)
+            rs = self._rng
+            out = rs.randint(0, self._max_sample_idx, size=n).astype(np.int64)
+            _, key, pos, _, _ = rs.get_state()
+            self._mt_key[:] = key
+            self._mt_pos.value = int(pos)
+            return out
         _lib.check(rc, "fdr_noise_draw_indices")
-        self._rng.set_state((name, key, p.value, has_gauss, cached))
         return out
 
     def peek_batch(self, n):

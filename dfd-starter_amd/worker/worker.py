@@ -142,9 +142,8 @@ class Worker(object):
         """Host lane arrays of one evaluate() call from its direction indices: (lidx, sign, det, lane_range,
         rank_lanes)."""
         lpd = 2 if antithetic else 1
-        lidx = np.repeat(idx, lpd)
-        sign = np.tile(np.array([1, -1], np.int8), n_dirs) if antithetic else np.ones(n_dirs, np.int8)
         rank_lanes = None
+        d_lo, d_hi = 0, n_dirs
         if lane_range is not None:
             from fdr import dist as fdist
             world, rank = fdist.world_rank()
@@ -156,7 +155,11 @@ class Worker(object):
             lo, hi = lane_range
             if lo % lpd or hi % lpd:
                 raise ValueError("lane_range must not split antithetic pairs")
-            lidx, sign = lidx[lo:hi], sign[lo:hi]
+            d_lo, d_hi = lo // lpd, hi // lpd
+        # only this rank's directions are expanded to lanes (at N = 8 one eighth of the stream)
+        nd = d_hi - d_lo
+        lidx = np.repeat(idx[d_lo:d_hi], lpd)
+        sign = np.tile(np.array([1, -1], np.int8), nd) if antithetic else np.ones(nd, np.int8)
         return lidx, sign, np.zeros(len(lidx), np.int8), lane_range, rank_lanes
 
     def evaluate(self, n_dirs, antithetic=True, seed=None, lane_range=None, out=None, novelty=False, prefetch=False,
