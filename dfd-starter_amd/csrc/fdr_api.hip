@@ -119,7 +119,7 @@ Context& default_context() {
     const char* m = getenv("FDR_CORE_MFMA");  // A/B switch: "0" selects the VALU fp16 pair core
     c->core_mfma = !(m && strcmp(m, "0") == 0);
     const char* h2 = getenv("FDR_CONV_H2");  // A/B switch: "0" selects conv_kernel_h (one workgroup per CU)
-    c->conv_h2 = !h2 ? 2 : strcmp(h2, "0") == 0 ? 0 : strcmp(h2, "1") == 0 ? 1 : 2;
+    c->conv_h2 = !h2 ? 2 : strcmp(h2, "0") == 0 ? 0 : strcmp(h2, "1") == 0 ? 1 : strcmp(h2, "3") == 0 ? 3 : 2;
     return c;
   }();
   return *d;
@@ -162,7 +162,7 @@ static int resolve(fdr_ctx* ctx, Context** out) {
 
 extern "C" {
 
-const char* fdr_version(void) { return "fdr 0.3 gfx950"; }
+const char* fdr_version(void) { return "fdr 0.4 gfx950"; }
 const char* fdr_last_error(void) { return g_err.c_str(); }
 
 static int set_impl(Context& c, int32_t impl) {
@@ -182,7 +182,7 @@ int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on) {
   return FDR_OK;
 }
 int fdr_ctx_set_conv_h2(fdr_ctx* ctx, int32_t on) {
-  if (on < 0 || on > 2) return set_error(FDR_ERR_INVALID, "conv_h2 must be 0, 1 or 2");
+  if (on < 0 || on > 3) return set_error(FDR_ERR_INVALID, "conv_h2 must be 0, 1, 2 or 3");
   (ctx ? ctx->c : default_context()).conv_h2 = on;
   return FDR_OK;
 }
@@ -299,6 +299,10 @@ int fdr_rollout_ex(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_de
     return set_error(FDR_ERR_INVALID, "env obs/act dims do not match the policy");
   if (env->kind == FDR_ENV_SYNTH) {
     if (!env->M || !env->K || !env->s0) return set_error(FDR_ERR_INVALID, "synthetic env needs M, K, s0");
+    if (!(env->done_threshold >= 0.f) || env->done_threshold > 3.0e38f)
+      return set_error(FDR_ERR_INVALID, "done_threshold must be finite and >= 0");
+    if (env->done_threshold > 0.f && (env->done_dim < 0 || env->done_dim >= env->obs_dim))
+      return set_error(FDR_ERR_INVALID, "done_dim out of range");
   } else if (env->kind == FDR_ENV_TRAP) {
     if (!env->walkable || env->map_w <= 0 || env->map_h <= 0)
       return set_error(FDR_ERR_INVALID, "trap env needs the walkable map");
@@ -319,6 +323,8 @@ int fdr_rollout_ex(fdr_ctx* ctx, const fdr_policy_desc* policy, const fdr_env_de
   a.M = env->M;
   a.K = env->K;
   a.s0 = env->s0;
+  a.done_thr = env->kind == FDR_ENV_SYNTH ? env->done_threshold : 0.f;
+  a.done_dim = env->kind == FDR_ENV_SYNTH && env->done_threshold > 0.f ? env->done_dim : 0;
   a.walkable = env->walkable;
   a.map_w = env->map_w;
   a.map_h = env->map_h;

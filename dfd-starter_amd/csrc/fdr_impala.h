@@ -218,8 +218,11 @@ __global__ void finish_kernel(int n_lanes, int envs, int T, int entropy, int jig
 // fp16 mode kernels (fdr_impala_h.hip)
 __global__ void conv_kernel_h(Layout L, StepArgs a);
 // same features as conv_kernel_h, 80 KiB LDS: 2 workgroups per CU; NTH = 256 (4 waves) or 512 (8 waves, 128 VGPRs)
-template <int NTH>
+// SPLIT3: stop after the stage-3 entry (X3 into the feature slot) -- conv_s3_kernel finishes the stack, 4 envs per WG
+template <int NTH, bool SPLIT3>
 __global__ void conv_kernel_h2(Layout L, StepArgs a);
+__global__ void conv_s3_kernel(Layout L, StepArgs a);
+constexpr int kS3EnvsPerWG = 4;  // conv_s3_kernel: envs per workgroup
 template <int E, int MODE>
 __global__ void core_kernel_h(Layout L, StepArgs a);
 template <int E>

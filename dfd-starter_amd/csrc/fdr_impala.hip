@@ -1344,12 +1344,19 @@ __global__ void pair_offsets_kernel(const int64_t* __restrict__ idx, int n_pairs
   if (p < n_pairs) idxe[p] = idx[2 * p];
 }
 
-// the fp16 conv stack over grid workgroups (one per env, XCD-interleaved lanes): either kernel, same features
+// the fp16 conv stack over grid workgroups (one per env, XCD-interleaved lanes): either kernel, same features;
+// h2 = 3: conv_kernel_h2<512> through the stage-3 entry, then conv_s3_kernel (4 envs per workgroup) -- the features of
+// h2 = 2 bit for bit
 static void launch_conv_h(int h2, int grid, const Layout& L, const StepArgs& a, hipStream_t stream) {
-  if (h2 == 2)
-    hipLaunchKernelGGL(conv_kernel_h2<512>, dim3(grid), dim3(512), 0, stream, L, a);
+  if (h2 == 3) {
+    hipLaunchKernelGGL((conv_kernel_h2<512, true>), dim3(grid), dim3(512), 0, stream, L, a);
+    const int64_t n_envs = (int64_t)a.n_lanes * a.envs;
+    hipLaunchKernelGGL(conv_s3_kernel, dim3((unsigned)((n_envs + kS3EnvsPerWG - 1) / kS3EnvsPerWG)), dim3(512), 0, stream,
+                       L, a);
+  } else if (h2 == 2)
+    hipLaunchKernelGGL((conv_kernel_h2<512, false>), dim3(grid), dim3(512), 0, stream, L, a);
   else if (h2)
-    hipLaunchKernelGGL(conv_kernel_h2<256>, dim3(grid), dim3(256), 0, stream, L, a);
+    hipLaunchKernelGGL((conv_kernel_h2<256, false>), dim3(grid), dim3(256), 0, stream, L, a);
   else
     hipLaunchKernelGGL(conv_kernel_h, dim3(grid), dim3(kHThreads), 0, stream, L, a);
 }

@@ -1416,9 +1416,13 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
   do {                       \
   } while (0)
 #endif
-template <int NTH>
+// SPLIT3 (conv_kernel_h2<512, true>, ctx conv_h2 = 3): stop after the stage-3 entry and hand X3 (8 x 8 x 32 f16, the
+// xidx layout) to conv_s3_kernel through the first 4 KB of the env's feature slot; the stage-3 residual blocks run
+// there, four envs per workgroup
+template <int NTH, bool SPLIT3>
 __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))) void conv_kernel_h2(Layout L, StepArgs a) {
   constexpr bool H3 = NTH >= 512 && FDR_H3_ENTRY;  // stage entries with the pool in registers
+  static_assert(!SPLIT3 || H3, "split stage 3: the h3 entries");
   static_assert(!H3 || NTH == kHThreads, "h3 entries: 8 waves (zero_border_h's thread count)");
   // experiment: FDR_H2_ONE_PER_CU pads the LDS past half the CU (one workgroup per CU) -- latency sensitivity
   __shared__ __attribute__((aligned(16))) unsigned char smem[kH2LdsBytes + (FDR_H2_ONE_PER_CU ? 4096 : 0)];
@@ -1630,7 +1634,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   // VGPRs) two bands of 9, so a wave's accumulators stay at 2 tiles x 2 channel tiles beside the 72 fragment VGPRs
   // (h3: one band of 16 rows, pool in registers) ----
   if constexpr (H3) {
-    st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
+    if constexpr (!SPLIT3) st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
     h4 prev[2], P[2], Bx[2];
     f32x4 acc[2][2];
     conv_band_nat<32, 16>(R + kH2T2, 0, R + kH2WBB, acc, wave, ln);
@@ -1640,7 +1644,15 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
 #pragma unroll
       for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[10 * 32 + nt * 16 + 4 * (ln >> 4) + k];
     pool_nat<16>(acc, bz, P, Bx);
-    band_out_h3<32, 16, false>(P, Bx, prev, R, R + kH3EX3, 0, wave, ln, R + kH2T3, bsc + 11 * 32, bsh + 11 * 32);
+    band_out_h3<32, 16, false>(P, Bx, prev, R, R + kH3EX3, 0, wave, ln, SPLIT3 ? nullptr : R + kH2T3, bsc + 11 * 32,
+                               bsh + 11 * 32);
+    if constexpr (SPLIT3) {
+      __syncthreads();  // X3 complete
+      FDR_STAMP(a, 45);
+      if (threadIdx.x < 8 * 8 * 32 / 8)   // X3 -> the env's feature slot (read back by conv_s3_kernel)
+        reinterpret_cast<u32x4*>(a.feat + env * kFeat)[threadIdx.x] = reinterpret_cast<const u32x4*>(R)[threadIdx.x];
+      return;
+    }
     zero_border_h<32, 8>(R + kH2T3);
     st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
     FDR_STAMP(a, 45);
@@ -1683,8 +1695,154 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   if (a.dbg && threadIdx.x == 0) a.dbg[256 + 4 * b + 1] = wall_clock64();
 #endif
 }
-template __global__ void conv_kernel_h2<256>(Layout, StepArgs);
-template __global__ void conv_kernel_h2<512>(Layout, StepArgs);
+template __global__ void conv_kernel_h2<256, false>(Layout, StepArgs);
+template __global__ void conv_kernel_h2<512, false>(Layout, StepArgs);
+template __global__ void conv_kernel_h2<512, true>(Layout, StepArgs);
+
+// =====================================================================================================
+// Stage-3 residual blocks, FOUR envs per workgroup: conv_s3_kernel (ctx conv_h2 = 3, after conv_kernel_h2<512, true>;
+// VERDICT r4 item 1).  In the one-env workgroup the stage-3 residual convs (8 x 8 x 32, 4 pixel tiles x 2 channel
+// tiles) gave each wave ONE dependent chain of 9 MFMAs between LDS reads, then a barrier, an epilogue and a barrier:
+// 8 barrier phases for 1.15 K MFMA slots per SIMD, ~7.6 K clocks of the env's ~80 K (profiles/r08o phases).  Here a
+// workgroup takes envs 4b .. 4b + 3 (the four envs of one lane when E = 4: one theta'), wave w = (env slot w / 2,
+// channel tile w % 2) runs FOUR independent chains (the env's 4 pixel tiles) per conv, and:
+//   * the residual stream X lives in the wave's registers (its own pixels x channels: the accumulator layout, 8 VGPRs)
+//     -- only the padded BN'd image T is shared, double-buffered per env (conv c reads T[c & 1], writes T[c + 1 & 1]),
+//     so each conv has ONE barrier and the epilogue follows the wave's own MFMAs;
+//   * the A fragments (this wave's channel tile, 9 K-steps = 36 VGPRs) come straight from the half pack (L2: the
+//     lane's other waves and envs read the same 9 KB), the next conv's issued right after the current K loop;
+//   * per output: the same K order, the same chained MFMAs and the same f32 epilogue arithmetic as res_blocks_h2,
+//     so the features equal conv_kernel_h2<512>'s bit for bit (tests/test_gpu_impala.py).
+// LDS: 4 envs x 2 x 10 x 10 x 32 halves (51 KB) + the BN / bias rows of convs 11..14 (6 KB): two workgroups per CU.
+// =====================================================================================================
+constexpr int kS3Envs = kS3EnvsPerWG;
+constexpr int kS3T = 10 * 10 * 32;  // halves of one padded 8 x 8 x 32 image
+
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv_s3_kernel(Layout L, StepArgs a) {
+  __shared__ __attribute__((aligned(16))) _Float16 Tb[kS3Envs][2][kS3T];
+  __shared__ float tab[kS3Envs][3][4][32];  // [slot][scale, shift, conv bias][index 11 .. 14][channel]
+  const int64_t n_envs = (int64_t)a.n_lanes * a.envs;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
+  const int slot = wave >> 1, nt = wave & 1, g = ln >> 4, ch0 = 16 * nt + 4 * g;
+  const int64_t ge = (int64_t)blockIdx.x * kS3Envs + slot;
+  const bool live = ge < n_envs;  // wave-uniform; a dead wave still meets every barrier
+  const int64_t lane_id = live ? ge / a.envs : 0;
+  const _Float16* hp = a.hpack + lane_id * a.hpack_stride;
+
+  // this wave's A fragments of conv 11 (channel tile nt), requested first
+  h8 af[9];
+  auto load_a = [&](int conv) {
+#pragma unroll
+    for (int s = 0; s < 9; ++s) af[s] = *reinterpret_cast<const h8*>(hp + L.conv_h[conv] + ((s * 2 + nt) * 64 + ln) * 8);
+  };
+  if (live) load_a(11);
+  // X3 of the env (conv_kernel_h2<512, true>'s copy, xidx layout): tile i, pixel 16 i + (ln & 15), channels ch0 ..
+  h4 x[4];
+  const _Float16* x3 = reinterpret_cast<const _Float16*>(a.feat + (live ? ge : 0) * kFeat);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x[i] = live ? *reinterpret_cast<const h4*>(x3 + xidx<32>(16 * i + (ln & 15), ch0)) : h4{0, 0, 0, 0};
+  // the BN / bias rows of convs 11 .. 14 per env slot (conv_kernel_h2's table arithmetic): thread = (slot, index, ch)
+  {
+    const int ts = threadIdx.x >> 7, ti = (threadIdx.x >> 5) & 3, ch = threadIdx.x & 31, bidx = 11 + ti;
+    const int64_t gs = (int64_t)blockIdx.x * kS3Envs + ts;
+    float sc = 0.f, sh = 0.f, cb = 0.f;
+    if (gs < n_envs) {
+      const float* pk = a.pack + (gs / a.envs) * a.pack_stride;
+      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[bidx] + ch] : 0.f;
+      const float rv = a.bn_var ? a.bn_var[L.bn_stat[bidx] + ch] : 1.f;
+      sc = pk[L.bn_w[bidx] + ch] * (1.f / sqrtf(rv + kBnEps));
+      sh = pk[L.bn_b[bidx] + ch] - rm * sc;
+      cb = pk[L.conv_b[bidx] + ch];
+    }
+    tab[ts][0][ti][ch] = sc;
+    tab[ts][1][ti][ch] = sh;
+    tab[ts][2][ti][ch] = cb;
+  }
+  // zero both images of every slot (the borders stay zero: every later store is interior)
+  {
+    u32x4* z = reinterpret_cast<u32x4*>(&Tb[0][0][0]);
+    for (int i = threadIdx.x; i < kS3Envs * 2 * kS3T / 8; i += 512) z[i] = u32x4{0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+  // padded pixel of this lane's output pixel in tile i (8 x 8 image, pitch 10)
+  auto qout = [&](int i) {
+    const int m = 16 * i + (ln & 15);
+    return ((m >> 3) + 1) * 10 + (m & 7) + 1;
+  };
+  const float* sct = &tab[slot][0][0][0];
+  const float* sht = &tab[slot][1][0][0];
+  const float* cbt = &tab[slot][2][0][0];
+  // T[0] = relu(BN_11(X3)) (t_store_h3's arithmetic)
+  if (live) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const h2 lo = lo2(x[i]), hi = hi2(x[i]);
+      const int c = ch0;
+      const h4 t = to_h4(fma_mix_lo(lo, sct[c], sht[c]), fma_mix_hi(lo, sct[c + 1], sht[c + 1]),
+                         fma_mix_lo(hi, sct[c + 2], sht[c + 2]), fma_mix_hi(hi, sct[c + 3], sht[c + 3]));
+      *reinterpret_cast<h4*>(&Tb[slot][0][0] + tidx<32>(qout(i), ch0)) = relu_h4(t);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {  // convs 11, 12 (block 0), 13, 14 (block 1)
+    const _Float16* Tin = &Tb[slot][c & 1][0];
+    _Float16* Tout = &Tb[slot][(c + 1) & 1][0];
+    f32x4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (live) {
+#pragma unroll
+      for (int s = 0; s < 9; ++s) {  // tap s = (s / 3, s % 3), channel chunk g: conv_h2's K order
+        h8 b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = 16 * i + (ln & 15), q = ((m >> 3) + s / 3) * 10 + (m & 7) + s % 3;
+          b[i] = *reinterpret_cast<const h8*>(Tin + q * 32 + ((g ^ tsw<32>(q)) << 3));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s], b[i], acc[i], 0, 0, 0);
+      }
+      if (c < 3) load_a(12 + c);  // the next conv's fragments, in flight under this epilogue and barrier
+      const int i0 = c;           // this conv's table index (conv 11 + c)
+      if ((c & 1) == 0) {
+        // conv0 of a block: T <- relu(BN_{next}(. + b0)) (res_blocks_h2 epilogue0)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float o[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            o[k] = fmaf(acc[i][k] + cbt[i0 * 32 + ch0 + k], sct[(i0 + 1) * 32 + ch0 + k], sht[(i0 + 1) * 32 + ch0 + k]);
+          *reinterpret_cast<h4*>(Tout + tidx<32>(qout(i), ch0)) = relu_h4(to_h4(o[0], o[1], o[2], o[3]));
+        }
+      } else {
+        // conv1: x' = f16((v + b1) + x); block 0: T <- relu(BN_13(x')); block 1 (the last): features relu(x')
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const h2 xl = lo2(x[i]), xh = hi2(x[i]);
+          const float* b1 = cbt + i0 * 32 + ch0;
+          const h4 xn = to_h4(fma_mix_lo(xl, 1.f, acc[i][0] + b1[0]), fma_mix_hi(xl, 1.f, acc[i][1] + b1[1]),
+                              fma_mix_lo(xh, 1.f, acc[i][2] + b1[2]), fma_mix_hi(xh, 1.f, acc[i][3] + b1[3]));
+          if (c == 3) {
+            float* out = a.feat + ge * kFeat;
+            const int m = 16 * i + (ln & 15);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) out[(ch0 + k) * 64 + m] = relu((float)xn[k]);  // flatten (C, H, W)
+          } else {
+            x[i] = xn;
+            const h2 nl = lo2(xn), nh = hi2(xn);
+            const float* s2 = sct + (i0 + 1) * 32 + ch0;
+            const float* t2 = sht + (i0 + 1) * 32 + ch0;
+            const h4 t = to_h4(fma_mix_lo(nl, s2[0], t2[0]), fma_mix_hi(nl, s2[1], t2[1]), fma_mix_lo(nh, s2[2], t2[2]),
+                               fma_mix_hi(nh, s2[3], t2[3]));
+            *reinterpret_cast<h4*>(Tout + tidx<32>(qout(i), ch0)) = relu_h4(t);
+          }
+        }
+      }
+    }
+    if (c < 3) __syncthreads();  // T[c + 1 & 1] complete; T[c & 1] free for the next conv's output
+  }
+}
 
 // ---- core (fc + LSTM + head) with f16 weights ------------------------------------------------------
 template <int E, int MODE>

@@ -22,7 +22,8 @@ struct Context {
   int rollout_impl = 2; // FDR_ROLLOUT_AUTO
   int replay_gemm = 1;
   int core_mfma = 1;    // fp16 pair-form core step on MFMA (core_kernel_hpm); 0: the VALU form (core_kernel_hp)
-  int conv_h2 = 2;      // fp16 conv stack, two workgroups per CU: 2 = conv_kernel_h2<512> (default), 1 = <256>; 0: conv_kernel_h
+  int conv_h2 = 2;      // fp16 conv stack, two workgroups per CU: 2 = conv_kernel_h2<512> (default), 1 = <256>; 0: conv_kernel_h;
+                        // 3 = conv_kernel_h2<512> through the stage-3 entry + conv_s3_kernel (4 envs per workgroup)
   uint64_t* debug_clock = nullptr;
   impala::Profile* prof = nullptr;  // owned, created on first enable
 };
@@ -85,6 +86,8 @@ struct RolloutArgs {
   const float* M;
   const float* K;
   const float* s0;
+  float done_thr;  // > 0: terminating env, done when |s'[done_dim]| > done_thr (fdr_env_desc.done_threshold)
+  int done_dim;
   // trap env
   const uint8_t* walkable;
   int map_w, map_h, trap_start_col, trap_start_row;

@@ -554,7 +554,10 @@ __global__ __launch_bounds__(64 * kLanesPerBlock) void policy_forward_kernel(
 // Whole-episode rollout: fdr_rollout
 // ---------------------------------------------------------------------------------------------
 // FEAT bit 0: record visited observations (fdr_rollout_states); bit 1: Welford obs statistics;
-// bit 2: observation normalisation (obs_mean / obs_std given); bit 3: host-injected draws (u_inject)
+// bit 2: observation normalisation (obs_mean / obs_std given); bit 3: host-injected draws (u_inject);
+// bit 4: terminating synthetic env (fdr_env_desc.done_threshold): the lane's episode ends after the step whose
+// next state has |s'[done_dim]| > done_threshold (worker/agent.py:50-52: done -> break), or at T
+// (one lane per wave: the wave leaves its loop -- only these instances carry the test)
 // WIDE (synthetic env, few lanes: <= 2 waves per SIMD): a 256-VGPR budget instead of 128, so the
 // step's loop invariants (M / K rows, the head's W3 slice) stay in registers; the policy input and env
 // state cross lanes by v_readlane instead of an LDS round trip (NIN <= 8); a discrete env's candidate
@@ -619,6 +622,8 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
   const int T = a.T;
   const uint64_t key = a.key;
   const uint64_t ulane = (uint64_t)(a.lanes.lane_offset + lane);  // global lane id
+  constexpr bool kTerm = (FEAT & 16) != 0;
+  int nsteps = T;  // env.step calls of the episode (agent.py:47)
   double racc = 0.0;
   float eacc = 0.f;  // per-lane entropy sum (f32: T terms of O(1), rel. error ~1e-7 * sqrt(T))
   const int o = j & 15;
@@ -835,6 +840,12 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
             s = tanh_fast(pre);
           }
           racc += (double)s;  // lane 0 holds the reward s'[0]; other lanes' sums are discarded
+          if constexpr (kTerm) {  // done after this step: the reward and entropy of step t count (agent.py:46-52)
+            if (fabsf(readlane_f(s, a.done_dim)) > a.done_thr) {
+              nsteps = t + 1;
+              return;
+            }
+          }
         } else {
           // custom_envs/simple_trap_env: node.py:9-14, tile_map.py:11-23, environment.py:33-48
           const int prev_x = col * 7;
@@ -866,10 +877,10 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
     double r = racc;
     if (a.jiggle) r += (hash_ctr(key, ulane, kJiggleT, 15) & 1ull) ? 1e-12 : -1e-12;
     a.ret[lane] = r;
-    double e = esum / (double)T;
+    double e = esum / (double)nsteps;  // mean over the visited states (agent.py:60-65)
     if constexpr (!DISC) e += (double)NA * 1.4189385332046727;  // 0.5 + 0.5*ln(2*pi) per dim
     a.ent[lane] = e;
-    a.steps[lane] = T;
+    a.steps[lane] = nsteps;
   }
   if constexpr (FEAT & 2) {
     if (j < NIN) {
@@ -1355,7 +1366,9 @@ __device__ __forceinline__ void row_bcast_all(float v, float (&out)[N], std::int
 }
 
 // FEAT bit 0: record visited observations; bit 2: observation normalisation (bit 1, the Welford
-// statistics, runs on rollout_kernel)
+// statistics, runs on rollout_kernel); bit 4: terminating synthetic env -- each half keeps a done flag (wave-uniform
+// scalars alive0 / alive1): a finished half's steps still execute in lockstep with its partner but add nothing to
+// its reward, entropy or step count, and the wave leaves the loop when both halves are done
 template <int NIN, int NA, bool DISC, int FEAT>
 __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(RolloutArgs a) {
   using Lane = MlpPair<NIN, NA, DISC>;
@@ -1407,6 +1420,10 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
   const int o = t & 15;
   constexpr int kDrawsPerStep = DISC ? 1 : NA;
   constexpr int kStepsPerBatch = 32 / kDrawsPerStep;
+  constexpr bool kTerm = (FEAT & 16) != 0;
+  bool alive0 = true, alive1 = true;  // wave-uniform: half 0 / half 1 still stepping (kTerm)
+  int n0 = T, n1 = T;                 // their env.step counts
+  auto alive_me = [&]() { return hh ? alive1 : alive0; };
   float rbuf = 0.f;
   const int zbase = 4 * (32 * hh + (DISC ? 0 : (o < NA ? o : 0)));
   auto* sc = &scratch[wv];
@@ -1443,7 +1460,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     const float zt = __builtin_bit_cast(
         float, __builtin_amdgcn_ds_bpermute(zbase + 4 * kDrawsPerStep * tb, __builtin_bit_cast(int, rbuf)));
     if constexpr (FEAT & 1) {
-      if (t < NIN && active) a.states[((int64_t)lane * T + st) * NIN + t] = s;
+      if (t < NIN && active && (!kTerm || alive_me())) a.states[((int64_t)lane * T + st) * NIN + t] = s;
     }
     float pre = 0.f;
     xs[t] = t < NIN ? policy_input(s) : (t == NIN ? 1.f : 0.f);
@@ -1478,22 +1495,42 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
           act_d += cs <= target ? 1 : 0;
         }
       }
-      eacc -= (o < NA) ? disc_entropy_term(p, tot) : 0.f;
+      eacc -= (o < NA && (!kTerm || alive_me())) ? disc_entropy_term(p, tot) : 0.f;
       pre += mrow[NX + act_d];
     } else {
       const float th = tanh_act<Lane::kPre>(y);
       const float sd = std_from_tanh(dpp_mov<kDppRowShl + NA>(th));
-      eacc += __builtin_amdgcn_logf(sd);
+      if constexpr (kTerm)
+        eacc += alive_me() ? __builtin_amdgcn_logf(sd) : 0.f;
+      else
+        eacc += __builtin_amdgcn_logf(sd);
       const float act_c = det ? th : gauss_action(th, sd, zt);
       mark(3, act_c);
       dpp_tail<NA>(pre, act_c, kr);  // a[m] sits in thread m of both rows of the half
     }
     s = tanh_pre(pre);  // M, K stored x kPreScale
-    racc += (double)s;  // thread 0 of the half holds the reward s'[0]
     mark(4, s);
+    if constexpr (kTerm) {
+      racc += alive_me() ? (double)s : 0.0;  // thread 0 of the half holds the reward s'[0]
+      // done after this step (agent.py:50-52): the half's state element done_dim sits in its thread done_dim
+      const bool d0 = fabsf(readlane_f(s, a.done_dim)) > a.done_thr;
+      const bool d1 = fabsf(readlane_f(s, 32 + a.done_dim)) > a.done_thr;
+      if (alive0 && d0) {
+        alive0 = false;
+        n0 = st + 1;
+      }
+      if (alive1 && d1) {
+        alive1 = false;
+        n1 = st + 1;
+      }
+      return !alive0 && !alive1;
+    } else {
+      racc += (double)s;  // thread 0 of the half holds the reward s'[0]
+      return false;
+    }
   };
   if constexpr (!DISC) {
-    {
+    [&] {
       // continuous: the loop unrolled by the draw batch (5 steps for 6 dims); the draw is issued
       // unconditionally at the top of the unrolled body (det lanes ignore it), so it schedules into the
       // first step's waits instead of sitting behind a branch
@@ -1508,7 +1545,7 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
             asm volatile("" ::: "memory");
             mark(-1, s);
           }
-          step(st + k, k);
+          if (step(st + k, k)) return;  // kTerm: both halves done
         }
       }
       if (st < T) {
@@ -1516,16 +1553,16 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
         for (int k = 0; st + k < T; ++k) {
           asm volatile("" ::: "memory");
           mark(-1, s);
-          step(st + k, k);
+          if (step(st + k, k)) return;
         }
       }
-    }
+    }();
   } else {
     for (int st = 0; st < T; ++st) {
       asm volatile("" ::: "memory");
       mark(-1, s);
       if (!det && tb == 0) draw(st);
-      step(st, tb);
+      if (step(st, tb)) break;
       tb = tb + 1 == kStepsPerBatch ? 0 : tb + 1;
     }
   }
@@ -1542,10 +1579,11 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     double r = racc;
     if (a.jiggle) r += (hash_ctr(key, ulane, kJiggleT, 15) & 1ull) ? 1e-12 : -1e-12;
     a.ret[lane] = r;
-    double e = esum / (double)T;
+    const int nsteps = hh ? n1 : n0;
+    double e = esum / (double)nsteps;
     if constexpr (!DISC) e += (double)NA * 1.4189385332046727;
     a.ent[lane] = e;
-    a.steps[lane] = T;
+    a.steps[lane] = nsteps;
   }
 }
 
@@ -1582,15 +1620,22 @@ static void launch_feat(const RolloutArgs& args, dim3 grid, dim3 block, hipStrea
   const int feat = (args.states ? 1 : 0) | (args.os_mean ? 2 : 0) | (args.obs_mean ? 4 : 0);
 #define FDR_FEAT_CASE(F) \
   case F: hipLaunchKernelGGL((rollout_kernel<NIN, NA, DISC, ENV, F, WIDE>), grid, block, 0, stream, args); break;
+  // terminating env instances (bit 4) only for the synthetic env, so the fixed-length kernels stay as they are
+  const int term = (ENV == FDR_ENV_SYNTH && args.done_thr > 0.f) ? 16 : 0;
   if constexpr (!WIDE) {
     if (args.u_inject) {  // injected draws (never with the Welford statistics: fdr_rollout_ex refuses it)
-      switch (feat | 8) { FDR_FEAT_CASE(8) FDR_FEAT_CASE(9) FDR_FEAT_CASE(12) FDR_FEAT_CASE(13) }
+      switch (feat | 8 | term) {
+        FDR_FEAT_CASE(8) FDR_FEAT_CASE(9) FDR_FEAT_CASE(12) FDR_FEAT_CASE(13)
+        FDR_FEAT_CASE(24) FDR_FEAT_CASE(25) FDR_FEAT_CASE(28) FDR_FEAT_CASE(29)
+      }
       return;
     }
   }
-  switch (feat) {
+  switch (feat | term) {
     FDR_FEAT_CASE(0) FDR_FEAT_CASE(1) FDR_FEAT_CASE(2) FDR_FEAT_CASE(3)
     FDR_FEAT_CASE(4) FDR_FEAT_CASE(5) FDR_FEAT_CASE(6) FDR_FEAT_CASE(7)
+    FDR_FEAT_CASE(16) FDR_FEAT_CASE(17) FDR_FEAT_CASE(18) FDR_FEAT_CASE(19)
+    FDR_FEAT_CASE(20) FDR_FEAT_CASE(21) FDR_FEAT_CASE(22) FDR_FEAT_CASE(23)
   }
 #undef FDR_FEAT_CASE
 }
@@ -1603,17 +1648,18 @@ static void launch_pair(const RolloutArgs& args, int round_lanes, hipStream_t st
   const int quantum = 2 * kPairWaves;
   const int n_rounds = round_lanes > 0 ? (args.n_lanes + round_lanes - 1) / round_lanes : 1;
   const int per = ((args.n_lanes + n_rounds - 1) / n_rounds + quantum - 1) / quantum * quantum;
-  const int feat = (args.states ? 1 : 0) | (args.obs_mean ? 4 : 0);
+  const int feat = (args.states ? 1 : 0) | (args.obs_mean ? 4 : 0) | (args.done_thr > 0.f ? 16 : 0);
   RolloutArgs r = args;
   for (int base = 0; base < args.n_lanes; base += per) {
     r.lane_base = base;
     const dim3 grid((std::min(per, args.n_lanes - base) + quantum - 1) / quantum), block(64 * kPairWaves);
+#define FDR_PAIR_CASE(F) \
+  case F: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, F>), grid, block, 0, stream, r); break;
     switch (feat) {
-      case 0: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 0>), grid, block, 0, stream, r); break;
-      case 1: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 1>), grid, block, 0, stream, r); break;
-      case 4: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 4>), grid, block, 0, stream, r); break;
-      default: hipLaunchKernelGGL((rollout_pair_kernel<NIN, NA, DISC, 5>), grid, block, 0, stream, r); break;
+      FDR_PAIR_CASE(0) FDR_PAIR_CASE(1) FDR_PAIR_CASE(4) FDR_PAIR_CASE(5)
+      FDR_PAIR_CASE(16) FDR_PAIR_CASE(17) FDR_PAIR_CASE(20) FDR_PAIR_CASE(21)
     }
+#undef FDR_PAIR_CASE
   }
 }
 

@@ -10,6 +10,8 @@ into the rollout kernel, so an env here is a *descriptor*: device tensors + shap
       M = 0.9 G / ||G||_2, G ~ randn(obs, obs);  K = randn(obs, act) * 0.5 / sqrt(act);
       s0 = 0.5 randn(obs)   (one RandomState(env_seed) stream, in that order)
       s <- tanh(M s + K a)  (a one-hot for discrete actions);  reward = s[0];  done at t = T.
+  With ``done_threshold`` > 0 the env also TERMINATES (CartPole-style failure, fdr 0.4): done after the step whose
+  next state has |s[done_dim]| > done_threshold -- episodes then end before T, per lane (worker/agent.py:50-52).
 * ``TrapEnv`` -- custom_envs/simple_trap_env (environment.py:8-61) on the GPU, integer-exact:
   the reference's walkable bitmap ships as data (custom_envs/simple_trap_env/trap_map.npz).
 * ``StackedFrameEnv`` -- the same hash frames as 4 x 84 x 84 stacks for AtariPolicy (fdr_atari_rollout).
@@ -31,6 +33,11 @@ TRAP_MAP = os.path.join(_PKG, "custom_envs", "simple_trap_env", "trap_map.npz")
 SHAPES = {
     "cartpole": dict(obs_dim=4, act_dim=2, discrete=True, episode_len=500),     # BASELINE config 2
     "halfcheetah": dict(obs_dim=17, act_dim=6, discrete=False, episode_len=1000),  # config 3
+    # CartPole-shaped with failure termination (|s[1]| > 0.4, a pole-angle analogue), 500-step time limit
+    # (thresholds chosen so a random-init policy's episodes spread from a few steps to the limit)
+    "cartpole_term": dict(obs_dim=4, act_dim=2, discrete=True, episode_len=500, done_threshold=0.4, done_dim=1),
+    # Hopper-shaped (obs 11, act 3) with an "unhealthy" termination on state element 1, 1000-step limit
+    "hopper_term": dict(obs_dim=11, act_dim=3, discrete=False, episode_len=1000, done_threshold=0.5, done_dim=1),
 }
 
 
@@ -44,9 +51,13 @@ def synthetic_matrices(obs_dim, act_dim, env_seed=0):
 
 
 class SyntheticEnv(object):
-    def __init__(self, obs_dim, act_dim, discrete, episode_len, env_seed=0, device=None):
+    def __init__(self, obs_dim, act_dim, discrete, episode_len, env_seed=0, device=None, done_threshold=0.0,
+                 done_dim=0):
         self.obs_dim, self.act_dim, self.discrete = int(obs_dim), int(act_dim), bool(discrete)
         self.episode_len = int(episode_len)
+        self.done_threshold, self.done_dim = float(done_threshold), int(done_dim)
+        if self.done_threshold < 0 or not (0 <= self.done_dim < self.obs_dim):
+            raise ValueError("done_threshold must be >= 0 and done_dim in [0, obs_dim)")
         self.env_seed = env_seed
         self.M_host, self.K_host, self.s0_host = synthetic_matrices(obs_dim, act_dim, env_seed)
         self.device = torch.device(device) if device is not None else torch.device("cuda")
@@ -62,7 +73,13 @@ class SyntheticEnv(object):
 
     def desc(self):
         return _lib.EnvDesc(_lib.FDR_ENV_SYNTH, self.obs_dim, self.act_dim, self.episode_len,
-                            self.M.data_ptr(), self.K.data_ptr(), self.s0.data_ptr(), None, 0, 0)
+                            self.M.data_ptr(), self.K.data_ptr(), self.s0.data_ptr(), None, 0, 0,
+                            self.done_threshold, self.done_dim)
+
+    @property
+    def terminates(self):
+        """Episodes may end before episode_len (steps then vary per lane)."""
+        return self.done_threshold > 0
 
 
 class TrapEnv(object):
@@ -79,7 +96,7 @@ class TrapEnv(object):
 
     def desc(self):
         return _lib.EnvDesc(_lib.FDR_ENV_TRAP, 2, 9, self.episode_len, None, None, None,
-                            self.walkable.data_ptr(), self.map_w, self.map_h)
+                            self.walkable.data_ptr(), self.map_w, self.map_h, 0.0, 0)
 
 
 class FrameEnv(object):

@@ -48,7 +48,7 @@ class EnvDesc(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32),
                 ("episode_len", ctypes.c_int32), ("M", ctypes.c_void_p), ("K", ctypes.c_void_p),
                 ("s0", ctypes.c_void_p), ("walkable", ctypes.c_void_p), ("map_w", ctypes.c_int32),
-                ("map_h", ctypes.c_int32)]
+                ("map_h", ctypes.c_int32), ("done_threshold", ctypes.c_float), ("done_dim", ctypes.c_int32)]
 
 
 class LanesDesc(ctypes.Structure):

@@ -23,6 +23,7 @@ class Agent(object):
         self.env = env
         self.rng = np.random.RandomState(random_seed)
         self.random_seed = random_seed
+        self._ts_pending = []          # device step counts not yet folded in (add_timesteps)
         self.cumulative_timesteps = 0
         self.ts_limit = TS_LIMIT
         if env.episode_len > self.ts_limit:
@@ -32,6 +33,24 @@ class Agent(object):
         self.obs_stats_update_chance = obs_stats_update_chance
         self.saved_states = []
         self._episodes = 0
+
+    @property
+    def cumulative_timesteps(self):
+        """env.step calls so far (agent.py:55).  Device counts queued by add_timesteps are summed on read, so a
+        batched step over a terminating env needs no host sync to count its true steps."""
+        if self._ts_pending:
+            self._ts_host += int(torch.stack(self._ts_pending).sum().item())
+            self._ts_pending = []
+        return self._ts_host
+
+    @cumulative_timesteps.setter
+    def cumulative_timesteps(self, v):
+        self._ts_pending = []
+        self._ts_host = int(v)
+
+    def add_timesteps(self, steps_dev):
+        """Queue a device tensor of per-lane step counts (summed on the device now, read on demand)."""
+        self._ts_pending.append(steps_dev.sum(dtype=torch.int64))
 
     def obs_norm_tensors(self, mean, std):
         if not self.normalize_obs:

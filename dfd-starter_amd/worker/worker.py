@@ -193,7 +193,10 @@ class Worker(object):
         E = getattr(self.agent.env, "envs_per_lane", 1)
         if E > 1:
             lidx, sign = np.repeat(lidx, E), np.repeat(sign, E)
-        self.agent.cumulative_timesteps += int(len(lidx)) * self.agent.env.episode_len
+        if getattr(self.agent.env, "terminates", False):   # episodes end before T: count the steps taken
+            self.agent.add_timesteps(res.timesteps)
+        else:
+            self.agent.cumulative_timesteps += int(len(lidx)) * self.agent.env.episode_len
         nov = self.lane_novelty(idx_d, sign_d) if novelty else None
         b = FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, lidx, sign, self.epoch,
                     lanes_per_dir=lpd * E, novelty=nov)

@@ -65,6 +65,11 @@ typedef struct fdr_env_desc {
   const float* s0;     /* SYNTH: [obs_dim] reset state */
   const uint8_t* walkable; /* TRAP: [map_h, map_w] 1 = walkable (tile_map.py:40) */
   int32_t map_w, map_h;
+  /* SYNTH (fdr 0.4): > 0 = a terminating env -- an episode ends after the step whose next state has
+     |s'[done_dim]| > done_threshold (CartPole-style failure; worker/agent.py:50-52: done -> reset, break), or at
+     episode_len (the time limit); steps / ret / ent then cover the steps taken.  0 = fixed-length episodes. */
+  float done_threshold;
+  int32_t done_dim;
 } fdr_env_desc;
 
 /* Where each lane's parameter vector comes from:
@@ -91,7 +96,7 @@ typedef struct fdr_lanes_desc {
  * is not shared across threads without external locking; two contexts -- on one device or on two -- are
  * independent.  ctx = NULL selects the process-wide default context (device-agnostic; FDR_ROLLOUT in the
  * environment sets its initial rollout selection, and new contexts copy it). */
-const char* fdr_version(void);
+const char* fdr_version(void); /* "fdr 0.4 gfx950" (0.4: fdr_env_desc.done_threshold / done_dim) */
 const char* fdr_last_error(void);
 typedef struct fdr_ctx fdr_ctx;
 int fdr_ctx_create(int device, fdr_ctx** out);
@@ -106,8 +111,10 @@ int fdr_ctx_set_replay_gemm(fdr_ctx* ctx, int32_t on);     /* see fdr_impala_set
 int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on);
 /* fp16 Impala conv stack (rollout, forward, strategies), identical features in every mode:
    2 (default) = conv_kernel_h2<512>: 8 waves, 80 KiB LDS, 128 VGPRs, two workgroups per CU;
-   1 = conv_kernel_h2<256>: 4 waves, two workgroups per CU;  0 = conv_kernel_h: 8 waves, 145 KiB LDS, one per CU.
-   Default context: FDR_CONV_H2 (0 / 1 / 2) or 2 */
+   1 = conv_kernel_h2<256>: 4 waves, two workgroups per CU;  0 = conv_kernel_h: 8 waves, 145 KiB LDS, one per CU;
+   3 = conv_kernel_h2<512> through the stage-3 entry, then the stage-3 residual blocks of four envs per workgroup
+   (conv_s3_kernel; features bit-identical to 2).
+   Default context: FDR_CONV_H2 (0 / 1 / 2 / 3) or 2 */
 int fdr_ctx_set_conv_h2(fdr_ctx* ctx, int32_t on);
 int fdr_ctx_impala_profile(fdr_ctx* ctx, int32_t enable);  /* see fdr_impala_profile */
 int fdr_ctx_impala_profile_read(fdr_ctx* ctx, double* ms);

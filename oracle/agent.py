@@ -69,11 +69,13 @@ def evaluate_lanes(kind, n_in, n_act, theta, table, idx, sign, sigma, env, seed,
     T = env.episode_len
     stats = [obs_stats.Welford(n_in) for _ in range(L)] if obs_chance is not None else None
     states = np.zeros((L, T, n_in), np.float32) if record_states else None
+    alive = np.ones(L, bool)
+    steps = np.zeros(L, np.int64)
     for t in range(T):
         if record_states:
-            states[:, t] = obs
+            states[alive, t] = obs[alive]
         if stats is not None:   # worker/agent.py:37-39 (raw obs, before normalisation)
-            coin = obs_stats.lane_coins(seed, lanes, t, obs_chance)
+            coin = obs_stats.lane_coins(seed, lanes, t, obs_chance) & alive
             for l in np.nonzero(coin)[0]:
                 stats[l].update(obs[l])
         x = obs
@@ -84,18 +86,25 @@ def evaluate_lanes(kind, n_in, n_act, theta, table, idx, sign, sigma, env, seed,
             u = crng.uniform(seed, lanes, t, 0)
             act = np.array([int(np.argmax(p[l])) if det[l] else pol.categorical_inverse_cdf(p[l], u[l])
                             for l in range(L)])
-            ent += pol.categorical_entropy(p)
+            step_ent = pol.categorical_entropy(p)
         else:
             mean, std = pol.lanes_forward(kind, n_in, n_act, thetas, x)
             z = crng.normal(seed, lanes[:, None], t, np.arange(n_act, dtype=np.uint64)[None, :])
             act = np.where(det[:, None], mean, (mean + std * z).astype(np.float32)).astype(np.float32)
-            ent += pol.normal_entropy(std)
+            step_ent = pol.normal_entropy(std)
         obs, r = env.step(act)
-        ret += r
-    ent /= T
+        # a terminating env (worker/agent.py:50-52): a lane's episode ends after its failing step -- that step's
+        # reward and entropy count, later steps of the batch do not
+        ret += np.where(alive, r, 0.0)
+        ent += np.where(alive, step_ent, 0.0)
+        steps += alive
+        alive &= ~env.failed()
+        if not alive.any():
+            break
+    ent /= steps
     if jiggle:
         ret += crng.jiggle(seed, lanes)
-    out = (ret, ent, np.full(L, T, dtype=np.int32), norm2)
+    out = (ret, ent, steps.astype(np.int32), norm2)
     if stats is not None:
         out = out + (stats,)
     if record_states:

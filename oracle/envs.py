@@ -11,6 +11,7 @@ linear-tanh system with the real observation/action shapes:
     s0 = 0.5 * randn(obs)                                     (same stream)
     step(a):  u = K[:, a] (discrete)  |  K @ a (continuous)
               s <- tanh(M s + u)   (f32);  reward = s[0];  t += 1;  done = t >= T
+              (terminating variant, done_threshold > 0:  done also when |s[done_dim]| > done_threshold)
 
 The per-step contract (obs returned after the step, reward, done, reset on done) is that of a
 gym env as consumed by worker/agent.py:35-52.
@@ -43,7 +44,8 @@ def synthetic_params(obs_dim, act_dim, env_seed=0):
 class SyntheticEnv(object):
     """One env instance (gym-style API) -- used by the per-lane CPU loop."""
 
-    def __init__(self, obs_dim, act_dim, discrete, episode_len, env_seed=0):
+    def __init__(self, obs_dim, act_dim, discrete, episode_len, env_seed=0, done_threshold=0.0, done_dim=0):
+        self.done_threshold, self.done_dim = float(done_threshold), int(done_dim)
         self.obs_dim = obs_dim
         self.act_dim = act_dim
         self.discrete = discrete
@@ -65,13 +67,15 @@ class SyntheticEnv(object):
             u = self.K @ a
         self.s = np.tanh(self.M @ self.s + u).astype(np.float32)
         self.t += 1
-        return self.s.copy(), float(self.s[0]), self.t >= self.episode_len, {}
+        done = self.t >= self.episode_len or (self.done_threshold > 0 and abs(self.s[self.done_dim]) > self.done_threshold)
+        return self.s.copy(), float(self.s[0]), bool(done), {}
 
 
 class BatchedSyntheticEnv(object):
     """Same dynamics over L lanes at once (numpy), for batched parity checks."""
 
-    def __init__(self, obs_dim, act_dim, discrete, episode_len, n_lanes, env_seed=0):
+    def __init__(self, obs_dim, act_dim, discrete, episode_len, n_lanes, env_seed=0, done_threshold=0.0, done_dim=0):
+        self.done_threshold, self.done_dim = float(done_threshold), int(done_dim)
         self.obs_dim, self.act_dim, self.discrete = obs_dim, act_dim, discrete
         self.episode_len = episode_len
         self.M, self.K, self.s0 = synthetic_params(obs_dim, act_dim, env_seed)
@@ -90,6 +94,12 @@ class BatchedSyntheticEnv(object):
         pre = np.einsum("ok,lk->lo", self.M, self.s).astype(np.float32) + u
         self.s = np.tanh(pre).astype(np.float32)
         return self.s.copy(), self.s[:, 0].astype(np.float64)
+
+    def failed(self):
+        """Per lane: the state after the last step ends the episode (terminating variant; the T limit aside)."""
+        if self.done_threshold <= 0:
+            return np.zeros(self.n, bool)
+        return np.abs(self.s[:, self.done_dim]) > self.done_threshold
 
 
 def load_trap_map(path=TRAP_MAP_PATH):

@@ -403,6 +403,42 @@ def g7_worker_synthetic():
     save("g7_worker_synthetic.npz", **out)
 
 
+TERM_ENVS = {"cartpole_term": (("discrete", 4, 2), 500, 0.4, 1), "hopper_term": (("mujoco", 11, 3), 1000, 0.5, 1)}
+
+
+def g13_worker_terminating():
+    """Reference Worker/Agent on TERMINATING synthetic envs (episodes end before T: worker/agent.py:35-52) with
+    injected draws, as G7: per-episode steps, rewards over the steps taken, entropy over the visited states, and
+    the Agent's cumulative_timesteps (agent.py:55).  The envs are the build's (oracle/envs.py, done_threshold)."""
+    out = {}
+    for name, ((kind, n_in, n_act), T, thr, dim) in TERM_ENVS.items():
+        env = SyntheticEnv(n_in, n_act, kind == "discrete", T, env_seed=0, done_threshold=thr, done_dim=dim)
+        pol = make_policy(kind, n_in, n_act, 124)
+        P = pol.num_params
+        cls = DiscretePolicy if kind == "discrete" else MujocoPolicy
+        inj = _InjectedDiscrete(31) if kind == "discrete" else _InjectedNormal(31)
+        orig = cls.get_action
+        cls.get_action = lambda self, x, deterministic=False: inj(self, x, deterministic)
+        try:
+            table = SharedNoiseTable(2 ** 22, P, random_seed=124)
+            agent = Agent(pol, env, random_seed=11)
+            handler = StrategyHandler(pol, math_helpers.categorical_tvd)
+            worker = Worker(pol, agent, table, handler, sigma=0.02, eval_prob=0.25, random_seed=3)
+            rets = worker.collect_returns(12)
+        finally:
+            cls.get_action = orig
+        out[name + "_theta"] = pol.get_trainable_flat().copy()
+        out[name + "_reward"] = np.array([r.reward for r in rets])
+        out[name + "_entropy"] = np.array([r.entropy for r in rets])
+        out[name + "_timesteps"] = np.array([r.timesteps for r in rets])
+        out[name + "_is_eval"] = np.array([r.is_eval for r in rets])
+        out[name + "_idx"] = np.array([int(r.encoded_noise) for r in rets])
+        out[name + "_T"] = np.array(T)
+        out[name + "_done"] = np.array([thr, dim], np.float64)
+        out[name + "_cumulative_timesteps"] = np.array(agent.cumulative_timesteps)
+    save("g13_worker_terminating.npz", **out)
+
+
 def g8_impala():
     """G3 for the ImpalaCNN (policies/impala.py:48-186): reference module, B=1 sequences.
 
@@ -672,7 +708,7 @@ def g12_impala(patched=True):
 
 
 GENERATORS = {"g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
-              "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g8": g8_impala,
+              "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g13": g13_worker_terminating, "g8": g8_impala,
               "g9": g9_novelty, "g10": g10_welford, "g11": g11_atari, "g12": g12_history,
               "g12i": g12_impala, "g12iu": lambda: g12_impala(patched=False)}
 

@@ -37,7 +37,7 @@ def test_version_and_workspace_queries():
     assert _lib.lib.fdr_fd_grad_workspace_bytes(2048, 6092) >= 6092 * 8
     assert _lib.lib.fdr_dsgd_workspace_bytes(6092) > 0
     # the MOMENTS output length is queryable and checked (fdr 0.3; it was 2P + 3 before)
-    assert _lib.version().startswith("fdr 0.3")
+    assert _lib.version().startswith("fdr 0.4")   # 0.4: fdr_env_desc.done_threshold / done_dim
     assert _lib.lib.fdr_fd_grad_fused_out_len(_lib.FDR_WEIGHT_ZSCORE, 6092, 4096) == 6092
     assert _lib.lib.fdr_fd_grad_fused_out_len(_lib.FDR_WEIGHT_MOMENTS, 6092, 4096) == 2 * 6092 + 1 + 4096
     assert _lib.lib.fdr_fd_grad_fused_out_len(_lib.FDR_WEIGHT_MOMENTS, 6092, 0) == -1

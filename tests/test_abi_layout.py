@@ -156,4 +156,4 @@ def test_parser_sees_known_shapes():
     assert protos["fdr_version"] == ("P", [])
     assert protos["fdr_fd_grad_fused_out_len"] == ("i64", ["i32", "i64", "i32"])
     assert protos["fdr_rollout"][1][:6] == ["P", "P", "P", "P", "i32", "u64"]
-    assert header_structs()["fdr_env_desc"][-2:] == ["map_w", "map_h"]
+    assert header_structs()["fdr_env_desc"][-4:] == ["map_w", "map_h", "done_threshold", "done_dim"]

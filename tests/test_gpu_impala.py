@@ -445,7 +445,7 @@ def test_fp16_pair_default_path_whole_episode_vs_f32_oracle(engine, table, core_
 
 
 def test_conv_h2_matches_conv_h(engine, table):
-    """conv_kernel_h2<256> (80 KiB LDS, two workgroups per CU; banded entry convs, single-buffered
+    """(Modes 0 / 1 / 2 / 3 of fdr_ctx_set_conv_h2.)  VERDICT r2 item 4: conv_kernel_h2<256> (80 KiB LDS, two workgroups per CU; banded entry convs, single-buffered
     residual blocks, 4 waves) computes every conv output with conv_kernel_h's fragments, K order and f32 epilogues,
     so its outputs are BITWISE equal to conv_kernel_h's: forward features / probs / LSTM state (13 envs, ragged over
     the 8 XCD slots), a recorded fp16 pair rollout with the entropy replay, and strategies.  The default
@@ -471,9 +471,9 @@ def test_conv_h2_matches_conv_h(engine, table):
     ctx = engine.context()
     import os
     env = os.environ.get("FDR_CONV_H2", "2")   # the default context's setting
-    prior = 0 if env == "0" else (1 if env == "1" else 2)
+    prior = {"0": 0, "1": 1, "3": 3}.get(env, 2)
     try:
-        for on in (0, 1, 2):
+        for on in (0, 1, 2, 3):
             ctx.set_conv_h2(on)
             h = torch.zeros(n, 256, device="cuda")
             c = torch.zeros(n, 256, device="cuda")
@@ -492,6 +492,11 @@ def test_conv_h2_matches_conv_h(engine, table):
     assert np.abs(res[1][1]).max() > 0 and np.all(np.isfinite(res[1][1]))
     for a, b in zip(res[0], res[1]):
         np.testing.assert_array_equal(a, b)
+    # mode 3 (r11): conv_kernel_h2<512> through the stage-3 entry + conv_s3_kernel (four envs per
+    # workgroup; 13 forward envs, 24 rollout envs and 30 strategy envs leave dead env slots) -- the same products, K
+    # order and epilogue arithmetic as mode 2: bitwise equal, recorded rollout and strategies included
+    for i, (a, b) in enumerate(zip(res[2], res[3])):
+        np.testing.assert_array_equal(a, b, err_msg=str(i))
     # conv_kernel_h2<512> runs the tap-8 remainder as a chained K = 32 MFMA (FDR_R32): the same products, summed in
     # another order -- forward probabilities / features / LSTM state and strategies within rounding of conv_kernel_h
     # (the recorded rollout's sampled actions may then differ; its parity is the oracle tests' subject)
