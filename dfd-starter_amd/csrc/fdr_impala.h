@@ -221,6 +221,7 @@ __global__ void conv_kernel_h(Layout L, StepArgs a);
 // SPLIT3: stop after the stage-3 entry (X3 into the feature slot) -- conv_s3_kernel finishes the stack, 4 envs per WG
 template <int NTH, bool SPLIT3>
 __global__ void conv_kernel_h2(Layout L, StepArgs a);
+template <bool SHARED>  // SHARED: the 4 env slots of a workgroup are one lane (envs % 4 == 0)
 __global__ void conv_s3_kernel(Layout L, StepArgs a);
 constexpr int kS3EnvsPerWG = 4;  // conv_s3_kernel: envs per workgroup
 template <int E, int MODE>

@@ -1351,8 +1351,11 @@ static void launch_conv_h(int h2, int grid, const Layout& L, const StepArgs& a, 
   if (h2 == 3) {
     hipLaunchKernelGGL((conv_kernel_h2<512, true>), dim3(grid), dim3(512), 0, stream, L, a);
     const int64_t n_envs = (int64_t)a.n_lanes * a.envs;
-    hipLaunchKernelGGL(conv_s3_kernel, dim3((unsigned)((n_envs + kS3EnvsPerWG - 1) / kS3EnvsPerWG)), dim3(512), 0, stream,
-                       L, a);
+    const dim3 g3((unsigned)((n_envs + kS3EnvsPerWG - 1) / kS3EnvsPerWG));
+    if (a.envs % kS3EnvsPerWG == 0)
+      hipLaunchKernelGGL(conv_s3_kernel<true>, g3, dim3(512), 0, stream, L, a);
+    else
+      hipLaunchKernelGGL(conv_s3_kernel<false>, g3, dim3(512), 0, stream, L, a);
   } else if (h2 == 2)
     hipLaunchKernelGGL((conv_kernel_h2<512, false>), dim3(grid), dim3(512), 0, stream, L, a);
   else if (h2)

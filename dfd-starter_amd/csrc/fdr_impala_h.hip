@@ -1456,19 +1456,30 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   // written.  The weight block of the first residual conv is issued now and committed in the first pool phase.
   constexpr int kTabIt = (kBnTab + NTH - 1) / NTH;
   float rm[kTabIt], rv[kTabIt], bnw[kTabIt], bnb[kTabIt], cbv[kTabIt];
+  // Branch-free (r11): every load unconditional from an in-bounds address, the unused values selected away after.
+  // A conditional load ends its basic block with s_waitcnt vmcnt(0), and the layout offsets were read per lane from
+  // the kernel argument block -- together 4-5 serialised global round trips in this phase (r11 probe of the same
+  // table in conv_s3_kernel: 3.3-3.9 K clocks); the offsets are now scalar loads (the wave's two table rows).
+  {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hi = (threadIdx.x >> 5) & 1;
+    const float* bmp = a.bn_mean ? a.bn_mean : pk;  // a valid address either way
+    const float* bvp = a.bn_var ? a.bn_var : pk;
 #pragma unroll
-  for (int k = 0; k < kTabIt; ++k) {
-    const int bi = threadIdx.x + k * NTH, bidx = bi >> 5, bch = bi & 31;
-    const bool has_bn = bi < kBnTab && bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
-    const bool has_cb = bi < kBnTab && bch < (bidx < 5 ? 16 : 32);
-    rm[k] = 0.f, rv[k] = 1.f, bnw[k] = 0.f, bnb[k] = 0.f, cbv[k] = 0.f;
-    if (has_bn) {
-      if (a.bn_mean) rm[k] = a.bn_mean[L.bn_stat[bidx] + bch];
-      if (a.bn_var) rv[k] = a.bn_var[L.bn_stat[bidx] + bch];
-      bnw[k] = pk[L.bn_w[bidx] + bch];
-      bnb[k] = pk[L.bn_b[bidx] + bch];
+    for (int k = 0; k < kTabIt; ++k) {
+      const int bi = threadIdx.x + k * NTH, bidx = bi >> 5, bch = bi & 31;
+      const int r0 = min((wv * 64 + k * NTH) >> 5, kConvs - 1), r1 = min(r0 + 1, kConvs - 1);  // wave-uniform rows
+      auto pick = [&](const int32_t* arr) { return hi ? arr[r1] : arr[r0]; };
+      const bool has_bn = bi < kBnTab && bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
+      const bool has_cb = bi < kBnTab && bch < (bidx < 5 ? 16 : 32);
+      const int so = pick(L.bn_stat) + bch;
+      const float m_ = bmp[so], v_ = bvp[so], w_ = pk[pick(L.bn_w) + bch], b_ = pk[pick(L.bn_b) + bch],
+                  c_ = pk[pick(L.conv_b) + bch];
+      rm[k] = has_bn && a.bn_mean ? m_ : 0.f;
+      rv[k] = has_bn && a.bn_var ? v_ : 1.f;
+      bnw[k] = has_bn ? w_ : 0.f;
+      bnb[k] = has_bn ? b_ : 0.f;
+      cbv[k] = has_cb ? c_ : 0.f;
     }
-    if (has_cb) cbv[k] = pk[L.conv_b[bidx] + bch];
   }
   h8 af3[KSteps<3>::N][1];
   h8 af3n[2];  // (h3 entries: conv_band_s1's K order)
@@ -1481,7 +1492,8 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   float fsc[3], fsh[3];  // BN2d(3) of the frame, per thread (table entries 0..2)
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
-    const float m = a.bn_mean ? a.bn_mean[L.bn_stat[0] + c] : 0.f, v = a.bn_var ? a.bn_var[L.bn_stat[0] + c] : 1.f;
+    const float m_ = (a.bn_mean ? a.bn_mean : pk)[L.bn_stat[0] + c], v_ = (a.bn_var ? a.bn_var : pk)[L.bn_stat[0] + c];
+    const float m = a.bn_mean ? m_ : 0.f, v = a.bn_var ? v_ : 1.f;
     fsc[c] = pk[L.bn_w[0] + c] * (1.f / sqrtf(v + kBnEps));
     fsh[c] = pk[L.bn_b[0] + c] - m * fsc[c];
   }
@@ -1718,55 +1730,119 @@ template __global__ void conv_kernel_h2<512, true>(Layout, StepArgs);
 constexpr int kS3Envs = kS3EnvsPerWG;
 constexpr int kS3T = 10 * 10 * 32;  // halves of one padded 8 x 8 x 32 image
 
+// Wave map (r11b): wave w = (env slot w / 2, pixel-tile pair w % 2) computes BOTH channel tiles of its two pixel tiles,
+// so each B fragment read from LDS feeds two MFMAs (the first form, one channel tile x four pixel tiles per wave,
+// read 1 KB of LDS per MFMA: the LDS port, not the MFMA pipe, bounded its convs -- 4.3 K clocks per conv against
+// 1.15 K of MFMA issue, phase clocks r11a).  A fragments of both channel tiles in registers (72 VGPRs).
+// SHARED (envs per lane a multiple of 4: the four env slots are ONE lane, one theta'): each conv's 18 KB weight block
+// is copied once per workgroup into LDS by global_load_lds_dwordx4 (no staging registers: 18 wave-instructions of 64 x
+// 16 B, issued while the previous conv runs, waited for before its closing barrier); otherwise every wave loads its
+// fragments from the half pack.
+template <bool SHARED>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv_s3_kernel(Layout L, StepArgs a) {
+  constexpr int WH = kBlockHalves<32, 2>;  // one 32 -> 32 conv's fragments, [k-step][channel tile][lane][8]
   __shared__ __attribute__((aligned(16))) _Float16 Tb[kS3Envs][2][kS3T];
   __shared__ float tab[kS3Envs][3][4][32];  // [slot][scale, shift, conv bias][index 11 .. 14][channel]
+  __shared__ __attribute__((aligned(16))) _Float16 WB[SHARED ? WH : 8];
   const int64_t n_envs = (int64_t)a.n_lanes * a.envs;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
-  const int slot = wave >> 1, nt = wave & 1, g = ln >> 4, ch0 = 16 * nt + 4 * g;
+  const int slot = wave >> 1, hp2 = wave & 1, g = ln >> 4;
   const int64_t ge = (int64_t)blockIdx.x * kS3Envs + slot;
   const bool live = ge < n_envs;  // wave-uniform; a dead wave still meets every barrier
   const int64_t lane_id = live ? ge / a.envs : 0;
-  const _Float16* hp = a.hpack + lane_id * a.hpack_stride;
+  const _Float16* hp = a.hpack + (SHARED ? (int64_t)blockIdx.x * kS3Envs / a.envs : lane_id) * a.hpack_stride;
+  FDR_STAMP(a, 100);  // phase clocks of workgroup 0 (tools/impala_phases_h2.py --mode 3): 100 .. 110
 
-  // this wave's A fragments of conv 11 (channel tile nt), requested first
-  h8 af[9];
-  auto load_a = [&](int conv) {
+  // this wave's A fragments (both channel tiles), from the pack or the workgroup's LDS copy
+  h8 af[9][2];
+  auto load_a = [&](const _Float16* src) {
 #pragma unroll
-    for (int s = 0; s < 9; ++s) af[s] = *reinterpret_cast<const h8*>(hp + L.conv_h[conv] + ((s * 2 + nt) * 64 + ln) * 8);
+    for (int s = 0; s < 9; ++s)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) af[s][nt] = *reinterpret_cast<const h8*>(src + ((s * 2 + nt) * 64 + ln) * 8);
   };
-  if (live) load_a(11);
-  // X3 of the env (conv_kernel_h2<512, true>'s copy, xidx layout): tile i, pixel 16 i + (ln & 15), channels ch0 ..
-  h4 x[4];
+  // WB <- conv `conv`'s block straight from global memory (LDS DMA): wave w copies 1 KB pieces w, w + 8, w + 16
+  auto copy_block = [&](int conv) {
+    typedef __attribute__((address_space(1))) const void gptr_t;
+    typedef __attribute__((address_space(3))) void lptr_t;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int piece = wave + 8 * k;
+      if (piece < WH / 512)
+        __builtin_amdgcn_global_load_lds((gptr_t*)(hp + L.conv_h[conv] + (piece * 64 + ln) * 8), (lptr_t*)(WB + piece * 512),
+                                         16, 0, 0);
+    }
+  };
+#ifdef FDR_S3_PROBE  // diagnostics build: each prologue load group waited for and stamped (dbg[112..])
+#define FDR_S3_P(k)                 \
+  do {                              \
+    __builtin_amdgcn_s_waitcnt(0);  \
+    FDR_STAMP(a, k);                \
+  } while (0)
+#else
+#define FDR_S3_P(k) \
+  do {              \
+  } while (0)
+#endif
+  FDR_S3_P(112);
+  if constexpr (SHARED) {
+    copy_block(11);
+    FDR_S3_P(113);
+  } else if (live) {
+    load_a(hp + L.conv_h[11]);
+  }
+  // X3 of the env (conv_kernel_h2<512, true>'s copy, xidx layout): tile 2 hp2 + j, pixel 16 tile + (ln & 15), channels
+  // 16 nt + 4 g ..
+  h4 x[2][2];
   const _Float16* x3 = reinterpret_cast<const _Float16*>(a.feat + (live ? ge : 0) * kFeat);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) x[i] = live ? *reinterpret_cast<const h4*>(x3 + xidx<32>(16 * i + (ln & 15), ch0)) : h4{0, 0, 0, 0};
-  // the BN / bias rows of convs 11 .. 14 per env slot (conv_kernel_h2's table arithmetic): thread = (slot, index, ch)
-  {
-    const int ts = threadIdx.x >> 7, ti = (threadIdx.x >> 5) & 3, ch = threadIdx.x & 31, bidx = 11 + ti;
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt)
+      x[j][nt] = live ? *reinterpret_cast<const h4*>(x3 + xidx<32>(16 * (2 * hp2 + j) + (ln & 15), 16 * nt + 4 * g))
+                      : h4{0, 0, 0, 0};
+  FDR_S3_P(114);
+  // the BN / bias rows of convs 11 .. 14 per env slot (conv_kernel_h2's table arithmetic): thread (slot, ch) < 128,
+  // the four indices unrolled (compile-time offsets into the layout: scalar loads)
+  if (threadIdx.x < 128) {
+    const int ts = threadIdx.x >> 5, ch = threadIdx.x & 31;
     const int64_t gs = (int64_t)blockIdx.x * kS3Envs + ts;
-    float sc = 0.f, sh = 0.f, cb = 0.f;
-    if (gs < n_envs) {
-      const float* pk = a.pack + (gs / a.envs) * a.pack_stride;
-      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[bidx] + ch] : 0.f;
-      const float rv = a.bn_var ? a.bn_var[L.bn_stat[bidx] + ch] : 1.f;
-      sc = pk[L.bn_w[bidx] + ch] * (1.f / sqrtf(rv + kBnEps));
-      sh = pk[L.bn_b[bidx] + ch] - rm * sc;
-      cb = pk[L.conv_b[bidx] + ch];
+    const float* pk = a.pack + (gs < n_envs ? gs / a.envs : 0) * a.pack_stride;
+    const float* bmp = a.bn_mean ? a.bn_mean : pk;  // unconditional loads (kernel A's table note)
+    const float* bvp = a.bn_var ? a.bn_var : pk;
+    float rm_[4], rv_[4], w_[4], b_[4], c_[4];
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti) {
+      const int bidx = 11 + ti;
+      rm_[ti] = bmp[L.bn_stat[bidx] + ch];
+      rv_[ti] = bvp[L.bn_stat[bidx] + ch];
+      w_[ti] = pk[L.bn_w[bidx] + ch];
+      b_[ti] = pk[L.bn_b[bidx] + ch];
+      c_[ti] = pk[L.conv_b[bidx] + ch];
     }
-    tab[ts][0][ti][ch] = sc;
-    tab[ts][1][ti][ch] = sh;
-    tab[ts][2][ti][ch] = cb;
+#pragma unroll
+    for (int ti = 0; ti < 4; ++ti) {
+      const float rm = a.bn_mean ? rm_[ti] : 0.f, rv = a.bn_var ? rv_[ti] : 1.f;
+      const float sc = w_[ti] * (1.f / sqrtf(rv + kBnEps));
+      const bool ok = gs < n_envs;
+      tab[ts][0][ti][ch] = ok ? sc : 0.f;
+      tab[ts][1][ti][ch] = ok ? b_[ti] - rm * sc : 0.f;
+      tab[ts][2][ti][ch] = ok ? c_[ti] : 0.f;
+    }
   }
+  FDR_S3_P(115);
   // zero both images of every slot (the borders stay zero: every later store is interior)
   {
     u32x4* z = reinterpret_cast<u32x4*>(&Tb[0][0][0]);
     for (int i = threadIdx.x; i < kS3Envs * 2 * kS3T / 8; i += 512) z[i] = u32x4{0u, 0u, 0u, 0u};
   }
+  FDR_S3_P(116);
+  if constexpr (SHARED) __builtin_amdgcn_s_waitcnt(0);  // the LDS DMA of conv 11's block has landed
   __syncthreads();
-  // padded pixel of this lane's output pixel in tile i (8 x 8 image, pitch 10)
-  auto qout = [&](int i) {
-    const int m = 16 * i + (ln & 15);
+  FDR_STAMP(a, 101);
+  // padded pixel of this lane's output pixel in its tile j (8 x 8 image, pitch 10)
+  auto qout = [&](int j) {
+    const int m = 16 * (2 * hp2 + j) + (ln & 15);
     return ((m >> 3) + 1) * 10 + (m & 7) + 1;
   };
   const float* sct = &tab[slot][0][0][0];
@@ -1775,74 +1851,94 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void c
   // T[0] = relu(BN_11(X3)) (t_store_h3's arithmetic)
   if (live) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const h2 lo = lo2(x[i]), hi = hi2(x[i]);
-      const int c = ch0;
-      const h4 t = to_h4(fma_mix_lo(lo, sct[c], sht[c]), fma_mix_hi(lo, sct[c + 1], sht[c + 1]),
-                         fma_mix_lo(hi, sct[c + 2], sht[c + 2]), fma_mix_hi(hi, sct[c + 3], sht[c + 3]));
-      *reinterpret_cast<h4*>(&Tb[slot][0][0] + tidx<32>(qout(i), ch0)) = relu_h4(t);
-    }
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        const int c = 16 * nt + 4 * g;
+        const h2 lo = lo2(x[j][nt]), hi = hi2(x[j][nt]);
+        const h4 t = to_h4(fma_mix_lo(lo, sct[c], sht[c]), fma_mix_hi(lo, sct[c + 1], sht[c + 1]),
+                           fma_mix_lo(hi, sct[c + 2], sht[c + 2]), fma_mix_hi(hi, sct[c + 3], sht[c + 3]));
+        *reinterpret_cast<h4*>(&Tb[slot][0][0] + tidx<32>(qout(j), c)) = relu_h4(t);
+      }
   }
   __syncthreads();
+  FDR_STAMP(a, 102);
 #pragma unroll
   for (int c = 0; c < 4; ++c) {  // convs 11, 12 (block 0), 13, 14 (block 1)
     const _Float16* Tin = &Tb[slot][c & 1][0];
     _Float16* Tout = &Tb[slot][(c + 1) & 1][0];
-    f32x4 acc[4];
+    if constexpr (SHARED) {
+      load_a(WB);        // WB = conv 11 + c
+      __syncthreads();   // every wave holds its fragments: WB is free for the next block
+      FDR_STAMP(a, 103 + 2 * c);
+      if (c < 3) copy_block(12 + c);
+    }
+    f32x4 acc[2][2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) acc[j][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (live) {
 #pragma unroll
       for (int s = 0; s < 9; ++s) {  // tap s = (s / 3, s % 3), channel chunk g: conv_h2's K order
-        h8 b[4];
+        // the pair's second tile is the first's two padded rows (20 pixels) further: tsw<32>(q + 20) = tsw<32>(q) ^ 2
+        const int q0 = (4 * hp2 + ((ln & 15) >> 3) + s / 3) * 10 + (ln & 7) + s % 3;
+        const int a0 = q0 * 32, sw0 = g ^ tsw<32>(q0);
+        const h8 b0 = *reinterpret_cast<const h8*>(Tin + a0 + (sw0 << 3));
+        const h8 b1 = *reinterpret_cast<const h8*>(Tin + a0 + 640 + ((sw0 ^ 2) << 3));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = 16 * i + (ln & 15), q = ((m >> 3) + s / 3) * 10 + (m & 7) + s % 3;
-          b[i] = *reinterpret_cast<const h8*>(Tin + q * 32 + ((g ^ tsw<32>(q)) << 3));
+        for (int nt = 0; nt < 2; ++nt) {
+          acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b0, acc[0][nt], 0, 0, 0);
+          acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b1, acc[1][nt], 0, 0, 0);
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s], b[i], acc[i], 0, 0, 0);
       }
-      if (c < 3) load_a(12 + c);  // the next conv's fragments, in flight under this epilogue and barrier
       const int i0 = c;           // this conv's table index (conv 11 + c)
-      if ((c & 1) == 0) {
-        // conv0 of a block: T <- relu(BN_{next}(. + b0)) (res_blocks_h2 epilogue0)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float o[4];
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int k = 0; k < 4; ++k)
-            o[k] = fmaf(acc[i][k] + cbt[i0 * 32 + ch0 + k], sct[(i0 + 1) * 32 + ch0 + k], sht[(i0 + 1) * 32 + ch0 + k]);
-          *reinterpret_cast<h4*>(Tout + tidx<32>(qout(i), ch0)) = relu_h4(to_h4(o[0], o[1], o[2], o[3]));
-        }
-      } else {
-        // conv1: x' = f16((v + b1) + x); block 0: T <- relu(BN_13(x')); block 1 (the last): features relu(x')
+        for (int nt = 0; nt < 2; ++nt) {
+          const int ch0 = 16 * nt + 4 * g;
+          const f32x4 v = acc[j][nt];
+          if ((c & 1) == 0) {
+            // conv0 of a block: T <- relu(BN_{next}(. + b0)) (res_blocks_h2 epilogue0)
+            float o[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const h2 xl = lo2(x[i]), xh = hi2(x[i]);
-          const float* b1 = cbt + i0 * 32 + ch0;
-          const h4 xn = to_h4(fma_mix_lo(xl, 1.f, acc[i][0] + b1[0]), fma_mix_hi(xl, 1.f, acc[i][1] + b1[1]),
-                              fma_mix_lo(xh, 1.f, acc[i][2] + b1[2]), fma_mix_hi(xh, 1.f, acc[i][3] + b1[3]));
-          if (c == 3) {
-            float* out = a.feat + ge * kFeat;
-            const int m = 16 * i + (ln & 15);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) out[(ch0 + k) * 64 + m] = relu((float)xn[k]);  // flatten (C, H, W)
+            for (int k = 0; k < 4; ++k)
+              o[k] = fmaf(v[k] + cbt[i0 * 32 + ch0 + k], sct[(i0 + 1) * 32 + ch0 + k], sht[(i0 + 1) * 32 + ch0 + k]);
+            *reinterpret_cast<h4*>(Tout + tidx<32>(qout(j), ch0)) = relu_h4(to_h4(o[0], o[1], o[2], o[3]));
           } else {
-            x[i] = xn;
-            const h2 nl = lo2(xn), nh = hi2(xn);
-            const float* s2 = sct + (i0 + 1) * 32 + ch0;
-            const float* t2 = sht + (i0 + 1) * 32 + ch0;
-            const h4 t = to_h4(fma_mix_lo(nl, s2[0], t2[0]), fma_mix_hi(nl, s2[1], t2[1]), fma_mix_lo(nh, s2[2], t2[2]),
-                               fma_mix_hi(nh, s2[3], t2[3]));
-            *reinterpret_cast<h4*>(Tout + tidx<32>(qout(i), ch0)) = relu_h4(t);
+            // conv1: x' = f16((v + b1) + x); block 0: T <- relu(BN_13(x')); block 1 (the last): features relu(x')
+            const h2 xl = lo2(x[j][nt]), xh = hi2(x[j][nt]);
+            const float* b1 = cbt + i0 * 32 + ch0;
+            const h4 xn = to_h4(fma_mix_lo(xl, 1.f, v[0] + b1[0]), fma_mix_hi(xl, 1.f, v[1] + b1[1]),
+                                fma_mix_lo(xh, 1.f, v[2] + b1[2]), fma_mix_hi(xh, 1.f, v[3] + b1[3]));
+            if (c == 3) {
+              float* out = a.feat + ge * kFeat;
+              const int m = 16 * (2 * hp2 + j) + (ln & 15);
+#pragma unroll
+              for (int k = 0; k < 4; ++k) out[(ch0 + k) * 64 + m] = relu((float)xn[k]);  // flatten (C, H, W)
+            } else {
+              x[j][nt] = xn;
+              const h2 nl = lo2(xn), nh = hi2(xn);
+              const float* s2 = sct + (i0 + 1) * 32 + ch0;
+              const float* t2 = sht + (i0 + 1) * 32 + ch0;
+              const h4 t = to_h4(fma_mix_lo(nl, s2[0], t2[0]), fma_mix_hi(nl, s2[1], t2[1]), fma_mix_lo(nh, s2[2], t2[2]),
+                                 fma_mix_hi(nh, s2[3], t2[3]));
+              *reinterpret_cast<h4*>(Tout + tidx<32>(qout(j), ch0)) = relu_h4(t);
+            }
           }
         }
-      }
     }
-    if (c < 3) __syncthreads();  // T[c + 1 & 1] complete; T[c & 1] free for the next conv's output
+    if (!SHARED && live && c < 3) load_a(hp + L.conv_h[12 + c]);  // the next conv's fragments
+    if (c < 3) {
+      if constexpr (SHARED) __builtin_amdgcn_s_waitcnt(0);  // conv 12 + c's block has landed in WB
+      __syncthreads();  // T[c + 1 & 1] and WB complete; T[c & 1] free for the next conv's output
+    }
+    FDR_STAMP(a, 104 + 2 * c);
   }
 }
+template __global__ void conv_s3_kernel<false>(Layout, StepArgs);
+template __global__ void conv_s3_kernel<true>(Layout, StepArgs);
 
 // ---- core (fc + LSTM + head) with f16 weights ------------------------------------------------------
 template <int E, int MODE>

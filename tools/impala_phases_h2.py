@@ -38,7 +38,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lanes", type=int, default=1024)
     ap.add_argument("--envs", type=int, default=4)
-    ap.add_argument("--mode", type=int, default=1, help="1: conv_kernel_h2<256>, 2: conv_kernel_h2<512>")
+    ap.add_argument("--mode", type=int, default=1, help="1: conv_kernel_h2<256>, 2: conv_kernel_h2<512>, 3: <512> + conv_s3_kernel")
     ap.add_argument("--old-entry", action="store_true", help="mode 2 built with FDR_H3_ENTRY=0 (banded S image entries)")
     args = ap.parse_args()
     A = 4
@@ -58,7 +58,22 @@ def main():
     torch.cuda.synchronize()
     ctx.impala_debug_clock(None)
     c = dbg.cpu().numpy().astype(np.int64)
-    n = names(h3=args.mode == 2 and not args.old_entry)
+    n = names(h3=args.mode in (2, 3) and not args.old_entry)
+    if args.mode == 3:  # conv_s3_kernel's workgroup 0 (stamps 100 .. 110), printed separately
+        s3 = {101: "s3 prologue (loads, tables, zero, W11)", 102: "s3 T0 = relu(BN(X3))"}
+        for k in range(4):
+            s3[103 + 2 * k] = "s3 conv%d fragments + barrier" % k
+            s3[104 + 2 * k] = "s3 conv%d K loop + epilogue" % k
+        t3 = c[110] - c[100]
+        print("conv_s3_kernel workgroup 0: %d clocks total" % t3)
+        for k in range(101, 111):
+            print("%-40s %9d  %5.1f%%" % (s3[k], c[k] - c[k - 1], 100.0 * (c[k] - c[k - 1]) / max(t3, 1)))
+        if c[112]:  # FDR_S3_PROBE build: the prologue's load groups, each waited for
+            for k, what in ((112, "entry -> first wait"), (113, "W11 LDS DMA"), (114, "X3 loads"), (115, "tables"),
+                            (116, "zero images")):
+                print("  probe %-30s %9d" % (what, c[k] - c[k - 1 if k > 112 else 100]))
+        for k in list(range(100, 111)) + list(range(112, 117)):
+            c[k] = 0
     order = [0] + sorted(k for k in n if c[k] != 0)  # the 4-wave kernel has one stage-3 band
     tot = c[order[-1]] - c[0]
     print("conv_kernel_h2 (mode %d) workgroup 0: %d clocks total" % (args.mode, tot))
