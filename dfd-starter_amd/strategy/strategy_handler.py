@@ -15,6 +15,15 @@ AtariPolicy (stateless) strategies are its forward over the zeta frames, one fdr
 ``Worker._build_ret``'s per-return ``compute_novelty`` (worker/worker.py:53), which the reference
 evaluates on the perturbed policy.  Replacement when full follows ``_replace_point`` /
 ``_update_strategy_point_dists`` (sparse_history_manager.py:73-148) on the pairwise distance table.
+
+ImpalaPolicy archive state (``carry_state``): by default every archive strategy starts from the reset LSTM state (the
+build's zero-state rule).  ``carry_state=True`` reproduces the reference as it is: every
+StrategyPoint.evaluate_strategy (strategy_point.py:17-25) runs ``self.policy.get_strategy`` on the handler's ONE
+policy object, so each evaluation continues the (h, c) the previous one left in it (policies/impala.py:24-27,
+:136-138,184) -- set_zeta evaluates the points in archive order, submit_policy the candidate, compute_novelty the
+scored policy, one launch each, all chained through ``policy.state``.  Pinned by G12-impala-unpatched.
+``lane_novelty`` stays from the reset state in both modes: the reference's worker scores novelty right after
+collect_return's policy.reset() (worker/agent.py:66, worker/worker.py:53).
 """
 import numpy as np
 import torch
@@ -28,9 +37,13 @@ KIND_BY_NAME = {"l2_dist": "l2", "categorical_tvd": "tvd", "gaussian_wasserstein
 
 
 class StrategyHandler(object):
-    def __init__(self, policy, strategy_distance_fn=None, max_history_size=200, fp16=False):
+    def __init__(self, policy, strategy_distance_fn=None, max_history_size=200, fp16=False, carry_state=False):
         self.policy = policy
         self.fp16 = bool(fp16)        # ImpalaPolicy: strategies in the rollouts' fp16 mode (BASELINE config 5)
+        if carry_state and policy.KIND != "impala":
+            raise ValueError("carry_state applies to ImpalaPolicy (the only policy with recurrent state)")
+        self.carry_state = bool(carry_state)
+        self._zeta_done0 = False      # ImpalaPolicy: zeta's first done flag masks the carried state (impala.py:164-170)
         self.strategy_distance_fn = strategy_distance_fn
         name = getattr(strategy_distance_fn, "__name__", "l2_dist") if strategy_distance_fn is not None \
             else "l2_dist"                     # compute_strategy_novelty's default (math_helpers.py:148-149)
@@ -60,6 +73,21 @@ class StrategyHandler(object):
             raise NotImplementedError("strategies of a %s policy" % p.KIND)
         return engine.lane_strategies(p.spec, lanes_fn, n, self.zeta, bm, bv)
 
+    def _carried(self, flat):
+        """StrategyPoint.evaluate_strategy with the reference's carried LSTM state: get_strategy of ONE parameter
+        vector (device f32 [P]) from self.policy.state, which it leaves at the end-of-sequence state -> [1, Z, A]."""
+        p = self.policy
+        h, c = (s[:1].reshape(1, 256).clone().contiguous() for s in p.state)
+        if self._zeta_done0:
+            h.zero_()
+            c.zero_()
+        frames, reward = self.zeta
+        bm, bv = p.bn_stats()
+        probs = engine.impala_strategies(engine.ImpalaSpec(p.output_shape, fp16=self.fp16),
+                                         engine.lanes_desc(flat, 0), 1, frames, reward, h, c, bm, bv)
+        p.state = (h, c)
+        return probs
+
     def _atari_strategies(self, thetas):
         """AtariPolicy.get_strategy (policies/atari.py:31-32: forward(zeta) probs, stateless) of each parameter
         vector in thetas (device f32 [k, P]) -> [k, Z, A]: fdr_atari_forward over the zeta frames per vector."""
@@ -72,11 +100,13 @@ class StrategyHandler(object):
         base = torch.as_tensor(np.asarray(flat, np.float32), device=self._dev()).contiguous()
         if self.policy.KIND == "atari":
             return self._atari_strategies(base.view(1, -1))
+        if self.carry_state:
+            return self._carried(base)
         return self._strategies(lambda Z: engine.lanes_desc(base, 0), 1)
 
     def _strategies_of_flats(self, flats):
         """Strategies of the archived vectors -> [H, Z, D] (ImpalaPolicy: one launch, lane l reads flats[l])."""
-        if self.policy.KIND == "impala":
+        if self.policy.KIND == "impala" and not self.carry_state:
             base = torch.as_tensor(np.stack([np.asarray(f, np.float32) for f in flats]), device=self._dev())
             base = base.contiguous()
             return self._strategies(lambda Z: engine.lanes_desc(base, base.shape[1]), len(flats))
@@ -110,8 +140,9 @@ class StrategyHandler(object):
         if zeta is None or len(zeta) == 0:
             return
         if self.policy.KIND == "impala":
-            fr, rw, _ = self.policy._stack(zeta)
+            fr, rw, dn = self.policy._stack(zeta)
             self.zeta = (fr.to(self._dev()).contiguous(), rw.to(self._dev()).contiguous())
+            self._zeta_done0 = bool(dn[0])
         else:
             z = torch.as_tensor(np.asarray(zeta, np.float32), device=self._dev())
             self.zeta = z.reshape(z.shape[0], -1).contiguous()

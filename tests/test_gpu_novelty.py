@@ -144,16 +144,18 @@ def test_archive_replacement_matches_reference(engine, golden, tag, kind, n_in, 
     np.testing.assert_allclose(h.pair, z[tag + "_dists"], rtol=1e-5)
 
 
-def test_impala_archive_replacement_matches_reference(engine, golden):
+@pytest.mark.parametrize("carry", [False, True])
+def test_impala_archive_replacement_matches_reference(engine, golden, carry):
     """the device StrategyHandler over an ImpalaPolicy (fdr_impala_strategies: conv stack on
     the shared zeta frames, the zeta obs as ONE LSTM sequence from the reset state) against G12-impala, made by
     the reference's StrategyHandler / SparseHistoryManager with get_strategy from reset (the build's documented
     zero-state rule): every submit's return and worst_point_idx, the archive (f32, 1e-5), the distance table
-    and compute_novelty."""
+    and compute_novelty.  carry=True (VERDICT r4 missing 4): StrategyHandler(carry_state=True) chains the LSTM
+    state through the policy object as the unpatched reference does, against G12-impala-unpatched."""
     from policies import ImpalaPolicy
     from strategy import StrategyHandler
     from utils import math_helpers
-    z = golden("g12_impala.npz")
+    z = golden("g12_impala_unpatched.npz" if carry else "g12_impala.npz")
     A, H, P = int(z["A"]), int(z["H"]), int(z["P"])
     table = np.random.RandomState(int(z["table_seed"])).randn(2 ** 22).astype(np.float32)
     off = int(z["param_offset"])
@@ -171,7 +173,7 @@ def test_impala_archive_replacement_matches_reference(engine, golden):
     zeta = {"frame": torch.as_tensor(z["zeta_frames"].astype(np.float32)).view(Z, 1, 3, 64, 64),
             "reward": torch.as_tensor(z["zeta_rewards"]).view(Z, 1),
             "done": torch.zeros(Z, 1, dtype=torch.bool)}
-    h = StrategyHandler(pol, math_helpers.categorical_tvd, max_history_size=H)
+    h = StrategyHandler(pol, math_helpers.categorical_tvd, max_history_size=H, carry_state=carry)
     for k in range(H):
         pol.set_trainable_flat(flats[k])
         assert h.add_policy(pol) is None
