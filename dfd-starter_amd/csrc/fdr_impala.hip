@@ -262,10 +262,12 @@ __global__ __launch_bounds__(kPrepThreads) void prep_kernel(Layout L, LanesArgs 
 constexpr int kTT = 64;  // transpose tile edge
 __host__ __device__ inline int transpose_tiles(const Section& s) { return ((s.a + kTT - 1) / kTT) * ((s.b + kTT - 1) / kTT); }
 
+// write = 0: the f32 call's n2 partials only (the same reads and reduce order, no tile, no stores) -- for fp16 calls,
+// whose kernels take these weights from the half pack / the pair images
 template <class OUT>
 __global__ __launch_bounds__(256) void prep_transpose_kernel(Layout L, LanesArgs lanes, OUT* __restrict__ pack,
                                                              double* __restrict__ n2_part, int half, int n2_slot0,
-                                                             int n2_slots) {
+                                                             int n2_slots, int write) {
   __shared__ float tile[kTT][kTT + 1];
   __shared__ double red[256 / kWave];
   const int lane = blockIdx.y;
@@ -293,13 +295,15 @@ __global__ __launch_bounds__(256) void prep_transpose_kernel(Layout L, LanesArgs
       const int64_t p = (int64_t)s.src + (int64_t)r * s.b + k;
       v = half ? src.get_nocount(p) : src.get(p);
     }
-    tile[jj][i] = v;
+    if (write) tile[jj][i] = v;
   }
-  __syncthreads();
+  if (write) {
+    __syncthreads();
 #pragma unroll
-  for (int m = 0; m < kTT * kTT / 256; ++m) {  // W^T[k][r] along r
-    const int e = threadIdx.x + 256 * m, jj = e / kTT, i = e % kTT, r = r0 + i, k = k0 + jj;
-    if (r < s.a && k < s.b) out[(int64_t)k * s.a + r] = (OUT)tile[jj][i];
+    for (int m = 0; m < kTT * kTT / 256; ++m) {  // W^T[k][r] along r
+      const int e = threadIdx.x + 256 * m, jj = e / kTT, i = e % kTT, r = r0 + i, k = k0 + jj;
+      if (r < s.a && k < s.b) out[(int64_t)k * s.a + r] = (OUT)tile[jj][i];
+    }
   }
   if (half) return;
   double n2 = wave_sum(src.n2);
@@ -324,17 +328,21 @@ static int transpose_prep_tiles(const Layout& L, bool half) {
   return n;
 }
 
-// theta' pack (half = 0, f32, with the per-lane n2 partials) or half pack (half = 1, f16)
+// theta' pack (half = 0, f32, with the per-lane n2 partials) or half pack (half = 1, f16).  The transposed sections
+// (fc W^T, [W_ih | W_hh]^T: 90 % of the pack) by tmode: kTrFull written; kTrNorm not written, n2 partials only (an
+// fp16 call's f32 pack: its kernels read those weights from the half pack or the pair images); kTrSkip nothing
+// (an fp16 call's f32 pack when n2 is not wanted, or its half pack under the pair core)
+enum TransposedMode { kTrFull = 0, kTrNorm = 1, kTrSkip = 2 };
 template <class OUT>
 static void launch_pack(const Layout& L, const LanesArgs& lanes, OUT* pack, double* n2, int n_lanes, int half,
-                        hipStream_t stream) {
-  const int g = generic_prep_blocks(L, half != 0), tt = transpose_prep_tiles(L, half != 0);
+                        hipStream_t stream, TransposedMode tmode = kTrFull) {
+  const int g = generic_prep_blocks(L, half != 0), tt = tmode == kTrSkip ? 0 : transpose_prep_tiles(L, half != 0);
   const int slots = prep_blocks(L);
   hipLaunchKernelGGL(prep_kernel<OUT>, dim3(g, n_lanes), dim3(kPrepThreads), 0, stream, L, lanes, pack, n2, half,
                      slots);
   if (tt > 0)
     hipLaunchKernelGGL(prep_transpose_kernel<OUT>, dim3(tt, n_lanes), dim3(256), 0, stream, L, lanes, pack, n2, half,
-                       generic_prep_blocks(L, false), slots);
+                       generic_prep_blocks(L, false), slots, tmode == kTrFull ? 1 : 0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1485,13 +1493,18 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
   a.dbg = c.ctx->debug_clock;
   double* n2 = reinterpret_cast<double*>(w + p.n2);
 
-  launch_pack<float>(L, c.lanes, const_cast<float*>(a.pack), n2, c.n_lanes, 0, stream);
+  const bool pair_core =
+      c.pairs && pair_core_supported(c.envs) && c.lanes.table && c.lanes.base_stride == 0 && c.n_lanes >= 2;
+  launch_pack<float>(L, c.lanes, const_cast<float*>(a.pack), n2, c.n_lanes, 0, stream, c.fp16 ? kTrNorm : kTrFull);
   if (c.fp16) {
     a.hpack = reinterpret_cast<_Float16*>(w + p.hpack);
     a.hpack_stride = L.hpack;
-    launch_pack<_Float16>(L, c.lanes, a.hpack, n2, c.n_lanes, 1, stream);
+    // the per-lane half pack's fc / LSTM weights are read only off the MFMA pair path: core_kernel_h (no pair core),
+    // lstm_xproj_kernel (pair core on VALU) and core_kernel_h<kReplay> (replay without the gate GEMM)
+    const bool pair_images = pair_core && c.ctx->core_mfma && (!c.entropy || c.ctx->replay_gemm);
+    launch_pack<_Float16>(L, c.lanes, a.hpack, n2, c.n_lanes, 1, stream, pair_images ? kTrSkip : kTrFull);
   }
-  if (c.pairs && pair_core_supported(c.envs) && c.lanes.table && c.lanes.base_stride == 0 && c.n_lanes >= 2) {
+  if (pair_core) {
     // the pair form's operands, built by the same pack kernels: theta's pack (no table: theta' = theta) and
     // per pair fl32(sigma eps) (a zero base, sign +1: fl32(0 + fl32(sigma eps))) -- f16 in fp16 mode
     const int np = c.n_lanes / 2;
@@ -1734,7 +1747,7 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
   a.c = c.c ? c.c : reinterpret_cast<float*>(w + p.c);
   a.probs = c.probs;
   double* n2 = reinterpret_cast<double*>(w + p.n2);
-  launch_pack<float>(L, c.lanes, const_cast<float*>(a.pack), n2, c.n_lanes, 0, stream);
+  launch_pack<float>(L, c.lanes, const_cast<float*>(a.pack), n2, c.n_lanes, 0, stream, half ? kTrSkip : kTrFull);
   if (half) {
     a.hpack = reinterpret_cast<_Float16*>(w + p.hpack);
     a.hpack_stride = L.hpack;
