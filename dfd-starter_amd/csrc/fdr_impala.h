@@ -13,12 +13,8 @@ constexpr int kFeat = 2048;  // 32 x 8 x 8 (policies/impala.py:113)
 constexpr int kHid = 256;    // fc width == LSTM hidden
 constexpr int kGates = 1024;
 constexpr int kCoreIn = 257; // fc output + clipped reward (policies/impala.py:116, 163-164)
-#ifndef FDR_CORE_UNROLL
-#define FDR_CORE_UNROLL 4  // weight-stream loop unroll of the core kernels (loads in flight per thread)
-#endif
-#ifndef FDR_CORE_UNROLL_H
+#define FDR_CORE_UNROLL 4    // weight-stream loop unroll of the core kernels (loads in flight per thread)
 #define FDR_CORE_UNROLL_H 2  // fp16 step kernel's fc / gate streams (A/B: 0.377 -> 0.360 ms per step vs 4)
-#endif
 // fp16 pair-form core step on MFMA (core_kernel_hpm): fc W^T and [W_ih | W_hh]^T as v_mfma_f32_16x16x32_f16
 // A-fragment images [k-step][16-column tile][64 lanes][8 halves] (lane l: W[16 nt + (l & 15)][32 ks + 8 (l >> 4) ..
 // + 7]), one for theta and one per pair for sigma-eps; K of the gates (513) zero-padded to 17 k-steps.

@@ -717,17 +717,11 @@ static_assert(kH2BR * 64 * 16 <= kH2FB0 && 3 * kBnTab * 2 >= 34 * 16, "band scra
 // up to 16 tiles; K-outer order keeps 5 pixel addresses per tile live at once (80 VGPRs in the stage-1
 // residual convs, which spilled), tile-outer order keeps one tile's.  Dependent MFMAs on one accumulator
 // issue back to back (SrcC forwarding of the same opcode), and the other workgroup's waves fill the SIMD.
-#ifndef FDR_H2_STAGGER
-#define FDR_H2_STAGGER 0
-#endif
 // STREAM (Cin = 32 at 8 waves, where 72 fragment VGPRs do not fit beside the accumulators under 128): the A
 // fragments are read from the LDS weight block ws per K-step (K-outer: both channel tiles' fragments, then every
 // tile's B fragment of that step) instead of af -- the same products in the same K order.
 // NTA / nt0 (streamed form): the block holds NTA channel tiles, this wave computes tiles nt0 .. nt0 + NT - 1.
-#ifndef FDR_R32
-#define FDR_R32 1
-#endif
-// R32 (conv_kernel_h2<512>, FDR_R32): the tap-8 remainder runs as one more v_mfma_f32_16x16x32_f16 on the pack's K = 32
+// R32 (conv_kernel_h2<512>): the tap-8 remainder runs as one more v_mfma_f32_16x16x32_f16 on the pack's K = 32
 // fragment (tap 8 + zeros) chained onto the accumulator -- a K = 16 MFMA takes the same 16-clock slot
 // (profiles/r08a_mfma_rate_probe.txt), and the separate accumulator's VALU add (the K = 16 product cannot be chained:
 // DESIGN.md 3.4 SrcC) and its registers go.  The sums differ from conv_h's in rounding only.
@@ -965,7 +959,7 @@ __device__ __forceinline__ void entry_band_h2(const _Float16* Tin, int qoff, _Fl
 }
 
 // -----------------------------------------------------------------------------------------------------
-// Stage entries with the max pool in registers (conv_kernel_h2<512>, FDR_H3_ENTRY; DESIGN.md 3.4 "r07 entries").
+// Stage entries with the max pool in registers (conv_kernel_h2<512>; docs/DESIGN_LOG.md 3.4 "r07 entries").
 // A band is 16 conv rows; wave w owns band rows 2w and 2w + 1, all their pixels, all output channels.  The 3 x 3 /
 // stride-2 pool then needs no image of the conv output: horizontally the window's three columns are in
 // neighbouring lanes (DPP), vertically pooled row w is max(row 2w - 1, 2w, 2w + 1) -- rows 2w, 2w + 1 are the
@@ -1106,7 +1100,7 @@ __device__ __forceinline__ void conv_band_nat(const _Float16* Tin, int r0, const
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[nt], b[i], acc[i][nt], 0, 0, 0);
   }
-  if constexpr (KSteps<CIN>::kRem && FDR_R32) {  // tap 8 + zeros on K = 32 (the pack's fragment), chained
+  if constexpr (KSteps<CIN>::kRem) {  // tap 8 + zeros on K = 32 (the pack's fragment), chained
     h8 a[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) a[nt] = *reinterpret_cast<const h8*>(ws + ((((KS - 1) * NT + nt) * 64) + lane) * 8);
@@ -1275,10 +1269,6 @@ __device__ __forceinline__ void pool_nat(const f32x4 (&acc)[2 * (H / 16)][2], co
 // commit only after a barrier that follows every wave's fragment load of the previous block.  On exit T holds
 // the next stage's input (or the features are written, LAST), and st holds the issued next-stage block (NEXTH
 // halves; committed by the caller, whose WB may differ).
-#ifndef FDR_H2_SPLIT
-#define FDR_H2_SPLIT 1
-#endif
-
 template <int NTH, int C, int H, int LAST, int NEXTH>
 __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)[KSteps<C>::N][C / 16],
                                               const _Float16* __restrict__ hp, const Layout& L, int stage,
@@ -1287,11 +1277,11 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
                                               const _Float16* __restrict__ next_w, const StepArgs& a, int stamp) {
   constexpr int CS = Pix<C>::CS, WP = H + 2, NTA = C / 16, MT = H * H / 16, NWA = NTH / 64;
   constexpr bool ST = NTH >= 512 && C == 32;  // A fragments streamed from wb (conv_h2 STREAM); af unused
-  constexpr bool R32 = NTH >= 512 && C == 16 && FDR_R32;  // tap 8 as a chained K = 32 MFMA (conv_h2 R32)
+  constexpr bool R32 = NTH >= 512 && C == 16;  // tap 8 as a chained K = 32 MFMA (conv_h2 R32)
   // SPLIT (8 x 8 stage at 8 waves: 4 pixel tiles x 2 channel tiles): wave = (pixel tile w % 4, channel tile w / 4), so
   // every wave runs one MFMA per K-step and streams only its own channel tile's A fragments (without it waves 4-7
   // had no tile but still read both channel tiles' fragments)
-  constexpr int SPLIT = FDR_H2_SPLIT && ST && MT * NTA == NWA ? NTA : 1;
+  constexpr int SPLIT = ST && MT * NTA == NWA ? NTA : 1;
   static_assert(SPLIT == 1 || (MT == 4 && NTA == 2), "split map");
   constexpr int NT = NTA / SPLIT, NW = NWA / SPLIT;
   const int nt0 = SPLIT > 1 ? (wave / NW) * NT : 0;
@@ -1400,15 +1390,6 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
   }
 }
 
-#ifndef FDR_H2_ONE_PER_CU
-#define FDR_H2_ONE_PER_CU 0
-#endif
-#ifndef FDR_H3_ENTRY
-#define FDR_H3_ENTRY 1
-#endif
-#ifndef FDR_S2_ISSUE
-#define FDR_S2_ISSUE 1
-#endif
 #ifdef FDR_H3_FINE  // diagnostics build: clocks inside the h3 entry bands (dbg[64..])
 #define FDR_FINE_STAMP(a, k) FDR_STAMP(a, k)
 #else
@@ -1421,18 +1402,13 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
 // there, four envs per workgroup
 template <int NTH, bool SPLIT3>
 __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))) void conv_kernel_h2(Layout L, StepArgs a) {
-  constexpr bool H3 = NTH >= 512 && FDR_H3_ENTRY;  // stage entries with the pool in registers
+  constexpr bool H3 = NTH >= 512;  // stage entries with the pool in registers
   static_assert(!SPLIT3 || H3, "split stage 3: the h3 entries");
   static_assert(!H3 || NTH == kHThreads, "h3 entries: 8 waves (zero_border_h's thread count)");
-  // experiment: FDR_H2_ONE_PER_CU pads the LDS past half the CU (one workgroup per CU) -- latency sensitivity
-  __shared__ __attribute__((aligned(16))) unsigned char smem[kH2LdsBytes + (FDR_H2_ONE_PER_CU ? 4096 : 0)];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kH2LdsBytes];
   const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
   const int lane = (slot / a.envs) * 8 + xcd, e = slot % a.envs;
   if (lane >= a.n_lanes) return;
-#if FDR_H2_STAGGER  // experiment: the second workgroup of each CU in the first dispatch round starts late
-  if (b >= 256 && b < 512)
-    for (int k = 0; k < FDR_H2_STAGGER / 8000; ++k) __builtin_amdgcn_s_sleep(125);
-#endif
   FDR_STAMP(a, 0);
 #ifdef FDR_WG_TIMELINE  // diagnostics build: every workgroup's start / end (s_memrealtime, 100 MHz) and HW_ID / XCC_ID
   if (a.dbg && threadIdx.x == 0) {
@@ -1556,7 +1532,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   // ---- stage 1 residual blocks (16 ch, 32 x 32) ----
   {
     h8 af[KSteps<16>::N][1];
-    load_af_lds<16, 1, NTH >= 512 && FDR_R32>(R + kH2WBA, af, ln);
+    load_af_lds<16, 1, NTH >= 512>(R + kH2WBA, af, ln);
     st.template issue<kBlockHalves<16, 1>>(hp + L.conv_h[2]);
     to_padded_h<16, 32, true, true, NTH>(R + kH2X1, R, bsc + 1 * 32, bsh + 1 * 32);
     __syncthreads();
@@ -1569,11 +1545,9 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   // ---- stage 2: entry (16 -> 32 at 32 x 32, pooled to 16 x 16) in 4 bands; X2 into T1's consumed rows (h3: 2
   // bands of 16 rows, pool in registers; band 1 reads padded rows 16..33, past X2's first half) ----
   if constexpr (H3) {
-    // FDR_S2_ISSUE (r10): where conv 6's weight block is requested.  0: before the two bands (its 9 staging VGPRs live
-    // across both bands' convs -- one 16-B chunk was spilled, the store waiting on its own global load, and the
-    // reload read back at the commit: the kernel's only scratch traffic, 33.5 MB written + read per launch);
-    // 1: after band 1's conv, once the accumulators are pooled (the lane's other envs have it in L2 by then)
-    if constexpr (FDR_S2_ISSUE == 0) st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
+    // conv 6's weight block is requested after band 1's conv, once the accumulators are pooled (r10: issued before
+    // the two bands, its 9 staging VGPRs lived across both bands' convs -- one 16-B chunk spilled, the kernel's only
+    // scratch traffic, 33.5 MB written + read per launch)
     for (int bd = 0; bd < 2; ++bd) {
       h4 prev[4], P[4], Bx[4];
       f32x4 acc[4][2];
@@ -1585,9 +1559,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
 #pragma unroll
         for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[5 * 32 + nt * 16 + 4 * (ln >> 4) + k];
       pool_nat<32>(acc, bz, P, Bx);
-      if constexpr (FDR_S2_ISSUE == 1) {
-        if (bd == 1) st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
-      }
+      if (bd == 1) st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
       FDR_FINE_STAMP(a, 81 + 4 * bd);
       band_prev_h3<32, 32, false>(prev, R + kH3EX2, bd, wave, ln);
       // (barrier inside).  Band 1 also writes T2 = relu(BN(X2)) of its rows: T2 lies over T1's rows 15.., which band

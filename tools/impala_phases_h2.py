@@ -39,7 +39,6 @@ def main():
     ap.add_argument("--lanes", type=int, default=1024)
     ap.add_argument("--envs", type=int, default=4)
     ap.add_argument("--mode", type=int, default=1, help="1: conv_kernel_h2<256>, 2: conv_kernel_h2<512>, 3: <512> + conv_s3_kernel")
-    ap.add_argument("--old-entry", action="store_true", help="mode 2 built with FDR_H3_ENTRY=0 (banded S image entries)")
     args = ap.parse_args()
     A = 4
     P = engine.impala_num_params(A)
@@ -58,7 +57,7 @@ def main():
     torch.cuda.synchronize()
     ctx.impala_debug_clock(None)
     c = dbg.cpu().numpy().astype(np.int64)
-    n = names(h3=args.mode in (2, 3) and not args.old_entry)
+    n = names(h3=args.mode in (2, 3))
     if args.mode == 3:  # conv_s3_kernel's workgroup 0 (stamps 100 .. 110), printed separately
         s3 = {101: "s3 prologue (loads, tables, zero, W11)", 102: "s3 T0 = relu(BN(X3))"}
         for k in range(4):

@@ -116,14 +116,17 @@ def main(d, tag, config="halfcheetah", dominant="rollout_kernel", secondary=None
                                                    if rollout["sq"].get("SQ_INSTS_VALU") else None),
                              wave_frac_active=q["SQ_ACTIVE_INST_ANY"] / q["SQ_WAVE_CYCLES"],
                              wave_frac_wait_any=q["SQ_WAIT_ANY"] / q["SQ_WAVE_CYCLES"],
-                             wave_frac_wait_inst=q["SQ_WAIT_INST_ANY"] / q["SQ_WAVE_CYCLES"])
+                             wave_frac_wait_inst=q["SQ_WAIT_INST_ANY"] / q["SQ_WAVE_CYCLES"],
+                             wave_frac_wait_inst_lds=(q["SQ_WAIT_INST_LDS"] / q["SQ_WAVE_CYCLES"]
+                                                      if "SQ_WAIT_INST_LDS" in q else None))
                 rollout["issue"] = issue
                 lines += ["", "Issue / wait PMC pass (quad-cycle SQ counters; SIMD VALU busy = SQ_ACTIVE_INST_VALU / "
                               "(1024 SIMDs x GRBM_GUI_ACTIVE/8 / 4)): VALU busy %.3f, %.2f cycles per VALU instruction; "
-                              "wave cycles: %.1f %% issuing, %.1f %% waiting on counters, %.1f %% issue-stalled." % (
+                              "wave cycles: %.1f %% issuing, %.1f %% waiting on counters, %.1f %% issue-stalled "
+                              "(of which LDS issue %.1f %%)." % (
                                   issue["simd_valu_busy"], issue["cycles_per_valu_inst"] or 0,
                                   100 * issue["wave_frac_active"], 100 * issue["wave_frac_wait_any"],
-                                  100 * issue["wave_frac_wait_inst"])]
+                                  100 * issue["wave_frac_wait_inst"], 100 * (issue["wave_frac_wait_inst_lds"] or 0))]
         if secondary:
             for k in fetch:
                 if secondary in k:
