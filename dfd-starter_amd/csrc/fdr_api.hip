@@ -116,8 +116,8 @@ Context& default_context() {
                          : strcmp(e, "single") == 0 ? FDR_ROLLOUT_SINGLE
                          : strcmp(e, "wide") == 0   ? FDR_ROLLOUT_WIDE
                                                     : strcmp(e, "pair") == 0 ? FDR_ROLLOUT_PAIR : FDR_ROLLOUT_AUTO;
-    const char* m = getenv("FDR_CORE_MFMA");  // A/B switch: "0" selects the VALU fp16 pair core
-    c->core_mfma = !(m && strcmp(m, "0") == 0);
+    const char* m = getenv("FDR_CORE_MFMA");  // A/B switch: "0" VALU, "1" one pair per workgroup, else two
+    c->core_mfma = !m ? 2 : strcmp(m, "0") == 0 ? 0 : strcmp(m, "1") == 0 ? 1 : 2;
     const char* h2 = getenv("FDR_CONV_H2");  // A/B switch: "0" selects conv_kernel_h (one workgroup per CU)
     c->conv_h2 = !h2 ? 2 : strcmp(h2, "0") == 0 ? 0 : strcmp(h2, "1") == 0 ? 1 : strcmp(h2, "3") == 0 ? 3 : 2;
     return c;
@@ -178,7 +178,8 @@ int fdr_ctx_set_replay_gemm(fdr_ctx* ctx, int32_t on) {
   return FDR_OK;
 }
 int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on) {
-  (ctx ? ctx->c : default_context()).core_mfma = on != 0;
+  if (on < 0 || on > 2) return set_error(FDR_ERR_INVALID, "core_mfma must be 0, 1 or 2");
+  (ctx ? ctx->c : default_context()).core_mfma = on;
   return FDR_OK;
 }
 int fdr_ctx_set_conv_h2(fdr_ctx* ctx, int32_t on) {

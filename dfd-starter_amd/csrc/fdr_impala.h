@@ -232,6 +232,8 @@ template <int E>
 __global__ void core_kernel_hpr(Layout L, StepArgs a); // fp16 pair form of the replay (with a.gx)
 template <int E, int MODE>
 __global__ void core_kernel_hpm(Layout L, StepArgs a); // fp16 pair form on MFMA (kRollout / kReplay), grid n_lanes / 2
+template <int E, int MODE>
+__global__ void core_kernel_hpm2(Layout L, StepArgs a); // two pairs per workgroup (512 threads), grid n_lanes / 4
 // replay input projection of a chunk in the fp16 pair form on MFMA: grid (n_lanes / 2, kGateNT / 4)
 template <int E>
 __global__ void xproj_pair_kernel(Layout L, StepArgs a, int t0, int tc, float* gx);

@@ -1392,7 +1392,11 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
     mark(prof, stream);
     bool pair_done = false;
     if constexpr (E <= 4) {
-      if (h && a.epm) {
+      if (h && a.epm && ctx.core_mfma == 2 && a.n_lanes % 4 == 0) {
+        hipLaunchKernelGGL((core_kernel_hpm2<E, kRollout>), dim3(a.n_lanes / 4), dim3(2 * kCoreThreads), 0, stream, L,
+                           a);
+        pair_done = true;
+      } else if (h && a.epm) {
         hipLaunchKernelGGL((core_kernel_hpm<E, kRollout>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
         pair_done = true;
       } else if (h && a.ep) {
@@ -1437,7 +1441,11 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
         a.t = t;
         bool pair_done = false;
         if constexpr (E <= 4) {
-          if (a.gx && h && a.epm) {
+          if (a.gx && h && a.epm && ctx.core_mfma == 2 && a.n_lanes % 4 == 0) {
+            hipLaunchKernelGGL((core_kernel_hpm2<E, kReplay>), dim3(a.n_lanes / 4), dim3(2 * kCoreThreads), 0, stream,
+                               L, a);
+            pair_done = true;
+          } else if (a.gx && h && a.epm) {
             hipLaunchKernelGGL((core_kernel_hpm<E, kReplay>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L,
                                a);
             pair_done = true;

@@ -2419,8 +2419,16 @@ struct MfmaRing {
     const int64_t o = frag(q);
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt) {
+#if defined(FDR_HPM_PROBE) && FDR_HPM_PROBE == 1  // diagnostics build: no theta loads (the stream alone from HBM)
+      e[jt] = ld_stream(reinterpret_cast<const h8*>(epm + o + 512 * jt));
+      t[jt] = e[jt];
+#elif defined(FDR_HPM_PROBE) && FDR_HPM_PROBE == 2  // diagnostics build: both operands from theta's image (L2 only)
+      t[jt] = *reinterpret_cast<const h8*>(thm + o + 512 * jt);
+      e[jt] = ld_stream(reinterpret_cast<const h8*>(thm + o + 512 * (jt ^ 1)));
+#else
       t[jt] = *reinterpret_cast<const h8*>(thm + o + 512 * jt);
       e[jt] = ld_stream(reinterpret_cast<const h8*>(epm + o + 512 * jt));
+#endif
     }
   }
   __device__ __forceinline__ void prime() {
@@ -2678,6 +2686,289 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
   __syncthreads();
   if (j < E2) core_finish<E, MODE>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
 }
+
+// ---- Two pairs per workgroup (ctx core_mfma = 2, the default) ------------------------------------------------------
+// theta's fragment of a k-step is the same for every pair, yet core_kernel_hpm loads it once per pair from L2 next to
+// the pair's streamed E (the probe build without those loads ran the launch 16 % faster: 0.237 -> 0.199 ms at config
+// 5).  Here a workgroup of 8 waves takes two pairs -- 4 lanes, their 4E envs as the B columns -- and issues per
+// 16-column tile and k-step  theta x X,  E_0 x (S X masked to pair 0's columns),  E_1 x (S X masked to pair 1's):
+// three MFMAs for two pairs where the one-pair form issues four, theta read once for both.  A masked column adds
+// exact zeros, so every accumulator sees core_kernel_hpm's products in its order: the two forms agree bit for bit.
+template <int NQ, class Frag>
+struct MfmaRing2 {
+  static constexpr int D = 4;
+  static_assert(NQ % D == 0, "ring depth divides the step count");
+  const _Float16* thm;
+  const _Float16* ep0;
+  const _Float16* ep1;
+  Frag frag;
+  h8 rt[D][2], ra[D][2], rb[D][2];
+  __device__ __forceinline__ void issue(int q, h8 (&t)[2], h8 (&ea)[2], h8 (&eb)[2]) {
+    const int64_t o = frag(q);
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) {
+      t[jt] = *reinterpret_cast<const h8*>(thm + o + 512 * jt);
+      ea[jt] = ld_stream(reinterpret_cast<const h8*>(ep0 + o + 512 * jt));
+      eb[jt] = ld_stream(reinterpret_cast<const h8*>(ep1 + o + 512 * jt));
+    }
+  }
+  __device__ __forceinline__ void prime() {
+#pragma unroll
+    for (int u = 0; u < D - 1; ++u) issue(u, rt[u], ra[u], rb[u]);
+  }
+  template <class Mma>
+  __device__ __forceinline__ void run(Mma&& mma) {
+#pragma unroll 1
+    for (int q0 = 0; q0 < NQ; q0 += D) {
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        const int q = q0 + u;
+        const int v = (u + D - 1) % D;
+        issue(min(q + D - 1, NQ - 1), rt[v], ra[v], rb[v]);  // past the end: a re-read
+        __builtin_amdgcn_sched_barrier(0);
+        mma(q, rt[u], ra[u], rb[u]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+};
+template <int NQ, class Frag>
+__device__ __forceinline__ MfmaRing2<NQ, Frag> mfma_ring2(const _Float16* thm, const _Float16* ep0, const _Float16* ep1,
+                                                          Frag f) {
+  return MfmaRing2<NQ, Frag>{thm, ep0, ep1, f};
+}
+
+template <int E, int MODE>
+__global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_eu(2))) void core_kernel_hpm2(
+    Layout L, StepArgs a) {
+  constexpr int E2 = 2 * E, NE = 4 * E;  // envs of a pair / of the workgroup's 4 lanes
+  constexpr bool kRep = MODE == kReplay;
+  constexpr int kKs0 = kRep ? kCoreIn / 32 : 0, kNks = kGateKS - kKs0;
+  static_assert(NE <= 16 && (NE & (NE - 1)) == 0, "the workgroup's envs are the B operand's columns (mod NE)");
+  constexpr int XP = kFeat + 16, GP = kGateKS * 32 + 16;  // f16 pitches, as core_kernel_hpm
+  constexpr int kXBytes = NE * XP * 2, kGBytes = kGates * NE * 4;
+  __shared__ __attribute__((aligned(16))) char xg[kXBytes > kGBytes ? kXBytes : kGBytes];
+  __shared__ __attribute__((aligned(16))) _Float16 gh[NE * GP];
+  __shared__ float hs[kHid * NE];
+  __shared__ float logit[NE * kMaxAct];
+  __shared__ float bsum[4 * kGates];               // b_ih + b_hh of the 4 lanes
+  _Float16* xh = reinterpret_cast<_Float16*>(xg);
+  float* gates = reinterpret_cast<float*>(xg);
+  const int j = threadIdx.x, w = j >> 6, l = j & 63;
+  const int u = j & (kHid - 1), hf = j >> 8;       // cell / BN roles: hidden unit u of pair hf's envs
+  const int l0 = 4 * blockIdx.x;
+  auto pkl = [&](int li) { return a.pack + (int64_t)(l0 + li) * a.pack_stride; };
+  const _Float16* ep0 = a.epm + (int64_t)(2 * blockIdx.x) * kMImg;
+  const _Float16* ep1 = ep0 + kMImg;
+  // wave w: fc column tiles 2w, 2w + 1; gate column tiles 8w .. 8w + 7, two at a time
+  auto fc_ring = mfma_ring2<kFcKS>(a.thm, ep0, ep1, [w, l](int q) { return ((int64_t)(q * kFcNT + 2 * w) * 64 + l) * 8; });
+  auto gate_ring = mfma_ring2<4 * kNks>(a.thm + kFcImg, ep0 + kFcImg, ep1 + kFcImg, [w, l](int q) {
+    const int g = q / kNks, ks = kKs0 + q - g * kNks;
+    return ((int64_t)(ks * kGateNT + 8 * w + 2 * g) * 64 + l) * 8;
+  });
+  if constexpr (kRep)
+    gate_ring.prime();
+  else
+    fc_ring.prime();
+  const int64_t e0 = (int64_t)l0 * E;
+  const int ep_ = hf * E2;  // this thread's first env in the workgroup (cell / BN roles)
+  float gxv[kRep ? E2 : 1][4];
+  if constexpr (kRep) {
+    const float* g = a.gx + ((int64_t)(a.t - a.gx_t0) * a.n_lanes * E + e0 + ep_) * kGates + u;
+#pragma unroll
+    for (int e = 0; e < E2; ++e)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gxv[e][q] = g[(int64_t)e * kGates + q * kHid];
+  }
+  const int8_t* sgp = a.sign ? a.sign + l0 : reinterpret_cast<const int8_t*>(a.pack);  // branch-free
+  const int8_t sg0 = sgp[0], sg1 = sgp[1], sg2 = sgp[2], sg3 = sgp[3];
+  const int A = a.n_act;
+  // this lane's B column: env benv of the workgroup (lane bl, pair bl / 2); S X flips the minus lanes' columns and
+  // the two E operands see only their own pair's columns
+  const int benv = (l & 15) & (NE - 1), bl = benv / E;
+  const int8_t bsg = bl == 0 ? sg0 : (bl == 1 ? sg1 : (bl == 2 ? sg2 : sg3));
+  const unsigned smask = (a.sign && bsg < 0) ? 0x80008000u : 0u;
+  const unsigned ma = bl < 2 ? ~0u : 0u, mb = ~ma;
+  auto bfrag = [&](const _Float16* rowp, int k0, h8& x, h8& xa, h8& xb) {
+    x = *reinterpret_cast<const h8*>(rowp + k0 + 8 * (l >> 4));
+    const u32x4 sx = __builtin_bit_cast(u32x4, x) ^ u32x4{smask, smask, smask, smask};
+    xa = __builtin_bit_cast(h8, sx & u32x4{ma, ma, ma, ma});
+    xb = __builtin_bit_cast(h8, sx & u32x4{mb, mb, mb, mb});
+  };
+
+  float cj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    gh[(ep_ + e) * GP + kCoreIn + u] = (_Float16)a.h[(e0 + ep_ + e) * kHid + u];
+    cj[e] = a.c[(e0 + ep_ + e) * kHid + u];
+  }
+  for (int i = j; i < NE * (GP - kGateK); i += 2 * kCoreThreads) {
+    const int e = i / (GP - kGateK);
+    gh[e * GP + kGateK + i - e * (GP - kGateK)] = (_Float16)0.f;
+  }
+#pragma unroll
+  for (int it = 0; it < 4 * kGates / (2 * kCoreThreads); ++it) {
+    const int i = j + it * 2 * kCoreThreads, li = i / kGates, col = i & (kGates - 1);
+    const float* pk = pkl(li);
+    bsum[i] = pk[L.lstm_bih + col] + pk[L.lstm_bhh + col];
+  }
+  if constexpr (kRep) {
+    if (j < NE) gh[j * GP + kHid] = (_Float16)0.f;  // W_ih's reward row: its product is inside a.gx
+  } else {
+  float4 fcb[2];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt)
+    fcb[jt] = *reinterpret_cast<const float4*>(pkl(bl) + L.fc_b + 16 * (2 * w + jt) + 4 * (l >> 4));
+  const bool has_m = a.bn_mean != nullptr, has_v = a.bn_var != nullptr;
+  const float* bmp = has_m ? a.bn_mean + L.bn_stat[15] : a.pack;
+  const float* bvp = has_v ? a.bn_var + L.bn_stat[15] : a.pack;
+  typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+  static_assert(kFeat == 4 * 2 * kCoreThreads, "BN1d prologue: 4 features per thread");
+  {
+    const int k = 4 * j;
+    float rm[4], rv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float rmv = bmp[k + c], rvv = bvp[k + c];
+      rm[c] = has_m ? rmv : 0.f;
+      rv[c] = has_v ? rvv : 1.f;
+    }
+    float4 f[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) f[e] = *reinterpret_cast<const float4*>(a.feat + (e0 + e) * kFeat + k);
+#pragma unroll
+    for (int li = 0; li < 4; ++li) {
+      const float* pk = pkl(li);
+      const float4 w4 = *reinterpret_cast<const float4*>(pk + L.bn_w[15] + k);
+      const float4 b4 = *reinterpret_cast<const float4*>(pk + L.bn_b[15] + k);
+      float sc[4], sh[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        sc[c] = w4[c] * (1.f / sqrtf(rv[c] + kBnEps));
+        sh[c] = b4[c] - rm[c] * sc[c];
+      }
+#pragma unroll
+      for (int e = li * E; e < li * E + E; ++e)
+        *reinterpret_cast<h4v*>(xh + e * XP + k) =
+            h4v{(_Float16)fmaf(f[e][0], sc[0], sh[0]), (_Float16)fmaf(f[e][1], sc[1], sh[1]),
+                (_Float16)fmaf(f[e][2], sc[2], sh[2]), (_Float16)fmaf(f[e][3], sc[3], sh[3])};
+    }
+  }
+  float* ci = a.ci ? a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn : nullptr;
+  {
+    const float r = fminf(fmaxf(a.rprev[e0 + (j & (NE - 1))], -1.f), 1.f);  // every thread loads: no branch
+    if (j < NE) {
+      gh[j * GP + kHid] = (_Float16)r;
+      if (ci) ci[j * kCoreIn + kHid] = r;
+    }
+  }
+  __syncthreads();
+  {  // fc
+    f32x4 acc[2];
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const _Float16* xrow = xh + benv * XP;
+    fc_ring.run([&](int q, const h8 (&tf)[2], const h8 (&fa)[2], const h8 (&fb)[2]) {
+      h8 x, xa, xb;
+      bfrag(xrow, 32 * q, x, xa, xb);
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(tf[jt], x, acc[jt], 0, 0, 0);
+        acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[jt], xa, acc[jt], 0, 0, 0);
+        acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[jt], xb, acc[jt], 0, 0, 0);
+      }
+    });
+    gate_ring.prime();
+    if ((l & 15) < NE) {
+      const int e = l & 15;
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = 16 * (2 * w + jt) + 4 * (l >> 4) + i;
+          const float y = relu(acc[jt][i] + fcb[jt][i]);
+          gh[e * GP + n] = (_Float16)y;
+          if (ci) ci[e * kCoreIn + n] = y;
+        }
+    }
+  }
+  }  // !kRep
+  __syncthreads();
+  {  // gates
+    f32x4 acc[2];
+    const _Float16* grow = gh + benv * GP;
+    gate_ring.run([&](int q, const h8 (&tf)[2], const h8 (&fa)[2], const h8 (&fb)[2]) {
+      const int g = q / kNks, ks = kKs0 + q - g * kNks;
+      if (ks == kKs0)
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      h8 x, xa, xb;
+      bfrag(grow, 32 * ks, x, xa, xb);
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(tf[jt], x, acc[jt], 0, 0, 0);
+        acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[jt], xa, acc[jt], 0, 0, 0);
+        acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[jt], xb, acc[jt], 0, 0, 0);
+      }
+      if (ks == kGateKS - 1 && (l & 15) < NE) {
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            gates[(16 * (8 * w + 2 * g + jt) + 4 * (l >> 4) + i) * NE + (l & 15)] = acc[jt][i];
+      }
+    });
+  }
+  __syncthreads();
+  float hj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    const int we = ep_ + e;  // the env in the workgroup; its lane we / E
+    float pre[4];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int col = g * kHid + u;
+      pre[g] = gates[col * NE + we] + bsum[(we / E) * kGates + col];
+      if constexpr (kRep) pre[g] += gxv[e][g];
+    }
+    auto sg = [](float x) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x)); };
+    const float gi = sg(pre[0]), gf = sg(pre[1]), gg = tanh_fast(pre[2]), go = sg(pre[3]);
+    cj[e] = gf * cj[e] + gi * gg;
+    hj[e] = go * tanh_fast(cj[e]);
+    a.h[(e0 + we) * kHid + u] = hj[e];
+    a.c[(e0 + we) * kHid + u] = cj[e];
+  }
+  {
+    const float rmv = (a.bn_mean ? a.bn_mean + L.bn_stat[16] : a.pack)[u];  // branch-free
+    const float rvv = (a.bn_var ? a.bn_var + L.bn_stat[16] : a.pack)[u];
+    const float rm = a.bn_mean ? rmv : 0.f, rv = a.bn_var ? rvv : 1.f;
+#pragma unroll
+    for (int h2i = 0; h2i < 2; ++h2i) {  // the pair's two lanes
+      const float* pk = pkl(2 * hf + h2i);
+      const float sc = pk[L.bn_w[16] + u] * (1.f / sqrtf(rv + kBnEps));
+      const float sh = pk[L.bn_b[16] + u] - rm * sc;
+#pragma unroll
+      for (int e = 0; e < E; ++e) hs[u * NE + ep_ + h2i * E + e] = fmaf(hj[h2i * E + e], sc, sh);
+    }
+  }
+  __syncthreads();
+  if (j < A * NE) {
+    const int ai = j / NE, e = j - ai * NE;
+    const float* pk = pkl(e / E);
+    const float* wh = pk + L.head_w + ai * kHid;
+    float s = 0.f;
+    for (int k = 0; k < kHid; ++k) s = fmaf(wh[k], hs[k * NE + e], s);
+    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
+  }
+  __syncthreads();
+  if (j < NE) core_finish<E, MODE>(a, logit + (j / E) * E * kMaxAct, l0 + j / E, j % E);
+}
+template __global__ void core_kernel_hpm2<1, kRollout>(Layout, StepArgs);
+template __global__ void core_kernel_hpm2<2, kRollout>(Layout, StepArgs);
+template __global__ void core_kernel_hpm2<4, kRollout>(Layout, StepArgs);
+template __global__ void core_kernel_hpm2<1, kReplay>(Layout, StepArgs);
+template __global__ void core_kernel_hpm2<2, kReplay>(Layout, StepArgs);
+template __global__ void core_kernel_hpm2<4, kReplay>(Layout, StepArgs);
 
 // Entropy replay, input projection of one chunk in the fp16 pair form on MFMA: gx = theta X + s (E X) with the
 // gate images' k-steps 0 .. 8 (rows 0 .. 287 = W_ih^T's 257 rows; X is zero beyond k = 256) -- the per-lane

@@ -43,8 +43,10 @@ class Context(object):
         check(lib.fdr_ctx_set_replay_gemm(self.handle, 1 if on else 0), "fdr_ctx_set_replay_gemm")
 
     def set_core_mfma(self, on):
-        """fp16 pair-form Impala core step: MFMA (True, default) or the VALU form (False)."""
-        check(lib.fdr_ctx_set_core_mfma(self.handle, 1 if on else 0), "fdr_ctx_set_core_mfma")
+        """fp16 pair-form Impala core step: 2 / True (default) MFMA with two pairs per workgroup, 1 MFMA with one pair
+        per workgroup (bit-identical), 0 / False the VALU form."""
+        mode = 2 if on is True else (0 if on is False else int(on))
+        check(lib.fdr_ctx_set_core_mfma(self.handle, mode), "fdr_ctx_set_core_mfma")
 
     def set_conv_h2(self, mode):
         """fp16 Impala conv stack: 1 / True = conv_kernel_h2<256> (two 4-wave workgroups per CU), 2 =

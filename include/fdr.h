@@ -105,9 +105,11 @@ int fdr_ctx_device(const fdr_ctx* ctx);
 /* per-context settings (ctx = NULL: the default context) */
 int fdr_ctx_set_rollout_impl(fdr_ctx* ctx, int32_t impl);  /* FDR_ROLLOUT_* below */
 int fdr_ctx_set_replay_gemm(fdr_ctx* ctx, int32_t on);     /* see fdr_impala_set_replay_gemm */
-/* fp16 pair-form Impala core step (fdr_impala_desc.fp16 && .pairs): 1 (default) = fc / LSTM GEMMs on
+/* fp16 pair-form Impala core step (fdr_impala_desc.fp16 && .pairs): 2 (default) = fc / LSTM GEMMs on
    v_mfma_f32_16x16x32_f16 as theta X + E (S X) over MFMA-fragment images of theta and each pair's sigma-eps
-   (activations rounded to f16); 0 = the VALU form (w = f16(theta) + s f16(sigma eps) formed per element) */
+   (activations rounded to f16), two pairs per workgroup (theta's fragments read once for both; needs n_lanes % 4 == 0,
+   else 1); 1 = the same, one pair per workgroup (bit-identical results); 0 = the VALU form (w = f16(theta) +
+   s f16(sigma eps) formed per element).  Default context: FDR_CORE_MFMA (0 / 1 / 2) or 2 */
 int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on);
 /* fp16 Impala conv stack (rollout, forward, strategies), identical features in every mode:
    2 (default) = conv_kernel_h2<512>: 8 waves, 80 KiB LDS, 128 VGPRs, two workgroups per CU;

@@ -357,6 +357,32 @@ def test_fp16_pair_core_matches_per_lane_core(engine, table):
     np.testing.assert_allclose(outs["pair"].entropy.cpu().numpy(), outs["f32"].entropy.cpu().numpy(), rtol=F16_RTOL)
 
 
+@pytest.mark.parametrize("E,n_pairs", [(4, 4), (4, 3), (1, 6), (2, 2)])
+def test_fp16_two_pairs_per_workgroup_bit_identical(engine, table, E, n_pairs):
+    """core_mfma 2 (core_kernel_hpm2, the default: two pairs per 8-wave workgroup, theta's fragments read once for
+    both, three MFMAs per tile and k-step) against core_mfma 1 (core_kernel_hpm, one pair per workgroup): a masked
+    B column adds exact zeros, so whole recorded episodes with the entropy replay are BITWISE equal -- actions,
+    probabilities, returns, entropies, norms.  3 pairs (6 lanes, n_lanes % 4 == 2) take the one-pair kernel."""
+    A, T = 5, 70
+    theta = _theta(A)
+    offs = np.array([77, 2_000_000, 3_000_000, 4_500_000, 1_111_111, 999], np.int64)[:n_pairs]
+    idx = np.repeat(offs, 2)
+    sign = np.tile(np.array([1, -1], np.int8), n_pairs)
+    dev = "cuda"
+    lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
+                              torch.tensor(idx, device=dev), torch.tensor(sign, device=dev), 0.02)
+    spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=True, pairs=True)
+    outs = []
+    for mode in (1, 2):
+        ctx = engine.Context()
+        ctx.set_core_mfma(mode)
+        outs.append(engine.impala_rollout(spec, lanes, len(idx), 11, record=True, ctx=ctx))
+    torch.cuda.synchronize()
+    for f in ("actions", "probs", "reward", "entropy", "norm2"):
+        np.testing.assert_array_equal(getattr(outs[0], f).cpu().numpy(), getattr(outs[1], f).cpu().numpy(), err_msg=f)
+    assert np.all(np.isfinite(outs[1].entropy.cpu().numpy()))
+
+
 def test_f32_pair_core_bit_identical(engine, table):
     """f32 pair form (fdr_impala_desc.pairs): w = fl32(theta + s fl32(sigma eps)) formed in registers is the
     per-lane pack's value bit for bit, and every env keeps core_kernel's fma chains -- whole episodes with the
