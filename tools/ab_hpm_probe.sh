@@ -1,6 +1,8 @@
 #!/bin/bash
 # Diagnostics A/B of the fp16 pair core stream (core_kernel_hpm): the product library against FDR_HPM_PROBE builds
-# (1: no theta loads, 2: no HBM stream).  Usage (GPU box): bash tools/ab_hpm_probe.sh -> gpurun_out/abh_<lib>.log
+# (1: no theta loads, 2: no HBM stream).  Build them first (container):
+#   make -C dfd-starter_amd/csrc variant VSRC=fdr_impala_h VFLAGS=-DFDR_HPM_PROBE=1 VOUT=../fdr/libfdr_hpm1.so  (and =2)
+# Usage (GPU box): bash tools/ab_hpm_probe.sh -> gpurun_out/abh_<lib>.log
 set -u
 mkdir -p gpurun_out
 for rep in 1 2; do
