@@ -1437,13 +1437,6 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
 #pragma unroll
   for (int m = 0; m < (DISC ? 1 : NA); ++m) kr[m] = mrow[NX + m];
   int tb = 0;
-#ifdef FDR_DEPHASE  // experiment: the second wave of each SIMD starts late (HW_ID wave slot), de-phasing the step chains
-  {
-    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-    if (hw & 1u)
-      for (int k = 0; k < FDR_DEPHASE; ++k) __builtin_amdgcn_s_sleep(8);
-  }
-#endif
 #ifdef FDR_PHASE_STAMPS
   uint64_t ph_acc[5] = {0, 0, 0, 0, 0};
   uint64_t ph_last = 0;
