@@ -638,20 +638,30 @@ __global__ __launch_bounds__(kConvThreads) void conv_kernel(Layout L, StepArgs a
   float bf3[7];
   load_frag<3, 1>(pk + L.conv_w[0], bf3, wave, ln);
   FDR_STAMP(a, 0);
-  // eval-mode BN folded per channel: y = x * (w / sqrt(rv + eps)) + (b - rm * scale)
-  for (int i = threadIdx.x; i < kBnTab; i += kConvThreads) {
-    const int idx = i >> 5, ch = i & 31;
+  // eval-mode BN folded per channel: y = x * (w / sqrt(rv + eps)) + (b - rm * scale).  Branch-free (r11, as
+  // conv_kernel_h2's table): every load unconditional from a valid address, the unused values selected away after,
+  // the layout offsets as scalar loads of the wave's two table rows -- a conditional load ends its basic block
+  // with a full vmcnt wait, and the per-lane offset reads were a dependent round trip of their own
+  static_assert(kBnTab <= kConvThreads, "one table entry per thread");
+  {
+    const int i = threadIdx.x, idx = i >> 5, ch = i & 31;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hi = (threadIdx.x >> 5) & 1;
+    const int r0 = min(2 * wv, kConvs - 1), r1 = min(2 * wv + 1, kConvs - 1);  // wave-uniform rows
+    auto pick = [&](const int32_t* arr) { return hi ? arr[r1] : arr[r0]; };
+    const float* bmp = a.bn_mean ? a.bn_mean : pk;
+    const float* bvp = a.bn_var ? a.bn_var : pk;
+    const int so = pick(L.bn_stat) + ch;
+    const float rm_ = bmp[so], rv_ = bvp[so], w_ = pk[pick(L.bn_w) + ch], b_ = pk[pick(L.bn_b) + ch];
     const int nch = idx == 0 ? 3 : (idx == 5 ? 16 : (idx < 5 ? 16 : 32));
-    float sc = 0.f, sh = 0.f;
-    if (ch < nch) {
-      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[idx] + ch] : 0.f;
-      const float rv = a.bn_var ? a.bn_var[L.bn_stat[idx] + ch] : 1.f;
-      const float inv = 1.f / sqrtf(rv + kBnEps);
-      sc = pk[L.bn_w[idx] + ch] * inv;
-      sh = pk[L.bn_b[idx] + ch] - rm * sc;
+    const bool live = i < kBnTab && ch < nch;
+    const float rm = a.bn_mean ? rm_ : 0.f, rv = a.bn_var ? rv_ : 1.f;
+    const float inv = 1.f / sqrtf(rv + kBnEps);
+    const float sc = live ? w_ * inv : 0.f;
+    const float sh = live ? b_ - rm * sc : 0.f;
+    if (i < kBnTab) {
+      bsc[i] = sc;
+      bsh[i] = sh;
     }
-    bsc[i] = sc;
-    bsh[i] = sh;
   }
   for (int i = threadIdx.x; i < kGuard + 3 * FPLANE; i += kConvThreads) lds[i] = 0.f;
   __syncthreads();
@@ -752,10 +762,11 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
 
   if constexpr (!seq_mode(MODE)) {
     for (int k = j; k < kFeat; k += kCoreThreads) {
-      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + k] : 0.f;
-      const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + k] : 1.f;
+      const float rmv = (a.bn_mean ? a.bn_mean + L.bn_stat[15] : a.pack)[k];  // branch-free
+      const float rvv = (a.bn_var ? a.bn_var + L.bn_stat[15] : a.pack)[k];
+      const float rm = a.bn_mean ? rmv : 0.f, rv = a.bn_var ? rvv : 1.f;
       const float sc = pk[L.bn_w[15] + k] * (1.f / sqrtf(rv + kBnEps));
-      const float sh = pk[L.bn_b[15] + k] - rm * sc;
+      const float sh = fmaf(-rm, sc, pk[L.bn_b[15] + k]);
 #pragma unroll
       for (int e = 0; e < E; ++e) xw[k * E + e] = fmaf(a.feat[(e0 + e) * kFeat + k], sc, sh);
     }
@@ -880,17 +891,17 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel(Layout L, StepArgs a
     const float gf = sigm(xw[(kHid + j) * E + e]);
     const float gg = tanhf(xw[(2 * kHid + j) * E + e]);
     const float go = sigm(xw[(3 * kHid + j) * E + e]);
-    cj[e] = gf * cj[e] + gi * gg;
+    cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
     hj[e] = go * tanhf(cj[e]);
     a.h[(e0 + e) * kHid + j] = hj[e];
     a.c[(e0 + e) * kHid + j] = cj[e];
   }
   {
-
-    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
-    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
+    const float rmv = (a.bn_mean ? a.bn_mean + L.bn_stat[16] : pk)[j];  // branch-free (see conv_kernel's table)
+    const float rvv = (a.bn_var ? a.bn_var + L.bn_stat[16] : pk)[j];
+    const float rm = a.bn_mean ? rmv : 0.f, rv = a.bn_var ? rvv : 1.f;
     const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
-    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+    const float sh = fmaf(-rm, sc, pk[L.bn_b[16] + j]);
 #pragma unroll
     for (int e = 0; e < E; ++e) hs[j * E + e] = fmaf(hj[e], sc, sh);
   }
@@ -961,7 +972,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_p(Layout L, StepArgs
     for (int hf = 0; hf < 2; ++hf) {
       const float* pk = hf ? pk1 : pk0;
       const float sc = pk[L.bn_w[15] + k] * (1.f / sqrtf(rv + kBnEps));
-      const float sh = pk[L.bn_b[15] + k] - rm * sc;
+      const float sh = fmaf(-rm, sc, pk[L.bn_b[15] + k]);
 #pragma unroll
       for (int e = 0; e < E; ++e) xw[k * E2 + hf * E + e] = fmaf(a.feat[(e0 + hf * E + e) * kFeat + k], sc, sh);
     }
@@ -1042,7 +1053,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_p(Layout L, StepArgs
     const float gf = sigm(xw[(kHid + j) * E2 + e]);
     const float gg = tanhf(xw[(2 * kHid + j) * E2 + e]);
     const float go = sigm(xw[(3 * kHid + j) * E2 + e]);
-    cj[e] = gf * cj[e] + gi * gg;
+    cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
     hj[e] = go * tanhf(cj[e]);
     a.h[(e0 + e) * kHid + j] = hj[e];
     a.c[(e0 + e) * kHid + j] = cj[e];
@@ -1050,10 +1061,11 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_p(Layout L, StepArgs
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
     const float* pk = hf ? pk1 : pk0;
-    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
-    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
+    const float rmv = (a.bn_mean ? a.bn_mean + L.bn_stat[16] : pk)[j];  // branch-free (see conv_kernel's table)
+    const float rvv = (a.bn_var ? a.bn_var + L.bn_stat[16] : pk)[j];
+    const float rm = a.bn_mean ? rmv : 0.f, rv = a.bn_var ? rvv : 1.f;
     const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
-    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+    const float sh = fmaf(-rm, sc, pk[L.bn_b[16] + j]);
 #pragma unroll
     for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
   }
@@ -1138,7 +1150,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_pr(Layout L, StepArg
     const float gf = sigm(xw[(kHid + j) * E2 + e]);
     const float gg = tanhf(xw[(2 * kHid + j) * E2 + e]);
     const float go = sigm(xw[(3 * kHid + j) * E2 + e]);
-    cj[e] = gf * cj[e] + gi * gg;
+    cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
     hj[e] = go * tanhf(cj[e]);
     a.h[(e0 + e) * kHid + j] = hj[e];
     a.c[(e0 + e) * kHid + j] = cj[e];
@@ -1147,10 +1159,11 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_pr(Layout L, StepArg
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
     const float* pk = hf ? pk1 : pk0;
-    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
-    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
+    const float rmv = (a.bn_mean ? a.bn_mean + L.bn_stat[16] : pk)[j];  // branch-free (see conv_kernel's table)
+    const float rvv = (a.bn_var ? a.bn_var + L.bn_stat[16] : pk)[j];
+    const float rm = a.bn_mean ? rmv : 0.f, rv = a.bn_var ? rvv : 1.f;
     const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
-    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+    const float sh = fmaf(-rm, sc, pk[L.bn_b[16] + j]);
 #pragma unroll
     for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
   }
@@ -1645,10 +1658,11 @@ __global__ __launch_bounds__(256) void fc_rows_kernel(Layout L, StepArgs a, int 
     for (int tj = 0; tj < 4; ++tj) acc[ti][tj] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int k0 = 0; k0 < kFeat; k0 += KC) {
     const int kk = k0 + (tid & 31);  // every X element this thread loads has this k
-    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + kk] : 0.f;
-    const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + kk] : 1.f;
+    const float rmv = (a.bn_mean ? a.bn_mean + L.bn_stat[15] : a.pack)[kk];  // branch-free
+    const float rvv = (a.bn_var ? a.bn_var + L.bn_stat[15] : a.pack)[kk];
+    const float rm = a.bn_mean ? rmv : 0.f, rv = a.bn_var ? rvv : 1.f;
     const float sc = pk[L.bn_w[15] + kk] * (1.f / sqrtf(rv + kBnEps));
-    const float sh = pk[L.bn_b[15] + kk] - rm * sc;
+    const float sh = fmaf(-rm, sc, pk[L.bn_b[15] + kk]);
 #pragma unroll
     for (int m = 0; m < 8; ++m) {
       const int i = tid + 256 * m, row = i >> 5, q = row0 + row;

@@ -1936,7 +1936,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
       const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + k] : 0.f;
       const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + k] : 1.f;
       const float sc = pk[L.bn_w[15] + k] * (1.f / sqrtf(rv + kBnEps));
-      const float sh = pk[L.bn_b[15] + k] - rm * sc;
+      const float sh = fmaf(-rm, sc, pk[L.bn_b[15] + k]);
 #pragma unroll
       for (int e = 0; e < E; ++e) xw[k * E + e] = fmaf(a.feat[(e0 + e) * kFeat + k], sc, sh);
     }
@@ -2075,7 +2075,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
       pre[g] = (xw[col * E + e] + pk[L.lstm_bih + col]) + (xw[(kGates + col) * E + e] + pk[L.lstm_bhh + col]);
     }
     const float gi = sigm(pre[0]), gf = sigm(pre[1]), gg = tanhf(pre[2]), go = sigm(pre[3]);
-    cj[e] = gf * cj[e] + gi * gg;
+    cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
     hj[e] = go * tanhf(cj[e]);
     a.h[(e0 + e) * kHid + j] = hj[e];
     a.c[(e0 + e) * kHid + j] = cj[e];
@@ -2084,7 +2084,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
     const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
     const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
     const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
-    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+    const float sh = fmaf(-rm, sc, pk[L.bn_b[16] + j]);
 #pragma unroll
     for (int e = 0; e < E; ++e) hs[j * E + e] = fmaf(hj[e], sc, sh);
   }
@@ -2133,7 +2133,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_hp(Layout L, StepArg
       const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + k] : 0.f;
       const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + k] : 1.f;
       const float sc = pk[L.bn_w[15] + k] * (1.f / sqrtf(rv + kBnEps));
-      const float sh = pk[L.bn_b[15] + k] - rm * sc;
+      const float sh = fmaf(-rm, sc, pk[L.bn_b[15] + k]);
 #pragma unroll
       for (int e = 0; e < E; ++e)
         xw[k * E2 + hf * E + e] = fmaf(a.feat[(e0 + hf * E + e) * kFeat + k], sc, sh);
@@ -2238,7 +2238,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_hp(Layout L, StepArg
       pre[g] = (xw[col * E2 + e] + pk[L.lstm_bih + col]) + (xw[(kGates + col) * E2 + e] + pk[L.lstm_bhh + col]);
     }
     const float gi = sigm(pre[0]), gf = sigm(pre[1]), gg = tanhf(pre[2]), go = sigm(pre[3]);
-    cj[e] = gf * cj[e] + gi * gg;
+    cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
     hj[e] = go * tanhf(cj[e]);
     a.h[(e0 + e) * kHid + j] = hj[e];
     a.c[(e0 + e) * kHid + j] = cj[e];
@@ -2249,7 +2249,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_hp(Layout L, StepArg
     const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
     const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
     const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
-    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+    const float sh = fmaf(-rm, sc, pk[L.bn_b[16] + j]);
 #pragma unroll
     for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
   }
@@ -2339,7 +2339,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_hpr(Layout L, StepAr
       pre[g] = (xw[col * E2 + e] + pk[L.lstm_bih + col]) + (xw[(kGates + col) * E2 + e] + pk[L.lstm_bhh + col]);
     }
     const float gi = sigm(pre[0]), gf = sigm(pre[1]), gg = tanhf(pre[2]), go = sigm(pre[3]);
-    cj[e] = gf * cj[e] + gi * gg;
+    cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
     hj[e] = go * tanhf(cj[e]);
     a.h[(e0 + e) * kHid + j] = hj[e];
     a.c[(e0 + e) * kHid + j] = cj[e];
@@ -2350,7 +2350,7 @@ __global__ __launch_bounds__(kCoreThreads) void core_kernel_hpr(Layout L, StepAr
     const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
     const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
     const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
-    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+    const float sh = fmaf(-rm, sc, pk[L.bn_b[16] + j]);
 #pragma unroll
     for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
   }
@@ -2658,7 +2658,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
     // under it, and the accurate expf / tanhf / IEEE division were ~1,500 instructions per thread
     auto sg = [](float x) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x)); };
     const float gi = sg(pre[0]), gf = sg(pre[1]), gg = tanh_fast(pre[2]), go = sg(pre[3]);
-    cj[e] = gf * cj[e] + gi * gg;
+    cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
     hj[e] = go * tanh_fast(cj[e]);
     a.h[(e0 + e) * kHid + j] = hj[e];
     a.c[(e0 + e) * kHid + j] = cj[e];
@@ -2670,7 +2670,7 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
     const float rvv = (a.bn_var ? a.bn_var + L.bn_stat[16] : pk0)[j];
     const float rm = a.bn_mean ? rmv : 0.f, rv = a.bn_var ? rvv : 1.f;
     const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
-    const float sh = pk[L.bn_b[16] + j] - rm * sc;
+    const float sh = fmaf(-rm, sc, pk[L.bn_b[16] + j]);
 #pragma unroll
     for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
   }
@@ -2933,7 +2933,7 @@ __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_e
     }
     auto sg = [](float x) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x)); };
     const float gi = sg(pre[0]), gf = sg(pre[1]), gg = tanh_fast(pre[2]), go = sg(pre[3]);
-    cj[e] = gf * cj[e] + gi * gg;
+    cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
     hj[e] = go * tanh_fast(cj[e]);
     a.h[(e0 + we) * kHid + u] = hj[e];
     a.c[(e0 + we) * kHid + u] = cj[e];
@@ -2946,7 +2946,7 @@ __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_e
     for (int h2i = 0; h2i < 2; ++h2i) {  // the pair's two lanes
       const float* pk = pkl(2 * hf + h2i);
       const float sc = pk[L.bn_w[16] + u] * (1.f / sqrtf(rv + kBnEps));
-      const float sh = pk[L.bn_b[16] + u] - rm * sc;
+      const float sh = fmaf(-rm, sc, pk[L.bn_b[16] + u]);
 #pragma unroll
       for (int e = 0; e < E; ++e) hs[u * NE + ep_ + h2i * E + e] = fmaf(hj[h2i * E + e], sc, sh);
     }

@@ -383,14 +383,16 @@ def test_fp16_two_pairs_per_workgroup_bit_identical(engine, table, E, n_pairs):
     assert np.all(np.isfinite(outs[1].entropy.cpu().numpy()))
 
 
-def test_f32_pair_core_bit_identical(engine, table):
+@pytest.mark.parametrize("E,n_pairs", [(4, 3), (4, 4), (1, 6), (2, 2)])
+def test_f32_pair_core_bit_identical(engine, table, E, n_pairs):
     """f32 pair form (fdr_impala_desc.pairs): w = fl32(theta + s fl32(sigma eps)) formed in registers is the
     per-lane pack's value bit for bit, and every env keeps core_kernel's fma chains -- whole episodes with the
     entropy replay are bitwise identical to the per-lane form (actions, probabilities, returns, entropies)."""
-    A, E, T = 6, 4, 40
+    A, T = 6, 40
     theta = _theta(A)
-    idx = np.repeat(np.array([77, 2_000_000, 3_000_000], np.int64), 2)
-    sign = np.tile(np.array([1, -1], np.int8), 3)
+    offs = np.array([77, 2_000_000, 3_000_000, 4_500_000, 1_111_111, 999], np.int64)[:n_pairs]
+    idx = np.repeat(offs, 2)
+    sign = np.tile(np.array([1, -1], np.int8), n_pairs)
     dev = "cuda"
     lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
                               torch.tensor(idx, device=dev), torch.tensor(sign, device=dev), 0.02)
