@@ -552,9 +552,13 @@ def main():
                                     "unit": "GB/s", "frac": round(core_gbs / HBM_PEAK_GBS, 4),
                                     "launch_ms": round(core_ms / T, 4), "bytes_per_lane_step": core_bytes,
                                     "hbm_bytes_per_launch_algorithmic": core_hbm,
-                                    "form": ("pair on MFMA: theta x + s (E x) over fragment images (core_kernel_hpm)"
-                                             if fp16 and os.environ.get("FDR_CORE_MFMA") != "0" else
-                                             "pair (theta + s sigma-eps)"),
+                                    "form": ({"0": "pair on the VALU (core_kernel_hp)",
+                                              "1": "pair on MFMA: theta x + s (E x) over fragment images, one pair per "
+                                                   "workgroup (core_kernel_hpm)"}
+                                             .get(os.environ.get("FDR_CORE_MFMA"),
+                                                  "pair on MFMA: theta x + s (E x) over fragment images, two pairs "
+                                                  "per workgroup (core_kernel_hpm2)")
+                                             if fp16 else "pair (theta + s sigma-eps)"),
                                     "traffic": None if core_prof is None else core_prof.get("hbm_bytes_per_launch")},
                     "entropy_replay_ms": round(replay_ms, 3),
                     "profile": None if prof is None else "profiles/%s_summary.md" % prof.get("tag"),
