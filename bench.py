@@ -412,6 +412,7 @@ def main():
         b_.record()
     torch.cuda.synchronize()
     cur = [None]
+    host_ms = [None]  # the timed loop's host enqueue time per step (before the closing synchronize)
 
     def fd_step(timed, n_dirs=n_dirs_global, rng=lane_range):
         timed = timed and cur[0] is not None
@@ -439,6 +440,11 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        prof = None
+        if os.environ.get("FDR_HOST_PROFILE") and not events:  # diagnostics: the host side of the timed steps
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         pairs = []
         out = None
@@ -447,6 +453,13 @@ def main():
             out, _ = fd_step(True, **kw)
             if cur[0] is not None:
                 pairs.append(cur[0])
+        t_host = time.perf_counter() - t0
+        host_ms[0] = t_host / steps * 1e3
+        if prof is not None:
+            prof.disable()
+            prof.dump_stats(os.environ["FDR_HOST_PROFILE"])
+            print("host time of the timed loop (enqueue only): %.1f us per step" % (t_host / steps * 1e6),
+                  file=sys.stderr)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -473,6 +486,7 @@ def main():
             out, _ = fd_step(False)
         settle_steps += 5
     elapsed, _, out = timed_loop(args.steps)
+    host_enqueue_ms = host_ms[0]
     # rollout-timing pass (outside the timed region): HIP events bracketing each rollout on its stream,
     # and for Impala the per-step-loop phase events of fdr_impala_profile
     if impala:
@@ -606,6 +620,7 @@ def main():
         "warmup": args.warmup, "settle_steps": settle_steps,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "sec_per_fd_step": round(elapsed / args.steps, 6),
+        "host_enqueue_ms_per_step": round(host_enqueue_ms, 4),  # < ms_per_step: the GPU, not the host, paces the job
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

@@ -90,8 +90,7 @@ class FiniteDifferences(object):
     # ------------------------------------------------------------------------------------------
     def _step_batch(self, b, policy_reward):
         table = self.noise_source.device_table(self.policy.flat.device)
-        train = torch.as_tensor(b.sign_host != 0)
-        if not bool(train.all()):
+        if not np.all(b.sign_host != 0):
             raise ValueError("FDBatch for the learner must not contain eval lanes (sign 0)")
         P = self.policy.num_params
         if not self._distributed():

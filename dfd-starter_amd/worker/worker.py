@@ -10,6 +10,8 @@ fdr_rollout launch.  theta' = theta + sign * fl32(sigma * eps) is formed inside 
 (worker.py:23) and index draws happen in the reference's order, then all n episodes run in one
 launch (eval lanes: unperturbed theta, deterministic actions, worker.py:33-35).
 """
+import os
+
 import numpy as np
 import torch
 
@@ -37,58 +39,63 @@ class Worker(object):
         self.rng = np.random.RandomState(random_seed)
         self.eval_prob = eval_prob
         self.fixed_obs_stats = WelfordRunningStat(policy.input_shape)
-        self._pinned = {}
+        self._pinned = {}      # lane count -> ring of pinned upload slots
         self._copy_stream = None
+        self._main_stream = None
+        self._lane_consts = {}  # (n_dirs, antithetic, lane_range, world, rank) -> the constant parts of _lanes_of
         self._next = None      # (key, host lanes, device lanes) uploaded ahead by evaluate(prefetch=True)
 
     # ---- hot path ---------------------------------------------------------------------------
-    def _to_device(self, arr, dtype, defer_wait=False):
-        """Async H2D through a small ring of pinned buffers on a side copy stream: the copy runs as soon as it
-        is enqueued (during the previous step's rollout, the host being ahead), and the compute stream only
-        waits on its event -- the upload is off the step's critical path.  An event guards each buffer's reuse.
-        defer_wait=True returns (tensor, event) and leaves the compute stream's wait to the consumer: a
+    def _lanes_to_device(self, idx, sign, det, defer_wait=False):
+        """The three per-lane descriptor arrays in ONE async host-to-device copy, [idx i64 | sign i8 | det i8],
+        through a ring of 4 pinned buffers (written in place) on a side copy stream: the copy runs as soon as it is
+        enqueued (during the previous step's rollout, the host being ahead), and the compute stream only waits on
+        its event -- the upload is off the step's critical path; a slot's event also guards its buffer's reuse.
+        defer_wait=True returns (arrays, copy event) and leaves the compute stream's wait to the consumer: a
         cross-stream wait enqueued behind a running kernel costs ~10 us of barrier processing when that kernel
-        ends (measured, rocprofv3 kernel trace), so it is placed right before the rollout that needs the data."""
+        ends (measured, rocprofv3 kernel trace), so it is placed right before the rollout that needs the data.
+        (Host cost ~10 us per step: the pinned slot, its event and the main stream are made once, r11.)"""
+        n = len(idx)
         dev = self.policy.flat.device
-        key = (dtype, len(arr))
-        ring = self._pinned.setdefault(key, {"bufs": [], "events": [], "next": 0})
-        if len(ring["bufs"]) < 4:
-            ring["bufs"].append(torch.empty(len(arr), dtype=dtype).pin_memory())
-            ring["events"].append(None)
-            slot = len(ring["bufs"]) - 1
+        ring = self._pinned.get(n)
+        if ring is None:
+            ring = self._pinned[n] = {"slots": [], "next": 0}
+        if len(ring["slots"]) < 4:
+            slot = {"buf": torch.empty(10 * n, dtype=torch.uint8).pin_memory(), "ev": torch.cuda.Event(),
+                    "used": False}
+            ring["slots"].append(slot)
         else:
-            slot = ring["next"]
-            ring["next"] = (slot + 1) % 4
-            if ring["events"][slot] is not None:
-                ring["events"][slot].synchronize()
-        buf = ring["bufs"][slot]
-        buf.numpy()[:] = arr
-        main = torch.cuda.current_stream(dev)
+            slot = ring["slots"][ring["next"]]
+            ring["next"] = (ring["next"] + 1) % 4
+            if slot["used"]:
+                slot["ev"].synchronize()  # its previous copy has left the pinned buffer
+        h = slot["buf"].numpy()
+        h[:8 * n].view(np.int64)[:] = idx
+        h[8 * n:9 * n].view(np.int8)[:] = sign
+        h[9 * n:].view(np.int8)[:] = det
+        if os.environ.get("FDR_LANES_UPLOAD") == "inline":  # experiment: the copy on the compute stream itself
+            if "dev" not in slot:
+                slot["dev"] = torch.empty(10 * n, dtype=torch.uint8, device=dev)
+            d = slot["dev"]
+            d.copy_(slot["buf"], non_blocking=True)  # stream order guards the device slot's reuse
+            ev = slot["ev"]
+            ev.record()
+            slot["used"] = True
+            arrs = (d[:8 * n].view(torch.int64), d[8 * n:9 * n].view(torch.int8), d[9 * n:].view(torch.int8))
+            return (arrs, ev) if defer_wait else arrs
         if self._copy_stream is None:
             self._copy_stream = torch.cuda.Stream(dev)
+            self._main_stream = torch.cuda.current_stream(dev)
+        main = self._main_stream if torch.cuda.current_stream(dev) == self._main_stream \
+            else torch.cuda.current_stream(dev)
         with torch.cuda.stream(self._copy_stream):
-            out = buf.to(dev, non_blocking=True)
-        ev = torch.cuda.Event()
+            d = slot["buf"].to(dev, non_blocking=True)
+        ev = slot["ev"]
         ev.record(self._copy_stream)
-        out.record_stream(main)
-        ring["events"][slot] = ev
-        if defer_wait:
-            return out, ev
-        main.wait_event(ev)
-        return out
-
-    def _lanes_to_device(self, idx, sign, det, defer_wait=False):
-        """The three per-lane descriptor arrays in ONE host-to-device copy: [idx i64 | sign i8 | det i8].
-        defer_wait: (arrays, copy event) -- the caller makes the compute stream wait on the event."""
-        n = len(idx)
-        packed = np.empty(10 * n, np.uint8)
-        packed[:8 * n] = np.asarray(idx, np.int64).view(np.uint8)
-        packed[8 * n:9 * n] = np.asarray(sign, np.int8).view(np.uint8)
-        packed[9 * n:] = np.asarray(det, np.int8).view(np.uint8)
-        d = self._to_device(packed, torch.uint8, defer_wait)
-        ev = None
-        if defer_wait:
-            d, ev = d
+        slot["used"] = True
+        d.record_stream(main)
+        if not defer_wait:
+            main.wait_event(ev)
         arrs = (d[:8 * n].view(torch.int64), d[8 * n:9 * n].view(torch.int8), d[9 * n:].view(torch.int8))
         return (arrs, ev) if defer_wait else arrs
 
@@ -140,27 +147,40 @@ class Worker(object):
 
     def _lanes_of(self, idx, n_dirs, antithetic, lane_range):
         """Host lane arrays of one evaluate() call from its direction indices: (lidx, sign, det, lane_range,
-        rank_lanes)."""
+        rank_lanes).  Everything but lidx depends only on the call's shape and the process group: computed once
+        (sign / det are shared read-only arrays)."""
         lpd = 2 if antithetic else 1
-        rank_lanes = None
-        d_lo, d_hi = 0, n_dirs
+        world, rank = (1, 0)
         if lane_range is not None:
             from fdr import dist as fdist
             world, rank = fdist.world_rank()
-            std = fdist.lane_range(n_dirs, lpd, world, rank)
-            if lane_range == "auto":
-                lane_range = std
-            if tuple(lane_range) == std:  # the standard split: every rank's lane count is known
-                rank_lanes = [hi - lo for lo, hi in (fdist.lane_range(n_dirs, lpd, world, k) for k in range(world))]
-            lo, hi = lane_range
-            if lo % lpd or hi % lpd:
-                raise ValueError("lane_range must not split antithetic pairs")
-            d_lo, d_hi = lo // lpd, hi // lpd
+        ckey = (int(n_dirs), bool(antithetic), lane_range if lane_range is None or lane_range == "auto"
+                else tuple(lane_range), world, rank)
+        c = self._lane_consts.get(ckey)
+        if c is None:
+            rank_lanes = None
+            d_lo, d_hi = 0, n_dirs
+            if lane_range is not None:
+                from fdr import dist as fdist
+                std = fdist.lane_range(n_dirs, lpd, world, rank)
+                if lane_range == "auto":
+                    lane_range = std
+                if tuple(lane_range) == std:  # the standard split: every rank's lane count is known
+                    rank_lanes = [hi - lo for lo, hi in (fdist.lane_range(n_dirs, lpd, world, k) for k in range(world))]
+                lo, hi = lane_range
+                if lo % lpd or hi % lpd:
+                    raise ValueError("lane_range must not split antithetic pairs")
+                d_lo, d_hi = lo // lpd, hi // lpd
+            nd = d_hi - d_lo
+            sign = np.tile(np.array([1, -1], np.int8), nd) if antithetic else np.ones(nd, np.int8)
+            det = np.zeros(nd * lpd, np.int8)
+            sign.setflags(write=False)
+            det.setflags(write=False)
+            c = self._lane_consts[ckey] = (d_lo, d_hi, sign, det, lane_range, rank_lanes)
+        d_lo, d_hi, sign, det, lane_range, rank_lanes = c
         # only this rank's directions are expanded to lanes (at N = 8 one eighth of the stream)
-        nd = d_hi - d_lo
         lidx = np.repeat(idx[d_lo:d_hi], lpd)
-        sign = np.tile(np.array([1, -1], np.int8), nd) if antithetic else np.ones(nd, np.int8)
-        return lidx, sign, np.zeros(len(lidx), np.int8), lane_range, rank_lanes
+        return lidx, sign, det, lane_range, rank_lanes
 
     def evaluate(self, n_dirs, antithetic=True, seed=None, lane_range=None, out=None, novelty=False, prefetch=False,
                  timing=None):
@@ -181,7 +201,11 @@ class Worker(object):
         lanes_dev = None
         if pre is not None and pre[0] == key and np.array_equal(pre[1], lidx):
             lanes_dev, ev = pre[2]
-            torch.cuda.current_stream(self.policy.flat.device).wait_event(ev)  # right before the rollout
+            # the upload was enqueued a step ago and has normally completed: then the rollout needs no device-side
+            # wait at all (a cross-stream wait costs ~10 us of barrier processing before the rollout starts, every
+            # step -- rocprofv3 trace); only a copy still in flight is waited for on the compute stream
+            if os.environ.get("FDR_PREFETCH_WAIT") == "always" or not ev.query():
+                torch.cuda.current_stream(self.policy.flat.device).wait_event(ev)
         lpd = 2 if antithetic else 1
         lo = 0 if lane_range is None else lane_range[0]
         res, idx_d, sign_d = self.launch(lidx, sign, det, seed=seed, out=out, lane_offset=lo, lanes_dev=lanes_dev,
