@@ -73,16 +73,6 @@ class Worker(object):
         h[:8 * n].view(np.int64)[:] = idx
         h[8 * n:9 * n].view(np.int8)[:] = sign
         h[9 * n:].view(np.int8)[:] = det
-        if os.environ.get("FDR_LANES_UPLOAD") == "inline":  # experiment: the copy on the compute stream itself
-            if "dev" not in slot:
-                slot["dev"] = torch.empty(10 * n, dtype=torch.uint8, device=dev)
-            d = slot["dev"]
-            d.copy_(slot["buf"], non_blocking=True)  # stream order guards the device slot's reuse
-            ev = slot["ev"]
-            ev.record()
-            slot["used"] = True
-            arrs = (d[:8 * n].view(torch.int64), d[8 * n:9 * n].view(torch.int8), d[9 * n:].view(torch.int8))
-            return (arrs, ev) if defer_wait else arrs
         if self._copy_stream is None:
             self._copy_stream = torch.cuda.Stream(dev)
             self._main_stream = torch.cuda.current_stream(dev)
