@@ -46,44 +46,63 @@ class Worker(object):
         self._next = None      # (key, host lanes, device lanes) uploaded ahead by evaluate(prefetch=True)
 
     # ---- hot path ---------------------------------------------------------------------------
+    _RING = 64  # upload slots per lane count: an FDBatch's device idx / sign stay valid for the next 63 uploads
+    _GEN = 8    # one compute-stream event per 8 uploads bounds slot reuse (_RING >= 2 * _GEN)
+
     def _lanes_to_device(self, idx, sign, det, defer_wait=False):
-        """The three per-lane descriptor arrays in ONE async host-to-device copy, [idx i64 | sign i8 | det i8],
-        through a ring of 4 pinned buffers (written in place) on a side copy stream: the copy runs as soon as it is
-        enqueued (during the previous step's rollout, the host being ahead), and the compute stream only waits on
-        its event -- the upload is off the step's critical path; a slot's event also guards its buffer's reuse.
-        defer_wait=True returns (arrays, copy event) and leaves the compute stream's wait to the consumer: a
-        cross-stream wait enqueued behind a running kernel costs ~10 us of barrier processing when that kernel
-        ends (measured, rocprofv3 kernel trace), so it is placed right before the rollout that needs the data.
-        (Host cost ~10 us per step: the pinned slot, its event and the main stream are made once, r11.)"""
+        """The three per-lane descriptor arrays in ONE async host-to-device copy, [idx i64 | sign i8 | det i8], on a
+        side copy stream: the copy runs as soon as it is enqueued (during the previous step's rollout, the host
+        being ahead), and the compute stream waits on its event only if it has not completed (evaluate()).
+        defer_wait=True returns (arrays, copy event) and leaves that wait to the consumer: a cross-stream wait
+        enqueued behind a running kernel costs ~6-10 us of barrier processing when that kernel ends (rocprofv3 trace).
+        r11: the slots (pinned source + device destination) form a ring of _RING -- a per-step device tensor freed
+        after cross-stream use (record_stream) made the caching allocator record an event on the compute stream
+        each step, which cost the GPU ~6 us of idle barrier processing before the learner (tools/worker_gaps.py).
+        A slot's device block is released only after the compute-stream event recorded at most _RING - 1 uploads
+        later has fired, i.e. after the rollout that read it."""
         n = len(idx)
         dev = self.policy.flat.device
-        ring = self._pinned.get(n)
-        if ring is None:
-            ring = self._pinned[n] = {"slots": [], "next": 0}
-        if len(ring["slots"]) < 4:
-            slot = {"buf": torch.empty(10 * n, dtype=torch.uint8).pin_memory(), "ev": torch.cuda.Event(),
-                    "used": False}
-            ring["slots"].append(slot)
-        else:
-            slot = ring["slots"][ring["next"]]
-            ring["next"] = (ring["next"] + 1) % 4
-            if slot["used"]:
-                slot["ev"].synchronize()  # its previous copy has left the pinned buffer
-        h = slot["buf"].numpy()
-        h[:8 * n].view(np.int64)[:] = idx
-        h[8 * n:9 * n].view(np.int8)[:] = sign
-        h[9 * n:].view(np.int8)[:] = det
         if self._copy_stream is None:
             self._copy_stream = torch.cuda.Stream(dev)
             self._main_stream = torch.cuda.current_stream(dev)
         main = self._main_stream if torch.cuda.current_stream(dev) == self._main_stream \
             else torch.cuda.current_stream(dev)
+        ring = self._pinned.get(n)
+        if ring is None:
+            ring = self._pinned[n] = {"slots": [], "count": 0, "gen": {}}
+        u = ring["count"]
+        ring["count"] = u + 1
+        k = u % self._RING
+        if k == len(ring["slots"]):
+            ring["slots"].append({"buf": torch.empty(10 * n, dtype=torch.uint8).pin_memory(), "dev": None,
+                                  "ev": torch.cuda.Event(), "used": False})
+        slot = ring["slots"][k]
+        if u >= self._RING:
+            # the event recorded at upload v (v <= u - _GEN) follows the launch of every rollout of uploads < v,
+            # which include upload u - _RING, the slot's previous reader
+            v = self._GEN * ((u - self._GEN) // self._GEN)
+            ring["gen"][v].synchronize()
+            ring["gen"].pop(v - self._GEN, None)  # an older generation is no longer needed
+        if slot["used"]:
+            slot["ev"].synchronize()  # its previous copy has left the pinned buffer (long done)
+        if u % self._GEN == 0:
+            gev = torch.cuda.Event()
+            gev.record(main)
+            ring["gen"][u] = gev
+        h = slot["buf"].numpy()
+        h[:8 * n].view(np.int64)[:] = idx
+        h[8 * n:9 * n].view(np.int8)[:] = sign
+        h[9 * n:].view(np.int8)[:] = det
+        # a fresh block of the copy stream's pool (torch's .to() from pinned memory: ~10 us of host time, where a
+        # copy_ into a kept tensor or a direct hipMemcpyAsync cost ~100 us here); no record_stream -- the slot keeps
+        # the block until the rollout that read it is proven done (above), so freeing it then records no event
+        slot["dev"] = None
         with torch.cuda.stream(self._copy_stream):
             d = slot["buf"].to(dev, non_blocking=True)
+        slot["dev"] = d
         ev = slot["ev"]
         ev.record(self._copy_stream)
         slot["used"] = True
-        d.record_stream(main)
         if not defer_wait:
             main.wait_event(ev)
         arrs = (d[:8 * n].view(torch.int64), d[8 * n:9 * n].view(torch.int8), d[9 * n:].view(torch.int8))
