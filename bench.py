@@ -620,7 +620,9 @@ def main():
         "warmup": args.warmup, "settle_steps": settle_steps,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "sec_per_fd_step": round(elapsed / args.steps, 6),
-        "host_enqueue_ms_per_step": round(host_enqueue_ms, 4),  # < ms_per_step: the GPU, not the host, paces the job
+        # the timed loop's host time per step before its closing synchronize; the upload ring bounds the host's lead
+        # (Worker._lanes_to_device), so it includes waiting: < ms_per_step means the GPU, not the host, paces the job
+        "host_enqueue_ms_per_step": round(host_enqueue_ms, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
