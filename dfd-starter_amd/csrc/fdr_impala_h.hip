@@ -2504,15 +2504,18 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2)
   const int8_t* sgp = a.sign ? a.sign + l0 : reinterpret_cast<const int8_t*>(pk0);
   const int8_t sg0v = sgp[0], sg1v = sgp[1];
   const bool neg0 = a.sign && sg0v < 0, neg1 = a.sign && sg1v < 0;
+  const bool zero0 = a.sign && sg0v == 0, zero1 = a.sign && sg1v == 0;
   const int A = a.n_act;
   auto pkof = [&](int e) { return e < E ? pk0 : pk1; };
-  // this lane's B column: env (l & 15) mod E2; S X flips the sign bits of the minus lane's column
+  // this lane's B column: env (l & 15) mod E2; S X flips the sign bits of the minus lane's column and zeroes a
+  // sign-0 (unperturbed) lane's: E then adds exact zeros
   const int benv = (l & 15) & (E2 - 1);
   const unsigned smask = (benv < E ? neg0 : neg1) ? 0x80008000u : 0u;
+  const unsigned zmask = (benv < E ? zero0 : zero1) ? 0u : ~0u;
   auto bfrag = [&](const _Float16* rowp, int k0, h8& x, h8& sx) {
     x = *reinterpret_cast<const h8*>(rowp + k0 + 8 * (l >> 4));
     u32x4 u = __builtin_bit_cast(u32x4, x);
-    u ^= u32x4{smask, smask, smask, smask};
+    u = (u ^ u32x4{smask, smask, smask, smask}) & u32x4{zmask, zmask, zmask, zmask};
     sx = __builtin_bit_cast(h8, u);
   };
 
@@ -2788,7 +2791,8 @@ __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_e
   const int benv = (l & 15) & (NE - 1), bl = benv / E;
   const int8_t bsg = bl == 0 ? sg0 : (bl == 1 ? sg1 : (bl == 2 ? sg2 : sg3));
   const unsigned smask = (a.sign && bsg < 0) ? 0x80008000u : 0u;
-  const unsigned ma = bl < 2 ? ~0u : 0u, mb = ~ma;
+  const unsigned zmask = (a.sign && bsg == 0) ? 0u : ~0u;  // a sign-0 (unperturbed) lane: E adds exact zeros
+  const unsigned ma = (bl < 2 ? ~0u : 0u) & zmask, mb = (bl < 2 ? 0u : ~0u) & zmask;
   auto bfrag = [&](const _Float16* rowp, int k0, h8& x, h8& xa, h8& xb) {
     x = *reinterpret_cast<const h8*>(rowp + k0 + 8 * (l >> 4));
     const u32x4 sx = __builtin_bit_cast(u32x4, x) ^ u32x4{smask, smask, smask, smask};
@@ -2988,6 +2992,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void x
   }
   const int l0 = 2 * pr;
   const bool neg0 = a.sign && a.sign[l0] < 0, neg1 = a.sign && a.sign[l0 + 1] < 0;
+  const bool zero0 = a.sign && a.sign[l0] == 0, zero1 = a.sign && a.sign[l0 + 1] == 0;
   const int64_t e0 = (int64_t)l0 * E, ne = (int64_t)a.n_lanes * E;
   const int rows = tc * E2;
   __syncthreads();
@@ -2997,6 +3002,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void x
     const int rr = ok ? row : 0, t = rr / E2, env = rr - t * E2;
     const float* xr = a.ci + ((int64_t)(t0 + t) * ne + e0 + env) * kCoreIn;
     const unsigned smask = (env < E ? neg0 : neg1) ? 0x80008000u : 0u;
+    const unsigned zmask = (env < E ? zero0 : zero1) ? 0u : ~0u;  // sign-0 lane: E X = 0
     f32x4 acc[4];
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -3010,7 +3016,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void x
         x[i] = (_Float16)(ok && k < kCoreIn ? v : 0.f);
       }
       u32x4 u = __builtin_bit_cast(u32x4, x);
-      u ^= u32x4{smask, smask, smask, smask};
+      u = (u ^ u32x4{smask, smask, smask, smask}) & u32x4{zmask, zmask, zmask, zmask};
       const h8 sx = __builtin_bit_cast(h8, u);
 #pragma unroll
       for (int jt = 0; jt < 4; ++jt) {

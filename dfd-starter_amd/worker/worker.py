@@ -130,8 +130,8 @@ class Worker(object):
             spec = self.agent.env.spec()
             if pairs and p.KIND == "impala":
                 ii, ss, dd = np.asarray(idx), np.asarray(sign).astype(np.int32), np.asarray(det)
-                # +eps / -eps lanes only: a sign-0 (eval) pair also satisfies s0 == -s1, but the pair cores take
-                # the pair's sign from its first lane and would perturb an eval lane
+                # +eps / -eps training batches only (the pair cores also take sign-0 lanes, include/fdr.h; eval
+                # batches keep the per-lane form they were measured in)
                 spec.pairs = bool(n % 2 == 0 and np.array_equal(ii[0::2], ii[1::2]) and np.all(ss[0::2] == 1)
                                   and np.all(ss[1::2] == -1) and not np.any(dd))
             if timing is not None:

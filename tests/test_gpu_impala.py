@@ -383,6 +383,45 @@ def test_fp16_two_pairs_per_workgroup_bit_identical(engine, table, E, n_pairs):
     assert np.all(np.isfinite(outs[1].entropy.cpu().numpy()))
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_fp16_pair_core_sign_zero_lanes(engine, table, mode):
+    """fdr_impala_desc.pairs allows signs +-1 or 0 in any combination (include/fdr.h): an unperturbed (sign-0) lane
+    of a pair sees theta alone.  The MFMA forms zero its S X column (E adds exact zeros), the VALU form multiplies E
+    by 0, so a sign-0 lane's recorded episode (with the entropy replay) is BITWISE the same whatever its pair's table
+    offset, and a +-1 lane's the same whatever its partner's sign.  Step 0's probabilities agree with the per-lane
+    form (f16(theta') per lane) within the fp16 tolerance, and the norms are the per-lane ones (0 for sign 0)."""
+    A, T, E = 5, 40, 4
+    theta = _theta(A)
+    offs = np.array([77, 2_000_001, 999_999, 5], np.int64)
+    signs = np.array([1, -1, 0, 0, 1, 0, 0, -1], np.int8)
+    dev = "cuda"
+
+    def run(offs_, signs_, pairs=True):
+        idx = np.repeat(offs_, 2)
+        lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
+                                  torch.tensor(idx, device=dev), torch.tensor(signs_, device=dev), 0.02)
+        spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=True, pairs=pairs)
+        ctx = engine.Context()
+        ctx.set_core_mfma(mode)
+        o = engine.impala_rollout(spec, lanes, len(idx), 11, record=True, ctx=ctx)
+        torch.cuda.synchronize()
+        return {f: getattr(o, f).cpu().numpy() for f in ("actions", "probs", "reward", "entropy", "norm2")}
+
+    a = run(offs, signs)
+    b = run(offs[::-1].copy(), signs)                 # every pair at another table offset
+    c = run(offs, np.array([1, -1] * 4, np.int8))     # every lane perturbed
+    per_lane = run(offs, signs, pairs=False)
+
+    def envs(x, lanes):
+        return np.concatenate([x[l * E:(l + 1) * E] for l in lanes])
+    for f in ("actions", "probs", "reward", "entropy"):
+        np.testing.assert_array_equal(envs(a[f], [2, 3, 5, 6]), envs(b[f], [2, 3, 5, 6]), err_msg=f)
+        np.testing.assert_array_equal(envs(a[f], [0, 1, 4, 7]), envs(c[f], [0, 1, 4, 7]), err_msg=f)
+    np.testing.assert_array_equal(a["norm2"], per_lane["norm2"])
+    assert np.all(a["norm2"][[2, 3, 5, 6]] == 0)
+    np.testing.assert_allclose(a["probs"][:, 0], per_lane["probs"][:, 0], atol=2e-2)
+
+
 @pytest.mark.parametrize("E,n_pairs", [(4, 3), (4, 4), (1, 6), (2, 2)])
 def test_f32_pair_core_bit_identical(engine, table, E, n_pairs):
     """f32 pair form (fdr_impala_desc.pairs): w = fl32(theta + s fl32(sigma eps)) formed in registers is the
