@@ -1360,9 +1360,19 @@ __global__ __launch_bounds__(256) void lstm_xproj_kernel(Layout L, StepArgs a, i
 }
 
 // the pairs' table offsets idx[2p] (fdr_impala_desc.pairs: idx[2p] == idx[2p+1] by contract)
-__global__ void pair_offsets_kernel(const int64_t* __restrict__ idx, int n_pairs, int64_t* __restrict__ idxe) {
+// idxe[p] = the pair's shared offset.  A pair whose lanes disagree (fdr_impala_desc.pairs violated) would run lane
+// 2p + 1 on lane 2p's noise: both lanes' norms are poisoned with NaN instead (slot 0 of their n2 partials, written by
+// the lanes' pack kernels before this launch), as for an out-of-range offset.
+__global__ void pair_offsets_kernel(const int64_t* __restrict__ idx, int n_pairs, int64_t* __restrict__ idxe,
+                                    double* __restrict__ n2, int nblk) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < n_pairs) idxe[p] = idx[2 * p];
+  if (p >= n_pairs) return;
+  const int64_t o0 = idx[2 * p], o1 = idx[2 * p + 1];
+  idxe[p] = o0;
+  if (o0 != o1) {
+    n2[(int64_t)(2 * p) * nblk] = __builtin_nan("");
+    n2[(int64_t)(2 * p + 1) * nblk] = __builtin_nan("");
+  }
 }
 
 // the fp16 conv stack over grid workgroups (one per env, XCD-interleaved lanes): either kernel, same features;
@@ -1532,7 +1542,8 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
     float* zeros = reinterpret_cast<float*>(w + p.zeros);
     int64_t* idxe = reinterpret_cast<int64_t*>(w + p.idxe);
     (void)hipMemsetAsync(zeros, 0, (size_t)L.P * 4, stream);
-    hipLaunchKernelGGL(pair_offsets_kernel, dim3((np + 255) / 256), dim3(256), 0, stream, c.lanes.idx, np, idxe);
+    hipLaunchKernelGGL(pair_offsets_kernel, dim3((np + 255) / 256), dim3(256), 0, stream, c.lanes.idx, np, idxe, n2,
+                       p.nblk);
     LanesArgs lt = c.lanes;
     lt.table = nullptr;
     LanesArgs le = c.lanes;

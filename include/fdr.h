@@ -365,8 +365,9 @@ typedef struct fdr_impala_desc {
   int32_t fp16;          /* 1 = fp16 mode (BASELINE config 5): theta' rounded to f16 for the convs, fc and
                             LSTM; f16 activations in the conv stack on f16 MFMA, f32 accumulation, state
                             and head (DESIGN.md "fp16 mode"); 0 = f32 throughout */
-  int32_t pairs;         /* 1 = lanes 2p, 2p+1 are an antithetic pair (same table offset, each sign +-1 or 0
-                            -- a sign-0 lane runs theta; n_lanes even; E <= 4) -- the rollout's fc / LSTM step streams the pair's
+  int32_t pairs;         /* 1 = lanes 2p, 2p+1 are an antithetic pair (same table offset -- a pair whose
+                            offsets differ reports norm2 = NaN on both lanes; each sign +-1 or 0 -- a sign-0
+                            lane runs theta; n_lanes even; E <= 4) -- the rollout's fc / LSTM step streams the pair's
                             fl32(sigma eps) once and theta's shared pack, forming each lane's weights in
                             registers (half the core kernel's HBM bytes; f32: the per-lane
                             weights bit for bit, fp16: f16(theta) + s f16(sigma eps)); 0 = per lane */

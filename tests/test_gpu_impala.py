@@ -422,6 +422,34 @@ def test_fp16_pair_core_sign_zero_lanes(engine, table, mode):
     np.testing.assert_allclose(a["probs"][:, 0], per_lane["probs"][:, 0], atol=2e-2)
 
 
+@pytest.mark.parametrize("fp16", [False, True])
+def test_pair_with_mismatched_offsets_poisons_its_norms(engine, table, fp16):
+    """fdr_impala_desc.pairs requires both lanes of a pair on one table offset; a pair that breaks it gets NaN norms
+    on both lanes (the FD step is poisoned visibly, as for an out-of-range offset) and no fault, and the other pairs'
+    episodes are bitwise those of a batch without the violation."""
+    A, T, E = 5, 20, 4
+    theta = _theta(A)
+    dev = "cuda"
+    spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=fp16, pairs=True)
+    sign = torch.tensor(np.array([1, -1] * 4, np.int8), device=dev)
+
+    def run(idx):
+        lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
+                                  torch.tensor(np.array(idx, np.int64), device=dev), sign, 0.02)
+        o = engine.impala_rollout(spec, lanes, len(idx), 11, record=True)
+        torch.cuda.synchronize()
+        return {f: getattr(o, f).cpu().numpy() for f in ("actions", "probs", "reward", "entropy", "norm2")}
+    bad = run([77, 77, 100, 200, 5, 5, 9, 9])
+    good = run([77, 77, 100, 100, 5, 5, 9, 9])
+    assert np.isnan(bad["norm2"][2]) and np.isnan(bad["norm2"][3])
+    keep = [0, 1, 4, 5, 6, 7]
+    assert np.all(np.isfinite(bad["norm2"][keep]))
+    np.testing.assert_array_equal(bad["norm2"][keep], good["norm2"][keep])
+    envs = np.concatenate([np.arange(l * E, (l + 1) * E) for l in keep])
+    for f in ("actions", "probs", "reward", "entropy"):
+        np.testing.assert_array_equal(bad[f][envs], good[f][envs], err_msg=f)
+
+
 @pytest.mark.parametrize("E,n_pairs", [(4, 3), (4, 4), (1, 6), (2, 2)])
 def test_f32_pair_core_bit_identical(engine, table, E, n_pairs):
     """f32 pair form (fdr_impala_desc.pairs): w = fl32(theta + s fl32(sigma eps)) formed in registers is the
