@@ -580,7 +580,7 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* d, const float* thet
 int64_t fdr_impala_strategies_workspace_bytes(const fdr_impala_desc* d, int32_t n_lanes, int32_t n_states) {
   impala::Layout L;
   if (!d || n_lanes < 0 || n_states < 0 || !impala::make_layout(d->n_act, &L)) return -1;
-  return impala::strategies_workspace_bytes(L, n_lanes, n_states, d->fp16 != 0);
+  return impala::strategies_workspace_bytes(L, n_lanes, n_states, d->fp16 != 0, d->pairs != 0);
 }
 
 int fdr_impala_strategies(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lanes_desc* lanes, int32_t n_lanes,
@@ -601,6 +601,9 @@ int fdr_impala_strategies(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lane
   sc.n_states = n_states;
   sc.fp16 = d->fp16 != 0;
   sc.conv_h2 = C->conv_h2;
+  sc.pairs = d->pairs != 0;
+  sc.core_mfma = C->core_mfma;
+  if (sc.pairs && (n_lanes & 1)) return set_error(FDR_ERR_INVALID, "pairs: n_lanes must be even");
   sc.frames = frames;
   sc.reward = reward;
   sc.h = h;

@@ -288,6 +288,8 @@ struct StrategiesCall {
   const Layout* layout;
   LanesArgs lanes;
   int n_lanes, n_states, fp16, conv_h2;
+  int pairs;             // fdr_impala_desc.pairs: fp16 + n_lanes % 4 == 0 + ctx core_mfma -> the pair form on MFMA
+  int core_mfma;
   const float* frames;   // [Z][3][64][64] f32 0..255
   const float* reward;   // [Z] or NULL
   float* h;              // [n_lanes][256] in/out initial state, or NULL (zero state)
@@ -296,7 +298,7 @@ struct StrategiesCall {
   const float* bn_mean;
   const float* bn_var;
 };
-int64_t strategies_workspace_bytes(const Layout& L, int n_lanes, int n_states, bool fp16);
+int64_t strategies_workspace_bytes(const Layout& L, int n_lanes, int n_states, bool fp16, bool pairs = false);
 int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipStream_t stream);
 int launch_env_frames(uint64_t env_seed, int n_act, uint64_t env_id, int t0, int n, const int32_t* actions,
                       float* frames, float* reward, hipStream_t stream);

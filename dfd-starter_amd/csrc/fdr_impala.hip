@@ -331,15 +331,17 @@ static int transpose_prep_tiles(const Layout& L, bool half) {
 // theta' pack (half = 0, f32, with the per-lane n2 partials) or half pack (half = 1, f16).  The transposed sections
 // (fc W^T, [W_ih | W_hh]^T: 90 % of the pack) by tmode: kTrFull written; kTrNorm not written, n2 partials only (an
 // fp16 call's f32 pack: its kernels read those weights from the half pack or the pair images); kTrSkip nothing
-// (an fp16 call's f32 pack when n2 is not wanted, or its half pack under the pair core)
+// (an fp16 call's f32 pack when n2 is not wanted, or its half pack under the pair core).  copies = false (half packs
+// only: no n2): the other sections are not written either -- the pairs' sigma-eps packs that feed only the MFMA images
 enum TransposedMode { kTrFull = 0, kTrNorm = 1, kTrSkip = 2 };
 template <class OUT>
 static void launch_pack(const Layout& L, const LanesArgs& lanes, OUT* pack, double* n2, int n_lanes, int half,
-                        hipStream_t stream, TransposedMode tmode = kTrFull) {
+                        hipStream_t stream, TransposedMode tmode = kTrFull, bool copies = true) {
   const int g = generic_prep_blocks(L, half != 0), tt = tmode == kTrSkip ? 0 : transpose_prep_tiles(L, half != 0);
   const int slots = prep_blocks(L);
-  hipLaunchKernelGGL(prep_kernel<OUT>, dim3(g, n_lanes), dim3(kPrepThreads), 0, stream, L, lanes, pack, n2, half,
-                     slots);
+  if (copies || !half)
+    hipLaunchKernelGGL(prep_kernel<OUT>, dim3(g, n_lanes), dim3(kPrepThreads), 0, stream, L, lanes, pack, n2, half,
+                       slots);
   if (tt > 0)
     hipLaunchKernelGGL(prep_transpose_kernel<OUT>, dim3(tt, n_lanes), dim3(256), 0, stream, L, lanes, pack, n2, half,
                        generic_prep_blocks(L, false), slots, tmode == kTrFull ? 1 : 0);
@@ -1555,7 +1557,8 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
       _Float16* th = reinterpret_cast<_Float16*>(w + p.thpack);
       _Float16* ep = reinterpret_cast<_Float16*>(w + p.epack);
       launch_pack<_Float16>(L, lt, th, n2, 1, 1, stream);
-      launch_pack<_Float16>(L, le, ep, n2, np, 1, stream);
+      // under the MFMA core only the images read the pairs' packs (their transposed sections)
+      launch_pack<_Float16>(L, le, ep, n2, np, 1, stream, kTrFull, c.ctx->core_mfma == 0);
       a.th = th;
       a.ep = ep;
       a.ep_stride = L.hpack;
@@ -1730,10 +1733,11 @@ __global__ __launch_bounds__(256) void fc_rows_kernel(Layout L, StepArgs a, int 
 
 namespace {
 struct StratPlan {
-  int64_t pack, hpack, feat, ci, gx, h, c, n2, total;
+  int64_t pack, hpack, feat, ci, gx, h, c, n2, zeros, thpack, epack, idxe, mimg, total;
   int nblk;
 };
-StratPlan strat_plan(const Layout& L, int n_lanes, int Z, bool fp16) {
+// pairs (fp16): theta's half pack, one sigma-eps half pack per pair and their MFMA images, as the rollout's pair form
+StratPlan strat_plan(const Layout& L, int n_lanes, int Z, bool fp16, bool pairs = false) {
   StratPlan p{};
   int64_t o = 0;
   auto take = [&](int64_t bytes) { const int64_t at = o; o += round_up(std::max<int64_t>(bytes, 0), 256); return at; };
@@ -1747,19 +1751,25 @@ StratPlan strat_plan(const Layout& L, int n_lanes, int Z, bool fp16) {
   p.h = take((int64_t)n_lanes * kHid * 4);
   p.c = take((int64_t)n_lanes * kHid * 4);
   p.n2 = take((int64_t)n_lanes * p.nblk * 8);
+  const bool pr = pairs && fp16;
+  p.zeros = take(pr ? L.P * 4 : 0);
+  p.thpack = take(pr ? L.hpack * 2 : 0);
+  p.epack = take(pr ? (int64_t)(n_lanes / 2) * L.hpack * 2 : 0);
+  p.idxe = take(pr ? (int64_t)(n_lanes / 2) * 8 : 0);
+  p.mimg = take(pr ? (int64_t)(n_lanes / 2 + 1) * kMImg * 2 : 0);
   p.total = o;
   return p;
 }
 }  // namespace
 
-int64_t strategies_workspace_bytes(const Layout& L, int n_lanes, int n_states, bool fp16) {
-  return strat_plan(L, n_lanes, n_states, fp16).total;
+int64_t strategies_workspace_bytes(const Layout& L, int n_lanes, int n_states, bool fp16, bool pairs) {
+  return strat_plan(L, n_lanes, n_states, fp16, pairs).total;
 }
 
 int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipStream_t stream) {
   const Layout& L = *c.layout;
   const int Z = c.n_states;
-  const StratPlan p = strat_plan(L, c.n_lanes, Z, c.fp16 != 0);
+  const StratPlan p = strat_plan(L, c.n_lanes, Z, c.fp16 != 0, c.pairs != 0);
   if (!ws || ws_bytes < p.total) return set_error(FDR_ERR_WORKSPACE, "impala strategies workspace too small");
   if (c.n_lanes == 0 || Z == 0) return FDR_OK;
   char* w = static_cast<char*>(ws);
@@ -1785,6 +1795,36 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
     a.hpack = reinterpret_cast<_Float16*>(w + p.hpack);
     a.hpack_stride = L.hpack;
     launch_pack<_Float16>(L, c.lanes, a.hpack, n2, c.n_lanes, 1, stream);
+  }
+  // antithetic pairs (fp16): the recurrence streams each pair's sigma-eps image once (core_kernel_hpm2<1, kStrategy>,
+  // x W_ih^T by xproj_pair_kernel), as the rollout's pair form -- conv and fc stay per lane (per-lane half pack)
+  const bool pair_form = half && c.pairs && c.core_mfma >= 1 && c.n_lanes % 4 == 0 && c.lanes.table &&
+                         c.lanes.base_stride == 0;
+  if (pair_form) {
+    const int np = c.n_lanes / 2;
+    float* zeros = reinterpret_cast<float*>(w + p.zeros);
+    int64_t* idxe = reinterpret_cast<int64_t*>(w + p.idxe);
+    _Float16* th = reinterpret_cast<_Float16*>(w + p.thpack);
+    _Float16* ep = reinterpret_cast<_Float16*>(w + p.epack);
+    _Float16* im = reinterpret_cast<_Float16*>(w + p.mimg);
+    (void)hipMemsetAsync(zeros, 0, (size_t)L.P * 4, stream);
+    hipLaunchKernelGGL(pair_offsets_kernel, dim3((np + 255) / 256), dim3(256), 0, stream, c.lanes.idx, np, idxe, n2,
+                       p.nblk);
+    LanesArgs lt = c.lanes;
+    lt.table = nullptr;
+    LanesArgs le = c.lanes;
+    le.base = zeros;
+    le.base_stride = 0;
+    le.idx = idxe;
+    le.sign = nullptr;
+    launch_pack<_Float16>(L, lt, th, n2, 1, 1, stream);
+    launch_pack<_Float16>(L, le, ep, n2, np, 1, stream, kTrFull, false);  // feeds only the images
+    const unsigned nb = kFcKS + 4 * kGateKS;
+    hipLaunchKernelGGL(mfma_image_kernel, dim3(nb, 1), dim3(256), 0, stream, L, th, (int64_t)0, im);
+    hipLaunchKernelGGL(mfma_image_kernel, dim3(nb, np), dim3(256), 0, stream, L, ep, (int64_t)L.hpack, im + kMImg);
+    a.thm = im;
+    a.epm = im + kMImg;
+    a.sign = c.lanes.sign;
   }
   if (!c.h || !c.c) {  // the reset state (worker/agent.py:66 resets the policy before compute_novelty)
     if (hipMemsetAsync(a.h, 0, (size_t)c.n_lanes * kHid * 4, stream) != hipSuccess ||
@@ -1812,7 +1852,10 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
     const int tc = std::min(kReplayChunk, Z - t0);
     const dim3 grid(c.n_lanes, (tc + 63) / 64, kGates / 256);
     a.gx = nullptr;
-    if (half)
+    if (pair_form)
+      hipLaunchKernelGGL((xproj_pair_kernel<1>), dim3(c.n_lanes / 2, kGateNT / 4), dim3(256), 0, stream, L, a, t0, tc,
+                         gx);
+    else if (half)
       hipLaunchKernelGGL(lstm_xproj_kernel<true>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);
     else
       hipLaunchKernelGGL(lstm_xproj_kernel<false>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);
@@ -1820,7 +1863,10 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
     a.gx_t0 = t0;
     for (int t = t0; t < t0 + tc; ++t) {
       a.t = t;
-      if (half)
+      if (pair_form)
+        hipLaunchKernelGGL((core_kernel_hpm2<1, kStrategy>), dim3(c.n_lanes / 4), dim3(2 * kCoreThreads), 0, stream, L,
+                           a);
+      else if (half)
         hipLaunchKernelGGL((core_kernel_h<1, kStrategy>), dim3(c.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
       else
         hipLaunchKernelGGL((core_kernel<1, kStrategy>), dim3(c.n_lanes), dim3(kCoreThreads), 0, stream, L, a);

@@ -2745,7 +2745,7 @@ template <int E, int MODE>
 __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_eu(2))) void core_kernel_hpm2(
     Layout L, StepArgs a) {
   constexpr int E2 = 2 * E, NE = 4 * E;  // envs of a pair / of the workgroup's 4 lanes
-  constexpr bool kRep = MODE == kReplay;
+  constexpr bool kRep = seq_mode(MODE);  // kReplay / kStrategy: the W_hh product on a.gx (x W_ih^T of the chunk)
   constexpr int kKs0 = kRep ? kCoreIn / 32 : 0, kNks = kGateKS - kKs0;
   static_assert(NE <= 16 && (NE & (NE - 1)) == 0, "the workgroup's envs are the B operand's columns (mod NE)");
   constexpr int XP = kFeat + 16, GP = kGateKS * 32 + 16;  // f16 pitches, as core_kernel_hpm
@@ -2973,6 +2973,7 @@ template __global__ void core_kernel_hpm2<4, kRollout>(Layout, StepArgs);
 template __global__ void core_kernel_hpm2<1, kReplay>(Layout, StepArgs);
 template __global__ void core_kernel_hpm2<2, kReplay>(Layout, StepArgs);
 template __global__ void core_kernel_hpm2<4, kReplay>(Layout, StepArgs);
+template __global__ void core_kernel_hpm2<1, kStrategy>(Layout, StepArgs);  // lane strategies of antithetic pairs
 
 // Entropy replay, input projection of one chunk in the fp16 pair form on MFMA: gx = theta X + s (E X) with the
 // gate images' k-steps 0 .. 8 (rows 0 .. 287 = W_ih^T's 257 rows; X is zero beyond k = 256) -- the per-lane

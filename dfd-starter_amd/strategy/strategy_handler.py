@@ -61,13 +61,14 @@ class StrategyHandler(object):
     def _dev(self):
         return self.policy.flat.device
 
-    def _strategies(self, lanes_fn, n):
-        """get_strategy(zeta) of n parameter vectors; lanes_fn(Z) -> lanes descriptor (see engine.lane_strategies)."""
+    def _strategies(self, lanes_fn, n, pairs=False):
+        """get_strategy(zeta) of n parameter vectors; lanes_fn(Z) -> lanes descriptor (see engine.lane_strategies).
+        pairs: lanes 2p, 2p+1 are antithetic pairs (ImpalaPolicy fp16: the recurrence in the rollout's pair form)."""
         p = self.policy
         bm, bv = p.bn_stats()
         if p.KIND == "impala":
             frames, reward = self.zeta
-            spec = engine.ImpalaSpec(p.output_shape, fp16=self.fp16)
+            spec = engine.ImpalaSpec(p.output_shape, fp16=self.fp16, pairs=pairs)
             return engine.impala_strategies(spec, lanes_fn(1), n, frames, reward, bn_mean=bm, bn_var=bv)
         if p.KIND != "discrete" and p.KIND != "mujoco":
             raise NotImplementedError("strategies of a %s policy" % p.KIND)
@@ -112,8 +113,9 @@ class StrategyHandler(object):
             return self._strategies(lambda Z: engine.lanes_desc(base, base.shape[1]), len(flats))
         return torch.cat([self._strategies_of_flat(f) for f in flats])
 
-    def lane_strategies(self, table, idx, sign, sigma):
-        """Strategies of the perturbed lanes theta + sign * sigma * table[idx:] -> [n, Z, D]."""
+    def lane_strategies(self, table, idx, sign, sigma, pairs=False):
+        """Strategies of the perturbed lanes theta + sign * sigma * table[idx:] -> [n, Z, D].  pairs: the lanes are
+        antithetic pairs (same offset, signs +1 / -1), as the rollout that produced them was told."""
         p = self.policy
         if p.KIND == "atari":   # theta' materialised per chunk of lanes (fdr_perturb), then one forward each
             out = [self._atari_strategies(engine.perturb(p.flat, table, idx[c:c + 64].contiguous(),
@@ -123,7 +125,7 @@ class StrategyHandler(object):
 
         def lanes(Z):
             return engine.lanes_desc(p.flat, 0, table, idx.repeat_interleave(Z), sign.repeat_interleave(Z), sigma)
-        return self._strategies(lanes, idx.numel())
+        return self._strategies(lanes, idx.numel(), pairs=pairs)
 
     @property
     def strategy_tensor(self):
@@ -206,9 +208,10 @@ class StrategyHandler(object):
                                           self.kind)
         return float(mn.item())
 
-    def lane_novelty(self, table, idx, sign, sigma):
+    def lane_novelty(self, table, idx, sign, sigma, pairs=False):
         """Novelty of every perturbed lane (device f64 [n]); zeros if the archive is not ready."""
         if not self._ready():
             return torch.zeros(idx.numel(), dtype=torch.float64, device=self._dev())
-        mn, _ = engine.strategy_distances(self.lane_strategies(table, idx, sign, sigma), self.archive, self.kind)
+        mn, _ = engine.strategy_distances(self.lane_strategies(table, idx, sign, sigma, pairs=pairs), self.archive,
+                                          self.kind)
         return mn

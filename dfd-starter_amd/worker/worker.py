@@ -44,6 +44,7 @@ class Worker(object):
         self._main_stream = None
         self._lane_consts = {}  # (n_dirs, antithetic, lane_range, world, rank) -> the constant parts of _lanes_of
         self._next = None      # (key, host lanes, device lanes) uploaded ahead by evaluate(prefetch=True)
+        self._launch_pairs = False  # the last launch's lanes were antithetic pairs (lane_novelty takes the pair form)
 
     # ---- hot path ---------------------------------------------------------------------------
     _RING = 64  # upload slots per lane count: an FDBatch's device idx / sign stay valid for the next 63 uploads
@@ -128,12 +129,14 @@ class Worker(object):
             E = self.agent.env.envs_per_lane
             roll = engine.impala_rollout if p.KIND == "impala" else engine.atari_rollout
             spec = self.agent.env.spec()
+            self._launch_pairs = False
             if pairs and p.KIND == "impala":
                 ii, ss, dd = np.asarray(idx), np.asarray(sign).astype(np.int32), np.asarray(det)
                 # +eps / -eps training batches only (the pair cores also take sign-0 lanes, include/fdr.h; eval
                 # batches keep the per-lane form they were measured in)
                 spec.pairs = bool(n % 2 == 0 and np.array_equal(ii[0::2], ii[1::2]) and np.all(ss[0::2] == 1)
                                   and np.all(ss[1::2] == -1) and not np.any(dd))
+                self._launch_pairs = spec.pairs
             if timing is not None:
                 timing[0].record()
             res = roll(spec, lanes, n, seed, jiggle=jiggle, bn_mean=bm, bn_var=bv, device=p.flat.device)
@@ -148,6 +151,7 @@ class Worker(object):
         chance = self.agent.obs_stats_update_chance if self.agent.normalize_obs else None
         if timing is not None:
             timing[0].record()
+        self._launch_pairs = False
         res = engine.rollout(p.spec, self.agent.env, lanes, n, seed, jiggle=jiggle, obs_mean=om, obs_std=osd,
                              bn_mean=bm, bn_var=bv, out=out, device=p.flat.device, obs_stats=chance)
         if timing is not None:
@@ -279,7 +283,8 @@ class Worker(object):
         E = getattr(self.agent.env, "envs_per_lane", 1)
         if E > 1:
             idx_d, sign_d = idx_d[::E].contiguous(), sign_d[::E].contiguous()
-        nov = h.lane_novelty(self.noise_source.device_table(self.policy.flat.device), idx_d, sign_d, self.sigma)
+        nov = h.lane_novelty(self.noise_source.device_table(self.policy.flat.device), idx_d, sign_d, self.sigma,
+                             pairs=self._launch_pairs)
         return nov.repeat_interleave(E) if E > 1 else nov
 
     def eval_states(self, max_states=None):

@@ -438,8 +438,10 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* desc, const float* t
  * _get_stacked_obs batch does.  frames [Z, 3, 64, 64] f32 (0..255) and reward [Z] (NULL = 0) are shared by
  * all lanes; h / c [n_lanes, 256] = the state the sequence starts from, updated in place to its end state
  * (NULL = the reset state, which is the state Worker._build_ret scores novelty in: worker/agent.py:66 resets
- * the policy before compute_novelty).  probs [n_lanes, Z, A] f32 out.  Only n_act, n_params, fp16, bn_mean,
- * bn_var of desc are read.  workspace: fdr_impala_strategies_workspace_bytes(desc, n_lanes, Z) bytes. */
+ * the policy before compute_novelty).  probs [n_lanes, Z, A] f32 out.  Only n_act, n_params, fp16, pairs, bn_mean,
+ * bn_var of desc are read; fp16 with pairs (lanes as for fdr_impala_rollout, n_lanes % 4 == 0, ctx core_mfma >= 1)
+ * runs the recurrence in the rollout's pair form on MFMA.
+ * workspace: fdr_impala_strategies_workspace_bytes(desc, n_lanes, Z) bytes. */
 int64_t fdr_impala_strategies_workspace_bytes(const fdr_impala_desc* desc, int32_t n_lanes, int32_t n_states);
 int fdr_impala_strategies(fdr_ctx* ctx, const fdr_impala_desc* desc, const fdr_lanes_desc* lanes, int32_t n_lanes,
                           int32_t n_states, const float* frames, const float* reward, float* h, float* c,

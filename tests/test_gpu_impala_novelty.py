@@ -75,10 +75,12 @@ def test_get_strategy_matches_reference(mods, golden):
         np.testing.assert_allclose(ph[0].cpu().numpy(), g8["ent_probs"][q], rtol=0, atol=2e-2)
 
 
-@pytest.mark.parametrize("fp16", [False, True])
-def test_lane_novelty_matches_oracle(mods, fp16):
+@pytest.mark.parametrize("fp16,pairs", [(False, False), (True, False), (True, True)])
+def test_lane_novelty_matches_oracle(mods, fp16, pairs):
     """Novelty of every perturbed lane against an archive (worker/worker.py:53 -> strategy_handler.py:25-30,
-    categorical_tvd) == the oracle's per-lane get_strategy + TVD min, 66 probe obs, antithetic lanes."""
+    categorical_tvd) == the oracle's per-lane get_strategy + TVD min, 66 probe obs, antithetic lanes.  pairs: the
+    fp16 recurrence in the rollout's pair form (core_kernel_hpm2<1, kStrategy> + xproj_pair_kernel: f16(theta) +
+    s f16(sigma eps) instead of f16(theta')) -- same tolerance, and not the per-lane path's bits."""
     engine, ImpalaPolicy, StrategyHandler, mh = mods
     A, Z, sigma = 4, 66, 0.02
     torch.manual_seed(5)
@@ -97,8 +99,12 @@ def test_lane_novelty_matches_oracle(mods, fp16):
     h.set_zeta({"frame": frames, "reward": rewards, "done": np.zeros(Z, bool)})
     tab_d = torch.as_tensor(tab, device="cuda")
     idx_d, sign_d = torch.as_tensor(idx, device="cuda"), torch.as_tensor(sign, device="cuda")
-    got = h.lane_strategies(tab_d, idx_d, sign_d, sigma).cpu().numpy()
-    nov = h.lane_novelty(tab_d, idx_d, sign_d, sigma).cpu().numpy()
+    got = h.lane_strategies(tab_d, idx_d, sign_d, sigma, pairs=pairs).cpu().numpy()
+    nov = h.lane_novelty(tab_d, idx_d, sign_d, sigma, pairs=pairs).cpu().numpy()
+    if pairs:
+        per_lane = h.lane_strategies(tab_d, idx_d, sign_d, sigma).cpu().numpy()
+        assert not np.array_equal(got, per_lane)
+        np.testing.assert_allclose(got, per_lane, rtol=0, atol=2e-2)
     zero = np.zeros(oi.num_bn(), np.float32)
     one = np.ones(oi.num_bn(), np.float32)
     ref = oi.lane_strategies(theta, tab, idx, sign, sigma, A, frames, rewards, zero, one)
