@@ -127,9 +127,13 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); 
 
 // Softmax, action (argmax / inverse CDF on the counter stream), synthetic reward and return, or the
 // entropy term (replay), or the probabilities (forward), for env e of lane `lane` (thread e < E).
+// ent_acc (kReplay, optional): accumulate the step's entropy into this register instead of a.ent (a kernel that runs
+// many replay steps stores it once)
+// t_step >= 0: the step in place of a.t (a kernel that runs many steps)
 template <int E, int MODE>
 __device__ __forceinline__ void core_finish(const StepArgs& a, const float* logit, int lane, int j,
-                                            bool step_entropy = false) {
+                                            bool step_entropy = false, double* ent_acc = nullptr, int t_step = -1) {
+  const int at_t = t_step >= 0 ? t_step : a.t;
   const int A = a.n_act;
   const int64_t e0 = (int64_t)lane * E;
     const int e = j;
@@ -149,7 +153,7 @@ __device__ __forceinline__ void core_finish(const StepArgs& a, const float* logi
       if (a.probs)
         for (int i = 0; i < A; ++i) a.probs[ge * A + i] = p[i];
     } else if constexpr (MODE == kStrategy) {
-      for (int i = 0; i < A; ++i) a.probs[(ge * a.T + a.t) * A + i] = p[i];
+      for (int i = 0; i < A; ++i) a.probs[(ge * a.T + at_t) * A + i] = p[i];
     } else if constexpr (MODE == kReplay) {
       // torch Categorical(probs).entropy(): normalise, log clamped at float min
       float tot = 0.f;
@@ -160,7 +164,10 @@ __device__ __forceinline__ void core_finish(const StepArgs& a, const float* logi
         const float l = pn > 0.f ? logf(pn) : -FLT_MAX;
         h -= pn * l;
       }
-      a.ent[ge] += (double)h;
+      if (ent_acc)
+        *ent_acc += (double)h;
+      else
+        a.ent[ge] += (double)h;
     } else {
       if (a.probs)
         for (int i = 0; i < A; ++i) a.probs[(ge * a.T + a.t) * A + i] = p[i];
@@ -237,6 +244,10 @@ __global__ void core_kernel_hpm2(Layout L, StepArgs a); // two pairs per workgro
 // replay input projection of a chunk in the fp16 pair form on MFMA: grid (n_lanes / 2, kGateNT / 4)
 template <int E>
 __global__ void xproj_pair_kernel(Layout L, StepArgs a, int t0, int tc, float* gx);
+// the entropy replay of one chunk (steps t0 .. t0 + tc - 1 on a.gx) in ONE launch: core_kernel_hpm<E, kReplay>'s
+// step for two pairs per workgroup in a loop, h / c / ent in registers, the next step's first W_hh fragments in flight under each epilogue
+template <int E, int MODE>  // kReplay (entropy sums) or kStrategy (probabilities over a probe sequence)
+__global__ void replay_chunk_hpm2(Layout L, StepArgs a, int t0, int tc);
 // MFMA images (kMImg halves each) of n half packs: grid (kFcKS + 4 kGateKS, n)
 __global__ void mfma_image_kernel(Layout L, const _Float16* src, int64_t src_stride, _Float16* dst);
 constexpr int kHThreads = 512;

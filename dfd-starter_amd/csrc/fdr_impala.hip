@@ -1462,15 +1462,19 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
         a.gx = gx;
         a.gx_t0 = t0;
       }
+      if constexpr (E <= 4) {
+        if (a.gx && h && a.epm && ctx.core_mfma == 2 && a.n_lanes % 4 == 0) {  // the whole chunk in one launch
+          hipLaunchKernelGGL((replay_chunk_hpm2<E, kReplay>), dim3(a.n_lanes / 4), dim3(2 * kCoreThreads), 0, stream, L,
+                             a, t0, tc);
+          for (int t = t0; t < t0 + tc; ++t) mark(prof, stream);  // the profiler's per-step marks
+          continue;
+        }
+      }
       for (int t = t0; t < t0 + tc; ++t) {
         a.t = t;
         bool pair_done = false;
         if constexpr (E <= 4) {
-          if (a.gx && h && a.epm && ctx.core_mfma == 2 && a.n_lanes % 4 == 0) {
-            hipLaunchKernelGGL((core_kernel_hpm2<E, kReplay>), dim3(a.n_lanes / 4), dim3(2 * kCoreThreads), 0, stream,
-                               L, a);
-            pair_done = true;
-          } else if (a.gx && h && a.epm) {
+          if (a.gx && h && a.epm) {
             hipLaunchKernelGGL((core_kernel_hpm<E, kReplay>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L,
                                a);
             pair_done = true;
@@ -1796,7 +1800,7 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
     a.hpack_stride = L.hpack;
     launch_pack<_Float16>(L, c.lanes, a.hpack, n2, c.n_lanes, 1, stream);
   }
-  // antithetic pairs (fp16): the recurrence streams each pair's sigma-eps image once (core_kernel_hpm2<1, kStrategy>,
+  // antithetic pairs (fp16): the recurrence streams each pair's sigma-eps image once (replay_chunk_hpm2<1, kStrategy>,
   // x W_ih^T by xproj_pair_kernel), as the rollout's pair form -- conv and fc stay per lane (per-lane half pack)
   const bool pair_form = half && c.pairs && c.core_mfma >= 1 && c.n_lanes % 4 == 0 && c.lanes.table &&
                          c.lanes.base_stride == 0;
@@ -1861,12 +1865,14 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
       hipLaunchKernelGGL(lstm_xproj_kernel<false>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);
     a.gx = gx;
     a.gx_t0 = t0;
+    if (pair_form) {  // the chunk's sequence steps in one launch
+      hipLaunchKernelGGL((replay_chunk_hpm2<1, kStrategy>), dim3(c.n_lanes / 4), dim3(2 * kCoreThreads), 0, stream, L, a,
+                         t0, tc);
+      continue;
+    }
     for (int t = t0; t < t0 + tc; ++t) {
       a.t = t;
-      if (pair_form)
-        hipLaunchKernelGGL((core_kernel_hpm2<1, kStrategy>), dim3(c.n_lanes / 4), dim3(2 * kCoreThreads), 0, stream, L,
-                           a);
-      else if (half)
+      if (half)
         hipLaunchKernelGGL((core_kernel_h<1, kStrategy>), dim3(c.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
       else
         hipLaunchKernelGGL((core_kernel<1, kStrategy>), dim3(c.n_lanes), dim3(kCoreThreads), 0, stream, L, a);

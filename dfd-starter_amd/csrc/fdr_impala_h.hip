@@ -2745,7 +2745,9 @@ template <int E, int MODE>
 __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_eu(2))) void core_kernel_hpm2(
     Layout L, StepArgs a) {
   constexpr int E2 = 2 * E, NE = 4 * E;  // envs of a pair / of the workgroup's 4 lanes
-  constexpr bool kRep = seq_mode(MODE);  // kReplay / kStrategy: the W_hh product on a.gx (x W_ih^T of the chunk)
+  // the rollout step only: the sequence modes run whole chunks per launch (replay_chunk_hpm2 below)
+  static_assert(MODE == kRollout, "core_kernel_hpm2 is the rollout step");
+  constexpr bool kRep = false;
   constexpr int kKs0 = kRep ? kCoreIn / 32 : 0, kNks = kGateKS - kKs0;
   static_assert(NE <= 16 && (NE & (NE - 1)) == 0, "the workgroup's envs are the B operand's columns (mod NE)");
   constexpr int XP = kFeat + 16, GP = kGateKS * 32 + 16;  // f16 pitches, as core_kernel_hpm
@@ -2970,10 +2972,168 @@ __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_e
 template __global__ void core_kernel_hpm2<1, kRollout>(Layout, StepArgs);
 template __global__ void core_kernel_hpm2<2, kRollout>(Layout, StepArgs);
 template __global__ void core_kernel_hpm2<4, kRollout>(Layout, StepArgs);
-template __global__ void core_kernel_hpm2<1, kReplay>(Layout, StepArgs);
-template __global__ void core_kernel_hpm2<2, kReplay>(Layout, StepArgs);
-template __global__ void core_kernel_hpm2<4, kReplay>(Layout, StepArgs);
-template __global__ void core_kernel_hpm2<1, kStrategy>(Layout, StepArgs);  // lane strategies of antithetic pairs
+
+// ---- The entropy replay of a whole chunk per launch (ctx core_mfma = 2) -----------------------------------------------
+// A per-step replay launch (two pairs per workgroup) streamed the pairs' W_hh images in ~38 us of its ~62 at config 5
+// and spent the rest on its prologue (h / c / biases / signs) and epilogue (cell, BN1d, head, entropy).  The pairs'
+// sequences are independent, so one workgroup runs every step of the chunk for its two pairs: the prologue runs once,
+// h / c / the entropy sums stay in registers, and the next step's first fragments load under the epilogue (the
+// weights do not depend on h).  Each step is core_kernel_hpm<E, kReplay>'s arithmetic in its order: bitwise equal to
+// the one-pair form (core_mfma 1) over whole episodes.
+template <int E, int MODE>
+__global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_eu(2))) void replay_chunk_hpm2(
+    Layout L, StepArgs a, int t0, int tc) {
+  static_assert(MODE == kReplay || MODE == kStrategy, "sequence modes");
+  constexpr int E2 = 2 * E, NE = 4 * E;
+  constexpr int kKs0 = kCoreIn / 32, kNks = kGateKS - kKs0, NQ = 4 * kNks;
+  static_assert(NE <= 16 && (NE & (NE - 1)) == 0, "the workgroup's envs are the B operand's columns (mod NE)");
+  constexpr int GP = kGateKS * 32 + 16;
+  __shared__ __attribute__((aligned(16))) float gates[kGates * NE];
+  __shared__ __attribute__((aligned(16))) _Float16 gh[NE * GP];
+  __shared__ float hs[kHid * NE];
+  __shared__ float logit[NE * kMaxAct];
+  __shared__ float bsum[4 * kGates];
+  const int j = threadIdx.x, w = j >> 6, l = j & 63;
+  const int u = j & (kHid - 1), hf = j >> 8;
+  const int l0 = 4 * blockIdx.x;
+  auto pkl = [&](int li) { return a.pack + (int64_t)(l0 + li) * a.pack_stride; };
+  const _Float16* ep0 = a.epm + (int64_t)(2 * blockIdx.x) * kMImg;
+  const _Float16* ep1 = ep0 + kMImg;
+  auto ring = mfma_ring2<NQ>(a.thm + kFcImg, ep0 + kFcImg, ep1 + kFcImg, [w, l](int q) {
+    const int g = q / kNks, ks = kKs0 + q - g * kNks;
+    return ((int64_t)(ks * kGateNT + 8 * w + 2 * g) * 64 + l) * 8;
+  });
+  ring.prime();
+  const int64_t e0 = (int64_t)l0 * E;
+  const int ep_ = hf * E2;
+  const int8_t* sgp = a.sign ? a.sign + l0 : reinterpret_cast<const int8_t*>(a.pack);  // branch-free
+  const int8_t sg0 = sgp[0], sg1 = sgp[1], sg2 = sgp[2], sg3 = sgp[3];
+  const int A = a.n_act;
+  const int benv = (l & 15) & (NE - 1), bl = benv / E;
+  const int8_t bsg = bl == 0 ? sg0 : (bl == 1 ? sg1 : (bl == 2 ? sg2 : sg3));
+  const unsigned smask = (a.sign && bsg < 0) ? 0x80008000u : 0u;
+  const unsigned zmask = (a.sign && bsg == 0) ? 0u : ~0u;
+  const unsigned ma = (bl < 2 ? ~0u : 0u) & zmask, mb = (bl < 2 ? 0u : ~0u) & zmask;
+  auto bfrag = [&](const _Float16* rowp, int k0, h8& x, h8& xa, h8& xb) {
+    x = *reinterpret_cast<const h8*>(rowp + k0 + 8 * (l >> 4));
+    const u32x4 sx = __builtin_bit_cast(u32x4, x) ^ u32x4{smask, smask, smask, smask};
+    xa = __builtin_bit_cast(h8, sx & u32x4{ma, ma, ma, ma});
+    xb = __builtin_bit_cast(h8, sx & u32x4{mb, mb, mb, mb});
+  };
+  float cj[E2], hj[E2];
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    gh[(ep_ + e) * GP + kCoreIn + u] = (_Float16)a.h[(e0 + ep_ + e) * kHid + u];
+    cj[e] = a.c[(e0 + ep_ + e) * kHid + u];
+    hj[e] = 0.f;
+  }
+  for (int i = j; i < NE * (GP - kGateK); i += 2 * kCoreThreads) {
+    const int e = i / (GP - kGateK);
+    gh[e * GP + kGateK + i - e * (GP - kGateK)] = (_Float16)0.f;
+  }
+#pragma unroll
+  for (int it = 0; it < 4 * kGates / (2 * kCoreThreads); ++it) {
+    const int i = j + it * 2 * kCoreThreads, li = i / kGates, col = i & (kGates - 1);
+    const float* pk = pkl(li);
+    bsum[i] = pk[L.lstm_bih + col] + pk[L.lstm_bhh + col];
+  }
+  if (j < NE) gh[j * GP + kHid] = (_Float16)0.f;  // W_ih's reward row: its product is inside a.gx
+  // head BN1d of unit u for the pair's two lanes (constant over the chunk)
+  float bsc[2], bsh[2];
+  {
+    const float rmv = (a.bn_mean ? a.bn_mean + L.bn_stat[16] : a.pack)[u];  // branch-free
+    const float rvv = (a.bn_var ? a.bn_var + L.bn_stat[16] : a.pack)[u];
+    const float rm = a.bn_mean ? rmv : 0.f, rv = a.bn_var ? rvv : 1.f;
+#pragma unroll
+    for (int h2i = 0; h2i < 2; ++h2i) {
+      const float* pk = pkl(2 * hf + h2i);
+      bsc[h2i] = pk[L.bn_w[16] + u] * (1.f / sqrtf(rv + kBnEps));
+      bsh[h2i] = fmaf(-rm, bsc[h2i], pk[L.bn_b[16] + u]);
+    }
+  }
+  // thread j < NE: env j's entropy sum, continued from a.ent in the per-step kernel's order and stored at the end
+  double ent = MODE == kReplay ? a.ent[e0 + (j & (NE - 1))] : 0.0;
+  for (int s = 0; s < tc; ++s) {
+    const int t = t0 + s;
+    float gxv[E2][4];
+    {
+      const float* g = a.gx + ((int64_t)(t - a.gx_t0) * a.n_lanes * E + e0 + ep_) * kGates + u;
+#pragma unroll
+      for (int e = 0; e < E2; ++e)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) gxv[e][q] = g[(int64_t)e * kGates + q * kHid];
+    }
+    __syncthreads();  // gh holds h_(t-1) (the prologue or the previous step's cell phase)
+    {
+      f32x4 acc[2];
+      const _Float16* grow = gh + benv * GP;
+      ring.run([&](int q, const h8 (&tf)[2], const h8 (&fa)[2], const h8 (&fb)[2]) {
+        const int g = q / kNks, ks = kKs0 + q - g * kNks;
+        if (ks == kKs0)
+#pragma unroll
+          for (int jt = 0; jt < 2; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        h8 x, xa, xb;
+        bfrag(grow, 32 * ks, x, xa, xb);
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+          acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(tf[jt], x, acc[jt], 0, 0, 0);
+          acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[jt], xa, acc[jt], 0, 0, 0);
+          acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[jt], xb, acc[jt], 0, 0, 0);
+        }
+        if (ks == kGateKS - 1 && (l & 15) < NE) {
+#pragma unroll
+          for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              gates[(16 * (8 * w + 2 * g + jt) + 4 * (l >> 4) + i) * NE + (l & 15)] = acc[jt][i];
+        }
+      });
+    }
+    if (s + 1 < tc) ring.prime();  // the next step's first fragments, under this step's epilogue
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E2; ++e) {
+      const int we = ep_ + e;
+      float pre[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = g * kHid + u;
+        pre[g] = gates[col * NE + we] + bsum[(we / E) * kGates + col];
+        pre[g] += gxv[e][g];
+      }
+      auto sg = [](float x) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x)); };
+      const float gi = sg(pre[0]), gf = sg(pre[1]), gg = tanh_fast(pre[2]), go = sg(pre[3]);
+      cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
+      hj[e] = go * tanh_fast(cj[e]);
+      gh[we * GP + kCoreIn + u] = (_Float16)hj[e];  // the next step's B rows (read after its first barrier)
+    }
+#pragma unroll
+    for (int h2i = 0; h2i < 2; ++h2i)
+#pragma unroll
+      for (int e = 0; e < E; ++e) hs[u * NE + ep_ + h2i * E + e] = fmaf(hj[h2i * E + e], bsc[h2i], bsh[h2i]);
+    __syncthreads();
+    if (j < A * NE) {
+      const int ai = j / NE, e = j - ai * NE;
+      const float* pk = pkl(e / E);
+      const float* wh = pk + L.head_w + ai * kHid;
+      float sacc = 0.f;
+      for (int k = 0; k < kHid; ++k) sacc = fmaf(wh[k], hs[k * NE + e], sacc);
+      logit[e * kMaxAct + ai] = sacc + pk[L.head_b + ai];
+    }
+    __syncthreads();
+    if (j < NE) core_finish<E, MODE>(a, logit + (j / E) * E * kMaxAct, l0 + j / E, j % E, false, &ent, t);
+  }
+#pragma unroll
+  for (int e = 0; e < E2; ++e) {
+    a.h[(e0 + ep_ + e) * kHid + u] = hj[e];
+    a.c[(e0 + ep_ + e) * kHid + u] = cj[e];
+  }
+  if (MODE == kReplay && j < NE) a.ent[e0 + j] = ent;
+}
+template __global__ void replay_chunk_hpm2<1, kReplay>(Layout, StepArgs, int, int);
+template __global__ void replay_chunk_hpm2<2, kReplay>(Layout, StepArgs, int, int);
+template __global__ void replay_chunk_hpm2<4, kReplay>(Layout, StepArgs, int, int);
+template __global__ void replay_chunk_hpm2<1, kStrategy>(Layout, StepArgs, int, int);
 
 // Entropy replay, input projection of one chunk in the fp16 pair form on MFMA: gx = theta X + s (E X) with the
 // gate images' k-steps 0 .. 8 (rows 0 .. 287 = W_ih^T's 257 rows; X is zero beyond k = 256) -- the per-lane
