@@ -577,6 +577,22 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* d, const float* thet
   return impala::launch_forward(f, ws, ws_bytes, (hipStream_t)stream);
 }
 
+int64_t fdr_impala_bn_refresh_workspace_bytes(int32_t n) { return n < 0 ? -1 : impala::vbn_workspace_bytes(n); }
+
+int fdr_impala_bn_refresh(fdr_ctx* ctx, const fdr_impala_desc* d, const float* theta, int32_t n, const float* frames,
+                          const float* reward, int32_t first_done, float* h, float* c, float momentum, float* bn_mean,
+                          float* bn_var, void* ws, int64_t ws_bytes, fdr_stream stream) {
+  FDR_CTX(ctx, C);
+  impala::Layout L;
+  int rc = impala_layout(d, &L);
+  if (rc) return rc;
+  if (!theta || !frames || !bn_mean || !bn_var) return set_error(FDR_ERR_INVALID, "NULL pointer");
+  if ((h == nullptr) != (c == nullptr)) return set_error(FDR_ERR_INVALID, "h and c must both be given or both NULL");
+  if (n < 2) return set_error(FDR_ERR_INVALID, "train-mode BatchNorm1d needs n >= 2 samples");
+  impala::VbnCall v{&L, theta, n, frames, reward, first_done != 0, h, c, momentum, bn_mean, bn_var};
+  return impala::launch_vbn(v, ws, ws_bytes, (hipStream_t)stream);
+}
+
 int64_t fdr_impala_strategies_workspace_bytes(const fdr_impala_desc* d, int32_t n_lanes, int32_t n_states) {
   impala::Layout L;
   if (!d || n_lanes < 0 || n_states < 0 || !impala::make_layout(d->n_act, &L)) return -1;

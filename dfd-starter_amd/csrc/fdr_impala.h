@@ -318,5 +318,22 @@ int read_profile(Context& ctx, double* out3);
 void destroy_profile(Profile* p);
 int launch_forward(const ForwardCall& c, void* ws, int64_t ws_bytes, hipStream_t stream);
 
+// ImpalaPolicy.compute_vbn (policies/impala.py:12-16): train-mode pass of an n-obs buffer (fdr_impala_vbn.hip)
+struct VbnCall {
+  const Layout* layout;
+  const float* theta;
+  int n;
+  const float* frames;   // [n][3][64][64] f32 0..255
+  const float* reward;   // [n] or NULL
+  int first_done;        // the first obs' done flag: zero the carried state
+  float* h;              // [256] in/out carried LSTM state, or NULL (zero, not written)
+  float* c;
+  float momentum;
+  float* bn_mean;        // [fdr_impala_num_bn_stats] running stats, updated in place
+  float* bn_var;
+};
+int64_t vbn_workspace_bytes(int n);
+int launch_vbn(const VbnCall& c, void* ws, int64_t ws_bytes, hipStream_t stream);
+
 }  // namespace impala
 }  // namespace fdr

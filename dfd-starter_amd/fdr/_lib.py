@@ -31,7 +31,8 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_fd_grad_fused_out_len",
            "fdr_fd_grad_fused", "fdr_rank_weights", "fdr_dsgd_step_ex", "fdr_fd_step",
            "fdr_ctx_set_rollout_impl", "fdr_ctx_set_replay_gemm", "fdr_ctx_set_core_mfma", "fdr_ctx_set_conv_h2", "fdr_ctx_impala_profile",
-           "fdr_ctx_impala_profile_read", "fdr_ctx_impala_debug_clock", "fdr_noise_draw_indices")
+           "fdr_ctx_impala_profile_read", "fdr_ctx_impala_debug_clock", "fdr_noise_draw_indices",
+           "fdr_impala_bn_refresh_workspace_bytes", "fdr_impala_bn_refresh")
 
 
 class FDRError(RuntimeError):
@@ -136,6 +137,9 @@ def _load():
         "fdr_atari_env_frames": (ctypes.c_int, [ctypes.c_uint64, I64, I32, I32, P, P]),
         "fdr_impala_num_params": (I64, [I32]),
         "fdr_impala_num_bn_stats": (I64, []),
+        "fdr_impala_bn_refresh_workspace_bytes": (I64, [I32]),
+        "fdr_impala_bn_refresh": (ctypes.c_int, [P, ctypes.POINTER(ImpalaDesc), P, I32, P, P, I32, P, P, F32, P, P, P,
+                                                 I64, P]),
         "fdr_impala_workspace_bytes": (I64, [ctypes.POINTER(ImpalaDesc), I32]),
         "fdr_impala_rollout": (ctypes.c_int, [P, ctypes.POINTER(ImpalaDesc), ctypes.POINTER(LanesDesc), I32, U64,
                                               I32, P, P, P, P, P, P, P, I64, P]),

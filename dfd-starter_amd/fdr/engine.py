@@ -502,6 +502,36 @@ def impala_strategies(spec, lanes, n_lanes, frames, reward=None, h=None, c=None,
     return probs
 
 
+def impala_bn_refresh(spec, theta, frames, bn_mean, bn_var, reward=None, first_done=False, h=None, c=None,
+                      momentum=0.1):
+    """ImpalaPolicy.compute_vbn on the device (policies/impala.py:12-16): a train-mode pass of the n-obs buffer
+    frames [n, 3, 64, 64] (0..255) / reward [n] updates bn_mean / bn_var (modules() order) in place; the LSTM runs
+    the n obs as one sequence from (h, c) [256] (zeroed first if first_done; None: zero state) and leaves its end
+    state in h / c."""
+    _check_dev(theta, frames, bn_mean, bn_var, reward, h, c)
+    dev = theta.device
+    frames = frames.to(torch.float32).reshape(-1, 3 * 64 * 64).contiguous()
+    n = frames.shape[0]
+    if reward is not None:
+        reward = reward.to(torch.float32).reshape(-1).contiguous()
+        if reward.numel() != n:
+            raise ValueError("reward must have one entry per buffer frame")
+    if (h is None) != (c is None):
+        raise ValueError("give both h and c, or neither")
+    for t in (h, c, bn_mean, bn_var):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous()):
+            raise ValueError("h / c / bn_mean / bn_var must be contiguous float32")
+    if h is not None and (h.numel() != 256 or c.numel() != 256):
+        raise ValueError("h / c must hold 256 floats")
+    if n < 2:
+        raise ValueError("Expected more than 1 value per channel when training (compute_vbn needs >= 2 obs)")
+    d = spec.desc(None, None)
+    ws = _workspace("impala_vbn", lib.fdr_impala_bn_refresh_workspace_bytes(n), dev)
+    check(lib.fdr_impala_bn_refresh(_c(dev), ctypes.byref(d), _p(theta), n, _p(frames), _p(reward),
+                                    1 if first_done else 0, _p(h), _p(c), float(momentum), _p(bn_mean), _p(bn_var),
+                                    _p(ws), ws.numel(), _stream(dev)), "fdr_impala_bn_refresh")
+
+
 def impala_env_frames(env_seed, n_act, env_id, t0, n, actions=None, device=None):
     """The frame env's observations frame_t (t0 <= t < t0 + n) of global env env_id -> (frames [n, 3, 64, 64]
     f32, rewards [n] f32 returned by the steps given actions [n] (device i32; None -> 0))."""

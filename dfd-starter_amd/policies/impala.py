@@ -50,18 +50,6 @@ class ImpalaNet(nn.Module):
     def bn_layers(self):
         return [m for m in self.modules() if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d))]
 
-    def stats_forward(self, frames, reward):
-        """torch forward used only by compute_vbn (train-mode BN statistics refresh, impala.py:11-15)."""
-        x = frames.float() / 255.0
-        for i in range(len(STAGES)):
-            x = self.feat_convs[i](x)
-            x = self.resnet1[i](x) + x
-            x = self.resnet2[i](x) + x
-        x = F.relu(self.fc(F.relu(x).flatten(1)))
-        ci = torch.cat([x, torch.clamp(reward, -1, 1).view(-1, 1)], dim=-1)
-        out, _ = self.core(ci.unsqueeze(0))        # batch_first: one sequence, as impala.py:166-182
-        return self.policy(out[0])
-
 
 class ImpalaPolicy(Policy):
     KIND = "impala"
@@ -77,11 +65,6 @@ class ImpalaPolicy(Policy):
 
     def _init_params(self):
         pass  # impala.py: the Sequential(ImpalaCNN, Softmax) has no .weight, so normc does nothing
-
-    def bn_stats(self):
-        bns = self.model.bn_layers()
-        return (torch.cat([m.running_mean for m in bns]).float().contiguous(),
-                torch.cat([m.running_var for m in bns]).float().contiguous())
 
     def reset(self, batch_size=1):
         dev = self.flat.device
@@ -150,9 +133,25 @@ class ImpalaPolicy(Policy):
 
     @torch.no_grad()
     def compute_vbn(self, buffer):
-        """impala.py:11-15: one train-mode pass refreshes the BN running stats (torch, off the hot path)."""
-        fr, rw, _ = self._stack(list(buffer) if not isinstance(buffer, dict) else buffer)
+        """impala.py:12-16 on the device (fdr_impala_bn_refresh): the stacked buffer (B = n, T = 1) in train mode --
+        every BatchNorm normalises with its batch statistics and folds them into its running stats (updated in
+        place: they are views of the flat stat buffers), and the batch_first LSTM reads the n obs as ONE sequence
+        from self.state, zeroed iff the first obs is done (impala.py:165-176); self.state becomes the sequence's
+        end state (impala.py:184)."""
+        fr, rw, dn = self._stack(list(buffer) if not isinstance(buffer, dict) else buffer)
         dev = self.flat.device
-        self.model.train()
-        self.model.stats_forward(fr.to(dev), rw.to(dev))
-        self.model.eval()
+        h, c = (s[:1].reshape(256).clone().contiguous() for s in self.state)
+        bns = self._bn_layers
+        bm, bv = self.bn_stats()
+        engine.impala_bn_refresh(self.spec, self.flat, fr.to(dev), bm, bv, reward=rw.to(dev), first_done=bool(dn[0]),
+                                 h=h, c=c, momentum=bns[0].momentum)
+        if not self._bn_views_intact(bns):   # a user replaced a buffer: write the refreshed stats back
+            off = 0
+            for m in bns:
+                k = m.num_features
+                m.running_mean.copy_(bm[off:off + k])
+                m.running_var.copy_(bv[off:off + k])
+                off += k
+        for m in bns:
+            m.num_batches_tracked += 1
+        self.state = (h.view(1, 256), c.view(1, 256))

@@ -46,27 +46,36 @@ class Policy(nn.Module):
                 p.data = flat[off:off + n].view_as(p)
                 off += n
         self.flat = flat
-        # the BN running statistics as views into two flat buffers too (the [n_in | 64 | 64] order the kernels
-        # read): bn_stats() hands them out without a concatenation kernel per launch; torch's train-mode update
-        # and load_state_dict write the buffers in place
+        # the BN running statistics as views into two flat buffers too (the concatenated order the kernels read):
+        # bn_stats() hands them out without a concatenation kernel per launch; torch's load_state_dict and the
+        # device BN refresh write the buffers in place
         self._bn_flat = None
-        bns = [m for m in self.model if isinstance(m, nn.BatchNorm1d)] if isinstance(self.model, nn.Sequential) else []
-        if bns and self.KIND == "discrete":
-            n = sum(m.num_features for m in bns)
-            fm = torch.empty(n, dtype=torch.float32, device=self._device)
-            fv = torch.empty(n, dtype=torch.float32, device=self._device)
-            off = 0
-            with torch.no_grad():
-                for m in bns:
-                    k = m.num_features
-                    fm[off:off + k].copy_(m.running_mean)
-                    fv[off:off + k].copy_(m.running_var)
-                    m.running_mean = fm[off:off + k]
-                    m.running_var = fv[off:off + k]
-                    off += k
-            self._bn_flat = (fm, fv)
+        self._bn_layers = self._bn_modules()
+        if self._bn_layers and self.KIND in ("discrete", "impala"):
+            self._alias_bn(self._bn_layers)
         if self.KIND in ("discrete", "mujoco"):
             self.spec = engine.PolicySpec(self.KIND, self.input_shape, self.output_shape, self.num_params)
+
+    def _bn_modules(self):
+        """BatchNorm layers in modules() order (= the order of the kernels' concatenated running stats)."""
+        if isinstance(self.model, nn.Sequential):
+            return [m for m in self.model if isinstance(m, nn.BatchNorm1d)]
+        return [m for m in self.model.modules() if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d))]
+
+    def _alias_bn(self, bns):
+        n = sum(m.num_features for m in bns)
+        fm = torch.empty(n, dtype=torch.float32, device=self._device)
+        fv = torch.empty(n, dtype=torch.float32, device=self._device)
+        off = 0
+        with torch.no_grad():
+            for m in bns:
+                k = m.num_features
+                fm[off:off + k].copy_(m.running_mean)
+                fv[off:off + k].copy_(m.running_var)
+                m.running_mean = fm[off:off + k]
+                m.running_var = fv[off:off + k]
+                off += k
+        self._bn_flat = (fm, fv)
 
     def _init_params(self):
         self._normc_init()
@@ -97,7 +106,7 @@ class Policy(nn.Module):
     # ---- kernel plumbing ---------------------------------------------------------------------
     def bn_stats(self):
         """(mean, var) device tensors of the BN layers concatenated, or (None, None)."""
-        bns = [m for m in self.model if isinstance(m, nn.BatchNorm1d)]
+        bns = self._bn_layers
         if not bns:
             return None, None
         fl = getattr(self, "_bn_flat", None)

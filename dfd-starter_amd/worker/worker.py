@@ -318,9 +318,12 @@ class Worker(object):
             return None
         states = torch.empty((1, T, p.input_shape), dtype=torch.float32, device=dev)
         om, osd = self.agent.obs_norm_tensors(self.fixed_obs_stats.mean, self.fixed_obs_stats.std)
-        engine.rollout(p.spec, self.agent.env, engine.lanes_desc(p.flat, 0, deterministic=det), 1, 0, jiggle=False,
-                       obs_mean=om, obs_std=osd, bn_mean=bm, bn_var=bv, device=dev, states=states)
-        out = states[0].cpu().numpy()
+        res = engine.rollout(p.spec, self.agent.env, engine.lanes_desc(p.flat, 0, deterministic=det), 1, 0,
+                             jiggle=False, obs_mean=om, obs_std=osd, bn_mean=bm, bn_var=bv, device=dev, states=states)
+        # a terminating env's episode visits only `steps` states (agent.py:36,58: saved_states holds visited obs);
+        # the rows after the done step are never written
+        steps = int(res.timesteps[0].item())
+        out = states[0, :steps].cpu().numpy()
         return out if max_states is None else out[:int(max_states)]
 
     def update(self, state):

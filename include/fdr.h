@@ -447,6 +447,21 @@ int fdr_impala_strategies(fdr_ctx* ctx, const fdr_impala_desc* desc, const fdr_l
                           int32_t n_states, const float* frames, const float* reward, float* h, float* c,
                           float* probs, void* workspace, int64_t workspace_bytes, fdr_stream stream);
 
+/* ImpalaPolicy.compute_vbn (policies/impala.py:12-16, run_sequential.py:156-157): one train-mode pass of the VBN
+ * buffer of n >= 2 obs -- frames [n, 3, 64, 64] f32 (0..255), reward [n] (NULL = 0) -- stacked as the reference
+ * stacks them (B = n, T = 1).  Every BatchNorm normalises with its batch statistics (biased variance; double
+ * accumulation) and updates its running stats in place, in modules() order as fdr_impala_desc.bn_mean:
+ *   rm <- momentum * mean + (1 - momentum) * rm,  rv <- momentum * var * N / (N - 1) + (1 - momentum) * rv
+ * (N = n * H * W per channel); the LSTM reads the n obs as ONE sequence from the carried state h / c [256]
+ * (in/out; NULL = zero state, not written), zeroed first iff first_done (the first obs' done flag,
+ * impala.py:165-176), and h / c receive the end-of-sequence state (impala.py:184).  Only n_act and n_params of
+ * desc are read.  workspace: fdr_impala_bn_refresh_workspace_bytes(n) bytes (~0.4 MB per obs). */
+int64_t fdr_impala_bn_refresh_workspace_bytes(int32_t n);
+int fdr_impala_bn_refresh(fdr_ctx* ctx, const fdr_impala_desc* desc, const float* theta, int32_t n,
+                          const float* frames, const float* reward, int32_t first_done, float* h, float* c,
+                          float momentum, float* bn_mean, float* bn_var, void* workspace, int64_t workspace_bytes,
+                          fdr_stream stream);
+
 /* Observations of the synthetic frame env outside a rollout (eval states and the probe set zeta,
  * run_sequential.py:142-143, 198-213): frames [n, 3, 64, 64] f32 (0..255) of global env `env_id`
  * (= lane_offset * E + lane * E + e of a rollout) at steps t0 .. t0+n-1, and -- given the actions [n] i32

@@ -707,10 +707,84 @@ def g12_impala(patched=True):
          dists=D, novelty=np.array(nov))
 
 
+def g14_impala_vbn():
+    """ImpalaPolicy.compute_vbn (policies/impala.py:12-16; called every epoch by run_sequential.py:156-157 with
+    the VBN buffer of :198-213): the stacked buffer (B = n obs, T = 1) runs through ImpalaCNN in train mode, so
+    every BatchNorm normalises with its batch statistics and folds them into its running stats, and the
+    batch_first LSTM reads the n obs as ONE sequence from the carried self.state, masked by the FIRST obs' done
+    flag (impala.py:165-176), leaving self.state at the sequence end (:184).  Params / initial running stats as
+    G8 (0.1 * table[1000:], table = RandomState(7).randn(2^22)).  Cases, each from the same starting running
+    stats and carried state (h0, c0):
+      a  done[0] = False            (the carried state enters the sequence)
+      b  done[0] = True             (the state is zeroed first)
+      a2 case a, then compute_vbn again on the same buffer (stats and state chained)
+    Records every BN running_mean / running_var (modules() order) and self.state after each case."""
+    from policies.impala import ImpalaPolicy
+    A, N = 6, 16
+    torch.manual_seed(124)
+    pol = ImpalaPolicy((64, 64, 3), A, seed=124)
+    P = pol.num_params
+    rs = np.random.RandomState(7)
+    table = rs.randn(2 ** 22).astype(np.float32)
+    flat = (table[1000:1000 + P] * np.float32(0.1)).astype(np.float32)
+    pol.set_trainable_flat(flat)
+    net = pol.model[0]
+    bns = [m for m in pol.modules() if isinstance(m, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d))]
+    nbn = sum(m.num_features for m in bns)
+    rm = (table[2000000:2000000 + nbn] * np.float32(0.1)).astype(np.float32)
+    rv = (1.0 + 0.5 * np.abs(table[3000000:3000000 + nbn])).astype(np.float32)
+    brs = np.random.RandomState(14)
+    frames = brs.randint(0, 256, size=(N, 3, 64, 64)).astype(np.uint8)
+    rewards = brs.choice([-2.0, -1.0, -0.5, 0.0, 0.25, 1.0, 3.0], size=N).astype(np.float32)
+    dones = brs.rand(N) < 0.25
+    h0 = (0.5 * brs.randn(256)).astype(np.float32)
+    c0 = (0.5 * brs.randn(256)).astype(np.float32)
+
+    def set_stats():
+        with torch.no_grad():
+            o = 0
+            for m in bns:
+                n = m.num_features
+                m.running_mean.copy_(torch.as_tensor(rm[o:o + n]))
+                m.running_var.copy_(torch.as_tensor(rv[o:o + n]))
+                m.num_batches_tracked.zero_()
+                o += n
+        net.state = (torch.as_tensor(h0).view(1, 1, 256).clone(), torch.as_tensor(c0).view(1, 1, 256).clone())
+
+    def buffer(first_done):
+        d = dones.copy()
+        d[0] = first_done
+        return [{"frame": torch.as_tensor(frames[i].astype(np.float32)).view(1, 1, 3, 64, 64),
+                 "reward": torch.as_tensor(rewards[i]).view(1, 1),
+                 "done": torch.as_tensor(bool(d[i])).view(1, 1)} for i in range(N)], d
+
+    def record(tag, out):
+        out[tag + "_rm"] = torch.cat([m.running_mean for m in bns]).numpy().copy()
+        out[tag + "_rv"] = torch.cat([m.running_var for m in bns]).numpy().copy()
+        out[tag + "_h"] = net.state[0].reshape(-1).numpy().copy()
+        out[tag + "_c"] = net.state[1].reshape(-1).numpy().copy()
+
+    out = {}
+    with torch.no_grad():
+        for tag, first_done in (("a", False), ("b", True)):
+            set_stats()
+            buf, d = buffer(first_done)
+            pol.compute_vbn(buf)
+            assert not pol.training
+            record(tag, out)
+            out[tag + "_dones"] = d
+            if tag == "a":
+                pol.compute_vbn(buf)
+                record("a2", out)
+    save("g14_impala_vbn.npz", A=np.array(A), P=np.array(P), N=np.array(N), table_seed=np.array(7),
+         param_offset=np.array(1000), rm=rm, rv=rv, frames=frames, rewards=rewards, h0=h0, c0=c0,
+         momentum=np.array(0.1), **out)
+
+
 GENERATORS = {"g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
               "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g13": g13_worker_terminating, "g8": g8_impala,
               "g9": g9_novelty, "g10": g10_welford, "g11": g11_atari, "g12": g12_history,
-              "g12i": g12_impala, "g12iu": lambda: g12_impala(patched=False)}
+              "g12i": g12_impala, "g12iu": lambda: g12_impala(patched=False), "g14": g14_impala_vbn}
 
 if __name__ == "__main__":
     torch.set_num_threads(1)

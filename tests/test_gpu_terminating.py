@@ -193,3 +193,29 @@ def test_worker_counts_true_steps(eng):
     assert steps < 2 * 128 * env.episode_len
     assert agent.cumulative_timesteps == steps
     assert agent.cumulative_timesteps == steps          # reading twice does not double count
+
+
+def test_worker_eval_states_hold_only_visited_states(eng):
+    """Worker.eval_states / collect_returns on a terminating env return exactly the visited
+    observations of the eval episode (agent.py:36,58 saved_states), never the unwritten rows after the done step."""
+    from envs import SyntheticEnv
+    from policies import DiscretePolicy
+    from utils import SharedNoiseTable
+    from worker import Agent, Worker
+    torch.manual_seed(124)
+    pol = DiscretePolicy(4, 2, seed=124, device=DEV)
+    env = SyntheticEnv.named("cartpole_term", device=DEV)
+    agent = Agent(pol, env, random_seed=7)
+    w = Worker(pol, agent, SharedNoiseTable(1 << 22, pol.num_params, 124), None, sigma=0.02, eval_prob=1.0)
+    # the eval episode's own length: one deterministic unperturbed lane
+    det = torch.ones(1, dtype=torch.int8, device=DEV)
+    res = eng.rollout(pol.spec, env, eng.lanes_desc(pol.flat, 0, deterministic=det), 1, 0, jiggle=False)
+    steps = int(res.timesteps[0].item())
+    assert steps < env.episode_len, "pick a case whose eval episode terminates"
+    st = w.eval_states()
+    assert st.shape == (steps, 4) and np.all(np.isfinite(st))
+    assert w.eval_states(max_states=3).shape == (min(3, steps), 4)
+    rets = w.collect_returns(2)
+    for r in rets:
+        assert r.is_eval and len(r.eval_states) == steps
+        assert np.all(np.isfinite(np.asarray(r.eval_states)))

@@ -109,3 +109,27 @@ def test_strategy_sequence_matches_reference_entropy_pass(g8):
                                        h, c, notdone=[0.0 if g8["dones"][q, t] else 1.0])
         pr, _, _ = oi.strategy(p, bn, g8["frames"][q].astype(np.float32), g8["rewards"][q], h, c)
         np.testing.assert_allclose(pr, g8["ent_probs"][q], atol=1e-6)
+
+
+def test_compute_vbn_matches_reference(golden):
+    """oracle.compute_vbn == the reference's ImpalaPolicy.compute_vbn (G14): every BN's running stats and the
+    carried LSTM state after a train-mode pass of the VBN buffer, for a carried state (a), a first-obs done (b)
+    and two chained calls (a2)."""
+    g = golden("g14_impala_vbn.npz")
+    A, P = int(g["A"]), int(g["P"])
+    tab = np.random.RandomState(int(g["table_seed"])).randn(2 ** 22).astype(np.float32)
+    off = int(g["param_offset"])
+    p = oi.unflatten((tab[off:off + P] * np.float32(0.1)).astype(np.float32), A)
+    fr = g["frames"].astype(np.float32)
+    mom = float(g["momentum"])
+    runs = {}
+    for tag in ("a", "b"):
+        runs[tag] = oi.compute_vbn(p, g["rm"], g["rv"], fr, g["rewards"], bool(g[tag + "_dones"][0]), g["h0"], g["c0"], mom)
+    rm, rv, h, c = runs["a"]
+    runs["a2"] = oi.compute_vbn(p, rm, rv, fr, g["rewards"], False, h, c, mom)
+    for tag, (rm, rv, h, c) in runs.items():
+        np.testing.assert_allclose(rm, g[tag + "_rm"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(rv, g[tag + "_rv"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(h, g[tag + "_h"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(c, g[tag + "_c"], rtol=1e-5, atol=1e-6)
+    assert not np.allclose(runs["a"][2], runs["b"][2])   # the carried state matters
