@@ -21,6 +21,9 @@ int launch_rollout(int n_act, int envs, int T, uint64_t env_seed, const LanesArg
 int launch_forward(int n_act, const float* theta, int n, const float* frames, const float* bn_mean,
                    const float* bn_var, float* probs, float* feat, void* ws, int64_t ws_bytes, hipStream_t stream);
 int launch_env_frames(uint64_t env_seed, uint64_t env_id, int t0, int n, float* frames, hipStream_t stream);
+int64_t strategies_workspace_bytes(int n_act, int n_lanes, int Z);
+int launch_strategies(int n_act, const LanesArgs& lanes, int n_lanes, int Z, const float* frames, const float* bn_mean,
+                      const float* bn_var, float* probs, void* ws, int64_t ws_bytes, hipStream_t stream);
 }  // namespace atari
 }  // namespace fdr
 
@@ -752,6 +755,27 @@ int fdr_atari_forward(fdr_ctx* ctx, const fdr_atari_desc* d, const float* theta,
   if (!theta || !frames || !probs || n < 0) return set_error(FDR_ERR_INVALID, "NULL pointer / bad n");
   return atari::launch_forward(d->n_act, theta, n, frames, d->bn_mean, d->bn_var, probs, feat, ws, ws_bytes,
                                (hipStream_t)stream);
+}
+
+int64_t fdr_atari_strategies_workspace_bytes(const fdr_atari_desc* d, int32_t n_lanes, int32_t n_states) {
+  if (!d) return -1;
+  return atari::strategies_workspace_bytes(d->n_act, n_lanes, n_states);
+}
+
+int fdr_atari_strategies(fdr_ctx* ctx, const fdr_atari_desc* d, const fdr_lanes_desc* lanes, int32_t n_lanes,
+                         int32_t n_states, const float* frames, float* probs, void* ws, int64_t ws_bytes,
+                         fdr_stream stream) {
+  FDR_CTX(ctx, C);
+  if (!d) return set_error(FDR_ERR_INVALID, "atari desc is NULL");
+  const int64_t P = atari::num_params(d->n_act);
+  if (P < 0) return set_error(FDR_ERR_UNSUPPORTED, "n_act must be in 1..32");
+  if (d->n_params != P) return set_error(FDR_ERR_INVALID, "n_params does not match the AtariPolicy layout");
+  if (n_states < 0 || (n_states > 0 && (!frames || !probs))) return set_error(FDR_ERR_INVALID, "NULL pointer / bad Z");
+  LanesArgs la;
+  int rc = lanes_args(lanes, n_lanes, P, &la);
+  if (rc) return rc;
+  return atari::launch_strategies(d->n_act, la, n_lanes, n_states, frames, d->bn_mean, d->bn_var, probs, ws, ws_bytes,
+                                  (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------------------------------------

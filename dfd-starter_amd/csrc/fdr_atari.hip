@@ -124,8 +124,8 @@ __global__ __launch_bounds__(kThreads) void atari_conv_kernel(Layout L, Args A) 
     bnt[2 * c] = sc;
     bnt[2 * c + 1] = pk[w_off + nch] - rm * sc;
   }
-  if (a.frames) {
-    const float* fr = a.frames + env * kFramePix;
+  if (a.frames) {  // shared_frames (strategies): every lane reads the probe frame e
+    const float* fr = a.frames + (a.shared_frames ? (int64_t)e : env) * kFramePix;
     for (int p = threadIdx.x; p < kFramePix; p += kThreads) frame[p] = fr[p];
   } else {  // oracle/atari.py frames: byte (p & 7) of the counter hash of word p >> 3
     const uint64_t gid = (uint64_t)(a.lane_offset * a.envs + env);
@@ -192,7 +192,8 @@ __global__ __launch_bounds__(impala::kCoreThreads) void atari_core_kernel(Layout
   float* logit = hs + kFc * E;
   static_assert((5 * kFc + impala::kMaxAct) * E <= kFeat * E, "atari core LDS aliasing");
   const int lane = blockIdx.x, j = threadIdx.x;
-  const float* pk = a.pack + (int64_t)lane * a.pack_stride;
+  // shared_frames (strategies, E = 1): block b is probe frame b % T of pack lane b / T
+  const float* pk = a.pack + (int64_t)(a.shared_frames ? lane / a.T : lane) * a.pack_stride;
   const int64_t e0 = (int64_t)lane * E;
   for (int i = j; i < kFeat * E; i += impala::kCoreThreads) {
     const int e = i / kFeat, k = i - e * kFeat;
@@ -377,6 +378,60 @@ int launch_forward(int n_act, const float* theta, int n, const float* frames, co
   hipLaunchKernelGGL(atari_conv_kernel, dim3((n + 7) / 8 * 8), dim3(kThreads), 0, stream, L, A);
   hipLaunchKernelGGL((atari_core_kernel<1, impala::kForward>), dim3(n), dim3(impala::kCoreThreads), 0, stream, L, A);
   return check_launch("atari forward");
+}
+
+// AtariPolicy.get_strategy of every lane's theta'_l over Z shared probe frames (policies/atari.py:30-31, the lane
+// novelty of worker.py:53 / strategy_handler.py:25-30): chunks of kStratLanes lanes, each chunk ONE prep, ONE conv
+// launch over (lane, frame) and ONE core launch -- the per-lane forwards of the host loop, batched.
+constexpr int kStratLanes = 256;
+
+int64_t strategies_workspace_bytes(int n_act, int n_lanes, int Z) {
+  Layout L;
+  Offsets o;
+  if (!make_layout(n_act, &L, &o) || n_lanes < 0 || Z < 0) return -1;
+  const int c = std::min(n_lanes, kStratLanes);
+  return plan(L, c, Z).total;
+}
+
+int launch_strategies(int n_act, const LanesArgs& lanes, int n_lanes, int Z, const float* frames, const float* bn_mean,
+                      const float* bn_var, float* probs, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  Layout L;
+  Args A{};
+  if (!make_layout(n_act, &L, &A.o)) return set_error(FDR_ERR_UNSUPPORTED, "n_act must be in 1..32");
+  const int chunk = std::min(n_lanes, kStratLanes);
+  const Plan p = plan(L, chunk, Z);
+  if (!ws || ws_bytes < p.total) return set_error(FDR_ERR_WORKSPACE, "atari strategies workspace too small");
+  if (n_lanes == 0 || Z == 0) return FDR_OK;
+  char* w = static_cast<char*>(ws);
+  StepArgs& a = A.s;
+  a.pack = reinterpret_cast<float*>(w + p.pack);
+  a.pack_stride = L.pack;
+  a.bn_mean = bn_mean;
+  a.bn_var = bn_var;
+  a.envs = Z;
+  a.T = Z;
+  a.n_act = n_act;
+  a.frames = frames;
+  a.shared_frames = 1;
+  a.feat = reinterpret_cast<float*>(w + p.feat);
+  double* n2 = reinterpret_cast<double*>(w + p.n2);
+  for (int l0 = 0; l0 < n_lanes; l0 += chunk) {
+    const int nl = std::min(chunk, n_lanes - l0);
+    LanesArgs la = lanes;
+    la.base = lanes.base + (int64_t)l0 * lanes.base_stride;
+    if (la.idx) la.idx += l0;
+    if (la.sign) la.sign += l0;
+    if (la.deterministic) la.deterministic += l0;
+    la.lane_offset += l0;
+    int rc = impala::launch_prep(L, la, const_cast<float*>(a.pack), n2, nl, stream);
+    if (rc) return rc;
+    a.n_lanes = nl;
+    a.probs = probs + (int64_t)l0 * Z * n_act;
+    hipLaunchKernelGGL(atari_conv_kernel, dim3((nl + 7) / 8 * 8 * Z), dim3(kThreads), 0, stream, L, A);
+    hipLaunchKernelGGL((atari_core_kernel<1, impala::kForward>), dim3(nl * Z), dim3(impala::kCoreThreads), 0, stream,
+                       L, A);
+  }
+  return check_launch("atari strategies");
 }
 
 // The env's frames at steps t0 .. t0 + n - 1 of global env env_id (the atari_conv_kernel hash; they do not depend

@@ -1770,6 +1770,15 @@ int64_t strategies_workspace_bytes(const Layout& L, int n_lanes, int n_states, b
   return strat_plan(L, n_lanes, n_states, fp16, pairs).total;
 }
 
+// The pair form ran lane 2p + 1 on lane 2p's noise: a pair whose offsets differ has no defined result, so both lanes'
+// probabilities become NaN (the rollout's pair form poisons their norms the same way, pair_offsets_kernel)
+__global__ void poison_pair_probs_kernel(const int64_t* __restrict__ idx, int64_t per_lane, float* __restrict__ probs) {
+  const int p = blockIdx.x;
+  if (idx[2 * p] == idx[2 * p + 1]) return;
+  float* q = probs + (int64_t)2 * p * per_lane;
+  for (int64_t e = threadIdx.x; e < 2 * per_lane; e += blockDim.x) q[e] = __builtin_nanf("");
+}
+
 int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipStream_t stream) {
   const Layout& L = *c.layout;
   const int Z = c.n_states;
@@ -1878,6 +1887,9 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
         hipLaunchKernelGGL((core_kernel<1, kStrategy>), dim3(c.n_lanes), dim3(kCoreThreads), 0, stream, L, a);
     }
   }
+  if (pair_form)
+    hipLaunchKernelGGL(poison_pair_probs_kernel, dim3(c.n_lanes / 2), dim3(256), 0, stream, c.lanes.idx,
+                       (int64_t)Z * L.n_act, c.probs);
   return check_launch("impala strategies");
 }
 

@@ -705,3 +705,21 @@ def atari_forward(spec, theta, frames, bn_mean=None, bn_var=None, feat=False):
     check(lib.fdr_atari_forward(_c(dev), ctypes.byref(d), _p(theta), n, _p(frames), _p(probs), _p(f), _p(ws), ws.numel(),
                                 _stream(dev)), "fdr_atari_forward")
     return (probs, f) if feat else probs
+
+
+def atari_strategies(spec, lanes, n_lanes, frames, bn_mean=None, bn_var=None):
+    """AtariPolicy.get_strategy of n_lanes parameter vectors (lanes descriptor) over the Z shared probe frames
+    [Z, 4, 84, 84] (0..255) -> probs [n_lanes, Z, A] f32, batched (fdr_atari_strategies)."""
+    _check_dev(frames)
+    dev = frames.device
+    frames = frames.to(torch.float32).reshape(-1, 4 * 84 * 84).contiguous()
+    Z = frames.shape[0]
+    probs = torch.empty((n_lanes, Z, spec.n_act), dtype=torch.float32, device=dev)
+    d = spec.desc(bn_mean, bn_var)
+    nb = lib.fdr_atari_strategies_workspace_bytes(ctypes.byref(d), n_lanes, Z)
+    if nb < 0:
+        raise ValueError("bad atari spec")
+    ws = _workspace("atari_strat", nb, dev)
+    check(lib.fdr_atari_strategies(_c(dev), ctypes.byref(d), ctypes.byref(lanes), n_lanes, Z, _p(frames), _p(probs),
+                                   _p(ws), ws.numel(), _stream(dev)), "fdr_atari_strategies")
+    return probs

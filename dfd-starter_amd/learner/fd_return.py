@@ -35,7 +35,12 @@ class FDReturn(object):
 
 class FDBatch(object):
     """One batched evaluation.  Lanes of one direction are contiguous (lanes_per_dir = 2 when
-    antithetic: +eps then -eps).  All tensors live on ``device``; ``idx_host`` mirrors idx."""
+    antithetic: +eps then -eps).  All tensors live on ``device``; ``idx_host`` mirrors idx.
+
+    ``idx`` / ``sign`` of a Worker.evaluate batch are views of the Worker's upload ring (64 slots per lane count):
+    a batch kept past the next 63 uploads of its shape stays valid -- the ring then hands the block to the
+    allocator with the compute stream recorded on it (Worker._lanes_to_device) -- so the views never alias a
+    newer upload."""
 
     def __init__(self, reward, entropy, timesteps, norm2, idx, sign, idx_host, sign_host, epoch,
                  lanes_per_dir=1, is_eval=None, novelty=None):
@@ -47,6 +52,8 @@ class FDBatch(object):
         self.is_eval = np.zeros(len(self.sign_host), bool) if is_eval is None else np.asarray(is_eval)
         self.novelty = novelty
         self.obs_stats = None   # (mean [n, d], m2 [n, d], count [n]) device Welford partials, or None
+        self.noise_table = None  # host noise sources: the batch's fl32(noise) rows (idx = row offsets into them)
+        self.encoded = None      # host noise sources: each lane's encoded perturbation
 
     def __len__(self):
         return len(self.sign_host)
@@ -74,7 +81,8 @@ class FDBatch(object):
             r = FDReturn()
             r.epoch = self.epoch
             r.is_eval = bool(self.is_eval[i])
-            r.encoded_noise = "0" if r.is_eval else "{}".format(int(self.idx_host[i]))
+            enc = getattr(self, "encoded", None)    # a host noise source's encoded draws (RNGNoiseSource states)
+            r.encoded_noise = enc[i] if enc is not None else ("0" if r.is_eval else "{}".format(int(self.idx_host[i])))
             r.sign = int(self.sign_host[i])
             r.reward, r.entropy, r.timesteps = float(rew[i]), float(ent[i]), int(ts[i])
             r.novelty = float(nov[i])

@@ -29,7 +29,7 @@ from dsgd import DSGD
 from fdr import dist as fdist
 from fdr import engine
 from utils import math_helpers
-from utils.noise_sources import require_device_table
+from utils.noise_sources import HostNoiseRows, is_host_noise, require_noise_source
 
 from .fd_return import FDBatch
 
@@ -48,8 +48,9 @@ class FiniteDifferences(object):
         self.noise_std = noise_std
         self.policy = policy
         self.gradient_optimizer = gradient_optimizer
-        require_device_table(noise_source, "FiniteDifferences")
+        require_noise_source(noise_source, "FiniteDifferences")
         self.noise_source = noise_source
+        self._host_noise = is_host_noise(noise_source)
         self.omega = omega
         self.batch_size = batch_size
         self.process_group = process_group
@@ -88,8 +89,17 @@ class FiniteDifferences(object):
         return self._step_returns(list(batch), float(policy_reward))
 
     # ------------------------------------------------------------------------------------------
+    def _table(self, b=None):
+        """What lambda is gathered from: a host-noise batch's own fl32(noise) rows, else the shared table."""
+        t = getattr(b, "noise_table", None) if b is not None else None
+        if t is not None:
+            return t
+        if self._host_noise:
+            raise ValueError("a host noise source's FDBatch carries its noise rows (Worker.evaluate sets noise_table)")
+        return self.noise_source.device_table(self.policy.flat.device)
+
     def _step_batch(self, b, policy_reward):
-        table = self.noise_source.device_table(self.policy.flat.device)
+        table = self._table(b)
         if not np.all(b.sign_host != 0):
             raise ValueError("FDBatch for the learner must not contain eval lanes (sign 0)")
         P = self.policy.num_params
@@ -179,8 +189,12 @@ class FiniteDifferences(object):
         if not keep:
             return None
         dev = self.policy.flat.device
-        table = self.noise_source.device_table(dev)
         P = self.policy.num_params
+        if self._host_noise:
+            # finite_differences.py:94: decode() regenerates each return's noise vector on the host (f64); the device
+            # gathers lambda_i = sign fl32(sigma fl32(noise_i)) (+ drift) from those rows
+            return self._step_returns_lambda(keep, policy_reward)
+        table = self.noise_source.device_table(dev)
         current = [r for r in keep if self.dist_map[r.epoch] is None]
         stale = [r for r in keep if self.dist_map[r.epoch] is not None]
         if stale:
@@ -208,9 +222,16 @@ class FiniteDifferences(object):
         all-reduce of g.  Every rank takes this path for every list step, stale returns or not, so the ranks'
         collectives always match."""
         dev = self.policy.flat.device
-        table = self.noise_source.device_table(dev)
         P = self.policy.num_params
         n = len(keep)
+        if self._host_noise:
+            noises = np.stack([self.noise_source.decode(r.encoded_noise) for r in keep]) if n else np.zeros((0, P))
+            rows = HostNoiseRows(np.zeros(P, np.float32), noises, np.arange(n), np.ones(n, np.int8), self.noise_std,
+                                 dev, with_theta=False)
+            table, idx_host = rows.table, rows.idx_host
+        else:
+            table = self.noise_source.device_table(dev)
+            idx_host = np.array([int(r.encoded_noise) for r in keep], np.int64)
         sizes = fdist.exchange_counts(n, dev, self.process_group)
         if sum(sizes) == 0:
             return None
@@ -221,7 +242,7 @@ class FiniteDifferences(object):
         rewards_all, lane_lo = fdist.gather_rewards(rewards, self.process_group, sizes)
         g = self.gradient_memory
         if n:
-            idx_d = torch.as_tensor(np.array([int(r.encoded_noise) for r in keep], np.int64), device=dev)
+            idx_d = torch.as_tensor(idx_host, device=dev)
             sign_d = torch.as_tensor(np.array([int(getattr(r, "sign", 1) or 1) for r in keep], np.int8), device=dev)
             slot_d = torch.as_tensor(np.array([slot_of.get(r.epoch, -1) for r in keep], np.int32), device=dev)
             n2 = engine.fd_lambda_norms(table, idx_d, sign_d, slot_d, self.noise_std, drift, P)

@@ -34,6 +34,7 @@ from learner import FDBatch, FDState, FiniteDifferences
 from policies import AtariPolicy, DiscretePolicy, ImpalaPolicy, MujocoPolicy
 from strategy import StrategyHandler
 from utils import AdaptiveOmega, SharedNoiseTable, math_helpers
+from utils.noise_sources import RNGNoiseSource, SimpleNoiseSource
 from worker import Agent, Worker
 
 
@@ -78,7 +79,7 @@ class SequentialRunner(object):
                  omega_min_value=0, omega_max_value=1, omega_steps_to_min=25, omega_steps_to_max=75,
                  log_to_wandb=False, wandb_project="fd-starter", wandb_group=None, wandb_run_name=None,
                  noise_table_size=25_000_000, antithetic=False, episode_len=None, device=None, verbose=True,
-                 envs_per_lane=1, fp16=False, policy=None):
+                 envs_per_lane=1, fp16=False, policy=None, noise_source="table"):
         if log_to_wandb:
             raise NotImplementedError("wandb logging is not part of the MI355X engine (no network)")
         self.verbose = verbose
@@ -108,7 +109,16 @@ class SequentialRunner(object):
             self.policy = MujocoPolicy(self.env.obs_dim, self.env.act_dim, seed=random_seed, device=self.device)
             dist_fn = math_helpers.gaussian_wasserstein_dist_from_strategies   # SURVEY finding 6 fixed
         opt = opt_fn(self.policy.parameters(), lr=learning_rate)
-        self.noise_source = SharedNoiseTable(noise_table_size, self.policy.num_params, random_seed=random_seed)
+        # noise_source: "table" (SharedNoiseTable, the GPU fast path: offsets into an HBM-resident table) or the
+        # reference runner's default "rng" (run_sequential.py:89, RNGNoiseSource) / "simple": host noise sources,
+        # theta' rows materialised per lane (slow, correct; utils/noise_sources.py HostNoiseRows)
+        if noise_source == "table":
+            self.noise_source = SharedNoiseTable(noise_table_size, self.policy.num_params, random_seed=random_seed)
+        elif noise_source in ("rng", "simple"):
+            cls = RNGNoiseSource if noise_source == "rng" else SimpleNoiseSource
+            self.noise_source = cls(self.policy.num_params, random_seed=random_seed)
+        else:
+            raise ValueError("noise_source must be 'table', 'rng' or 'simple'")
         self.strategy_handler = StrategyHandler(self.policy, dist_fn, max_history_size=max_strategy_history_size,
                                                 fp16=getattr(self.env, "fp16", False))
         self.agent = Agent(self.policy, self.env, random_seed, normalize_obs=normalize_obs)
@@ -217,19 +227,28 @@ class SequentialRunner(object):
             t1 = time.perf_counter()
             is_eval = self._schedule()
             n_dirs = int((~is_eval).sum())
-            idx_dirs = self.noise_source.sample_batch(n_dirs)
             lpd = 2 if self.antithetic else 1
-            # lane layout: training lanes first (lanes of a direction contiguous), eval lanes last
-            lidx = np.concatenate([np.repeat(idx_dirs, lpd), np.zeros(int(is_eval.sum()), np.int64)])
             sign = np.concatenate([np.tile(np.array([1, -1], np.int8), n_dirs) if self.antithetic
                                    else np.ones(n_dirs, np.int8), np.zeros(int(is_eval.sum()), np.int8)])
             det = (sign == 0).astype(np.int8)
-            res, idx_d, sign_d = self.worker.launch(lidx, sign, det, jiggle=False)
+            rows = None
+            if self.worker._host_noise:      # worker.py:27-28: one sample() per direction, theta' rows materialised
+                draws = [self.noise_source.sample() for _ in range(n_dirs)]
+                idx_dirs = [d[0] for d in draws]
+                noises = np.stack([d[1] for d in draws]) if n_dirs else np.zeros((0, self.policy.num_params))
+                row = np.concatenate([np.repeat(np.arange(n_dirs), lpd), np.zeros(int(is_eval.sum()), np.int64)])
+                res, idx_d, sign_d, rows = self.worker._launch_host(noises, row, sign, det, jiggle=False)
+                lidx = rows.idx_host
+            else:
+                idx_dirs = self.noise_source.sample_batch(n_dirs)
+                # lane layout: training lanes first (lanes of a direction contiguous), eval lanes last
+                lidx = np.concatenate([np.repeat(idx_dirs, lpd), np.zeros(int(is_eval.sum()), np.int64)])
+                res, idx_d, sign_d = self.worker.launch(lidx, sign, det, jiggle=False)
             # E envs per lane (frame envs): one return per (lane, env), lane-major; idx_d / sign_d repeat per env
             lidx, sign = np.repeat(lidx, E), np.repeat(sign, E)
             if self.global_obs is not None and getattr(res, "obs_mean", None) is not None:
                 engine.obs_stats_merge(res.obs_mean, res.obs_m2, res.obs_count, *self.global_obs)
-            nov = self.worker.lane_novelty(idx_d, sign_d)          # worker.py:53, every lane at once
+            nov = self.worker.lane_novelty(idx_d, sign_d, table=None if rows is None else rows.table)  # worker.py:53
             nov = np.zeros(len(lidx)) if nov is None else nov.cpu().numpy()
             rew = res.reward.cpu().numpy() + np.array([self.agent.rng.choice((-1e-12, 1e-12)) for _ in lidx])
             ent = res.entropy.cpu().numpy()
@@ -252,6 +271,8 @@ class SequentialRunner(object):
             batch = FDBatch(torch.as_tensor(rew[:n_train], device=dev), res.entropy[:n_train],
                             res.timesteps[:n_train], res.norm2[:n_train], idx_d[:n_train], sign_d[:n_train],
                             lidx[:n_train], sign[:n_train], self.learner.epoch, lanes_per_dir=lpd * E)
+            if rows is not None:
+                batch.noise_table = rows.table
             update_magnitude = self.learner.step(batch, self.policy_reward, self.policy_novelty, self.policy_entropy)
             if self.vbn_buffer is not None:
                 self.policy.compute_vbn(self.vbn_buffer)

@@ -10,7 +10,8 @@ sequence) started from the reset state -- the state Worker._build_ret scores nov
 (worker/agent.py:66 resets the policy before worker.py:53).  Distances and novelty come from
 ``fdr_strategy_distances`` (the reference's
 ``l2_dist`` / ``categorical_tvd`` / ``gaussian_wasserstein_dist_from_strategies``, f64 accumulation).
-AtariPolicy (stateless) strategies are its forward over the zeta frames, one fdr_atari_forward per vector.
+AtariPolicy (stateless) strategies are its forward over the zeta frames (fdr_atari_strategies: every lane or
+archived vector of a call batched, one prep / conv / core launch per 256 vectors).
 ``lane_novelty`` scores every perturbed lane of a batch in two launches -- the batched form of
 ``Worker._build_ret``'s per-return ``compute_novelty`` (worker/worker.py:53), which the reference
 evaluates on the perturbed policy.  Replacement when full follows ``_replace_point`` /
@@ -91,10 +92,12 @@ class StrategyHandler(object):
 
     def _atari_strategies(self, thetas):
         """AtariPolicy.get_strategy (policies/atari.py:31-32: forward(zeta) probs, stateless) of each parameter
-        vector in thetas (device f32 [k, P]) -> [k, Z, A]: fdr_atari_forward over the zeta frames per vector."""
+        vector in thetas (device f32 [k, P]) -> [k, Z, A]: fdr_atari_strategies over the zeta frames, one call."""
         p = self.policy
         bm, bv = p.bn_stats()
-        return torch.stack([engine.atari_forward(p.spec, th, self.zeta, bm, bv) for th in thetas])
+        thetas = thetas.contiguous()
+        zeta = torch.as_tensor(self.zeta, dtype=torch.float32, device=self._dev())
+        return engine.atari_strategies(p.spec, engine.lanes_desc(thetas, thetas.shape[1]), thetas.shape[0], zeta, bm, bv)
 
     def _strategies_of_flat(self, flat):
         """get_strategy(zeta) of one parameter vector -> [1, Z, D]."""
@@ -117,11 +120,11 @@ class StrategyHandler(object):
         """Strategies of the perturbed lanes theta + sign * sigma * table[idx:] -> [n, Z, D].  pairs: the lanes are
         antithetic pairs (same offset, signs +1 / -1), as the rollout that produced them was told."""
         p = self.policy
-        if p.KIND == "atari":   # theta' materialised per chunk of lanes (fdr_perturb), then one forward each
-            out = [self._atari_strategies(engine.perturb(p.flat, table, idx[c:c + 64].contiguous(),
-                                                         sign[c:c + 64].contiguous(), sigma))
-                   for c in range(0, idx.numel(), 64)]
-            return torch.cat(out)
+        if p.KIND == "atari":   # every lane over the zeta frames, batched (fdr_atari_strategies)
+            bm, bv = p.bn_stats()
+            zeta = torch.as_tensor(self.zeta, dtype=torch.float32, device=self._dev())
+            return engine.atari_strategies(p.spec, engine.lanes_desc(p.flat, 0, table, idx, sign, sigma), idx.numel(),
+                                           zeta, bm, bv)
 
         def lanes(Z):
             return engine.lanes_desc(p.flat, 0, table, idx.repeat_interleave(Z), sign.repeat_interleave(Z), sigma)

@@ -16,8 +16,6 @@ import ctypes
 import numpy as np
 import torch
 
-from fdr import _lib
-
 
 class SharedNoiseTable(object):
     def __init__(self, size, n_params, random_seed=123):
@@ -63,9 +61,13 @@ class SharedNoiseTable(object):
         out = np.empty(n, np.int64)
         if n == 0:
             return out
-        rc = _lib.lib.fdr_noise_draw_indices(self._mt_key.ctypes.data, ctypes.byref(self._mt_pos), self._max_sample_idx,
+        try:
+            from fdr import _lib                # loaded on first draw: utils stays importable without libfdr.so
+        except ImportError:
+            _lib = None
+        rc = 2 if _lib is None else _lib.lib.fdr_noise_draw_indices(self._mt_key.ctypes.data, ctypes.byref(self._mt_pos), self._max_sample_idx,
                                              n, out.ctypes.data)
-        if rc == _lib.FDR_ERR_UNSUPPORTED:      # a table wider than 2^32 entries: numpy's own 64-bit path
+        if rc == 2:   # FDR_ERR_UNSUPPORTED (a table wider than 2^32 entries) or no libfdr.so: numpy's own draw
             rs = self._rng
             out = rs.randint(0, self._max_sample_idx, size=n).astype(np.int64)
             _, key, pos, _, _ = rs.get_state()
@@ -105,9 +107,19 @@ class SharedNoiseTable(object):
 
 
 class RNGNoiseSource(object):
-    """noise_sources.py:4-20 (PCG64 state string).  Uses bit_generator.state: Generator.__getstate__
-    returns None on numpy >= 2, which breaks the reference (SURVEY.md finding 3).  Host-only: the
-    GPU path needs a table (SharedNoiseTable)."""
+    """noise_sources.py:4-20 (the reference runner's default source, run_sequential.py:89): every perturbation is a
+    fresh standard_normal(P) draw (f64) of one PCG64 stream, encoded as that stream's state string.  Uses
+    bit_generator.state: Generator.__getstate__ returns None on numpy >= 2, which breaks the reference (SURVEY.md
+    finding 3).  decode() regenerates from a fresh bit generator instead of rewinding self.rng (the reference
+    restores the state into its shared rng: in its synchronous loop that leaves the stream where the worker's
+    last draw left it, which is where this stream stays).
+
+    A host noise source: the GPU path materialises each lane's theta' = fl32(theta + sigma * noise) on the host,
+    exactly the reference's f64 arithmetic (worker.py:28), and hands the rows to the kernels through
+    fdr_lanes_desc.base_stride; the learner gathers lambda from the fl32(noise) rows (Worker / FiniteDifferences,
+    HostNoiseRows).  Correct, and slow: numpy draws P normals per perturbation on one core."""
+
+    host_noise = True
 
     def __init__(self, n_params, random_seed=123):
         self.rng = np.random.default_rng(np.random.SeedSequence(random_seed))
@@ -123,12 +135,16 @@ class RNGNoiseSource(object):
         bg = np.random.PCG64()
         st = bg.state
         st["state"]["state"], st["state"]["inc"] = s, inc
+        st["has_uint32"], st["uinteger"] = 0, 0
         bg.state = st
         return np.random.Generator(bg).standard_normal(size=self.n_params)
 
 
 class SimpleNoiseSource(object):
-    """noise_sources.py:23-33: ships the raw noise vector.  Host-only."""
+    """noise_sources.py:23-33: ships the raw noise vector (RandomState.randn, f64).  A host noise source like
+    RNGNoiseSource: its encoded perturbation IS the vector."""
+
+    host_noise = True
 
     def __init__(self, n_params, random_seed=123):
         self.rng = np.random.RandomState(random_seed)
@@ -142,13 +158,49 @@ class SimpleNoiseSource(object):
         return noise
 
 
-def require_device_table(noise_source, who):
-    """The GPU path gathers perturbations from an HBM-resident table by offset (theta' is never materialised), so
-    only a SharedNoiseTable (or an object with its device_table / sample_batch interface) can drive it.  The
-    reference's RNGNoiseSource / SimpleNoiseSource (utils/noise_sources.py:4-33, the default of
-    run_sequential.py:89) regenerate each vector on the host and have no table to gather from: refuse them at
-    construction with a clear error rather than an AttributeError in the middle of a step."""
-    if not (hasattr(noise_source, "device_table") and hasattr(noise_source, "sample_batch")):
-        raise TypeError("%s needs a SharedNoiseTable noise source (the GPU path gathers table[idx : idx + P] from "
-                        "HBM); got %s -- construct SharedNoiseTable(size, n_params, random_seed) instead"
-                        % (who, type(noise_source).__name__))
+def is_device_table(noise_source):
+    """A table source the kernels gather from by offset (SharedNoiseTable's device_table / sample_batch interface)."""
+    return hasattr(noise_source, "device_table") and hasattr(noise_source, "sample_batch")
+
+
+def is_host_noise(noise_source):
+    """A host source with the reference interface sample() -> (encoded, noise) / decode(encoded) -> noise."""
+    return (not is_device_table(noise_source) and hasattr(noise_source, "sample") and
+            hasattr(noise_source, "decode"))
+
+
+def require_noise_source(noise_source, who):
+    """Worker / FiniteDifferences take a SharedNoiseTable (the fast path: offsets into an HBM-resident table, theta'
+    never materialised) or a host source with the reference's sample / decode interface (RNGNoiseSource,
+    SimpleNoiseSource: theta' rows materialised per lane).  Anything else is refused at construction with a clear
+    error rather than an AttributeError in the middle of a step."""
+    if not (is_device_table(noise_source) or is_host_noise(noise_source)):
+        raise TypeError("%s needs a noise source with the reference interface (SharedNoiseTable, RNGNoiseSource or "
+                        "SimpleNoiseSource); got %s" % (who, type(noise_source).__name__))
+
+
+class HostNoiseRows(object):
+    """Device rows of a host noise source's perturbations for one launch / learner step.
+      theta   [n_lanes, P] f32: theta'_l = fl32(theta + s_l * sigma * noise_l) in f64 as worker.py:28 forms it
+              (set_trainable_flat rounds to f32), theta for eval lanes (s = 0); fdr_lanes_desc base / base_stride P
+      table   [n_rows * P] f32: fl32(noise_r), the "table" the norms / gradient / lane strategies gather from
+      idx     [n_lanes] int64 offsets row * P into table (0 for eval lanes)"""
+
+    def __init__(self, flat_host, noises, row_of_lane, sign, sigma, device, with_theta=True):
+        P = flat_host.size
+        noises = np.asarray(noises, dtype=np.float64).reshape(-1, P)
+        row_of_lane = np.asarray(row_of_lane, np.int64)
+        sign = np.asarray(sign)
+        self.table = torch.as_tensor(noises.astype(np.float32).reshape(-1), device=device)
+        self.idx_host = np.where(sign != 0, row_of_lane * P, 0).astype(np.int64)
+        self.theta = None
+        if with_theta:
+            f64 = flat_host.astype(np.float64)
+            th = np.empty((len(sign), P), np.float32)
+            for l in range(len(sign)):
+                if sign[l] == 0:
+                    th[l] = flat_host
+                else:
+                    th[l] = (f64 + float(sigma) * noises[row_of_lane[l]]) if sign[l] > 0 else \
+                        (f64 - float(sigma) * noises[row_of_lane[l]])
+            self.theta = torch.as_tensor(th, device=device)

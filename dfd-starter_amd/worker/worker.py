@@ -18,7 +18,7 @@ import torch
 from fdr import engine
 from learner.fd_return import FDBatch
 from utils.math_helpers import WelfordRunningStat
-from utils.noise_sources import require_device_table
+from utils.noise_sources import HostNoiseRows, is_host_noise, require_noise_source
 
 
 def obs_partials(res):
@@ -31,8 +31,9 @@ class Worker(object):
     def __init__(self, policy, agent, noise_source, strategy_handler, sigma=0.02, eval_prob=0.1, random_seed=123):
         self.policy = policy
         self.agent = agent
-        require_device_table(noise_source, "Worker")
+        require_noise_source(noise_source, "Worker")
         self.noise_source = noise_source
+        self._host_noise = is_host_noise(noise_source)   # RNGNoiseSource / SimpleNoiseSource: theta' rows per lane
         self.strategy_handler = strategy_handler
         self.sigma = sigma
         self.epoch = -1
@@ -97,6 +98,12 @@ class Worker(object):
         # a fresh block of the copy stream's pool (torch's .to() from pinned memory: ~10 us of host time, where a
         # copy_ into a kept tensor or a direct hipMemcpyAsync cost ~100 us here); no record_stream -- the slot keeps
         # the block until the rollout that read it is proven done (above), so freeing it then records no event
+        old = slot["dev"]
+        if old is not None and torch._C._storage_Use_Count(old.untyped_storage()._cdata) > 2:
+            # a view of the retiring block outlives the ring (an FDBatch kept > _RING - 1 uploads): tell the allocator
+            # the compute stream may still read it, so the block is not handed out before that work is done
+            old.record_stream(main)
+        del old
         slot["dev"] = None
         with torch.cuda.stream(self._copy_stream):
             d = slot["buf"].to(dev, non_blocking=True)
@@ -110,7 +117,7 @@ class Worker(object):
         return (arrs, ev) if defer_wait else arrs
 
     def launch(self, idx, sign, det, seed=None, out=None, jiggle=True, lane_offset=0, lanes_dev=None, pairs=False,
-               timing=None):
+               timing=None, rows=None):
         """Run one rollout over explicit lanes (host arrays) -> FDBatch (asynchronous).  lanes_dev: the same lanes
         already on the device (idx, sign, det), e.g. uploaded ahead by evaluate(prefetch=True).  pairs: lanes 2p,
         2p+1 are antithetic pairs (checked here) -- an Impala rollout then streams each pair's sigma-eps once
@@ -119,8 +126,14 @@ class Worker(object):
         p = self.policy
         n = len(idx)
         idx_d, sign_d, det_d = lanes_dev if lanes_dev is not None else self._lanes_to_device(idx, sign, det)
-        table = self.noise_source.device_table(p.flat.device)
-        lanes = engine.lanes_desc(p.flat, 0, table, idx_d, sign_d, self.sigma, det_d, lane_offset)
+        if rows is not None:
+            # a host noise source: each lane runs its materialised theta' row, unperturbed in the kernel
+            # (fdr_lanes_desc.base_stride = P, no table); norm2 comes from the rows afterwards (_launch_host)
+            lanes = engine.lanes_desc(rows.theta, p.num_params, None, idx_d, sign_d, self.sigma, det_d, lane_offset)
+            pairs = False
+        else:
+            table = self.noise_source.device_table(p.flat.device)
+            lanes = engine.lanes_desc(p.flat, 0, table, idx_d, sign_d, self.sigma, det_d, lane_offset)
         bm, bv = p.bn_stats()
         if seed is None:
             seed = self.agent.next_seed(n)
@@ -157,6 +170,27 @@ class Worker(object):
         if timing is not None:
             timing[1].record()
         return res, idx_d, sign_d
+
+    def _launch_host(self, noises, row_of_lane, sign, det, lane_offset=0, jiggle=True, seed=None, out=None,
+                     timing=None):
+        """One rollout over lanes whose perturbations come from a host noise source (RNGNoiseSource /
+        SimpleNoiseSource): noises [n_rows, P] f64 in the source's draw order, lane l runs
+        theta + sign_l * sigma * noises[row_of_lane[l]] (HostNoiseRows: the reference's f64 formula, rounded to f32).
+        -> (res, idx_d, sign_d, rows); res.norm2 = ||sign fl32(sigma fl32(noise))||^2 per lane, idx_d the lanes' row
+        offsets into rows.table (what the learner and the lane strategies gather from)."""
+        p = self.policy
+        rows = HostNoiseRows(p.get_trainable_flat(), noises, row_of_lane, sign, self.sigma, p.flat.device)
+        res, idx_d, sign_d = self.launch(rows.idx_host, sign, det, seed=seed, out=out, jiggle=jiggle,
+                                         lane_offset=lane_offset, timing=timing, rows=rows)
+        E = getattr(self.agent.env, "envs_per_lane", 1)
+        li, ls = (idx_d[::E].contiguous(), sign_d[::E].contiguous()) if E > 1 else (idx_d, sign_d)
+        if rows.table.numel() >= p.num_params:
+            # fd_lambda_norms reads a sign-0 (eval) lane as +1; the rollout reports 0 for it, as here
+            n2 = engine.fd_lambda_norms(rows.table, li, ls, None, self.sigma, None, p.num_params) * (ls != 0)
+        else:                               # eval lanes only: nothing was drawn
+            n2 = torch.zeros(li.numel(), dtype=torch.float64, device=p.flat.device)
+        res.norm2 = n2.repeat_interleave(E) if E > 1 else n2
+        return res, idx_d, sign_d, rows
 
     def _lanes_of(self, idx, n_dirs, antithetic, lane_range):
         """Host lane arrays of one evaluate() call from its direction indices: (lidx, sign, det, lane_range,
@@ -206,6 +240,8 @@ class Worker(object):
         (SharedNoiseTable.peek_batch: the index stream is unchanged) and uploaded on the copy stream, so the
         next rollout does not wait for its host-to-device copy; a next call with other arguments ignores it.
         timing: (start, end) events around the rollout launch (Worker.launch)."""
+        if self._host_noise:
+            return self._evaluate_host(n_dirs, antithetic, seed, lane_range, out, novelty, timing)
         pre, self._next = self._next, None
         idx = self.noise_source.sample_batch(n_dirs)
         lidx, sign, det, lane_range, rank_lanes = self._lanes_of(idx, n_dirs, antithetic, lane_range)
@@ -241,17 +277,61 @@ class Worker(object):
         b.rank_lanes = None if rank_lanes is None else [k * E for k in rank_lanes]
         return b
 
+    def _evaluate_host(self, n_dirs, antithetic, seed, lane_range, out, novelty, timing):
+        """evaluate() with a host noise source: every rank draws all n_dirs vectors in the source's order (the
+        stream has no skip-ahead) and materialises the theta' rows of its own directions."""
+        draws = [self.noise_source.sample() for _ in range(int(n_dirs))]
+        lpd = 2 if antithetic else 1
+        _, sign, det, lane_range, rank_lanes = self._lanes_of(np.zeros(int(n_dirs), np.int64), n_dirs, antithetic,
+                                                              lane_range)
+        lo = 0 if lane_range is None else lane_range[0]
+        d_lo = lo // lpd
+        nd = len(sign) // lpd
+        noises = np.stack([draws[d_lo + d][1] for d in range(nd)]) if nd else np.zeros((0, self.policy.num_params))
+        row = np.repeat(np.arange(nd, dtype=np.int64), lpd)
+        res, idx_d, sign_d, rows = self._launch_host(noises, row, sign, det, lane_offset=lo, seed=seed, out=out,
+                                                     timing=timing)
+        lidx = rows.idx_host
+        enc = [str(draws[d_lo + d][0]) if not isinstance(draws[d_lo + d][0], np.ndarray) else draws[d_lo + d][0]
+               for d in range(nd) for _ in range(lpd)]
+        E = getattr(self.agent.env, "envs_per_lane", 1)
+        if E > 1:
+            lidx, sign = np.repeat(lidx, E), np.repeat(sign, E)
+            enc = [e for e in enc for _ in range(E)]
+        if getattr(self.agent.env, "terminates", False):
+            self.agent.add_timesteps(res.timesteps)
+        else:
+            self.agent.cumulative_timesteps += int(len(lidx)) * self.agent.env.episode_len
+        nov = self.lane_novelty(idx_d, sign_d, table=rows.table) if novelty else None
+        b = FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, lidx, sign, self.epoch,
+                    lanes_per_dir=lpd * E, novelty=nov)
+        b.noise_table, b.encoded = rows.table, enc
+        b.obs_stats = obs_partials(res)
+        b.rank_lanes = None if rank_lanes is None else [k * E for k in rank_lanes]
+        return b
+
     # ---- reference API ----------------------------------------------------------------------
     @torch.no_grad()
     def collect_returns(self, n=1):
         is_eval = np.array([self.rng.uniform(0, 1) < self.eval_prob for _ in range(n)])
         idx = np.zeros(n, np.int64)
         k = int((~is_eval).sum())
-        if k:
-            idx[~is_eval] = self.noise_source.sample_batch(k)
         sign = np.where(is_eval, 0, 1).astype(np.int8)
-        res, idx_d, sign_d = self.launch(idx, sign, is_eval.astype(np.int8), jiggle=False)
-        nov = self.lane_novelty(idx_d, sign_d)
+        host_rows, enc = None, None
+        if self._host_noise:        # worker.py:27-28 per training lane: sample() in order, theta' materialised
+            draws = [self.noise_source.sample() for _ in range(k)]
+            row = np.cumsum(~is_eval) - 1
+            noises = np.stack([d[1] for d in draws]) if k else np.zeros((0, self.policy.num_params))
+            res, idx_d, sign_d, host_rows = self._launch_host(noises, np.maximum(row, 0), sign,
+                                                              is_eval.astype(np.int8), jiggle=False)
+            idx = host_rows.idx_host
+            it = iter(draws)
+            enc = ["0" if e else next(it)[0] for e in is_eval]
+        else:
+            if k:
+                idx[~is_eval] = self.noise_source.sample_batch(k)
+            res, idx_d, sign_d = self.launch(idx, sign, is_eval.astype(np.int8), jiggle=False)
+        nov = self.lane_novelty(idx_d, sign_d, table=None if host_rows is None else host_rows.table)
         E = getattr(self.agent.env, "envs_per_lane", 1)
         if E > 1:
             idx, sign, is_eval = np.repeat(idx, E), np.repeat(sign, E), np.repeat(is_eval, E)
@@ -260,6 +340,9 @@ class Worker(object):
             eval_states = [{k: v[i:i + 1] for k, v in eval_states.items()} for i in range(len(eval_states["frame"]))]
         b = FDBatch(res.reward, res.entropy, res.timesteps, res.norm2, idx_d, sign_d, idx, sign, self.epoch,
                     is_eval=is_eval)
+        if enc is not None:
+            b.encoded = [e for e in enc for _ in range(E)] if E > 1 else enc
+            b.noise_table = host_rows.table
         b.novelty = None if nov is None else nov.cpu().numpy()
         b.obs_stats = obs_partials(res)
         rets = b.to_returns()
@@ -273,7 +356,7 @@ class Worker(object):
         return rets
 
     # ---- novelty path -----------------------------------------------------------
-    def lane_novelty(self, idx_d, sign_d):
+    def lane_novelty(self, idx_d, sign_d, table=None):
         """compute_novelty of every lane's (perturbed) policy, worker.py:53, batched on the device
         (f64 [n]); None without a strategy handler.  With E envs per lane (ImpalaPolicy / AtariPolicy)
         idx_d / sign_d repeat per env: one strategy per lane, its novelty repeated for the lane's envs."""
@@ -283,8 +366,9 @@ class Worker(object):
         E = getattr(self.agent.env, "envs_per_lane", 1)
         if E > 1:
             idx_d, sign_d = idx_d[::E].contiguous(), sign_d[::E].contiguous()
-        nov = h.lane_novelty(self.noise_source.device_table(self.policy.flat.device), idx_d, sign_d, self.sigma,
-                             pairs=self._launch_pairs)
+        if table is None:      # the shared table; a host noise source passes its launch's rows (HostNoiseRows)
+            table = self.noise_source.device_table(self.policy.flat.device)
+        nov = h.lane_novelty(table, idx_d, sign_d, self.sigma, pairs=self._launch_pairs)
         return nov.repeat_interleave(E) if E > 1 else nov
 
     def eval_states(self, max_states=None):

@@ -420,6 +420,15 @@ int64_t fdr_atari_forward_workspace_bytes(int32_t n_act, int32_t n);
 int fdr_atari_forward(fdr_ctx* ctx, const fdr_atari_desc* desc, const float* theta, int32_t n, const float* frames,
                       float* probs, float* feat, void* workspace, int64_t workspace_bytes, fdr_stream stream);
 
+/* AtariPolicy.get_strategy (policies/atari.py:30-31) of every lane's theta'_l (lanes as for fdr_atari_rollout) over
+ * Z shared probe frames [Z, 4, 84, 84] f32 (0..255): probs [n_lanes, Z, A] -- the lane novelty's strategies
+ * (worker/worker.py:53, strategy/strategy_handler.py:25-30) in one prep / conv / core launch per 256 lanes.
+ * workspace: fdr_atari_strategies_workspace_bytes(desc, n_lanes, Z) bytes. */
+int64_t fdr_atari_strategies_workspace_bytes(const fdr_atari_desc* desc, int32_t n_lanes, int32_t n_states);
+int fdr_atari_strategies(fdr_ctx* ctx, const fdr_atari_desc* desc, const fdr_lanes_desc* lanes, int32_t n_lanes,
+                         int32_t n_states, const float* frames, float* probs, void* workspace, int64_t workspace_bytes,
+                         fdr_stream stream);
+
 /* One step of ImpalaPolicy.forward (policies/impala.py:18-19, 144-186) for n_envs independent
  * envs sharing theta [P]: frames [n_envs, 3, 64, 64] f32 (0..255), reward [n_envs] (NULL = 0),
  * notdone [n_envs] (NULL = 1; multiplies the incoming state), h / c [n_envs, 256] updated in
@@ -440,7 +449,8 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* desc, const float* t
  * (NULL = the reset state, which is the state Worker._build_ret scores novelty in: worker/agent.py:66 resets
  * the policy before compute_novelty).  probs [n_lanes, Z, A] f32 out.  Only n_act, n_params, fp16, pairs, bn_mean,
  * bn_var of desc are read; fp16 with pairs (lanes as for fdr_impala_rollout, n_lanes % 4 == 0, ctx core_mfma >= 1)
- * runs the recurrence in the rollout's pair form on MFMA.
+ * runs the recurrence in the rollout's pair form on MFMA; a pair whose two lanes carry different table offsets then
+ * gets NaN probabilities on both lanes (it would otherwise run lane 2p + 1 on lane 2p's noise).
  * workspace: fdr_impala_strategies_workspace_bytes(desc, n_lanes, Z) bytes. */
 int64_t fdr_impala_strategies_workspace_bytes(const fdr_impala_desc* desc, int32_t n_lanes, int32_t n_states);
 int fdr_impala_strategies(fdr_ctx* ctx, const fdr_impala_desc* desc, const fdr_lanes_desc* lanes, int32_t n_lanes,

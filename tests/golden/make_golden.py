@@ -781,7 +781,83 @@ def g14_impala_vbn():
          momentum=np.array(0.1), **out)
 
 
-GENERATORS = {"g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
+def _patch_rng_noise_source():
+    """SURVEY finding 3: RNGNoiseSource reads Generator.__getstate__(), which returns None on numpy >= 2; the
+    harness patch reads / writes bit_generator.state instead -- otherwise the reference's code as it is
+    (utils/noise_sources.py:4-20: sample() reports the PCG64 state, then draws; decode() restores it and redraws)."""
+    from utils import noise_sources as ns
+    cls = ns.RNGNoiseSource
+    orig = (cls.__init__, cls.sample, cls.decode)
+
+    def __init__(self, n_params, random_seed=123):
+        self.rng = np.random.default_rng(np.random.SeedSequence(random_seed))
+        self.base_state = self.rng.bit_generator.state
+        self.n_params = n_params
+
+    def sample(self):
+        st = self.rng.bit_generator.state
+        state = "{},{}".format(st['state']['state'], st['state']['inc'])
+        noise = self.rng.standard_normal(size=self.n_params)
+        return state, noise
+
+    def decode(self, state):
+        state_data = state.split(",")
+        self.base_state['state']['state'] = int(state_data[0])
+        self.base_state['state']['inc'] = int(state_data[1])
+        self.rng.bit_generator.state = self.base_state
+        return self.rng.standard_normal(size=self.n_params)
+    cls.__init__, cls.sample, cls.decode = __init__, sample, decode
+    return cls, orig
+
+
+def g15_rng_noise_source():
+    """The reference's DEFAULT noise source (run_sequential.py:89: RNGNoiseSource, one noise source object shared
+    by the Worker and the learner) through Worker.collect_returns + FiniteDifferences.step, two epochs, with the
+    finding-3 patch and injected action draws as G7: every return's encoded PCG64 state, reward, entropy, steps,
+    eval flag; the learner's update magnitude, gradient and theta after each step."""
+    from utils.noise_sources import RNGNoiseSource
+    cls, orig = _patch_rng_noise_source()
+    out = {}
+    try:
+        for name, (kind, n_in, n_act), T in (("cheetah", SHAPES["cheetah"], 40), ("cartpole", SHAPES["cartpole"], 30)):
+            env = SyntheticEnv(n_in, n_act, kind == "discrete", T, env_seed=0)
+            pol = make_policy(kind, n_in, n_act, 124)
+            P = pol.num_params
+            pcls = DiscretePolicy if kind == "discrete" else MujocoPolicy
+            inj = _InjectedDiscrete(31) if kind == "discrete" else _InjectedNormal(31)
+            orig_act = pcls.get_action
+            pcls.get_action = lambda self, x, deterministic=False: inj(self, x, deterministic)
+            try:
+                src = RNGNoiseSource(P, random_seed=5)
+                agent = Agent(pol, env, random_seed=11)
+                handler = StrategyHandler(pol, math_helpers.categorical_tvd)
+                worker = Worker(pol, agent, src, handler, sigma=0.02, eval_prob=0.25, random_seed=3)
+                opt = DSGD(pol.parameters(), lr=0.01)
+                omega = AdaptiveOmega()
+                learner = FiniteDifferences(pol, opt, omega, src, noise_std=0.02, batch_size=8, max_delayed_return=10)
+                out[name + "_theta0"] = pol.get_trainable_flat().copy()
+                for e in range(2):
+                    worker.epoch = learner.epoch          # what run_sequential.py:168's worker.update(state) sets
+                    rets = worker.collect_returns(8)
+                    train = [r for r in rets if not r.is_eval]
+                    pre = "%s_e%d_" % (name, e)
+                    out[pre + "reward"] = np.array([r.reward for r in rets])
+                    out[pre + "entropy"] = np.array([r.entropy for r in rets])
+                    out[pre + "timesteps"] = np.array([r.timesteps for r in rets])
+                    out[pre + "is_eval"] = np.array([r.is_eval for r in rets])
+                    out[pre + "encoded"] = np.array([str(r.encoded_noise) for r in rets])
+                    out[pre + "update"] = np.array(learner.step(train, 0.25 * e, 0, 0))
+                    out[pre + "g"] = learner.gradient_memory.copy()
+                    out[pre + "theta"] = pol.get_trainable_flat().copy()
+            finally:
+                pcls.get_action = orig_act
+            out[name + "_T"] = np.array(T)
+    finally:
+        cls.__init__, cls.sample, cls.decode = orig
+    save("g15_rng_noise_source.npz", **out)
+
+
+GENERATORS = {"g15": g15_rng_noise_source, "g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
               "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g13": g13_worker_terminating, "g8": g8_impala,
               "g9": g9_novelty, "g10": g10_welford, "g11": g11_atari, "g12": g12_history,
               "g12i": g12_impala, "g12iu": lambda: g12_impala(patched=False), "g14": g14_impala_vbn}

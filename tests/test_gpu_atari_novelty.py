@@ -82,3 +82,29 @@ def test_sequential_runner_atari_novelty():
         assert np.isfinite(rep["Noisy Reward"]) and np.isfinite(rep["Noisy Novelty"])
     assert r.strategy_handler.archive is not None and r.strategy_handler.archive.shape[1:] == (4, 6)
     assert any(rep["Noisy Novelty"] > 0 for rep in r.history[1:])
+
+
+def test_batched_atari_strategies_equal_per_lane_forwards():
+    """fdr_atari_strategies (every lane's theta' over the Z shared frames, one prep / conv / core
+    launch per 256 lanes) is bitwise the per-lane path it replaced (fdr_perturb, then fdr_atari_forward over zeta
+    for each lane) -- 300 lanes, so two chunks, with out-of-order offsets and a sign-0 lane."""
+    from fdr import engine
+    from policies import AtariPolicy
+    A, Z, n = 5, 3, 300
+    dev = torch.device("cuda", 0)
+    pol = AtariPolicy((84, 84, 4), A, seed=124, device=dev)
+    P = pol.num_params
+    t = onoise.NoiseTable(1 << 21, P, 124)
+    g = np.random.RandomState(4)
+    idx = g.randint(0, t.table.size - P, size=n).astype(np.int64)
+    sign = np.where(g.rand(n) < 0.5, 1, -1).astype(np.int8)
+    sign[7] = 0
+    tab = torch.as_tensor(t.table, device=dev)
+    idx_d, sign_d = torch.as_tensor(idx, device=dev), torch.as_tensor(sign, device=dev)
+    zeta = engine.atari_env_frames(5, 0, 0, Z)
+    bm, bv = pol.bn_stats()
+    got = engine.atari_strategies(pol.spec, engine.lanes_desc(pol.flat, 0, tab, idx_d, sign_d, 0.02), n, zeta, bm, bv)
+    thetas = engine.perturb(pol.flat, tab, idx_d, sign_d, 0.02)
+    want = torch.stack([engine.atari_forward(pol.spec, thetas[l].contiguous(), zeta, bm, bv) for l in range(n)])
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(got.cpu().numpy(), want.cpu().numpy())

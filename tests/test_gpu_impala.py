@@ -450,6 +450,30 @@ def test_pair_with_mismatched_offsets_poisons_its_norms(engine, table, fp16):
         np.testing.assert_array_equal(bad[f][envs], good[f][envs], err_msg=f)
 
 
+def test_strategies_pair_with_mismatched_offsets_poisons_its_probs(engine, table):
+    """fdr_impala_strategies in the fp16 pair form with a pair whose two lanes carry different offsets
+    returns NaN probabilities on both lanes (it would otherwise score lane 2p + 1 with lane 2p's noise); the other
+    pairs' strategies are bitwise those of a batch without the violation."""
+    A, Z = 5, 6
+    theta = _theta(A)
+    dev = "cuda"
+    spec = engine.ImpalaSpec(A, fp16=True, pairs=True)
+    sign = torch.tensor(np.array([1, -1] * 4, np.int8), device=dev)
+    frames = torch.tensor(np.random.RandomState(3).randint(0, 256, size=(Z, 3, 64, 64)).astype(np.float32), device=dev)
+
+    def run(idx):
+        lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
+                                  torch.tensor(np.array(idx, np.int64), device=dev), sign, 0.02)
+        pr = engine.impala_strategies(spec, lanes, len(idx), frames)
+        torch.cuda.synchronize()
+        return pr.cpu().numpy()
+    bad = run([77, 77, 100, 200, 5, 5, 9, 9])
+    good = run([77, 77, 100, 100, 5, 5, 9, 9])
+    assert np.all(np.isnan(bad[2:4]))
+    assert np.all(np.isfinite(good))
+    np.testing.assert_array_equal(bad[[0, 1, 4, 5, 6, 7]], good[[0, 1, 4, 5, 6, 7]])
+
+
 @pytest.mark.parametrize("E,n_pairs", [(4, 3), (4, 4), (1, 6), (2, 2)])
 def test_f32_pair_core_bit_identical(engine, table, E, n_pairs):
     """f32 pair form (fdr_impala_desc.pairs): w = fl32(theta + s fl32(sigma eps)) formed in registers is the

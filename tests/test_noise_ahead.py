@@ -20,21 +20,34 @@ def test_peek_then_sample_is_the_sequential_stream():
     assert list(pk) == seq[:10]
 
 
-def test_host_only_noise_sources_are_refused_at_construction():
-    """the reference's default RNGNoiseSource (run_sequential.py:89) and SimpleNoiseSource have no
-    table for the GPU path to gather from -- a TypeError naming SharedNoiseTable at construction, not an
-    AttributeError mid-step."""
+def test_noise_source_kinds_and_refusal():
+    """the reference's default RNGNoiseSource (run_sequential.py:89) and SimpleNoiseSource are
+    accepted as host noise sources (theta' rows materialised per lane); an object with neither the table nor the
+    sample / decode interface is refused with a TypeError at construction, not an AttributeError mid-step.  The
+    host sources keep the reference's streams: RNGNoiseSource.decode(sample()[0]) regenerates the sampled vector."""
     import pytest
     from learner.finite_differences import FiniteDifferences
-    from utils.noise_sources import RNGNoiseSource, SharedNoiseTable, SimpleNoiseSource
+    from utils.noise_sources import (RNGNoiseSource, SharedNoiseTable, SimpleNoiseSource, is_device_table,
+                                     is_host_noise, require_noise_source)
     from worker.worker import Worker
+    assert is_device_table(SharedNoiseTable(1 << 12, 100, 1)) and not is_host_noise(SharedNoiseTable(1 << 12, 100, 1))
     for src in (RNGNoiseSource(100, 1), SimpleNoiseSource(100, 1)):
-        with pytest.raises(TypeError, match="SharedNoiseTable"):
-            Worker(object(), object(), src, None)
-        with pytest.raises(TypeError, match="SharedNoiseTable"):
-            FiniteDifferences(object(), None, 0.0, src)
-    from utils.noise_sources import require_device_table
-    require_device_table(SharedNoiseTable(1 << 12, 100, 1), "Worker")   # accepted
+        assert is_host_noise(src) and not is_device_table(src)
+        require_noise_source(src, "Worker")
+        enc, noise = src.sample()
+        np.testing.assert_array_equal(src.decode(enc), noise)
+        assert noise.dtype == np.float64 and noise.shape == (100,)
+    with pytest.raises(TypeError, match="noise source"):
+        Worker(object(), object(), object(), None)
+    with pytest.raises(TypeError, match="noise source"):
+        FiniteDifferences(object(), None, 0.0, object())
+    r = RNGNoiseSource(50, 5)
+    ref = np.random.default_rng(np.random.SeedSequence(5))
+    for _ in range(3):
+        enc, noise = r.sample()
+        st = ref.bit_generator.state["state"]
+        assert enc == "{},{}".format(st["state"], st["inc"])
+        np.testing.assert_array_equal(noise, ref.standard_normal(size=50))
 
 
 def test_native_index_draw_is_numpy_randint():
