@@ -554,10 +554,7 @@ def main():
         core_prof = None if prof is None else prof.get("core_kernel")
         roofline = {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": peak, "unit": "TFLOP/s",
                     "frac": round(achieved_tf / peak, 4), "traffic": traffic,
-                    "kernel": ({"0": "impala conv_kernel_h (15 convs, v_mfma_f32_16x16x32_f16; 1 x 8 waves / CU)",
-                                "1": "impala conv_kernel_h2<256> (15 convs, v_mfma_f32_16x16x32_f16; 2 x 4 waves / CU)"}
-                               .get(os.environ.get("FDR_CONV_H2"),
-                                    "impala conv_kernel_h2<512> (15 convs, v_mfma_f32_16x16x32_f16; 2 x 8 waves / CU)")
+                    "kernel": ("impala conv_kernel_h2 (15 convs, v_mfma_f32_16x16x32_f16; 2 x 8 waves / CU)"
                                if fp16 else "impala conv_kernel (15 convs, v_mfma_f32_16x16x4_f32)"),
                     "conv_launch_ms": round(conv_launch_ms, 4), "flop_per_env_step": IMPALA_CONV_FLOP,
                     "envs_per_launch": L * E, "rollout_ms": round(rollout_ms, 3),
@@ -566,13 +563,8 @@ def main():
                                     "unit": "GB/s", "frac": round(core_gbs / HBM_PEAK_GBS, 4),
                                     "launch_ms": round(core_ms / T, 4), "bytes_per_lane_step": core_bytes,
                                     "hbm_bytes_per_launch_algorithmic": core_hbm,
-                                    "form": ({"0": "pair on the VALU (core_kernel_hp)",
-                                              "1": "pair on MFMA: theta x + s (E x) over fragment images, one pair per "
-                                                   "workgroup (core_kernel_hpm)"}
-                                             .get(os.environ.get("FDR_CORE_MFMA"),
-                                                  "pair on MFMA: theta x + s (E x) over fragment images, two pairs "
-                                                  "per workgroup (core_kernel_hpm2)")
-                                             if fp16 else "pair (theta + s sigma-eps)"),
+                                    "form": ("pair on MFMA: theta x + s (E x) over fragment images, two pairs "
+                                             "per workgroup (core_kernel_hpm2)" if fp16 else "pair (theta + s sigma-eps)"),
                                     "traffic": None if core_prof is None else core_prof.get("hbm_bytes_per_launch")},
                     "entropy_replay_ms": round(replay_ms, 3),
                     "profile": None if prof is None else "profiles/%s_summary.md" % prof.get("tag"),

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <string>
 
+#include "../../include/fdr_diag.h"
 #include "fdr_impala.h"
 #include "fdr_internal.h"
 
@@ -119,10 +120,6 @@ Context& default_context() {
                          : strcmp(e, "single") == 0 ? FDR_ROLLOUT_SINGLE
                          : strcmp(e, "wide") == 0   ? FDR_ROLLOUT_WIDE
                                                     : strcmp(e, "pair") == 0 ? FDR_ROLLOUT_PAIR : FDR_ROLLOUT_AUTO;
-    const char* m = getenv("FDR_CORE_MFMA");  // A/B switch: "0" VALU, "1" one pair per workgroup, else two
-    c->core_mfma = !m ? 2 : strcmp(m, "0") == 0 ? 0 : strcmp(m, "1") == 0 ? 1 : 2;
-    const char* h2 = getenv("FDR_CONV_H2");  // A/B switch: "0" selects conv_kernel_h (one workgroup per CU)
-    c->conv_h2 = !h2 ? 2 : strcmp(h2, "0") == 0 ? 0 : strcmp(h2, "1") == 0 ? 1 : strcmp(h2, "3") == 0 ? 3 : 2;
     return c;
   }();
   return *d;
@@ -165,7 +162,7 @@ static int resolve(fdr_ctx* ctx, Context** out) {
 
 extern "C" {
 
-const char* fdr_version(void) { return "fdr 0.4 gfx950"; }
+const char* fdr_version(void) { return "fdr 0.5 gfx950"; }
 const char* fdr_last_error(void) { return g_err.c_str(); }
 
 static int set_impl(Context& c, int32_t impl) {
@@ -178,16 +175,6 @@ int fdr_rollout_set_impl(int32_t impl) { return set_impl(default_context(), impl
 int fdr_ctx_set_rollout_impl(fdr_ctx* ctx, int32_t impl) { return set_impl(ctx ? ctx->c : default_context(), impl); }
 int fdr_ctx_set_replay_gemm(fdr_ctx* ctx, int32_t on) {
   (ctx ? ctx->c : default_context()).replay_gemm = on != 0;
-  return FDR_OK;
-}
-int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on) {
-  if (on < 0 || on > 2) return set_error(FDR_ERR_INVALID, "core_mfma must be 0, 1 or 2");
-  (ctx ? ctx->c : default_context()).core_mfma = on;
-  return FDR_OK;
-}
-int fdr_ctx_set_conv_h2(fdr_ctx* ctx, int32_t on) {
-  if (on < 0 || on > 3) return set_error(FDR_ERR_INVALID, "conv_h2 must be 0, 1, 2 or 3");
-  (ctx ? ctx->c : default_context()).conv_h2 = on;
   return FDR_OK;
 }
 int fdr_ctx_impala_profile(fdr_ctx* ctx, int32_t enable) { return impala::set_profile(ctx ? ctx->c : default_context(), enable); }
@@ -212,8 +199,6 @@ int fdr_ctx_create(int device, fdr_ctx** out) {
   c->c.device = device;
   c->c.cus = cus;
   c->c.rollout_impl = default_context().rollout_impl;  // FDR_ROLLOUT applies to new contexts too
-  c->c.core_mfma = default_context().core_mfma;        // and FDR_CORE_MFMA
-  c->c.conv_h2 = default_context().conv_h2;            // and FDR_CONV_H2
   *out = c;
   return FDR_OK;
 }
@@ -565,7 +550,6 @@ int fdr_impala_forward(fdr_ctx* ctx, const fdr_impala_desc* d, const float* thet
   impala::ForwardCall f{};
   f.layout = &L;
   f.fp16 = d->fp16 != 0;
-  f.conv_h2 = C->conv_h2;
   f.theta = theta;
   f.n_envs = n_envs;
   f.frames = frames;
@@ -619,9 +603,7 @@ int fdr_impala_strategies(fdr_ctx* ctx, const fdr_impala_desc* d, const fdr_lane
   sc.n_lanes = n_lanes;
   sc.n_states = n_states;
   sc.fp16 = d->fp16 != 0;
-  sc.conv_h2 = C->conv_h2;
   sc.pairs = d->pairs != 0;
-  sc.core_mfma = C->core_mfma;
   if (sc.pairs && (n_lanes & 1)) return set_error(FDR_ERR_INVALID, "pairs: n_lanes must be even");
   sc.frames = frames;
   sc.reward = reward;

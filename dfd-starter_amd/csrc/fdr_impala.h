@@ -15,7 +15,7 @@ constexpr int kGates = 1024;
 constexpr int kCoreIn = 257; // fc output + clipped reward (policies/impala.py:116, 163-164)
 #define FDR_CORE_UNROLL 4    // weight-stream loop unroll of the core kernels (loads in flight per thread)
 #define FDR_CORE_UNROLL_H 2  // fp16 step kernel's fc / gate streams (A/B: 0.377 -> 0.360 ms per step vs 4)
-// fp16 pair-form core step on MFMA (core_kernel_hpm): fc W^T and [W_ih | W_hh]^T as v_mfma_f32_16x16x32_f16
+// fp16 pair-form core step on MFMA (core_kernel_hpm2): fc W^T and [W_ih | W_hh]^T as v_mfma_f32_16x16x32_f16
 // A-fragment images [k-step][16-column tile][64 lanes][8 halves] (lane l: W[16 nt + (l & 15)][32 ks + 8 (l >> 4) ..
 // + 7]), one for theta and one per pair for sigma-eps; K of the gates (513) zero-padded to 17 k-steps.
 constexpr int kFcKS = kFeat / 32, kFcNT = kHid / 16;
@@ -92,7 +92,7 @@ struct StepArgs {
   const float* ep32;
   int64_t ep_stride;
   const int8_t* sign;
-  // MFMA form (fp16 pairs, ctx core_mfma): theta's image and the pairs' sigma-eps images [n_lanes / 2][kMImg]
+  // MFMA form (fp16 pairs): theta's image and the pairs' sigma-eps images [n_lanes / 2][kMImg]
   const _Float16* thm;
   const _Float16* epm;
 };
@@ -219,33 +219,26 @@ __global__ void finish_kernel(int n_lanes, int envs, int T, int entropy, int jig
                               double* ent, int32_t* steps, double* norm2);
 
 // fp16 mode kernels (fdr_impala_h.hip)
-__global__ void conv_kernel_h(Layout L, StepArgs a);
-// same features as conv_kernel_h, 80 KiB LDS: 2 workgroups per CU; NTH = 256 (4 waves) or 512 (8 waves, 128 VGPRs)
-// SPLIT3: stop after the stage-3 entry (X3 into the feature slot) -- conv_s3_kernel finishes the stack, 4 envs per WG
-template <int NTH, bool SPLIT3>
+// the conv stack: one env per 8-wave workgroup (kHThreads), 80 KiB LDS, <= 128 VGPRs -- two workgroups per CU
+template <int NTH>
 __global__ void conv_kernel_h2(Layout L, StepArgs a);
-template <bool SHARED>  // SHARED: the 4 env slots of a workgroup are one lane (envs % 4 == 0)
-__global__ void conv_s3_kernel(Layout L, StepArgs a);
-constexpr int kS3EnvsPerWG = 4;  // conv_s3_kernel: envs per workgroup
 template <int E, int MODE>
-__global__ void core_kernel_h(Layout L, StepArgs a);
-template <int E>
-__global__ void core_kernel_hp(Layout L, StepArgs a);  // pair form (rollout mode), grid n_lanes / 2
+__global__ void core_kernel_h(Layout L, StepArgs a);   // per-lane form (non-pair batches, forward)
 template <int E>
 __global__ void core_kernel_p(Layout L, StepArgs a);   // f32 pair form (rollout mode, bit-exact), grid n_lanes / 2
 template <int E>
 __global__ void core_kernel_pr(Layout L, StepArgs a);  // f32 pair form of the replay (with a.gx)
-template <int E>
-__global__ void core_kernel_hpr(Layout L, StepArgs a); // fp16 pair form of the replay (with a.gx)
+// fp16 pair form on MFMA: theta x + s (E x) over fragment images, two antithetic pairs per workgroup (512 threads),
+// grid n_lanes / 4 (n_lanes % 4 == 0)
 template <int E, int MODE>
-__global__ void core_kernel_hpm(Layout L, StepArgs a); // fp16 pair form on MFMA (kRollout / kReplay), grid n_lanes / 2
-template <int E, int MODE>
-__global__ void core_kernel_hpm2(Layout L, StepArgs a); // two pairs per workgroup (512 threads), grid n_lanes / 4
-// replay input projection of a chunk in the fp16 pair form on MFMA: grid (n_lanes / 2, kGateNT / 4)
+__global__ void core_kernel_hpm2(Layout L, StepArgs a);
+// replay input projection of a chunk in the fp16 pair form on MFMA: grid xproj_grid(n_lanes) (XCD-aware, 1-D)
 template <int E>
 __global__ void xproj_pair_kernel(Layout L, StepArgs a, int t0, int tc, float* gx);
-// the entropy replay of one chunk (steps t0 .. t0 + tc - 1 on a.gx) in ONE launch: core_kernel_hpm<E, kReplay>'s
-// step for two pairs per workgroup in a loop, h / c / ent in registers, the next step's first W_hh fragments in flight under each epilogue
+inline dim3 xproj_grid(int n_lanes) { return dim3((unsigned)(((n_lanes / 2 + 7) / 8) * 8 * (kGateNT / 4))); }
+// the entropy replay of one chunk (steps t0 .. t0 + tc - 1 on a.gx) in ONE launch: the W_hh step of the pair form
+// for two pairs per workgroup in a loop, h / c / ent in registers, the next step's first W_hh fragments in flight
+// under each epilogue
 template <int E, int MODE>  // kReplay (entropy sums) or kStrategy (probabilities over a probe sequence)
 __global__ void replay_chunk_hpm2(Layout L, StepArgs a, int t0, int tc);
 // MFMA images (kMImg halves each) of n half packs: grid (kFcKS + 4 kGateKS, n)
@@ -279,7 +272,7 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
 
 struct ForwardCall {
   const Layout* layout;
-  int fp16, conv_h2;
+  int fp16;
   const float* theta;
   int n_envs;
   const float* frames;
@@ -298,9 +291,8 @@ int64_t forward_workspace_bytes(const Layout& L, int n_envs, bool fp16 = false);
 struct StrategiesCall {
   const Layout* layout;
   LanesArgs lanes;
-  int n_lanes, n_states, fp16, conv_h2;
-  int pairs;             // fdr_impala_desc.pairs: fp16 + n_lanes % 4 == 0 + ctx core_mfma -> the pair form on MFMA
-  int core_mfma;
+  int n_lanes, n_states, fp16;
+  int pairs;             // fdr_impala_desc.pairs: fp16 + n_lanes % 4 == 0 -> the pair form on MFMA
   const float* frames;   // [Z][3][64][64] f32 0..255
   const float* reward;   // [Z] or NULL
   float* h;              // [n_lanes][256] in/out initial state, or NULL (zero state)

@@ -1377,24 +1377,9 @@ __global__ void pair_offsets_kernel(const int64_t* __restrict__ idx, int n_pairs
   }
 }
 
-// the fp16 conv stack over grid workgroups (one per env, XCD-interleaved lanes): either kernel, same features;
-// h2 = 3: conv_kernel_h2<512> through the stage-3 entry, then conv_s3_kernel (4 envs per workgroup) -- the features of
-// h2 = 2 bit for bit
-static void launch_conv_h(int h2, int grid, const Layout& L, const StepArgs& a, hipStream_t stream) {
-  if (h2 == 3) {
-    hipLaunchKernelGGL((conv_kernel_h2<512, true>), dim3(grid), dim3(512), 0, stream, L, a);
-    const int64_t n_envs = (int64_t)a.n_lanes * a.envs;
-    const dim3 g3((unsigned)((n_envs + kS3EnvsPerWG - 1) / kS3EnvsPerWG));
-    if (a.envs % kS3EnvsPerWG == 0)
-      hipLaunchKernelGGL(conv_s3_kernel<true>, g3, dim3(512), 0, stream, L, a);
-    else
-      hipLaunchKernelGGL(conv_s3_kernel<false>, g3, dim3(512), 0, stream, L, a);
-  } else if (h2 == 2)
-    hipLaunchKernelGGL((conv_kernel_h2<512, false>), dim3(grid), dim3(512), 0, stream, L, a);
-  else if (h2)
-    hipLaunchKernelGGL((conv_kernel_h2<256, false>), dim3(grid), dim3(256), 0, stream, L, a);
-  else
-    hipLaunchKernelGGL(conv_kernel_h, dim3(grid), dim3(kHThreads), 0, stream, L, a);
+// the fp16 conv stack over grid workgroups (one per env, XCD-interleaved lanes)
+static void launch_conv_h(int grid, const Layout& L, const StepArgs& a, hipStream_t stream) {
+  hipLaunchKernelGGL((conv_kernel_h2<kHThreads>), dim3(grid), dim3(kHThreads), 0, stream, L, a);
 }
 
 template <int E>
@@ -1411,21 +1396,15 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
   for (int t = 0; t < a.T; ++t) {
     a.t = t;
     if (h)
-      launch_conv_h(ctx.conv_h2, conv_grid, L, a, stream);
+      launch_conv_h(conv_grid, L, a, stream);
     else
       hipLaunchKernelGGL(conv_kernel, dim3(conv_grid), dim3(kConvThreads), 0, stream, L, a);
     mark(prof, stream);
     bool pair_done = false;
     if constexpr (E <= 4) {
-      if (h && a.epm && ctx.core_mfma == 2 && a.n_lanes % 4 == 0) {
+      if (h && a.epm) {  // (launch_rollout builds the images only for n_lanes % 4 == 0)
         hipLaunchKernelGGL((core_kernel_hpm2<E, kRollout>), dim3(a.n_lanes / 4), dim3(2 * kCoreThreads), 0, stream, L,
                            a);
-        pair_done = true;
-      } else if (h && a.epm) {
-        hipLaunchKernelGGL((core_kernel_hpm<E, kRollout>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
-        pair_done = true;
-      } else if (h && a.ep) {
-        hipLaunchKernelGGL((core_kernel_hp<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
         pair_done = true;
       } else if (!h && a.ep32) {
         hipLaunchKernelGGL((core_kernel_p<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
@@ -1449,7 +1428,7 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
         bool pair_xproj = false;
         if constexpr (E <= 4) {
           if (h && a.epm) {  // fp16 pair form on MFMA: theta X + s (E X) from the gate images
-            hipLaunchKernelGGL((xproj_pair_kernel<E>), dim3(a.n_lanes / 2, kGateNT / 4), dim3(256), 0, stream, L, a,
+            hipLaunchKernelGGL((xproj_pair_kernel<E>), xproj_grid(a.n_lanes), dim3(256), 0, stream, L, a,
                                t0, tc, gx);
             pair_xproj = true;
           }
@@ -1463,7 +1442,7 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
         a.gx_t0 = t0;
       }
       if constexpr (E <= 4) {
-        if (a.gx && h && a.epm && ctx.core_mfma == 2 && a.n_lanes % 4 == 0) {  // the whole chunk in one launch
+        if (a.gx && h && a.epm) {  // the whole chunk in one launch
           hipLaunchKernelGGL((replay_chunk_hpm2<E, kReplay>), dim3(a.n_lanes / 4), dim3(2 * kCoreThreads), 0, stream, L,
                              a, t0, tc);
           for (int t = t0; t < t0 + tc; ++t) mark(prof, stream);  // the profiler's per-step marks
@@ -1474,14 +1453,7 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
         a.t = t;
         bool pair_done = false;
         if constexpr (E <= 4) {
-          if (a.gx && h && a.epm) {
-            hipLaunchKernelGGL((core_kernel_hpm<E, kReplay>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L,
-                               a);
-            pair_done = true;
-          } else if (a.gx && h && a.ep) {
-            hipLaunchKernelGGL((core_kernel_hpr<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
-            pair_done = true;
-          } else if (a.gx && !h && a.ep32) {
+          if (a.gx && !h && a.ep32) {
             hipLaunchKernelGGL((core_kernel_pr<E>), dim3(a.n_lanes / 2), dim3(kCoreThreads), 0, stream, L, a);
             pair_done = true;
           }
@@ -1530,15 +1502,16 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
   a.dbg = c.ctx->debug_clock;
   double* n2 = reinterpret_cast<double*>(w + p.n2);
 
-  const bool pair_core =
-      c.pairs && pair_core_supported(c.envs) && c.lanes.table && c.lanes.base_stride == 0 && c.n_lanes >= 2;
+  // fp16: the MFMA pair core takes two pairs per workgroup (n_lanes % 4 == 0); other lane counts run per lane
+  const bool pair_core = c.pairs && pair_core_supported(c.envs) && c.lanes.table && c.lanes.base_stride == 0 &&
+                         c.n_lanes >= 2 && (!c.fp16 || c.n_lanes % 4 == 0);
   launch_pack<float>(L, c.lanes, const_cast<float*>(a.pack), n2, c.n_lanes, 0, stream, c.fp16 ? kTrNorm : kTrFull);
   if (c.fp16) {
     a.hpack = reinterpret_cast<_Float16*>(w + p.hpack);
     a.hpack_stride = L.hpack;
     // the per-lane half pack's fc / LSTM weights are read only off the MFMA pair path: core_kernel_h (no pair core),
     // lstm_xproj_kernel (pair core on VALU) and core_kernel_h<kReplay> (replay without the gate GEMM)
-    const bool pair_images = pair_core && c.ctx->core_mfma && (!c.entropy || c.ctx->replay_gemm);
+    const bool pair_images = pair_core && (!c.entropy || c.ctx->replay_gemm);
     launch_pack<_Float16>(L, c.lanes, a.hpack, n2, c.n_lanes, 1, stream, pair_images ? kTrSkip : kTrFull);
   }
   if (pair_core) {
@@ -1562,11 +1535,11 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
       _Float16* ep = reinterpret_cast<_Float16*>(w + p.epack);
       launch_pack<_Float16>(L, lt, th, n2, 1, 1, stream);
       // under the MFMA core only the images read the pairs' packs (their transposed sections)
-      launch_pack<_Float16>(L, le, ep, n2, np, 1, stream, kTrFull, c.ctx->core_mfma == 0);
+      launch_pack<_Float16>(L, le, ep, n2, np, 1, stream, kTrFull, false);
       a.th = th;
       a.ep = ep;
       a.ep_stride = L.hpack;
-      if (c.ctx->core_mfma) {  // MFMA-fragment images of theta's and the pairs' fc / LSTM weights
+      {  // MFMA-fragment images of theta's and the pairs' fc / LSTM weights
         _Float16* im = reinterpret_cast<_Float16*>(w + p.mimg);
         const unsigned nb = kFcKS + 4 * kGateKS;
         hipLaunchKernelGGL(mfma_image_kernel, dim3(nb, 1), dim3(256), 0, stream, L, th, (int64_t)0, im);
@@ -1641,7 +1614,7 @@ int launch_forward(const ForwardCall& c, void* ws, int64_t ws_bytes, hipStream_t
     launch_pack<_Float16>(L, lanes, a.hpack, reinterpret_cast<double*>(w + p.n2), 1, 1, stream);
   }
   if (c.fp16) {
-    launch_conv_h(c.conv_h2, (c.n_envs + 7) / 8 * 8, L, a, stream);
+    launch_conv_h((c.n_envs + 7) / 8 * 8, L, a, stream);
     hipLaunchKernelGGL((core_kernel_h<1, kForward>), dim3(c.n_envs), dim3(kCoreThreads), 0, stream, L, a);
   } else {
     hipLaunchKernelGGL(conv_kernel, dim3((c.n_envs + 7) / 8 * 8), dim3(kConvThreads), 0, stream, L, a);
@@ -1811,7 +1784,7 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
   }
   // antithetic pairs (fp16): the recurrence streams each pair's sigma-eps image once (replay_chunk_hpm2<1, kStrategy>,
   // x W_ih^T by xproj_pair_kernel), as the rollout's pair form -- conv and fc stay per lane (per-lane half pack)
-  const bool pair_form = half && c.pairs && c.core_mfma >= 1 && c.n_lanes % 4 == 0 && c.lanes.table &&
+  const bool pair_form = half && c.pairs && c.n_lanes % 4 == 0 && c.lanes.table &&
                          c.lanes.base_stride == 0;
   if (pair_form) {
     const int np = c.n_lanes / 2;
@@ -1850,7 +1823,7 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
     a.frames = c.frames + (int64_t)z0 * kFramePix;
     const int conv_grid = (c.n_lanes + 7) / 8 * 8 * zc;
     if (half)
-      launch_conv_h(c.conv_h2, conv_grid, L, a, stream);
+      launch_conv_h(conv_grid, L, a, stream);
     else
       hipLaunchKernelGGL(conv_kernel, dim3(conv_grid), dim3(kConvThreads), 0, stream, L, a);
     const dim3 grid(c.n_lanes, (zc + 63) / 64);
@@ -1866,7 +1839,7 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
     const dim3 grid(c.n_lanes, (tc + 63) / 64, kGates / 256);
     a.gx = nullptr;
     if (pair_form)
-      hipLaunchKernelGGL((xproj_pair_kernel<1>), dim3(c.n_lanes / 2, kGateNT / 4), dim3(256), 0, stream, L, a, t0, tc,
+      hipLaunchKernelGGL((xproj_pair_kernel<1>), xproj_grid(c.n_lanes), dim3(256), 0, stream, L, a, t0, tc,
                          gx);
     else if (half)
       hipLaunchKernelGGL(lstm_xproj_kernel<true>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);

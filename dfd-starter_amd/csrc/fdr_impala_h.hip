@@ -49,31 +49,12 @@ __device__ __forceinline__ int tidx(int q, int ch) { return q * Pix<C>::CS + (((
 template <int C>
 __device__ __forceinline__ int xidx(int m, int ch) { return m * C + (((ch >> 3) ^ xsw<C>(m)) << 3) + (ch & 7); }
 
-constexpr int kHGuard = 832;  // halves: one padded row of the widest entry-conv input (18 * 40) + slack
-constexpr int kBR1 = 33, kBR2 = 17, kBR3 = 17;   // entry-conv band heights (conv rows) per stage
-// region offsets (halves) inside R = lds_h + kHGuard  (DESIGN.md "fp16 mode")
-constexpr int kFrame = 66 * 66 * 4;              // stage-1 input image [66][66][4]
-constexpr int kT1 = 34 * 34 * Pix<16>::CS;       // stage-1 res / stage-2 entry input [34][34][16]
-constexpr int kT2 = 18 * 18 * Pix<32>::CS;       // stage-2 res / stage-3 entry input [18][18][32]
-constexpr int kS1 = kFrame;                       // S1 [33][64][16] after the frame
-constexpr int kX1 = kS1 + kBR1 * 64 * 16;         // X1 [32][32][16]
-constexpr int kS2 = kT1;                          // S2 [17][32][32] after T1
-constexpr int kX2 = kS2 + kBR2 * 32 * 32;         // X2 [16][16][32] (over the dead X1)
-constexpr int kS3 = kT2;                          // S3 [17][16][32] after T2
-constexpr int kX3 = kS3 + kBR3 * 16 * 32;         // X3 [8][8][32]
-constexpr int kRegion = kX1 + 32 * 32 * 16;       // max extent
-constexpr int kT3 = 10 * 10 * Pix<32>::CS;       // stage-3 res input [10][10][32]
-// the residual blocks' second image Tb follows Ta = R: over the dead frame/S1, S2 and T2 regions
-static_assert(2 * kT1 <= kX1 && 2 * kT2 <= kX2 && 2 * kT3 <= kS3, "fp16 LDS plan: second residual image");
-static_assert(kT1 <= kX1 && kX2 + 16 * 16 * 32 <= kRegion && kX3 + 8 * 8 * 32 <= kX2, "fp16 LDS plan");
 // conv weight staging buffer WB (halves): the A fragments of the widest conv (32 -> 32, 9 k-steps x 2
 // channel tiles).  Every wave of the workgroup needs the same fragments; fetched from the pack by
 // all 8 waves they cost 8 x 18 KB of vector-memory traffic per conv (~2,000 clocks of TA issue the
 // waves stall on).  Instead the workgroup copies each conv's block ONCE into WB (16 B per thread per
 // chunk) and the waves read their fragments from LDS.
 constexpr int kWB = 9 * 2 * 64 * 8;
-constexpr int kHLdsBytes = (kHGuard + kRegion) * 2 + 3 * kBnTab * 4 + kWB * 2;  // + BN scale / shift, conv bias
-static_assert(kHLdsBytes <= 160 * 1024, "fp16 conv LDS");
 
 // ---- conv on f16 MFMA ---------------------------------------------------------------------------
 template <int CIN>
@@ -106,17 +87,8 @@ __device__ __forceinline__ void rem_fragment(const _Float16* w, h8 (&af)[KSteps<
   }
 }
 
-// A fragments of one conv for ALL output-channel tiles: af[s][nt] (4 VGPRs each)
-template <int CIN, int NT>
-__device__ __forceinline__ void load_af(const _Float16* __restrict__ wf, h8 (&af)[KSteps<CIN>::N][NT], int lane) {
-#pragma unroll
-  for (int s = 0; s < KSteps<CIN>::N; ++s)
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) af[s][nt] = *reinterpret_cast<const h8*>(wf + (((s * NT + nt) * 64) + lane) * 8);
-  rem_fragment<CIN, NT>(wf, af, lane);
-}
-
-// The same fragments from the workgroup's LDS copy of the block (layout identical to the pack's).  R32: the last
+// A fragments of one conv for ALL output-channel tiles, af[s][nt] (4 VGPRs each), from the workgroup's LDS copy of
+// the block (layout identical to the pack's).  R32: the last
 // fragment stays in the pack's K = 32 layout (tap 8 + zeros; conv_h2 R32).
 template <int CIN, int NT, bool R32 = false>
 __device__ __forceinline__ void load_af_lds(const _Float16* wb, h8 (&af)[KSteps<CIN>::N][NT], int lane) {
@@ -185,94 +157,6 @@ __device__ __forceinline__ int k_offset(int s, int g, int part) {
   return ((tap / 3) * WP + tap % 3) * CS + ch;
 }
 
-// acc[i][nt] += W(nt) * P(tile q = wave + 8 i) over the whole K; Tin = padded HWC image whose row 0 is
-// the padded row of output row 0 (callers offset it for bands).  Pixel tile = 16 consecutive output
-// pixels (row-major, width W).
-// qoff: padded-pixel index of Tin within its image (band offset of an entry conv; the swizzle is a
-// function of the image's own pixel index).
-template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT, int NW = 8>
-__device__ __forceinline__ void conv_h(const _Float16* Tin, const h8 (&af)[KSteps<CIN>::N][NT],
-                                       f32x4 (&acc)[TPW][NT], int wave, int lane, int qoff = 0) {
-  constexpr int KS = KSteps<CIN>::N;
-  const int g = lane >> 4;
-  // tile i of this wave exists (wave-uniform): only the last i of a conv whose MT is not a multiple of 8
-  // can be past the end -- skipped, not recomputed (the clamped duplicate cost 21 % of the executed MFMA
-  // FLOP: stage-3 residual convs have 4 tiles for 8 waves, r05 PMC)
-  auto live = [&](int i) { return TPW * NW == MT || i < TPW - 1 || wave + NW * i < MT; };
-  int base[TPW];
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    int mt = wave + NW * i;
-    mt = mt < MT ? mt : MT - 1;
-    const int m = mt * 16 + (lane & 15);
-    base[i] = (m / W) * WP + (m % W);  // padded pixel of tap 0
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) acc[i][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int s = 0; s < KSteps<CIN>::NF; ++s) {
-    if constexpr (CIN == 3) {
-      const int o0 = k_offset<CIN, CS, WP>(s, g, 0), o1 = k_offset<CIN, CS, WP>(s, g, 1);
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-        if (!live(i)) continue;
-        const h4 lo = *reinterpret_cast<const h4*>(Tin + base[i] * CS + o0);
-        const h4 hi = *reinterpret_cast<const h4*>(Tin + base[i] * CS + o1);
-        const h8 b = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b, acc[i][nt], 0, 0, 0);
-      }
-    }
-  }
-  if constexpr (CIN != 3) {
-#pragma unroll
-    for (int s = 0; s < KSteps<CIN>::NF; ++s) {
-      // tap and channel chunk of this lane's 8 K-elements (k_offset's decomposition, swizzled chunk)
-      constexpr int cpg = CIN / 8, tpk = 32 / CIN;
-      const int tap = s * tpk + g / cpg, chunk = g % cpg, tq = (tap / 3) * WP + tap % 3;
-#pragma unroll
-      for (int i = 0; i < TPW; ++i) {
-        if (!live(i)) continue;
-        const int q = base[i] + tq;
-        const h8 b = *reinterpret_cast<const h8*>(Tin + q * CS + ((chunk ^ tsw<CIN>(q + qoff)) << 3));
-#pragma unroll
-        for (int nt = 0; nt < NT; ++nt) acc[i][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b, acc[i][nt], 0, 0, 0);
-      }
-    }
-  }
-  // tap 8 on K = 16 (lane group g: channel slots 4g .. 4g+3).  Its products go to a fresh accumulator and
-  // are added by VALU: accumulating the K = 16 MFMA straight onto the K = 32 MFMAs' result (SrcC) gave
-  // wrong sums on gfx950 with this hipcc (a mixed-pass-count SrcC dependency; fp16 golden test, measured),
-  // the separate form is exact.
-  if constexpr (KSteps<CIN>::kRem) {
-#pragma unroll
-    for (int i = 0; i < TPW; ++i) {
-      if (!live(i)) continue;
-      const int q = base[i] + 2 * WP + 2;  // tap 8
-      const int o = CIN == 3 ? q * CS : q * CS + (((g >> 1) ^ tsw<CIN>(q + qoff)) << 3) + 4 * (g & 1);
-      const h4 b = *reinterpret_cast<const h4*>(Tin + o);
-#pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        const h8 w = af[KS - 1][nt];
-        acc[i][nt] += __builtin_amdgcn_mfma_f32_16x16x16f16(h4{w[0], w[1], w[2], w[3]}, b, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      }
-    }
-  }
-}
-
-// Visit the outputs: f(ch0, m, v4) -- channels ch0 .. ch0+3 of output pixel m
-template <int NT, int TPW, int MT, int NW = 8, typename F>
-__device__ __forceinline__ void conv_out_h(const f32x4 (&acc)[TPW][NT], int wave, int lane, F f) {
-#pragma unroll
-  for (int i = 0; i < TPW; ++i) {
-    const int mt = wave + NW * i;
-    if (mt >= MT) continue;
-    const int m = mt * 16 + (lane & 15);
-#pragma unroll
-    for (int nt = 0; nt < NT; ++nt) f(nt * 16 + 4 * (lane >> 4), m, acc[i][nt]);
-  }
-}
-
 __device__ __forceinline__ h4 to_h4(float a, float b, float c, float d) {
   return h4{(_Float16)a, (_Float16)b, (_Float16)c, (_Float16)d};
 }
@@ -336,63 +220,6 @@ __device__ __forceinline__ void to_padded_h(const _Float16* X, _Float16* T, cons
   }
 }
 
-// Stage entry: X <- maxpool3s2p1(conv3x3(T) + b) in bands of BR conv rows through S [BR][H][COUT]
-// (conv row -1 of band 0 stored as -inf); pool: one thread per (pooled pixel, 8-channel group).
-// WB: the next conv's block (issued by the caller into st) is committed in band 0's pool phase.
-template <int CIN, int COUT, int H, int BR, int NH>
-__device__ __forceinline__ void stage_entry_h(const _Float16* T, _Float16* S, _Float16* X,
-                                              const h8 (&af)[KSteps<CIN>::N][COUT / 16],
-                                              const float* __restrict__ bias, int wave, int lane,
-                                              const StepArgs& a, int kst, WStage& st, _Float16* wb) {
-  constexpr int CS = Pix<CIN>::CS, WP = H + 2, NT = COUT / 16, MT = BR * H / 16;
-  constexpr int TPW = (MT + 7) / 8, HO = H / 2, PRB = (BR - 1) / 2, G = COUT / 8;
-  float bz[NT][4];
-#pragma unroll
-  for (int nt = 0; nt < NT; ++nt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bz[nt][r] = bias[nt * 16 + 4 * (lane >> 4) + r];
-  for (int b = 0; b < H / (BR - 1); ++b) {
-    f32x4 acc[TPW][NT];
-    conv_h<CIN, CS, NT, TPW, H, WP, MT>(T + ((BR - 1) * b - 1) * WP * CS, af, acc, wave, lane, ((BR - 1) * b - 1) * WP);
-    conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
-      const int nt = ch0 >> 4;
-      const bool neg = b == 0 && m < H;  // conv row -1
-      const float ninf = -INFINITY;
-      *reinterpret_cast<h4*>(S + xidx<COUT>(m, ch0)) =
-          neg ? to_h4(ninf, ninf, ninf, ninf)
-              : to_h4(v[0] + bz[nt][0], v[1] + bz[nt][1], v[2] + bz[nt][2], v[3] + bz[nt][3]);
-    });
-    __syncthreads();
-    FDR_STAMP(a, kst + 2 * b);  // diagnostics: band b conv + store done
-    if (b == 0) st.commit<NH>(wb);
-    // 3x3 / stride-2 max pool, branch-free (the left tap of column 0 is clamped onto column 0,
-    // which the window holds anyway) and fully unrolled so every load of a thread is in flight
-    constexpr int NI = PRB * HO * G, IT = (NI + kHThreads - 1) / kHThreads;
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int i = threadIdx.x + it * kHThreads;
-      if (NI % kHThreads != 0 && i >= NI) break;
-      const int cg = i % G, r = i / G, px = r % HO, pr = r / HO;
-      const int xl = 2 * px > 0 ? 2 * px - 1 : 0;
-      h8 v[9];
-#pragma unroll
-      for (int dr = 0; dr < 3; ++dr) {
-        const int row = (2 * pr + dr) * H;
-        v[3 * dr] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + xl, 8 * cg));
-        v[3 * dr + 1] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + 2 * px, 8 * cg));
-        v[3 * dr + 2] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + 2 * px + 1, 8 * cg));
-      }
-      const h8 m01 = __builtin_elementwise_max(v[0], v[1]), m23 = __builtin_elementwise_max(v[2], v[3]);
-      const h8 m45 = __builtin_elementwise_max(v[4], v[5]), m67 = __builtin_elementwise_max(v[6], v[7]);
-      const h8 mx = __builtin_elementwise_max(
-          __builtin_elementwise_max(__builtin_elementwise_max(m01, m23), __builtin_elementwise_max(m45, m67)), v[8]);
-      *reinterpret_cast<h8*>(X + xidx<COUT>((PRB * b + pr) * HO + px, 8 * cg)) = mx;
-    }
-    __syncthreads();
-    FDR_STAMP(a, kst + 2 * b + 1);  // band b pool done
-  }
-}
-
 // Zero border of a padded image [H+2][H+2][CS] (the interior is written by a conv epilogue).
 template <int C, int H>
 __device__ __forceinline__ void zero_border_h(_Float16* T) {  // (kHThreads = conv_kernel_h2<512>'s block too)
@@ -405,317 +232,35 @@ __device__ __forceinline__ void zero_border_h(_Float16* T) {  // (kHThreads = co
   }
 }
 
-// Two residual blocks; same fusion as the f32 path (fdr_impala.hip res_blocks).  af holds block 0's
-// first conv on entry, st the issued copy of its second conv; Ta holds relu(bn0(X)) with a zero border,
-// Tb (same geometry) a zero border.  Each conv reads one image and its epilogue writes the other -- conv0
-// Ta -> Tb, conv1 Tb -> Ta (+ X) -- so the epilogue follows a wave's own MFMAs with no barrier between:
-// one wave's BN / ReLU / residual VALU overlaps the other wave's MFMAs on the SIMD, and a conv costs one
-// full barrier (the other one only follows the fragment load from WB, all waves arriving together).
-// Weight pipeline (convs A B C D = i0, i1 of blocks 0 and 1, E = the next stage's entry conv): a conv
-// phase commits the block issued earlier to WB; after its barrier af <- WB, a barrier, and the next
-// block is issued.  On exit WB holds E (NEXTH halves; NEXTH == 0: last stage, nothing staged) and Ta
-// the next stage's input.
-template <int C, int H, int LAST, int NEXTH>
-__device__ __forceinline__ void res_blocks_h(_Float16* Ta, _Float16* Tb, _Float16* X, h8 (&af)[KSteps<C>::N][C / 16],
-                                             const _Float16* __restrict__ hp, const float* __restrict__ pk,
-                                             const Layout& L, int stage, const float* bsc, const float* bsh, const float* bcb, int wave,
-                                             int lane, const StepArgs& a, int k0, float* __restrict__ out,
-                                             WStage& st, _Float16* wb, const _Float16* __restrict__ next_w) {
-  constexpr int CS = Pix<C>::CS, WP = H + 2, NT = C / 16, MT = H * H / 16;
-  constexpr int TPW = (MT + 7) / 8, WH = kBlockHalves<C, C / 16>;
-  auto tpos = [&](int m, int ch0) { return tidx<C>((m / H + 1) * WP + (m % H) + 1, ch0); };
-  const int cl = 4 * (lane >> 4);  // this lane's 4 channels within an output-channel tile
-  // SPLIT (8 x 8 stage: 4 pixel tiles x 2 channel tiles): one (tile, channel tile) pair per wave instead of
-  // 2 channel tiles on waves 0-3 and nothing on waves 4-7.  ntw is wave-uniform; the wave's fragments and
-  // epilogue constants are those of its channel tile only (constant register indices).
-  constexpr bool SPLIT = MT < 8 && MT * NT == 8;
-  static_assert(!SPLIT || NT == 2, "split: two channel tiles");
-  constexpr int NTC = SPLIT ? 1 : NT, TPC = SPLIT ? 1 : TPW;
-  const int ntw = SPLIT ? wave % NT : 0, mtw = SPLIT ? wave / NT : wave;
-  h8 af1[KSteps<C>::N][1];
-  // this wave's fragments from WB: all channel tiles (af) or, SPLIT, channel tile ntw only (af1; a select
-  // between af[s][0] and af[s][1] became a dynamically indexed scratch copy)
-  auto load_frags = [&]() {
-    if constexpr (SPLIT) {
-      static_assert(!KSteps<C>::kRem, "split: full K-steps only");
-#pragma unroll
-      for (int s = 0; s < KSteps<C>::N; ++s) af1[s][0] = *reinterpret_cast<const h8*>(wb + (((s * NT + ntw) * 64) + lane) * 8);
-    } else {
-      load_af_lds<C, NT>(wb, af, lane);
-    }
-  };
-  auto conv = [&](const _Float16* Tin, f32x4 (&acc)[TPC][NTC]) {
-    if constexpr (SPLIT) {
-      conv_h<C, CS, 1, 1, H, WP, MT>(Tin, af1, acc, mtw, lane);
-    } else {
-      conv_h<C, CS, NT, TPW, H, WP, MT>(Tin, af, acc, wave, lane);
-    }
-  };
-  // f(ch0, ci, m, v): ci = the index of ch0's channel tile in this wave's constants
-  auto visit = [&](const f32x4 (&acc)[TPC][NTC], auto&& f) {
-    if constexpr (SPLIT) {
-      conv_out_h<1, 1, MT>(acc, mtw, lane, [&](int ch0, int m, f32x4 v) { f(ch0 + 16 * ntw, 0, m, v); });
-    } else {
-      conv_out_h<NT, TPW, MT>(acc, wave, lane, [&](int ch0, int m, f32x4 v) { f(ch0, ch0 >> 4, m, v); });
-    }
-  };
-  if constexpr (SPLIT) {  // the caller's af came from the same WB block, still in place
-    load_frags();
-    __syncthreads();  // before any wave's first commit overwrites WB
-  }
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int i0 = stage * 5 + 1 + 2 * r, i1 = i0 + 1;
-    const int inext = r == 0 ? i1 + 1 : (stage + 1) * 5;
-    // per-lane epilogue constants: bias of both convs, BN after conv0, BN after conv1
-    float b0[NTC][4], s1[NTC][4], h1[NTC][4], b1[NTC][4], s2[NTC][4], h2[NTC][4];
-#pragma unroll
-    for (int nt = 0; nt < NTC; ++nt)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int ch = (SPLIT ? ntw : nt) * 16 + cl + k;
-        b0[nt][k] = bcb[i0 * 32 + ch];  // LDS: a global load here would wait (vmcnt) on the issued WB block
-        b1[nt][k] = bcb[i1 * 32 + ch];
-        s1[nt][k] = bsc[i1 * 32 + ch];
-        h1[nt][k] = bsh[i1 * 32 + ch];
-        s2[nt][k] = (r == 1 && LAST) ? 0.f : bsc[inext * 32 + ch];
-        h2[nt][k] = (r == 1 && LAST) ? 0.f : bsh[inext * 32 + ch];
-      }
-    FDR_STAMP(a, k0 + 4 * r);
-    // ---- conv0: Ta -> Tb ----
-    f32x4 acc[TPC][NTC];
-    conv(Ta, acc);
-    visit(acc, [&](int ch0, int nt, int m, f32x4 v) {
-      float o[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) o[k] = relu(fmaf(v[k] + b0[nt][k], s1[nt][k], h1[nt][k]));
-      *reinterpret_cast<h4*>(Tb + tpos(m, ch0)) = to_h4(o[0], o[1], o[2], o[3]);
-    });
-    st.commit<WH>(wb);  // conv i1 (every wave loaded conv i0's fragments before the last barrier)
-    __syncthreads();
-    FDR_STAMP(a, k0 + 4 * r + 1);
-    load_frags();
-    __syncthreads();  // WB may be overwritten once every wave holds af
-    if (r == 0) {
-      st.issue<WH>(hp + L.conv_h[i1 + 1]);  // block 1 conv0
-    } else if constexpr (NEXTH > 0) {
-      st.issue<NEXTH>(next_w);
-    }
-    FDR_STAMP(a, k0 + 4 * r + 2);
-    // ---- conv1: Tb -> Ta (+ X) ----
-    conv(Tb, acc);
-    visit(acc, [&](int ch0, int nt, int m, f32x4 v) {
-      const h4 xo = *reinterpret_cast<const h4*>(X + xidx<C>(m, ch0));
-      float xn[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) xn[k] = (float)(_Float16)((v[k] + b1[nt][k]) + (float)xo[k]);
-      if (r == 0) {
-        *reinterpret_cast<h4*>(X + xidx<C>(m, ch0)) = to_h4(xn[0], xn[1], xn[2], xn[3]);
-        float t[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) t[k] = relu(fmaf(xn[k], s2[nt][k], h2[nt][k]));
-        *reinterpret_cast<h4*>(Ta + tpos(m, ch0)) = to_h4(t[0], t[1], t[2], t[3]);
-      } else if (!LAST) {
-        float t[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) t[k] = fmaf(xn[k], s2[nt][k], h2[nt][k]);
-        *reinterpret_cast<h4*>(Ta + tpos(m, ch0)) = to_h4(t[0], t[1], t[2], t[3]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) out[(ch0 + k) * H * H + m] = relu(xn[k]);  // flatten (C,H,W)
-      }
-    });
-    if (r == 0) {
-      st.commit<WH>(wb);
-    } else if constexpr (NEXTH > 0) {
-      st.commit<NEXTH>(wb);
-    }
-    __syncthreads();
-    FDR_STAMP(a, k0 + 4 * r + 3);
-    if (r == 0) {
-      load_frags();  // block 1 conv0
-      __syncthreads();
-      st.issue<WH>(hp + L.conv_h[i1 + 2]);  // block 1 conv1
-    }
-  }
-}
-
-__global__ __launch_bounds__(kHThreads) void conv_kernel_h(Layout L, StepArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[kHLdsBytes];
-  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-  const int lane = (slot / a.envs) * 8 + xcd, e = slot % a.envs;
-  if (lane >= a.n_lanes) return;
-  const int wave = threadIdx.x >> 6, ln = threadIdx.x & 63;
-  const int64_t env = (int64_t)lane * a.envs + e;
-  const float* pk = a.pack + (int64_t)lane * a.pack_stride;
-  const _Float16* hp = a.hpack + (int64_t)lane * a.hpack_stride;
-  float* bsc = reinterpret_cast<float*>(smem);
-  float* bsh = bsc + kBnTab;
-  float* bcb = bsh + kBnTab;  // conv biases [15][32]
-  _Float16* R = reinterpret_cast<_Float16*>(smem + 3 * kBnTab * 4) + kHGuard;
-
-  _Float16* wb = reinterpret_cast<_Float16*>(smem + kHLdsBytes - kWB * 2);
-  // BN / bias table inputs first (global loads; vmcnt retires in order, so they go ahead of the weight
-  // loads), folded after the frame hash below has covered their latency
-  static_assert(kBnTab <= kHThreads, "one table entry per thread");
-  const int bi = threadIdx.x, bidx = bi >> 5, bch = bi & 31;
-  const bool has_bn = bi < kBnTab && bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
-  const bool has_cb = bi < kBnTab && bch < (bidx < 5 ? 16 : 32);  // kConvs == 15: conv bidx's bias
-  float rm = 0.f, rv = 1.f, bnw = 0.f, bnb = 0.f, cbv = 0.f;
-  if (has_bn) {
-    if (a.bn_mean) rm = a.bn_mean[L.bn_stat[bidx] + bch];
-    if (a.bn_var) rv = a.bn_var[L.bn_stat[bidx] + bch];
-    bnw = pk[L.bn_w[bidx] + bch];
-    bnb = pk[L.bn_b[bidx] + bch];
-  }
-  if (has_cb) cbv = pk[L.conv_b[bidx] + bch];
-  h8 af3[KSteps<3>::N][1];
-  load_af<3, 1>(hp + L.conv_h[0], af3, ln);
-  WStage st;
-  st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);  // committed in the stage-1 entry
-  FDR_STAMP(a, 0);
-  // ---- frame (policies/impala.py:147: frame / 255): values of this thread's 8 pixels x 3 channels ----
-  const int fw = threadIdx.x;  // 512 threads x 8 pixels = 64 x 64
-  const int fy = fw >> 3, fx0 = (fw & 7) * 8;
-  float fv[3][8];
-  if (a.frames) {
-    const float* fr = a.frames + (a.shared_frames ? (int64_t)e : env) * kFramePix;
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) fv[c][j] = fr[c * 4096 + fy * 64 + fx0 + j];
-  } else {
-    const uint64_t gid = (uint64_t)(a.lane_offset * a.envs + env);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const uint64_t word = (uint64_t)(c * 512 + fw);
-      const uint64_t hb = mix64(a.fkey + ((gid << 32) | ((uint64_t)a.t << 11) | word) * kGolden);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) fv[c][j] = (float)((uint32_t)(hb >> (8 * j)) & 255u);
-    }
-  }
-  if (bi < kBnTab) {  // eval-mode BN folded per channel: y = x * (w / sqrt(rv + eps)) + (b - rm * scale)
-    const float sc = has_bn ? bnw * (1.f / sqrtf(rv + kBnEps)) : 0.f;
-    bsc[bi] = sc;
-    bsh[bi] = has_bn ? bnb - rm * sc : 0.f;
-    bcb[bi] = cbv;
-  }
-  {  // zero the guard + frame image (its border and 4th channel slot stay 0)
-    uint4* z = reinterpret_cast<uint4*>(R - kHGuard);
-    for (int i = threadIdx.x; i < (kHGuard + kFrame) / 8; i += kHThreads) z[i] = uint4{0, 0, 0, 0};
-  }
-  __syncthreads();
-  FDR_STAMP(a, 1);
-
-  // ---- frame -> BN2d(3) -> padded HWC [66][66][4] f16 ----
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    h4 o;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) o[c] = (_Float16)fmaf(fv[c][j] / 255.0f, bsc[c], bsh[c]);
-    o[3] = (_Float16)0.f;
-    *reinterpret_cast<h4*>(R + ((fy + 1) * 66 + fx0 + j + 1) * 4) = o;
-  }
-  __syncthreads();
-  FDR_STAMP(a, 2);
-
-  // ---- stage 1 ----
-  stage_entry_h<3, 16, 64, kBR1, kBlockHalves<16, 1>>(R, R + kS1, R + kX1, af3, bcb + 0 * 32, wave, ln, a, 40,
-                                                     st, wb);
-  {
-    h8 af[KSteps<16>::N][1];
-    load_af_lds<16, 1>(wb, af, ln);
-    st.issue<kBlockHalves<16, 1>>(hp + L.conv_h[2]);
-    to_padded_h<16, 32, true, true>(R + kX1, R, bsc + 1 * 32, bsh + 1 * 32);
-    zero_border_h<16, 32>(R + kT1);
-    __syncthreads();
-    FDR_STAMP(a, 3);
-    res_blocks_h<16, 32, 0, kBlockHalves<16, 2>>(R, R + kT1, R + kX1, af, hp, pk, L, 0, bsc, bsh, bcb, wave, ln, a, 4, nullptr, st,
-                                                 wb, hp + L.conv_h[5]);
-  }
-  // ---- stage 2 ----
-  {
-    h8 af[KSteps<16>::N][2];
-    load_af_lds<16, 2>(wb, af, ln);
-    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
-    FDR_STAMP(a, 12);
-    stage_entry_h<16, 32, 32, kBR2, kBlockHalves<32, 2>>(R, R + kS2, R + kX2, af, bcb + 5 * 32, wave, ln, a, 48,
-                                                         st, wb);
-  }
-  {
-    h8 af[KSteps<32>::N][2];
-    load_af_lds<32, 2>(wb, af, ln);
-    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[7]);
-    to_padded_h<32, 16, true, true>(R + kX2, R, bsc + 6 * 32, bsh + 6 * 32);
-    zero_border_h<32, 16>(R + kT2);
-    __syncthreads();
-    FDR_STAMP(a, 13);
-    res_blocks_h<32, 16, 0, kBlockHalves<32, 2>>(R, R + kT2, R + kX2, af, hp, pk, L, 1, bsc, bsh, bcb, wave, ln, a, 14, nullptr, st,
-                                                 wb, hp + L.conv_h[10]);
-  }
-  // ---- stage 3 ----
-  {
-    h8 af[KSteps<32>::N][2];
-    load_af_lds<32, 2>(wb, af, ln);
-    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
-    FDR_STAMP(a, 22);
-    stage_entry_h<32, 32, 16, kBR3, kBlockHalves<32, 2>>(R, R + kS3, R + kX3, af, bcb + 10 * 32, wave, ln, a, 56,
-                                                         st, wb);
-  }
-  {
-    h8 af[KSteps<32>::N][2];
-    load_af_lds<32, 2>(wb, af, ln);
-    st.issue<kBlockHalves<32, 2>>(hp + L.conv_h[12]);
-    to_padded_h<32, 8, true, true>(R + kX3, R, bsc + 11 * 32, bsh + 11 * 32);
-    zero_border_h<32, 8>(R + kT3);
-    __syncthreads();
-    FDR_STAMP(a, 23);
-    res_blocks_h<32, 8, 1, 0>(R, R + kT3, R + kX3, af, hp, pk, L, 2, bsc, bsh, bcb, wave, ln, a, 24, a.feat + env * kFeat, st, wb,
-                              nullptr);
-  }
-  FDR_STAMP(a, 32);
-}
-
 // =====================================================================================================
-// conv_kernel_h2: the same conv stack as conv_kernel_h in TWO workgroups per CU.
-// conv_kernel_h's 145 KiB LDS admits one 8-wave workgroup per CU, so its ~45 barrier-separated phases per env
-// step -- entry convs, pools, BN passes, epilogues -- run one after the other with the MFMA pipe idle between
-// them (busy 0.20).  Here a workgroup is 4 waves (1 per SIMD, <= 256 VGPRs) in <= 80 KiB, and two of them (two
-// envs) share a CU: one's pool / epilogue / barrier phases overlap the other's MFMA phases.  What changes to fit:
-//   * the stage-1 frame is generated per entry band (11 padded rows, double-buffered: band b+1's rows are made
-//     during band b's pool phase) instead of as a whole 66 x 66 image;
-//   * entry bands of 9 conv rows (4 pooled rows): 8 bands at stage 1, 4 at stage 2, 1 (17 rows) at stage 3;
-//   * residual convs are single-buffered: conv -> accumulators -> barrier -> in-place epilogue;
-//   * the stage-2 entry writes its pooled rows into the dead rows of its own input image;
-//   * WB is placed per stage (2,560 halves beside X1 in stage 1, 9,216 after X1 dies).
+// conv_kernel_h2: the fp16 conv stack, one env per 8-wave workgroup, TWO workgroups per CU (<= 80 KiB LDS, <= 128
+// VGPRs: 4 waves per SIMD -- the register file, not the LDS, is what admits no third workgroup).  One env's ~36
+// barrier-separated phases per step (entry convs, pools, BN passes, epilogues) overlap the other workgroup's MFMA
+// phases.  The stage-1 frame is generated per 16-row entry band (double-buffered: band b+1's rows are made during
+// band b's pool phase); the stage entries pool in registers (below); residual convs are single-buffered (conv ->
+// accumulators -> barrier -> in-place epilogue); the stage-2 entry writes its pooled rows into the dead rows of its
+// own input image; WB is placed per stage (2,560 halves beside X1 in stage 1, 9,216 after X1 dies).
 // LDS map (halves, R = arena after the BN / bias tables; every buffer below R + 38,080):
-//   stage 1 entry : S1 [0, 9216) | FB0 [9216, 12120) | FB1 [12120, 15024) | X1 [18496, 34880) | WB_A [34880, 37440)
+//   stage 1 entry : FB0 | FB1 | EX1 (kH3*) | X1 [18496, 34880) | WB_A [34880, 37440)
 //   stage 1 res   : T1 [0, 18496) | X1 | WB_A
-//   stage 2 entry : T1 (X2 into [0, 8192) band by band) | S2 [18496, 27712) | WB_B [27712, 36928)
+//   stage 2 entry : T1 (X2 into [0, 8192) band by band) | EX2 | WB_B [27712, 36928)
 //   stage 2 res   : X2 [0, 8192) | T2 [8192, 18560) | WB_B
-//   stage 3 entry : X3 [0, 2048) | T2 | S3 [18560, 27264) | WB_B
+//   stage 3 entry : X3 [0, 2048) | T2 | EX3 | WB_B
 //   stage 3 res   : X3 | T3 [2048, 5248) | WB_B
-// Arithmetic per output is conv_kernel_h's (same fragments, same K order, same f32 epilogues), so the two
-// kernels' features are identical.
 // =====================================================================================================
-constexpr int kH2BR = 9;                                  // entry band: conv rows (4 pooled rows)
-constexpr int kH2FBRows = kH2BR + 2;                      // padded frame rows per band
-constexpr int kH2FB = kH2FBRows * 66 * 4;                 // halves
 constexpr int kH2Arena = 38080;                           // halves
-constexpr int kH2S1 = 0, kH2FB0 = 9216, kH2FB1 = kH2FB0 + kH2FB, kH2X1 = 18496, kH2WBA = 34880;
-constexpr int kH2S2 = 18496, kH2WBB = 27712, kH2T2 = 8192, kH2S3 = 18560, kH2T3 = 2048;
+constexpr int kH2X1 = 18496, kH2WBA = 34880, kH2WBB = 27712, kH2T2 = 8192, kH2T3 = 2048;
 constexpr int kH2LdsBytes = 3 * kBnTab * 4 + kH2Arena * 2;
 static_assert(kH2LdsBytes <= 80 * 1024, "two conv_kernel_h2 workgroups per CU");
-static_assert(kH2FB1 + kH2FB <= kH2X1 && kH2X1 + 32 * 32 * 16 == kH2WBA && kH2WBA + 2560 <= kH2Arena, "stage 1 map");
-static_assert(34 * 34 * 16 <= kH2X1 && kH2S2 + kH2BR * 32 * 32 <= kH2WBB && kH2WBB + kWB <= kH2Arena, "stage 2 map");
-static_assert(16 * 16 * 32 <= kH2T2 && kH2T2 + 18 * 18 * 32 <= kH2S3 && kH2S3 + 17 * 16 * 32 <= kH2WBB, "stage 3 map");
+static_assert(kH2X1 + 32 * 32 * 16 == kH2WBA && kH2WBA + 2560 <= kH2Arena, "stage 1 map");
+static_assert(34 * 34 * 16 <= kH2X1 && kH2WBB + kWB <= kH2Arena, "stage 2 map");
+static_assert(16 * 16 * 32 <= kH2T2 && kH2T2 + 18 * 18 * 32 <= kH2WBB, "stage 3 map");
 static_assert(8 * 8 * 32 <= kH2T3 && kH2T3 + 10 * 10 * 32 <= kH2T2, "stage 3 res map");
-static_assert(kH2BR * 64 * 16 <= kH2FB0 && 3 * kBnTab * 2 >= 34 * 16, "band scratch / row -1 guard");
+static_assert(3 * kBnTab * 2 >= 34 * 16, "row -1 guard");
 
-// conv_h's arithmetic in tile-outer order (every K-step of tile i, then tile i + 1): per output the same K
-// order and the same separate tap-8 product, so the sums are conv_h's bit for bit.  With 4 waves a wave owns
-// up to 16 tiles; K-outer order keeps 5 pixel addresses per tile live at once (80 VGPRs in the stage-1
-// residual convs, which spilled), tile-outer order keeps one tile's.  Dependent MFMAs on one accumulator
+// The residual convs in tile-outer order (every K-step of tile i, then tile i + 1): K-outer order keeps 5 pixel
+// addresses per tile live at once (80 VGPRs in the stage-1 residual convs, which spilled), tile-outer order keeps
+// one tile's.  Dependent MFMAs on one accumulator
 // issue back to back (SrcC forwarding of the same opcode), and the other workgroup's waves fill the SIMD.
 // STREAM (Cin = 32 at 8 waves, where 72 fragment VGPRs do not fit beside the accumulators under 128): the A
 // fragments are read from the LDS weight block ws per K-step (K-outer: both channel tiles' fragments, then every
@@ -724,7 +269,7 @@ static_assert(kH2BR * 64 * 16 <= kH2FB0 && 3 * kBnTab * 2 >= 34 * 16, "band scra
 // R32 (conv_kernel_h2<512>): the tap-8 remainder runs as one more v_mfma_f32_16x16x32_f16 on the pack's K = 32
 // fragment (tap 8 + zeros) chained onto the accumulator -- a K = 16 MFMA takes the same 16-clock slot
 // (profiles/r08a_mfma_rate_probe.txt), and the separate accumulator's VALU add (the K = 16 product cannot be chained:
-// DESIGN.md 3.4 SrcC) and its registers go.  The sums differ from conv_h's in rounding only.
+// DESIGN.md 3.4 SrcC) and its registers go.
 template <int CIN, int CS, int NT, int TPW, int W, int WP, int MT, int NW, bool STREAM = false, int NTA = NT,
           bool R32 = false>
 __device__ __forceinline__ void conv_h2(const _Float16* Tin, const h8 (&af)[KSteps<CIN>::N][NT],
@@ -864,7 +409,7 @@ __device__ __forceinline__ float div255_byte(float x) {
 struct FrameBn {  // BN2d(3) of the frame: per-channel scale / shift (scalars: the struct is passed by value)
   float s0, s1, s2, h0, h1, h2;
 };
-template <int NTH, int FR = kH2FBRows>
+template <int NTH, int FR>
 __device__ __forceinline__ void frame_band_h2(_Float16* FB, const _Float16* prev, int r0, int p0, const StepArgs& a,
                                               int64_t env, int e, FrameBn bn) {
   const int nitem = (FR - r0) * 24;
@@ -908,54 +453,6 @@ __device__ __forceinline__ void frame_band_h2(_Float16* FB, const _Float16* prev
     else
       reinterpret_cast<uint4*>(FB)[i - npad] = reinterpret_cast<const uint4*>(prev + (FR - r0) * 66 * 4)[i - npad];
   }
-}
-
-// One entry band: conv rows [(BR-1) b - 1, +BR) of the padded input Tin (its row 0 = padded row (BR-1) b - 1,
-// qoff its padded-pixel index) + bias -> S (conv row -1 as -inf), barrier, then the 3x3 / stride-2 max pool of
-// the band's PRB pooled rows -> X rows [PRB b, +PRB).  between(): work for the pool phase (frame rows of the next
-// band, a weight commit) -- it must not touch S, Tin or X.
-template <int NTH, int CIN, int COUT, int H, int BR, bool STREAM, class Between>
-__device__ __forceinline__ void entry_band_h2(const _Float16* Tin, int qoff, _Float16* S, _Float16* X,
-                                              const h8 (&af)[KSteps<CIN>::N][COUT / 16], const _Float16* ws,
-                                              const float (&bz)[COUT / 16][4], int b, int wave, int lane,
-                                              const StepArgs& a, int stamp, Between&& between) {
-  constexpr int CS = Pix<CIN>::CS, WP = H + 2, NT = COUT / 16, MT = BR * H / 16;
-  constexpr int NW = NTH / 64, TPW = (MT + NW - 1) / NW, HO = H / 2, PRB = (BR - 1) / 2, G = COUT / 8;
-  f32x4 acc[TPW][NT];
-  conv_h2<CIN, CS, NT, TPW, H, WP, MT, NW, STREAM>(Tin, af, acc, wave, lane, qoff, ws);
-  conv_out_h<NT, TPW, MT, NW>(acc, wave, lane, [&](int ch0, int m, f32x4 v) {
-    const int nt = ch0 >> 4;
-    const bool neg = b == 0 && m < H;  // conv row -1
-    const float ninf = -INFINITY;
-    *reinterpret_cast<h4*>(S + xidx<COUT>(m, ch0)) =
-        neg ? to_h4(ninf, ninf, ninf, ninf) : to_h4(v[0] + bz[nt][0], v[1] + bz[nt][1], v[2] + bz[nt][2], v[3] + bz[nt][3]);
-  });
-  __syncthreads();
-  FDR_STAMP(a, stamp);
-  between();
-  constexpr int NI = PRB * HO * G, IT = (NI + NTH - 1) / NTH;
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int i = threadIdx.x + it * NTH;
-    if (NI % NTH != 0 && i >= NI) break;
-    const int cg = i % G, r = i / G, px = r % HO, pr = r / HO;
-    const int xl = 2 * px > 0 ? 2 * px - 1 : 0;
-    h8 v[9];
-#pragma unroll
-    for (int dr = 0; dr < 3; ++dr) {
-      const int row = (2 * pr + dr) * H;
-      v[3 * dr] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + xl, 8 * cg));
-      v[3 * dr + 1] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + 2 * px, 8 * cg));
-      v[3 * dr + 2] = *reinterpret_cast<const h8*>(S + xidx<COUT>(row + 2 * px + 1, 8 * cg));
-    }
-    const h8 m01 = __builtin_elementwise_max(v[0], v[1]), m23 = __builtin_elementwise_max(v[2], v[3]);
-    const h8 m45 = __builtin_elementwise_max(v[4], v[5]), m67 = __builtin_elementwise_max(v[6], v[7]);
-    const h8 mx = __builtin_elementwise_max(
-        __builtin_elementwise_max(__builtin_elementwise_max(m01, m23), __builtin_elementwise_max(m45, m67)), v[8]);
-    *reinterpret_cast<h8*>(X + xidx<COUT>((PRB * b + pr) * HO + px, 8 * cg)) = mx;
-  }
-  __syncthreads();
-  FDR_STAMP(a, stamp + 1);
 }
 
 // -----------------------------------------------------------------------------------------------------
@@ -1397,14 +894,9 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
   do {                       \
   } while (0)
 #endif
-// SPLIT3 (conv_kernel_h2<512, true>, ctx conv_h2 = 3): stop after the stage-3 entry and hand X3 (8 x 8 x 32 f16, the
-// xidx layout) to conv_s3_kernel through the first 4 KB of the env's feature slot; the stage-3 residual blocks run
-// there, four envs per workgroup
-template <int NTH, bool SPLIT3>
+template <int NTH>
 __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))) void conv_kernel_h2(Layout L, StepArgs a) {
-  constexpr bool H3 = NTH >= 512;  // stage entries with the pool in registers
-  static_assert(!SPLIT3 || H3, "split stage 3: the h3 entries");
-  static_assert(!H3 || NTH == kHThreads, "h3 entries: 8 waves (zero_border_h's thread count)");
+  static_assert(NTH == kHThreads, "8 waves (zero_border_h's thread count; the h3 entries' band rows)");
   __shared__ __attribute__((aligned(16))) unsigned char smem[kH2LdsBytes];
   const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
   const int lane = (slot / a.envs) * 8 + xcd, e = slot % a.envs;
@@ -1457,12 +949,8 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
       cbv[k] = has_cb ? c_ : 0.f;
     }
   }
-  h8 af3[KSteps<3>::N][1];
-  h8 af3n[2];  // (h3 entries: conv_band_s1's K order)
-  if constexpr (H3)
-    s1_frag(hp + L.conv_h[0], af3n, ln);
-  else
-    load_af<3, 1>(hp + L.conv_h[0], af3, ln);
+  h8 af3n[2];  // conv_band_s1's K order
+  s1_frag(hp + L.conv_h[0], af3n, ln);
   WStageT<NTH> st;
   st.template issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);
   float fsc[3], fsh[3];  // BN2d(3) of the frame, per thread (table entries 0..2)
@@ -1474,15 +962,10 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     fsh[c] = pk[L.bn_b[0] + c] - m * fsc[c];
   }
   const FrameBn fbn{fsc[0], fsc[1], fsc[2], fsh[0], fsh[1], fsh[2]};
-  auto FB = [&](int k) { return R + ((k & 1) ? kH2FB1 : kH2FB0); };  // the two frame-band buffers
   auto FB3 = [&](int k) { return R + ((k & 1) ? kH3FB1 : kH3FB0); };
-  if constexpr (H3) {
-    frame_band_h2<NTH, kH3FR>(FB3(0), nullptr, 0, 0, a, env, e, fbn);
-    if (threadIdx.x < 2)  // the frame buffers' pad pixels (conv_band_s1)
-      *reinterpret_cast<h4*>(R + (threadIdx.x ? kH3FB1 : kH3FB0) + kH3FB) = h4{0, 0, 0, 0};
-  }
-  else
-    frame_band_h2<NTH>(FB(0), nullptr, 0, -1, a, env, e, fbn);
+  frame_band_h2<NTH, kH3FR>(FB3(0), nullptr, 0, 0, a, env, e, fbn);
+  if (threadIdx.x < 2)  // the frame buffers' pad pixels (conv_band_s1)
+    *reinterpret_cast<h4*>(R + (threadIdx.x ? kH3FB1 : kH3FB0) + kH3FB) = h4{0, 0, 0, 0};
 #pragma unroll
   for (int k = 0; k < kTabIt; ++k) {
     const int bi = threadIdx.x + k * NTH, bidx = bi >> 5, bch = bi & 31;
@@ -1496,8 +979,8 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   __syncthreads();
   FDR_STAMP(a, 1);
 
-  // ---- stage 1: entry (3 -> 16 at 64 x 64, pooled to 32 x 32) in 8 bands (h3: 4 bands, pool in registers) ----
-  if constexpr (H3) {
+  // ---- stage 1: entry (3 -> 16 at 64 x 64, pooled to 32 x 32) in 4 bands of 16 rows, pool in registers ----
+  {
     for (int bd = 0; bd < 4; ++bd) {
       h4 prev[2], P[2], Bx[2];
       f32x4 acc[8];
@@ -1517,22 +1000,11 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     }
     __syncthreads();
     FDR_STAMP(a, 6);
-  } else {
-    float bz[1][4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) bz[0][k] = bcb[0 * 32 + 4 * (ln >> 4) + k];
-    for (int bd = 0; bd < 64 / (kH2BR - 1); ++bd) {
-      entry_band_h2<NTH, 3, 16, 64, kH2BR, false>(FB(bd), 0, R + kH2S1, R + kH2X1, af3, nullptr, bz, bd, wave, ln, a, 2 + 2 * bd, [&]() {
-        if (bd == 0) st.template commit<kBlockHalves<16, 1>>(R + kH2WBA);
-        if (bd + 1 < 64 / (kH2BR - 1))
-          frame_band_h2<NTH>(FB(bd + 1), FB(bd), 3, (kH2BR - 1) * (bd + 1) - 1, a, env, e, fbn);
-      });
-    }
   }
   // ---- stage 1 residual blocks (16 ch, 32 x 32) ----
   {
     h8 af[KSteps<16>::N][1];
-    load_af_lds<16, 1, NTH >= 512>(R + kH2WBA, af, ln);
+    load_af_lds<16, 1, true>(R + kH2WBA, af, ln);
     st.template issue<kBlockHalves<16, 1>>(hp + L.conv_h[2]);
     to_padded_h<16, 32, true, true, NTH>(R + kH2X1, R, bsc + 1 * 32, bsh + 1 * 32);
     __syncthreads();
@@ -1542,9 +1014,9 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     st.template commit<kBlockHalves<16, 2>>(R + kH2WBB);  // X1 is dead: the stage-2 entry block goes to WB_B
     __syncthreads();
   }
-  // ---- stage 2: entry (16 -> 32 at 32 x 32, pooled to 16 x 16) in 4 bands; X2 into T1's consumed rows (h3: 2
-  // bands of 16 rows, pool in registers; band 1 reads padded rows 16..33, past X2's first half) ----
-  if constexpr (H3) {
+  // ---- stage 2: entry (16 -> 32 at 32 x 32, pooled to 16 x 16) in 2 bands of 16 rows, pool in registers; X2 into
+  // T1's consumed rows (band 1 reads padded rows 16..33, past X2's first half) ----
+  {
     // conv 6's weight block is requested after band 1's conv, once the accumulators are pooled (r10: issued before
     // the two bands, its 9 staging VGPRs lived across both bands' convs -- one 16-B chunk spilled, the kernel's only
     // scratch traffic, 33.5 MB written + read per launch)
@@ -1581,44 +1053,19 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     zero_border_h<32, 16>(R + kH2T2);
     __syncthreads();  // X2, T2 complete
     FDR_STAMP(a, 30);
-  } else {
-    h8 af[KSteps<16>::N][2];
-    constexpr bool ST = NTH >= 512;  // conv 5 streamed from WB_B: conv 6's block is committed after the last band
-    if constexpr (!ST) load_af_lds<16, 2>(R + kH2WBB, af, ln);
-    st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[6]);
-    float bz[2][4];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[5 * 32 + nt * 16 + 4 * (ln >> 4) + k];
-    for (int bd = 0; bd < 32 / (kH2BR - 1); ++bd) {
-      const int q0 = ((kH2BR - 1) * bd - 1) * 34;
-      entry_band_h2<NTH, 16, 32, 32, kH2BR, ST>(R + q0 * 16, q0, R + kH2S2, R, af, R + kH2WBB, bz, bd, wave, ln, a,
-                                                28 + 2 * bd, [&]() {
-        if (bd == (ST ? 32 / (kH2BR - 1) - 1 : 0)) st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
-      });
-    }
   }
   // ---- stage 2 residual blocks (32 ch, 16 x 16) ----
   {
-    h8 af[KSteps<32>::N][2];
-    if constexpr (NTH < 512) load_af_lds<32, 2>(R + kH2WBB, af, ln);
+    h8 af[KSteps<32>::N][2];  // (unread: the 32-channel convs stream their A fragments from WB)
     st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[7]);
-    if constexpr (!H3) {  // (h3: T2 written by the entry)
-      to_padded_h<32, 16, true, true, NTH>(R, R + kH2T2, bsc + 6 * 32, bsh + 6 * 32);
-      __syncthreads();
-      FDR_STAMP(a, 36);
-    }
     res_blocks_h2<NTH, 32, 16, 0, kBlockHalves<32, 2>>(R + kH2T2, R, af, hp, L, 1, bsc, bsh, bcb, wave, ln, nullptr, st,
                                                   R + kH2WBB, hp + L.conv_h[10], a, 37);
     st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
     __syncthreads();
   }
-  // ---- stage 3: entry (32 -> 32 at 16 x 16, pooled to 8 x 8): one band of 17 rows at 4 waves; at 8 waves (128
-  // VGPRs) two bands of 9, so a wave's accumulators stay at 2 tiles x 2 channel tiles beside the 72 fragment VGPRs
-  // (h3: one band of 16 rows, pool in registers) ----
-  if constexpr (H3) {
-    if constexpr (!SPLIT3) st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
+  // ---- stage 3: entry (32 -> 32 at 16 x 16, pooled to 8 x 8): one band of 16 rows, pool in registers ----
+  {
+    st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
     h4 prev[2], P[2], Bx[2];
     f32x4 acc[2][2];
     conv_band_nat<32, 16>(R + kH2T2, 0, R + kH2WBB, acc, wave, ln);
@@ -1628,49 +1075,17 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
 #pragma unroll
       for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[10 * 32 + nt * 16 + 4 * (ln >> 4) + k];
     pool_nat<16>(acc, bz, P, Bx);
-    band_out_h3<32, 16, false>(P, Bx, prev, R, R + kH3EX3, 0, wave, ln, SPLIT3 ? nullptr : R + kH2T3, bsc + 11 * 32,
-                               bsh + 11 * 32);
-    if constexpr (SPLIT3) {
-      __syncthreads();  // X3 complete
-      FDR_STAMP(a, 45);
-      if (threadIdx.x < 8 * 8 * 32 / 8)   // X3 -> the env's feature slot (read back by conv_s3_kernel)
-        reinterpret_cast<u32x4*>(a.feat + env * kFeat)[threadIdx.x] = reinterpret_cast<const u32x4*>(R)[threadIdx.x];
-      return;
-    }
+    band_out_h3<32, 16, false>(P, Bx, prev, R, R + kH3EX3, 0, wave, ln, R + kH2T3, bsc + 11 * 32, bsh + 11 * 32);
     zero_border_h<32, 8>(R + kH2T3);
     st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
     FDR_STAMP(a, 45);
     __syncthreads();  // X3, T3 complete
     FDR_STAMP(a, 46);
-  } else {
-    h8 af[KSteps<32>::N][2];
-    constexpr bool ST = NTH >= 512;  // conv 10 streamed from WB_B: conv 11's block is committed after the last band
-    if constexpr (!ST) load_af_lds<32, 2>(R + kH2WBB, af, ln);
-    st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[11]);
-    float bz[2][4];
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) bz[nt][k] = bcb[10 * 32 + nt * 16 + 4 * (ln >> 4) + k];
-    constexpr int BR3 = NTH >= 512 ? 9 : 17;
-    for (int bd = 0; bd < 16 / (BR3 - 1); ++bd) {
-      const int q0 = ((BR3 - 1) * bd - 1) * 18;
-      entry_band_h2<NTH, 32, 32, 16, BR3, ST>(R + kH2T2 + q0 * 32, q0, R + kH2S3, R, af, R + kH2WBB, bz, bd, wave, ln, a,
-                                              45 + 2 * bd, [&]() {
-        if (bd == (ST ? 16 / (BR3 - 1) - 1 : 0)) st.template commit<kBlockHalves<32, 2>>(R + kH2WBB);
-      });
-    }
   }
   // ---- stage 3 residual blocks (32 ch, 8 x 8) -> features ----
   {
     h8 af[KSteps<32>::N][2];
-    if constexpr (NTH < 512) load_af_lds<32, 2>(R + kH2WBB, af, ln);
     st.template issue<kBlockHalves<32, 2>>(hp + L.conv_h[12]);
-    if constexpr (!H3) {  // (h3: T3 written by the entry)
-      to_padded_h<32, 8, true, true, NTH>(R, R + kH2T3, bsc + 11 * 32, bsh + 11 * 32);
-      __syncthreads();
-      FDR_STAMP(a, 49);
-    }
     res_blocks_h2<NTH, 32, 8, 1, 0>(R + kH2T3, R, af, hp, L, 2, bsc, bsh, bcb, wave, ln, a.feat + env * kFeat, st,
                                R + kH2WBB, nullptr, a, 50);
   }
@@ -1679,238 +1094,7 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
   if (a.dbg && threadIdx.x == 0) a.dbg[256 + 4 * b + 1] = wall_clock64();
 #endif
 }
-template __global__ void conv_kernel_h2<256, false>(Layout, StepArgs);
-template __global__ void conv_kernel_h2<512, false>(Layout, StepArgs);
-template __global__ void conv_kernel_h2<512, true>(Layout, StepArgs);
-
-// =====================================================================================================
-// Stage-3 residual blocks, FOUR envs per workgroup: conv_s3_kernel (ctx conv_h2 = 3, after conv_kernel_h2<512, true>;
-// VERDICT r4 item 1).  In the one-env workgroup the stage-3 residual convs (8 x 8 x 32, 4 pixel tiles x 2 channel
-// tiles) gave each wave ONE dependent chain of 9 MFMAs between LDS reads, then a barrier, an epilogue and a barrier:
-// 8 barrier phases for 1.15 K MFMA slots per SIMD, ~7.6 K clocks of the env's ~80 K (profiles/r08o phases).  Here a
-// workgroup takes envs 4b .. 4b + 3 (the four envs of one lane when E = 4: one theta'), wave w = (env slot w / 2,
-// channel tile w % 2) runs FOUR independent chains (the env's 4 pixel tiles) per conv, and:
-//   * the residual stream X lives in the wave's registers (its own pixels x channels: the accumulator layout, 8 VGPRs)
-//     -- only the padded BN'd image T is shared, double-buffered per env (conv c reads T[c & 1], writes T[c + 1 & 1]),
-//     so each conv has ONE barrier and the epilogue follows the wave's own MFMAs;
-//   * the A fragments (this wave's channel tile, 9 K-steps = 36 VGPRs) come straight from the half pack (L2: the
-//     lane's other waves and envs read the same 9 KB), the next conv's issued right after the current K loop;
-//   * per output: the same K order, the same chained MFMAs and the same f32 epilogue arithmetic as res_blocks_h2,
-//     so the features equal conv_kernel_h2<512>'s bit for bit (tests/test_gpu_impala.py).
-// LDS: 4 envs x 2 x 10 x 10 x 32 halves (51 KB) + the BN / bias rows of convs 11..14 (6 KB): two workgroups per CU.
-// =====================================================================================================
-constexpr int kS3Envs = kS3EnvsPerWG;
-constexpr int kS3T = 10 * 10 * 32;  // halves of one padded 8 x 8 x 32 image
-
-// Wave map (r11b): wave w = (env slot w / 2, pixel-tile pair w % 2) computes BOTH channel tiles of its two pixel tiles,
-// so each B fragment read from LDS feeds two MFMAs (the first form, one channel tile x four pixel tiles per wave,
-// read 1 KB of LDS per MFMA: the LDS port, not the MFMA pipe, bounded its convs -- 4.3 K clocks per conv against
-// 1.15 K of MFMA issue, phase clocks r11a).  A fragments of both channel tiles in registers (72 VGPRs).
-// SHARED (envs per lane a multiple of 4: the four env slots are ONE lane, one theta'): each conv's 18 KB weight block
-// is copied once per workgroup into LDS by global_load_lds_dwordx4 (no staging registers: 18 wave-instructions of 64 x
-// 16 B, issued while the previous conv runs, waited for before its closing barrier); otherwise every wave loads its
-// fragments from the half pack.
-template <bool SHARED>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void conv_s3_kernel(Layout L, StepArgs a) {
-  constexpr int WH = kBlockHalves<32, 2>;  // one 32 -> 32 conv's fragments, [k-step][channel tile][lane][8]
-  __shared__ __attribute__((aligned(16))) _Float16 Tb[kS3Envs][2][kS3T];
-  __shared__ float tab[kS3Envs][3][4][32];  // [slot][scale, shift, conv bias][index 11 .. 14][channel]
-  __shared__ __attribute__((aligned(16))) _Float16 WB[SHARED ? WH : 8];
-  const int64_t n_envs = (int64_t)a.n_lanes * a.envs;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
-  const int slot = wave >> 1, hp2 = wave & 1, g = ln >> 4;
-  const int64_t ge = (int64_t)blockIdx.x * kS3Envs + slot;
-  const bool live = ge < n_envs;  // wave-uniform; a dead wave still meets every barrier
-  const int64_t lane_id = live ? ge / a.envs : 0;
-  const _Float16* hp = a.hpack + (SHARED ? (int64_t)blockIdx.x * kS3Envs / a.envs : lane_id) * a.hpack_stride;
-  FDR_STAMP(a, 100);  // phase clocks of workgroup 0 (tools/impala_phases_h2.py --mode 3): 100 .. 110
-
-  // this wave's A fragments (both channel tiles), from the pack or the workgroup's LDS copy
-  h8 af[9][2];
-  auto load_a = [&](const _Float16* src) {
-#pragma unroll
-    for (int s = 0; s < 9; ++s)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) af[s][nt] = *reinterpret_cast<const h8*>(src + ((s * 2 + nt) * 64 + ln) * 8);
-  };
-  // WB <- conv `conv`'s block straight from global memory (LDS DMA): wave w copies 1 KB pieces w, w + 8, w + 16
-  auto copy_block = [&](int conv) {
-    typedef __attribute__((address_space(1))) const void gptr_t;
-    typedef __attribute__((address_space(3))) void lptr_t;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int piece = wave + 8 * k;
-      if (piece < WH / 512)
-        __builtin_amdgcn_global_load_lds((gptr_t*)(hp + L.conv_h[conv] + (piece * 64 + ln) * 8), (lptr_t*)(WB + piece * 512),
-                                         16, 0, 0);
-    }
-  };
-#ifdef FDR_S3_PROBE  // diagnostics build: each prologue load group waited for and stamped (dbg[112..])
-#define FDR_S3_P(k)                 \
-  do {                              \
-    __builtin_amdgcn_s_waitcnt(0);  \
-    FDR_STAMP(a, k);                \
-  } while (0)
-#else
-#define FDR_S3_P(k) \
-  do {              \
-  } while (0)
-#endif
-  FDR_S3_P(112);
-  if constexpr (SHARED) {
-    copy_block(11);
-    FDR_S3_P(113);
-  } else if (live) {
-    load_a(hp + L.conv_h[11]);
-  }
-  // X3 of the env (conv_kernel_h2<512, true>'s copy, xidx layout): tile 2 hp2 + j, pixel 16 tile + (ln & 15), channels
-  // 16 nt + 4 g ..
-  h4 x[2][2];
-  const _Float16* x3 = reinterpret_cast<const _Float16*>(a.feat + (live ? ge : 0) * kFeat);
-#pragma unroll
-  for (int j = 0; j < 2; ++j)
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-      x[j][nt] = live ? *reinterpret_cast<const h4*>(x3 + xidx<32>(16 * (2 * hp2 + j) + (ln & 15), 16 * nt + 4 * g))
-                      : h4{0, 0, 0, 0};
-  FDR_S3_P(114);
-  // the BN / bias rows of convs 11 .. 14 per env slot (conv_kernel_h2's table arithmetic): thread (slot, ch) < 128,
-  // the four indices unrolled (compile-time offsets into the layout: scalar loads)
-  if (threadIdx.x < 128) {
-    const int ts = threadIdx.x >> 5, ch = threadIdx.x & 31;
-    const int64_t gs = (int64_t)blockIdx.x * kS3Envs + ts;
-    const float* pk = a.pack + (gs < n_envs ? gs / a.envs : 0) * a.pack_stride;
-    const float* bmp = a.bn_mean ? a.bn_mean : pk;  // unconditional loads (kernel A's table note)
-    const float* bvp = a.bn_var ? a.bn_var : pk;
-    float rm_[4], rv_[4], w_[4], b_[4], c_[4];
-#pragma unroll
-    for (int ti = 0; ti < 4; ++ti) {
-      const int bidx = 11 + ti;
-      rm_[ti] = bmp[L.bn_stat[bidx] + ch];
-      rv_[ti] = bvp[L.bn_stat[bidx] + ch];
-      w_[ti] = pk[L.bn_w[bidx] + ch];
-      b_[ti] = pk[L.bn_b[bidx] + ch];
-      c_[ti] = pk[L.conv_b[bidx] + ch];
-    }
-#pragma unroll
-    for (int ti = 0; ti < 4; ++ti) {
-      const float rm = a.bn_mean ? rm_[ti] : 0.f, rv = a.bn_var ? rv_[ti] : 1.f;
-      const float sc = w_[ti] * (1.f / sqrtf(rv + kBnEps));
-      const bool ok = gs < n_envs;
-      tab[ts][0][ti][ch] = ok ? sc : 0.f;
-      tab[ts][1][ti][ch] = ok ? b_[ti] - rm * sc : 0.f;
-      tab[ts][2][ti][ch] = ok ? c_[ti] : 0.f;
-    }
-  }
-  FDR_S3_P(115);
-  // zero both images of every slot (the borders stay zero: every later store is interior)
-  {
-    u32x4* z = reinterpret_cast<u32x4*>(&Tb[0][0][0]);
-    for (int i = threadIdx.x; i < kS3Envs * 2 * kS3T / 8; i += 512) z[i] = u32x4{0u, 0u, 0u, 0u};
-  }
-  FDR_S3_P(116);
-  if constexpr (SHARED) __builtin_amdgcn_s_waitcnt(0);  // the LDS DMA of conv 11's block has landed
-  __syncthreads();
-  FDR_STAMP(a, 101);
-  // padded pixel of this lane's output pixel in its tile j (8 x 8 image, pitch 10)
-  auto qout = [&](int j) {
-    const int m = 16 * (2 * hp2 + j) + (ln & 15);
-    return ((m >> 3) + 1) * 10 + (m & 7) + 1;
-  };
-  const float* sct = &tab[slot][0][0][0];
-  const float* sht = &tab[slot][1][0][0];
-  const float* cbt = &tab[slot][2][0][0];
-  // T[0] = relu(BN_11(X3)) (t_store_h3's arithmetic)
-  if (live) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const int c = 16 * nt + 4 * g;
-        const h2 lo = lo2(x[j][nt]), hi = hi2(x[j][nt]);
-        const h4 t = to_h4(fma_mix_lo(lo, sct[c], sht[c]), fma_mix_hi(lo, sct[c + 1], sht[c + 1]),
-                           fma_mix_lo(hi, sct[c + 2], sht[c + 2]), fma_mix_hi(hi, sct[c + 3], sht[c + 3]));
-        *reinterpret_cast<h4*>(&Tb[slot][0][0] + tidx<32>(qout(j), c)) = relu_h4(t);
-      }
-  }
-  __syncthreads();
-  FDR_STAMP(a, 102);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {  // convs 11, 12 (block 0), 13, 14 (block 1)
-    const _Float16* Tin = &Tb[slot][c & 1][0];
-    _Float16* Tout = &Tb[slot][(c + 1) & 1][0];
-    if constexpr (SHARED) {
-      load_a(WB);        // WB = conv 11 + c
-      __syncthreads();   // every wave holds its fragments: WB is free for the next block
-      FDR_STAMP(a, 103 + 2 * c);
-      if (c < 3) copy_block(12 + c);
-    }
-    f32x4 acc[2][2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[j][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (live) {
-#pragma unroll
-      for (int s = 0; s < 9; ++s) {  // tap s = (s / 3, s % 3), channel chunk g: conv_h2's K order
-        // the pair's second tile is the first's two padded rows (20 pixels) further: tsw<32>(q + 20) = tsw<32>(q) ^ 2
-        const int q0 = (4 * hp2 + ((ln & 15) >> 3) + s / 3) * 10 + (ln & 7) + s % 3;
-        const int a0 = q0 * 32, sw0 = g ^ tsw<32>(q0);
-        const h8 b0 = *reinterpret_cast<const h8*>(Tin + a0 + (sw0 << 3));
-        const h8 b1 = *reinterpret_cast<const h8*>(Tin + a0 + 640 + ((sw0 ^ 2) << 3));
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          acc[0][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b0, acc[0][nt], 0, 0, 0);
-          acc[1][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[s][nt], b1, acc[1][nt], 0, 0, 0);
-        }
-      }
-      const int i0 = c;           // this conv's table index (conv 11 + c)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-          const int ch0 = 16 * nt + 4 * g;
-          const f32x4 v = acc[j][nt];
-          if ((c & 1) == 0) {
-            // conv0 of a block: T <- relu(BN_{next}(. + b0)) (res_blocks_h2 epilogue0)
-            float o[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              o[k] = fmaf(v[k] + cbt[i0 * 32 + ch0 + k], sct[(i0 + 1) * 32 + ch0 + k], sht[(i0 + 1) * 32 + ch0 + k]);
-            *reinterpret_cast<h4*>(Tout + tidx<32>(qout(j), ch0)) = relu_h4(to_h4(o[0], o[1], o[2], o[3]));
-          } else {
-            // conv1: x' = f16((v + b1) + x); block 0: T <- relu(BN_13(x')); block 1 (the last): features relu(x')
-            const h2 xl = lo2(x[j][nt]), xh = hi2(x[j][nt]);
-            const float* b1 = cbt + i0 * 32 + ch0;
-            const h4 xn = to_h4(fma_mix_lo(xl, 1.f, v[0] + b1[0]), fma_mix_hi(xl, 1.f, v[1] + b1[1]),
-                                fma_mix_lo(xh, 1.f, v[2] + b1[2]), fma_mix_hi(xh, 1.f, v[3] + b1[3]));
-            if (c == 3) {
-              float* out = a.feat + ge * kFeat;
-              const int m = 16 * (2 * hp2 + j) + (ln & 15);
-#pragma unroll
-              for (int k = 0; k < 4; ++k) out[(ch0 + k) * 64 + m] = relu((float)xn[k]);  // flatten (C, H, W)
-            } else {
-              x[j][nt] = xn;
-              const h2 nl = lo2(xn), nh = hi2(xn);
-              const float* s2 = sct + (i0 + 1) * 32 + ch0;
-              const float* t2 = sht + (i0 + 1) * 32 + ch0;
-              const h4 t = to_h4(fma_mix_lo(nl, s2[0], t2[0]), fma_mix_hi(nl, s2[1], t2[1]), fma_mix_lo(nh, s2[2], t2[2]),
-                                 fma_mix_hi(nh, s2[3], t2[3]));
-              *reinterpret_cast<h4*>(Tout + tidx<32>(qout(j), ch0)) = relu_h4(t);
-            }
-          }
-        }
-    }
-    if (!SHARED && live && c < 3) load_a(hp + L.conv_h[12 + c]);  // the next conv's fragments
-    if (c < 3) {
-      if constexpr (SHARED) __builtin_amdgcn_s_waitcnt(0);  // conv 12 + c's block has landed in WB
-      __syncthreads();  // T[c + 1 & 1] and WB complete; T[c & 1] free for the next conv's output
-    }
-    FDR_STAMP(a, 104 + 2 * c);
-  }
-}
-template __global__ void conv_s3_kernel<false>(Layout, StepArgs);
-template __global__ void conv_s3_kernel<true>(Layout, StepArgs);
+template __global__ void conv_kernel_h2<kHThreads>(Layout, StepArgs);
 
 // ---- core (fc + LSTM + head) with f16 weights ------------------------------------------------------
 template <int E, int MODE>
@@ -2100,272 +1284,6 @@ __global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(E 
   if (j < E) core_finish<E, MODE>(a, logit, lane, j);
 }
 
-// ---- pair form of the fp16 rollout core step (fdr_impala_desc.pairs) --------------------------------
-// Lanes 2p, 2p+1 of an antithetic pair share their table offset, so their fc / LSTM weights are
-// theta + s_l fl32(sigma eps).  One workgroup per pair streams the pair's sigma-eps half pack ONCE from HBM
-// (non-temporal) and theta's half pack (2.1 MB, read by every workgroup: L2-resident) and forms each lane's
-// weight w = f16(theta) + s_l f16(sigma eps) in registers -- half core_kernel_h's HBM bytes per lane.  The
-// pair's 2E envs are contiguous (envs 2pE .. 2pE + 2E - 1), so the state / feature / output indexing is
-// core_kernel_h's with E -> 2E; biases, BN and the head are each lane's own (its f32 pack).
-// Numerics: f16(theta) + s f16(sigma eps) in f32 vs f16(theta + s sigma eps): within the fp16 tolerance.
-template <int E>
-__global__ __launch_bounds__(kCoreThreads) void core_kernel_hp(Layout L, StepArgs a) {
-  constexpr int E2 = 2 * E;
-  __shared__ float xw[kFeat * E2];
-  __shared__ float hs[kHid * E2];
-  float* cis = xw + kFeat * E2 / 2;
-  float* logit = xw;
-  static_assert(kCoreIn * E2 <= kFeat * E2 / 2 && E2 * kMaxAct <= kFeat * E2, "core LDS aliasing");
-  const int pr = blockIdx.x, j = threadIdx.x;
-  const int l0 = 2 * pr;
-  const float* pk0 = a.pack + (int64_t)l0 * a.pack_stride;
-  const float* pk1 = pk0 + a.pack_stride;
-  const float sg0 = a.sign ? (float)a.sign[l0] : 1.f, sg1 = a.sign ? (float)a.sign[l0 + 1] : 1.f;
-  const _Float16* eh = a.ep + (int64_t)pr * a.ep_stride;
-  const int64_t e0 = (int64_t)l0 * E;
-  const int A = a.n_act;
-  auto pkof = [&](int e) { return e < E ? pk0 : pk1; };
-
-  for (int k = j; k < kFeat; k += kCoreThreads) {  // BN1d(2048), each lane's own parameters
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      const float* pk = hf ? pk1 : pk0;
-      const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[15] + k] : 0.f;
-      const float rv = a.bn_var ? a.bn_var[L.bn_stat[15] + k] : 1.f;
-      const float sc = pk[L.bn_w[15] + k] * (1.f / sqrtf(rv + kBnEps));
-      const float sh = fmaf(-rm, sc, pk[L.bn_b[15] + k]);
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-        xw[k * E2 + hf * E + e] = fmaf(a.feat[(e0 + hf * E + e) * kFeat + k], sc, sh);
-    }
-  }
-  __syncthreads();
-  // one streamed weight row (8 columns): w = theta + s_l E for each lane of the pair, 2E envs of FMAs
-  auto accum = [&](float (&acc)[8][E2], h8 wt, h8 we, const float* x) {
-    float wp[8], wm[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const float t = (float)wt[c], d = (float)we[c];
-      wp[c] = fmaf(sg0, d, t);
-      wm[c] = fmaf(sg1, d, t);
-    }
-#pragma unroll
-    for (int e = 0; e < E2; ++e) {
-      const float xv = x[e];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) acc[c][e] = fmaf(e < E ? wp[c] : wm[c], xv, acc[c][e]);
-    }
-  };
-  {  // fc: thread = (8 columns, one of 8 K-slices of 256 rows)
-    const int c8 = j & 31, ks = j >> 5;
-    float acc[8][E2];
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-#pragma unroll
-      for (int e = 0; e < E2; ++e) acc[c][e] = 0.f;
-    const h8* t8 = reinterpret_cast<const h8*>(a.th + L.fc_wt_h) + c8;
-    const h8* e8 = reinterpret_cast<const h8*>(eh + L.fc_wt_h) + c8;
-#pragma unroll FDR_CORE_UNROLL_H
-    for (int k = ks * 256; k < ks * 256 + 256; ++k)
-      accum(acc, t8[(int64_t)k * (kHid / 8)], ld_stream(e8 + (int64_t)k * (kHid / 8)), xw + k * E2);
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-#pragma unroll
-      for (int e = 0; e < E2; ++e) xw[(ks * kHid + 8 * c8 + c) * E2 + e] = acc[c][e];
-  }
-  __syncthreads();
-  {
-    const float bj0 = pk0[L.fc_b + j], bj1 = pk1[L.fc_b + j];
-    float yv[E2];
-#pragma unroll
-    for (int e = 0; e < E2; ++e) {
-      float y = 0.f;
-#pragma unroll
-      for (int q = 0; q < 8; ++q) y += xw[(q * kHid + j) * E2 + e];
-      yv[e] = relu(y + (e < E ? bj0 : bj1));
-    }
-    __syncthreads();  // every partial read before cis (inside xw) is written
-#pragma unroll
-    for (int e = 0; e < E2; ++e) cis[j * E2 + e] = yv[e];
-  }
-  if (j < E2) cis[kHid * E2 + j] = fminf(fmaxf(a.rprev[e0 + j], -1.f), 1.f);
-  if (a.ci) {
-    __syncthreads();
-    float* dst = a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn;
-    for (int i = j; i < kCoreIn * E2; i += kCoreThreads) {
-      const int e = i / kCoreIn, k = i - e * kCoreIn;
-      dst[i] = cis[k * E2 + e];
-    }
-  }
-  float cj[E2];
-#pragma unroll
-  for (int e = 0; e < E2; ++e) {
-    hs[j * E2 + e] = a.h[(e0 + e) * kHid + j];
-    cj[e] = a.c[(e0 + e) * kHid + j];
-  }
-  __syncthreads();
-  {  // gates: threads 0..127 stream W_ih^T (x part), 128..255 W_hh^T (h part), 8 columns each
-    const int cg = j & 127, part = j >> 7;
-    float acc[8][E2];
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-#pragma unroll
-      for (int e = 0; e < E2; ++e) acc[c][e] = 0.f;
-    const int k_lo = part ? kCoreIn : 0, k_n = part ? kHid : kCoreIn;
-    const float* xin = part ? hs : cis;
-    const h8* t8 = reinterpret_cast<const h8*>(a.th + L.lstm_wt_h) + cg;
-    const h8* e8 = reinterpret_cast<const h8*>(eh + L.lstm_wt_h) + cg;
-#pragma unroll FDR_CORE_UNROLL_H
-    for (int k = 0; k < k_n; ++k)
-      accum(acc, t8[(int64_t)(k_lo + k) * (kGates / 8)], ld_stream(e8 + (int64_t)(k_lo + k) * (kGates / 8)),
-            xin + k * E2);
-    __syncthreads();  // every read of cis (inside xw) is done before the gates overwrite it
-#pragma unroll
-    for (int c = 0; c < 8; ++c)
-#pragma unroll
-      for (int e = 0; e < E2; ++e) xw[(part * kGates + 8 * cg + c) * E2 + e] = acc[c][e];
-  }
-  __syncthreads();
-  float hj[E2];
-#pragma unroll
-  for (int e = 0; e < E2; ++e) {
-    const float* pk = pkof(e);
-    float pre[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int col = g * kHid + j;
-      pre[g] = (xw[col * E2 + e] + pk[L.lstm_bih + col]) + (xw[(kGates + col) * E2 + e] + pk[L.lstm_bhh + col]);
-    }
-    const float gi = sigm(pre[0]), gf = sigm(pre[1]), gg = tanhf(pre[2]), go = sigm(pre[3]);
-    cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
-    hj[e] = go * tanhf(cj[e]);
-    a.h[(e0 + e) * kHid + j] = hj[e];
-    a.c[(e0 + e) * kHid + j] = cj[e];
-  }
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    const float* pk = hf ? pk1 : pk0;
-    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
-    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
-    const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
-    const float sh = fmaf(-rm, sc, pk[L.bn_b[16] + j]);
-#pragma unroll
-    for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
-  }
-  __syncthreads();
-  if (j < A * E2) {  // head in f32 (A x 256, tiny), each lane's own
-    const int ai = j / E2, e = j - ai * E2;
-    const float* pk = pkof(e);
-    const float* w = pk + L.head_w + ai * kHid;
-    float s = 0.f;
-    for (int k = 0; k < kHid; ++k) s = fmaf(w[k], hs[k * E2 + e], s);
-    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
-  }
-  __syncthreads();
-  if (j < E2) core_finish<E, kRollout>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
-}
-
-// Replay (entropy pass) in the fp16 pair form: x W_ih^T precomputed per env (a.gx), W_hh^T streamed as
-// f16(theta) + s_l f16(sigma eps) for the pair (4 columns per thread, as core_kernel_h's replay).
-template <int E>
-__global__ __launch_bounds__(kCoreThreads) void core_kernel_hpr(Layout L, StepArgs a) {
-  constexpr int E2 = 2 * E;
-  typedef _Float16 h4v __attribute__((ext_vector_type(4)));
-  __shared__ float xw[2 * kGates * E2];
-  __shared__ float hs[kHid * E2];
-  float* logit = xw;
-  const int pr = blockIdx.x, j = threadIdx.x;
-  const int l0 = 2 * pr;
-  const float* pk0 = a.pack + (int64_t)l0 * a.pack_stride;
-  const float* pk1 = pk0 + a.pack_stride;
-  const float sg0 = a.sign ? (float)a.sign[l0] : 1.f, sg1 = a.sign ? (float)a.sign[l0 + 1] : 1.f;
-  const _Float16* eh = a.ep + (int64_t)pr * a.ep_stride;
-  const int64_t e0 = (int64_t)l0 * E;
-  const int A = a.n_act;
-  float cj[E2];
-#pragma unroll
-  for (int e = 0; e < E2; ++e) {
-    hs[j * E2 + e] = a.h[(e0 + e) * kHid + j];
-    cj[e] = a.c[(e0 + e) * kHid + j];
-  }
-  __syncthreads();
-  {
-    float acc[4][E2];
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-#pragma unroll
-      for (int e = 0; e < E2; ++e) acc[c][e] = 0.f;
-    const h4v* t4 = reinterpret_cast<const h4v*>(a.th + L.lstm_wt_h) + j;
-    const h4v* d4 = reinterpret_cast<const h4v*>(eh + L.lstm_wt_h) + j;
-#pragma unroll FDR_CORE_UNROLL
-    for (int k = 0; k < kHid; ++k) {
-      const h4v t = t4[(int64_t)(kCoreIn + k) * (kGates / 4)];
-      const h4v d = ld_stream(d4 + (int64_t)(kCoreIn + k) * (kGates / 4));
-      float wp[4], wm[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        wp[c] = fmaf(sg0, (float)d[c], (float)t[c]);
-        wm[c] = fmaf(sg1, (float)d[c], (float)t[c]);
-      }
-#pragma unroll
-      for (int e = 0; e < E2; ++e) {
-        const float xv = hs[k * E2 + e];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c][e] = fmaf(e < E ? wp[c] : wm[c], xv, acc[c][e]);
-      }
-    }
-    const float4* g4 = reinterpret_cast<const float4*>(a.gx + ((int64_t)(a.t - a.gx_t0) * a.n_lanes * E + e0) * kGates);
-#pragma unroll
-    for (int e = 0; e < E2; ++e) {
-      const float4 g = ld_stream(g4 + (int64_t)e * (kGates / 4) + j);
-      const float gx4[4] = {g.x, g.y, g.z, g.w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        xw[(4 * j + c) * E2 + e] = gx4[c];
-        xw[(kGates + 4 * j + c) * E2 + e] = acc[c][e];
-      }
-    }
-  }
-  __syncthreads();
-  float hj[E2];
-#pragma unroll
-  for (int e = 0; e < E2; ++e) {
-    const float* pk = e < E ? pk0 : pk1;
-    float pre[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int col = g * kHid + j;
-      pre[g] = (xw[col * E2 + e] + pk[L.lstm_bih + col]) + (xw[(kGates + col) * E2 + e] + pk[L.lstm_bhh + col]);
-    }
-    const float gi = sigm(pre[0]), gf = sigm(pre[1]), gg = tanhf(pre[2]), go = sigm(pre[3]);
-    cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
-    hj[e] = go * tanhf(cj[e]);
-    a.h[(e0 + e) * kHid + j] = hj[e];
-    a.c[(e0 + e) * kHid + j] = cj[e];
-  }
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    const float* pk = hf ? pk1 : pk0;
-    const float rm = a.bn_mean ? a.bn_mean[L.bn_stat[16] + j] : 0.f;
-    const float rv = a.bn_var ? a.bn_var[L.bn_stat[16] + j] : 1.f;
-    const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
-    const float sh = fmaf(-rm, sc, pk[L.bn_b[16] + j]);
-#pragma unroll
-    for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
-  }
-  __syncthreads();  // gates read (xw) and BN(h') written before the logits reuse xw
-  if (j < A * E2) {
-    const int ai = j / E2, e = j - ai * E2;
-    const float* pk = e < E ? pk0 : pk1;
-    const float* w = pk + L.head_w + ai * kHid;
-    float s = 0.f;
-    for (int k = 0; k < kHid; ++k) s = fmaf(w[k], hs[k * E2 + e], s);
-    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
-  }
-  __syncthreads();
-  if (j < E2) core_finish<E, kReplay>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
-}
 // ---- MFMA form of the fp16 pair core step (ctx core_mfma, the default) ---------------------------------------
 // The pair's lanes share theta and sigma-eps E, so each GEMM of the step is  W_l x = theta x + s_l (E x):
 // one v_mfma_f32_16x16x32_f16 of theta's A fragment against the B fragment X (the pair's 2E envs as columns,
@@ -2402,292 +1320,6 @@ __global__ __launch_bounds__(256) void mfma_image_kernel(Layout L, const _Float1
     for (int jj = 0; jj < 8; ++jj) v[jj] = tile[(8 * (l >> 4) + jj) * TP + 16 * nt + (l & 15)];
     *reinterpret_cast<h8*>(d + (((int64_t)ks * nt_n + 16 * q + nt) * 64 + l) * 8) = v;
   }
-}
-
-// Stream NQ k-steps of 4 column tiles through a D-deep register ring: frag(q) = the images' offset (halves)
-// of step q's first tile (the next 3 follow at +512).  prime() issues the first D - 1 steps (called ahead of
-// the phase before the stream, so the loads overlap it); run(mma) consumes step q with mma(q, th, ep).
-template <int NQ, class Frag>
-struct MfmaRing {
-  static constexpr int D = 4;
-  static_assert(NQ % D == 0, "ring depth divides the step count");
-  const _Float16* thm;
-  const _Float16* epm;
-  Frag frag;
-  h8 rt[D][4], re[D][4];
-  __device__ __forceinline__ void issue(int q, h8 (&t)[4], h8 (&e)[4]) {
-    const int64_t o = frag(q);
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) {
-#if defined(FDR_HPM_PROBE) && FDR_HPM_PROBE == 1  // diagnostics build: no theta loads (the stream alone from HBM)
-      e[jt] = ld_stream(reinterpret_cast<const h8*>(epm + o + 512 * jt));
-      t[jt] = e[jt];
-#elif defined(FDR_HPM_PROBE) && FDR_HPM_PROBE == 2  // diagnostics build: both operands from theta's image (L2 only)
-      t[jt] = *reinterpret_cast<const h8*>(thm + o + 512 * jt);
-      e[jt] = ld_stream(reinterpret_cast<const h8*>(thm + o + 512 * (jt ^ 1)));
-#else
-      t[jt] = *reinterpret_cast<const h8*>(thm + o + 512 * jt);
-      e[jt] = ld_stream(reinterpret_cast<const h8*>(epm + o + 512 * jt));
-#endif
-    }
-  }
-  __device__ __forceinline__ void prime() {
-#pragma unroll
-    for (int u = 0; u < D - 1; ++u) issue(u, rt[u], re[u]);
-  }
-  template <class Mma>
-  __device__ __forceinline__ void run(Mma&& mma) {
-#pragma unroll 1
-    for (int q0 = 0; q0 < NQ; q0 += D) {
-#pragma unroll
-      for (int u = 0; u < D; ++u) {
-        const int q = q0 + u;
-        issue(min(q + D - 1, NQ - 1), rt[(u + D - 1) % D], re[(u + D - 1) % D]);  // past the end: a re-read
-        __builtin_amdgcn_sched_barrier(0);  // keep the ring: the scheduler would sink each load to its use
-        mma(q, rt[u], re[u]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-  }
-};
-template <int NQ, class Frag>
-__device__ __forceinline__ MfmaRing<NQ, Frag> mfma_ring(const _Float16* thm, const _Float16* epm, Frag f) {
-  return MfmaRing<NQ, Frag>{thm, epm, f};
-}
-
-// MODE kRollout: the step (fc + gates).  MODE kReplay (entropy pass, a.gx = x W_ih^T of the chunk): the W_hh
-// product only -- the gate images' k-steps 8 .. 16 (rows 256 .. 543) against B rows [0 | h | 0].
-template <int E, int MODE>
-__global__ __launch_bounds__(kCoreThreads) __attribute__((amdgpu_waves_per_eu(2))) void core_kernel_hpm(Layout L,
-                                                                                                       StepArgs a) {
-  constexpr int E2 = 2 * E;
-  constexpr bool kRep = MODE == kReplay;
-  constexpr int kKs0 = kRep ? kCoreIn / 32 : 0, kNks = kGateKS - kKs0;  // the gate k-steps streamed
-  static_assert(E2 <= 16 && (E2 & (E2 - 1)) == 0, "the pair's envs are the B operand's columns (mod E2)");
-  constexpr int XP = kFeat + 16;         // f16 pitch of BN(features) rows [env][k]
-  constexpr int GP = kGateKS * 32 + 16;  // f16 pitch of the gate input rows [env][cis (257) | h (256) | 0]
-  constexpr int kXBytes = E2 * XP * 2, kGBytes = kGates * E2 * 4;
-  __shared__ __attribute__((aligned(16))) char xg[kXBytes > kGBytes ? kXBytes : kGBytes];
-  __shared__ __attribute__((aligned(16))) _Float16 gh[E2 * GP];
-  __shared__ float hs[kHid * E2];
-  __shared__ float logit[E2 * kMaxAct];
-  __shared__ float bsum[2 * kGates];               // b_ih + b_hh of the pair's two lanes
-  _Float16* xh = reinterpret_cast<_Float16*>(xg);  // fc input, dead after the fc MFMAs
-  float* gates = reinterpret_cast<float*>(xg);     // gate pre-activations [1024][E2] (over xh)
-  const int pr = blockIdx.x, j = threadIdx.x, w = j >> 6, l = j & 63;
-  const int l0 = 2 * pr;
-  const float* pk0 = a.pack + (int64_t)l0 * a.pack_stride;
-  const float* pk1 = pk0 + a.pack_stride;
-  const _Float16* epm = a.epm + (int64_t)pr * kMImg;
-  // the weight streams (issued first: their first steps load during the BN prologue)
-  auto fc_ring = mfma_ring<kFcKS>(a.thm, epm, [w, l](int q) { return ((int64_t)(q * kFcNT + 4 * w) * 64 + l) * 8; });
-  auto gate_ring = mfma_ring<4 * kNks>(a.thm + kFcImg, epm + kFcImg, [w, l](int q) {
-    const int g = q / kNks, ks = kKs0 + q - g * kNks;
-    return ((int64_t)(ks * kGateNT + 16 * w + 4 * g) * 64 + l) * 8;
-  });
-  if constexpr (kRep)
-    gate_ring.prime();
-  else
-    fc_ring.prime();
-  const int64_t e0 = (int64_t)l0 * E;
-  // replay: this thread's x W_ih^T gate inputs (unit j of the 4 gates, every env), loaded ahead of the stream
-  // (used after it: a load there is a dependent round trip per env)
-  float gxv[kRep ? E2 : 1][4];
-  if constexpr (kRep) {
-    const float* g = a.gx + ((int64_t)(a.t - a.gx_t0) * a.n_lanes * E + e0) * kGates + j;
-#pragma unroll
-    for (int e = 0; e < E2; ++e)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) gxv[e][q] = g[(int64_t)e * kGates + q * kHid];
-  }
-  // branch-free sign loads (a conditional load would end its block with a full vmcnt wait behind the ring)
-  const int8_t* sgp = a.sign ? a.sign + l0 : reinterpret_cast<const int8_t*>(pk0);
-  const int8_t sg0v = sgp[0], sg1v = sgp[1];
-  const bool neg0 = a.sign && sg0v < 0, neg1 = a.sign && sg1v < 0;
-  const bool zero0 = a.sign && sg0v == 0, zero1 = a.sign && sg1v == 0;
-  const int A = a.n_act;
-  auto pkof = [&](int e) { return e < E ? pk0 : pk1; };
-  // this lane's B column: env (l & 15) mod E2; S X flips the sign bits of the minus lane's column and zeroes a
-  // sign-0 (unperturbed) lane's: E then adds exact zeros
-  const int benv = (l & 15) & (E2 - 1);
-  const unsigned smask = (benv < E ? neg0 : neg1) ? 0x80008000u : 0u;
-  const unsigned zmask = (benv < E ? zero0 : zero1) ? 0u : ~0u;
-  auto bfrag = [&](const _Float16* rowp, int k0, h8& x, h8& sx) {
-    x = *reinterpret_cast<const h8*>(rowp + k0 + 8 * (l >> 4));
-    u32x4 u = __builtin_bit_cast(u32x4, x);
-    u = (u ^ u32x4{smask, smask, smask, smask}) & u32x4{zmask, zmask, zmask, zmask};
-    sx = __builtin_bit_cast(h8, u);
-  };
-
-  float cj[E2];
-#pragma unroll
-  for (int e = 0; e < E2; ++e) {
-    gh[e * GP + kCoreIn + j] = (_Float16)a.h[(e0 + e) * kHid + j];
-    cj[e] = a.c[(e0 + e) * kHid + j];
-  }
-  for (int i = j; i < E2 * (GP - kGateK); i += kCoreThreads) {
-    const int e = i / (GP - kGateK);
-    gh[e * GP + kGateK + i - e * (GP - kGateK)] = (_Float16)0.f;
-  }
-#pragma unroll
-  for (int it = 0; it < 2 * kGates / kCoreThreads; ++it) {  // b_ih + b_hh per lane of the pair
-    const int i = j + it * kCoreThreads;
-    const float* pk = i < kGates ? pk0 : pk1;
-    const int col = i & (kGates - 1);
-    bsum[i] = pk[L.lstm_bih + col] + pk[L.lstm_bhh + col];
-  }
-  if constexpr (kRep) {
-    if (j < E2) gh[j * GP + kHid] = (_Float16)0.f;  // W_ih's reward row: its product is inside a.gx
-  } else {
-  // the fc biases of this lane's 16 outputs (rows 4 (l >> 4) .. +3 of its 4 tiles; env column l & 15)
-  float4 fcb[4];
-#pragma unroll
-  for (int jt = 0; jt < 4; ++jt)
-    fcb[jt] = *reinterpret_cast<const float4*>(pkof(benv) + L.fc_b + 16 * (4 * w + jt) + 4 * (l >> 4));
-  // branch-free loads (a conditional load ends its block with a full vmcnt wait): without running statistics
-  // the loads read the pack and the values are replaced by 0 / 1
-  const bool has_m = a.bn_mean != nullptr, has_v = a.bn_var != nullptr;
-  const float* bmp = has_m ? a.bn_mean + L.bn_stat[15] : pk0;
-  const float* bvp = has_v ? a.bn_var + L.bn_stat[15] : pk0;
-  typedef _Float16 h4v __attribute__((ext_vector_type(4)));
-#pragma unroll
-  for (int it = 0; it < kFeat / (4 * kCoreThreads); ++it) {  // BN1d(2048) -> f16 rows; 4 features per thread
-    const int k = 4 * j + 4 * kCoreThreads * it;
-    float rm[4], rv[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float rmv = bmp[k + c], rvv = bvp[k + c];
-      rm[c] = has_m ? rmv : 0.f;
-      rv[c] = has_v ? rvv : 1.f;
-    }
-    float4 f[E2];
-#pragma unroll
-    for (int e = 0; e < E2; ++e) f[e] = *reinterpret_cast<const float4*>(a.feat + (e0 + e) * kFeat + k);
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      const float* pk = hf ? pk1 : pk0;
-      const float4 w4 = *reinterpret_cast<const float4*>(pk + L.bn_w[15] + k);
-      const float4 b4 = *reinterpret_cast<const float4*>(pk + L.bn_b[15] + k);
-      float sc[4], sh[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        sc[c] = w4[c] * (1.f / sqrtf(rv[c] + kBnEps));
-        sh[c] = b4[c] - rm[c] * sc[c];
-      }
-#pragma unroll
-      for (int e = hf * E; e < hf * E + E; ++e)
-        *reinterpret_cast<h4v*>(xh + e * XP + k) =
-            h4v{(_Float16)fmaf(f[e][0], sc[0], sh[0]), (_Float16)fmaf(f[e][1], sc[1], sh[1]),
-                (_Float16)fmaf(f[e][2], sc[2], sh[2]), (_Float16)fmaf(f[e][3], sc[3], sh[3])};
-    }
-  }
-  float* ci = a.ci ? a.ci + ((int64_t)a.t * a.n_lanes * E + e0) * kCoreIn : nullptr;
-  {
-    const float r = fminf(fmaxf(a.rprev[e0 + (j & (E2 - 1))], -1.f), 1.f);  // every thread loads: no branch
-    if (j < E2) {
-      gh[j * GP + kHid] = (_Float16)r;
-      if (ci) ci[j * kCoreIn + kHid] = r;
-    }
-  }
-  __syncthreads();
-  {  // fc: wave w owns column tiles 4w .. 4w+3 over the 64 k-steps
-    f32x4 acc[4];
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const _Float16* xrow = xh + benv * XP;
-    fc_ring.run(
-        [&](int q, const h8 (&tf)[4], const h8 (&ef)[4]) {
-          h8 x, sx;
-          bfrag(xrow, 32 * q, x, sx);
-#pragma unroll
-          for (int jt = 0; jt < 4; ++jt) {
-            acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(tf[jt], x, acc[jt], 0, 0, 0);
-            acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ef[jt], sx, acc[jt], 0, 0, 0);
-          }
-        });
-    gate_ring.prime();  // the gate weights' first steps load during the epilogue and the barrier
-    if ((l & 15) < E2) {  // lane: rows 4 (l >> 4) .. +3 of each tile, env column l & 15
-      const int e = l & 15;
-#pragma unroll
-      for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = 16 * (4 * w + jt) + 4 * (l >> 4) + i;
-          const float y = relu(acc[jt][i] + fcb[jt][i]);
-          gh[e * GP + n] = (_Float16)y;
-          if (ci) ci[e * kCoreIn + n] = y;
-        }
-    }
-  }
-  }  // !kRep
-  __syncthreads();  // gate input complete; xh dead (the gates region reuses it)
-  {  // gates: wave w owns column tiles 16w .. 16w+15, four at a time over the kNks k-steps
-    f32x4 acc[4];
-    const _Float16* grow = gh + benv * GP;
-    gate_ring.run(
-        [&](int q, const h8 (&tf)[4], const h8 (&ef)[4]) {
-          const int g = q / kNks, ks = kKs0 + q - g * kNks;
-          if (ks == kKs0)
-#pragma unroll
-            for (int jt = 0; jt < 4; ++jt) acc[jt] = f32x4{0.f, 0.f, 0.f, 0.f};
-          h8 x, sx;
-          bfrag(grow, 32 * ks, x, sx);
-#pragma unroll
-          for (int jt = 0; jt < 4; ++jt) {
-            acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(tf[jt], x, acc[jt], 0, 0, 0);
-            acc[jt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ef[jt], sx, acc[jt], 0, 0, 0);
-          }
-          if (ks == kGateKS - 1 && (l & 15) < E2) {
-#pragma unroll
-            for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-              for (int i = 0; i < 4; ++i)
-                gates[(16 * (16 * w + 4 * g + jt) + 4 * (l >> 4) + i) * E2 + (l & 15)] = acc[jt][i];
-          }
-        });
-  }
-  __syncthreads();
-  float hj[E2];
-#pragma unroll
-  for (int e = 0; e < E2; ++e) {
-    float pre[4];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int col = g * kHid + j;
-      pre[g] = gates[col * E2 + e] + bsum[(e < E ? 0 : kGates) + col];
-      if constexpr (kRep) pre[g] += gxv[e][g];
-    }
-    // v_exp / v_rcp forms (abs error ~3e-7, inside the fp16 tolerance): the cell phase has no HBM stream
-    // under it, and the accurate expf / tanhf / IEEE division were ~1,500 instructions per thread
-    auto sg = [](float x) { return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x)); };
-    const float gi = sg(pre[0]), gf = sg(pre[1]), gg = tanh_fast(pre[2]), go = sg(pre[3]);
-    cj[e] = fmaf(gf, cj[e], gi * gg);  // explicit: the same rounding in every core form
-    hj[e] = go * tanh_fast(cj[e]);
-    a.h[(e0 + e) * kHid + j] = hj[e];
-    a.c[(e0 + e) * kHid + j] = cj[e];
-  }
-#pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    const float* pk = hf ? pk1 : pk0;
-    const float rmv = (a.bn_mean ? a.bn_mean + L.bn_stat[16] : pk0)[j];  // branch-free (see the BN1d prologue)
-    const float rvv = (a.bn_var ? a.bn_var + L.bn_stat[16] : pk0)[j];
-    const float rm = a.bn_mean ? rmv : 0.f, rv = a.bn_var ? rvv : 1.f;
-    const float sc = pk[L.bn_w[16] + j] * (1.f / sqrtf(rv + kBnEps));
-    const float sh = fmaf(-rm, sc, pk[L.bn_b[16] + j]);
-#pragma unroll
-    for (int e = 0; e < E; ++e) hs[j * E2 + hf * E + e] = fmaf(hj[hf * E + e], sc, sh);
-  }
-  __syncthreads();
-  if (j < A * E2) {  // head in f32 (A x 256, tiny), each lane's own
-    const int ai = j / E2, e = j - ai * E2;
-    const float* pk = pkof(e);
-    const float* wh = pk + L.head_w + ai * kHid;
-    float s = 0.f;
-    for (int k = 0; k < kHid; ++k) s = fmaf(wh[k], hs[k * E2 + e], s);
-    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
-  }
-  __syncthreads();
-  if (j < E2) core_finish<E, MODE>(a, logit + (j >= E ? E * kMaxAct : 0), l0 + (j >= E ? 1 : 0), j % E);
 }
 
 // ---- Two pairs per workgroup (ctx core_mfma = 2, the default) ------------------------------------------------------
@@ -3138,14 +1770,21 @@ template __global__ void replay_chunk_hpm2<1, kStrategy>(Layout, StepArgs, int, 
 // Entropy replay, input projection of one chunk in the fp16 pair form on MFMA: gx = theta X + s (E X) with the
 // gate images' k-steps 0 .. 8 (rows 0 .. 287 = W_ih^T's 257 rows; X is zero beyond k = 256) -- the per-lane
 // f32 GEMM (lstm_xproj_kernel<true>) ran at the f32 MFMA rate and re-read each lane's W_ih per row block.
-// Grid (n_pairs, kGateNT / 4): a workgroup holds its 4 column tiles' theta / E fragments in LDS (72 KiB) and
-// its 4 waves take the pair's row tiles (rows = (t, env of the pair), B columns; X rounded to f16).
+// A workgroup = (pair, group of 4 column tiles): it holds the group's theta / E fragments in LDS (72 KiB) and its 4
+// waves take the pair's row tiles (rows = (t, env of the pair), B columns; X rounded to f16).  XCD-aware grid
+// (xproj_grid): the kGateNT / 4 = 16 workgroups of a pair are dispatched together onto ONE XCD, so the pair's chunk of
+// core inputs (64 steps x 2E envs x 257 f32, 0.5 MB) is fetched from HBM once and re-read from that XCD's L2 by the
+// other 15 (with the pair as the fast grid index the 16 readers were ~n_pairs workgroups apart: 16 HBM reads).
+constexpr int kXprojGroups = kGateNT / 4;
 template <int E>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void xproj_pair_kernel(Layout L, StepArgs a, int t0,
                                                                                             int tc, float* __restrict__ gx) {
   constexpr int E2 = 2 * E, KS = (kCoreIn + 31) / 32;
   __shared__ h8 af[2][KS][4][64];
-  const int pr = blockIdx.x, nt0 = 4 * blockIdx.y, tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+  const int pr = (slot / kXprojGroups) * 8 + xcd, nt0 = 4 * (slot % kXprojGroups);
+  if (2 * pr >= a.n_lanes) return;  // (the grid rounds the pairs up to a multiple of 8)
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   const _Float16* src[2] = {a.thm + kFcImg, a.epm + (int64_t)pr * kMImg + kFcImg};
   for (int i = tid; i < 2 * KS * 4 * 64; i += 256) {
     const int sidx = i / (KS * 256), rem = i - sidx * (KS * 256), ks = rem >> 8, jt = (rem >> 6) & 3, ll = rem & 63;
@@ -3196,21 +1835,6 @@ template __global__ void xproj_pair_kernel<1>(Layout, StepArgs, int, int, float*
 template __global__ void xproj_pair_kernel<2>(Layout, StepArgs, int, int, float*);
 template __global__ void xproj_pair_kernel<4>(Layout, StepArgs, int, int, float*);
 
-template __global__ void core_kernel_hpm<1, kRollout>(Layout, StepArgs);
-template __global__ void core_kernel_hpm<2, kRollout>(Layout, StepArgs);
-template __global__ void core_kernel_hpm<4, kRollout>(Layout, StepArgs);
-template __global__ void core_kernel_hpm<1, kReplay>(Layout, StepArgs);
-template __global__ void core_kernel_hpm<2, kReplay>(Layout, StepArgs);
-template __global__ void core_kernel_hpm<4, kReplay>(Layout, StepArgs);
-
-template __global__ void core_kernel_hpr<1>(Layout, StepArgs);
-template __global__ void core_kernel_hpr<2>(Layout, StepArgs);
-template __global__ void core_kernel_hpr<4>(Layout, StepArgs);
-
-template __global__ void core_kernel_hp<1>(Layout, StepArgs);
-template __global__ void core_kernel_hp<2>(Layout, StepArgs);
-template __global__ void core_kernel_hp<4>(Layout, StepArgs);
-
 template __global__ void core_kernel_h<1, kRollout>(Layout, StepArgs);
 template __global__ void core_kernel_h<1, kReplay>(Layout, StepArgs);
 template __global__ void core_kernel_h<1, kForward>(Layout, StepArgs);
@@ -3222,7 +1846,6 @@ template __global__ void core_kernel_h<4, kReplay>(Layout, StepArgs);
 template __global__ void core_kernel_h<8, kRollout>(Layout, StepArgs);
 template __global__ void core_kernel_h<8, kReplay>(Layout, StepArgs);
 
-int conv_h_lds_bytes() { return kHLdsBytes; }
 
 }  // namespace impala
 }  // namespace fdr

@@ -21,10 +21,6 @@ struct Context {
   int cus = 0;          // compute units of `device` (0: query the current device)
   int rollout_impl = 2; // FDR_ROLLOUT_AUTO
   int replay_gemm = 1;
-  int core_mfma = 2;    // fp16 pair-form core step: 2 MFMA, two pairs per workgroup (core_kernel_hpm2); 1 MFMA, one
-                        // pair (core_kernel_hpm); 0 the VALU form (core_kernel_hp)
-  int conv_h2 = 2;      // fp16 conv stack, two workgroups per CU: 2 = conv_kernel_h2<512> (default), 1 = <256>; 0: conv_kernel_h;
-                        // 3 = conv_kernel_h2<512> through the stage-3 entry + conv_s3_kernel (4 envs per workgroup)
   uint64_t* debug_clock = nullptr;
   impala::Profile* prof = nullptr;  // owned, created on first enable
 };

@@ -30,7 +30,7 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_impala_env_frames", "fdr_fd_grad_fused_workspace_bytes", "fdr_fd_grad_fused_counter_bytes",
            "fdr_fd_grad_fused_out_len",
            "fdr_fd_grad_fused", "fdr_rank_weights", "fdr_dsgd_step_ex", "fdr_fd_step",
-           "fdr_ctx_set_rollout_impl", "fdr_ctx_set_replay_gemm", "fdr_ctx_set_core_mfma", "fdr_ctx_set_conv_h2", "fdr_ctx_impala_profile",
+           "fdr_ctx_set_rollout_impl", "fdr_ctx_set_replay_gemm", "fdr_ctx_impala_profile",
            "fdr_ctx_impala_profile_read", "fdr_ctx_impala_debug_clock", "fdr_noise_draw_indices",
            "fdr_impala_bn_refresh_workspace_bytes", "fdr_impala_bn_refresh", "fdr_atari_strategies_workspace_bytes",
            "fdr_atari_strategies")
@@ -118,8 +118,6 @@ def _load():
         "fdr_rollout_set_impl": (ctypes.c_int, [I32]),
         "fdr_ctx_set_rollout_impl": (ctypes.c_int, [P, I32]),
         "fdr_ctx_set_replay_gemm": (ctypes.c_int, [P, I32]),
-        "fdr_ctx_set_core_mfma": (ctypes.c_int, [P, I32]),
-        "fdr_ctx_set_conv_h2": (ctypes.c_int, [P, I32]),
         "fdr_ctx_impala_profile": (ctypes.c_int, [P, I32]),
         "fdr_ctx_impala_profile_read": (ctypes.c_int, [P, P]),
         "fdr_ctx_impala_debug_clock": (ctypes.c_int, [P, P]),

@@ -54,18 +54,9 @@ class Context(object):
         check(lib.fdr_ctx_set_rollout_impl(self.handle, code), "fdr_ctx_set_rollout_impl")
 
     def set_replay_gemm(self, on):
+        """Diagnostics (include/fdr_diag.h): the entropy replay's input projection as a GEMM per chunk (default) or
+        streamed per step -- bit-identical gates."""
         check(lib.fdr_ctx_set_replay_gemm(self.handle, 1 if on else 0), "fdr_ctx_set_replay_gemm")
-
-    def set_core_mfma(self, on):
-        """fp16 pair-form Impala core step: 2 / True (default) MFMA with two pairs per workgroup, 1 MFMA with one pair
-        per workgroup (bit-identical), 0 / False the VALU form."""
-        mode = 2 if on is True else (0 if on is False else int(on))
-        check(lib.fdr_ctx_set_core_mfma(self.handle, mode), "fdr_ctx_set_core_mfma")
-
-    def set_conv_h2(self, mode):
-        """fp16 Impala conv stack: 1 / True = conv_kernel_h2<256> (two 4-wave workgroups per CU), 2 =
-        conv_kernel_h2<512> (two 8-wave workgroups per CU), 0 / False = conv_kernel_h (one per CU)."""
-        check(lib.fdr_ctx_set_conv_h2(self.handle, int(mode)), "fdr_ctx_set_conv_h2")
 
     def impala_profile(self, enable):
         check(lib.fdr_ctx_impala_profile(self.handle, 1 if enable else 0), "fdr_ctx_impala_profile")

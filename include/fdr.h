@@ -90,13 +90,13 @@ typedef struct fdr_lanes_desc {
 } fdr_lanes_desc;
 
 /* ---- context / errors ----------------------------------------------------------------
- * An fdr_ctx is the engine state of ONE device: the rollout kernel selection (fdr_ctx_set_rollout_impl),
- * the Impala phase profiler, the entropy-replay GEMM switch and the debug clock buffer.  Every compute call
- * takes a ctx; the caller's current HIP device must be the ctx's device (FDR_ERR_INVALID otherwise).  A ctx
- * is not shared across threads without external locking; two contexts -- on one device or on two -- are
- * independent.  ctx = NULL selects the process-wide default context (device-agnostic; FDR_ROLLOUT in the
- * environment sets its initial rollout selection, and new contexts copy it). */
-const char* fdr_version(void); /* "fdr 0.4 gfx950" (0.4: fdr_env_desc.done_threshold / done_dim) */
+ * An fdr_ctx is the engine state of ONE device: the rollout kernel selection (fdr_ctx_set_rollout_impl) and the
+ * diagnostics state of include/fdr_diag.h.  Every compute call takes a ctx; the caller's current HIP device must be
+ * the ctx's device (FDR_ERR_INVALID otherwise).  A ctx is not shared across threads without external locking; two
+ * contexts -- on one device or on two -- are independent.  ctx = NULL selects the process-wide default context
+ * (device-agnostic; FDR_ROLLOUT in the environment sets its initial rollout selection, and new contexts copy it). */
+const char* fdr_version(void); /* "fdr 0.5 gfx950" (0.5: fdr_impala_bn_refresh, fdr_atari_strategies; 0.4:
+                                  fdr_env_desc.done_threshold / done_dim) */
 const char* fdr_last_error(void);
 typedef struct fdr_ctx fdr_ctx;
 int fdr_ctx_create(int device, fdr_ctx** out);
@@ -104,23 +104,6 @@ int fdr_ctx_destroy(fdr_ctx* ctx);
 int fdr_ctx_device(const fdr_ctx* ctx);
 /* per-context settings (ctx = NULL: the default context) */
 int fdr_ctx_set_rollout_impl(fdr_ctx* ctx, int32_t impl);  /* FDR_ROLLOUT_* below */
-int fdr_ctx_set_replay_gemm(fdr_ctx* ctx, int32_t on);     /* see fdr_impala_set_replay_gemm */
-/* fp16 pair-form Impala core step (fdr_impala_desc.fp16 && .pairs): 2 (default) = fc / LSTM GEMMs on
-   v_mfma_f32_16x16x32_f16 as theta X + E (S X) over MFMA-fragment images of theta and each pair's sigma-eps
-   (activations rounded to f16), two pairs per workgroup (theta's fragments read once for both; needs n_lanes % 4 == 0,
-   else 1); 1 = the same, one pair per workgroup (bit-identical results); 0 = the VALU form (w = f16(theta) +
-   s f16(sigma eps) formed per element).  Default context: FDR_CORE_MFMA (0 / 1 / 2) or 2 */
-int fdr_ctx_set_core_mfma(fdr_ctx* ctx, int32_t on);
-/* fp16 Impala conv stack (rollout, forward, strategies), identical features in every mode:
-   2 (default) = conv_kernel_h2<512>: 8 waves, 80 KiB LDS, 128 VGPRs, two workgroups per CU;
-   1 = conv_kernel_h2<256>: 4 waves, two workgroups per CU;  0 = conv_kernel_h: 8 waves, 145 KiB LDS, one per CU;
-   3 = conv_kernel_h2<512> through the stage-3 entry, then the stage-3 residual blocks of four envs per workgroup
-   (conv_s3_kernel; features bit-identical to 2).
-   Default context: FDR_CONV_H2 (0 / 1 / 2 / 3) or 2 */
-int fdr_ctx_set_conv_h2(fdr_ctx* ctx, int32_t on);
-int fdr_ctx_impala_profile(fdr_ctx* ctx, int32_t enable);  /* see fdr_impala_profile */
-int fdr_ctx_impala_profile_read(fdr_ctx* ctx, double* ms);
-int fdr_ctx_impala_debug_clock(fdr_ctx* ctx, uint64_t* buf);
 
 /* ---- perturbation batch (worker/worker.py:26-30) ------------------------------------
  * out[l, p] = fl32(theta[p] + sign_l * fl32(fl32(sigma) * table[idx_l + p]))  (no FMA)   */
@@ -478,22 +461,6 @@ int fdr_impala_bn_refresh(fdr_ctx* ctx, const fdr_impala_desc* desc, const float
  * taken at those steps (NULL -> 0) -- reward [n] f32 (nullable) that each step returns. */
 int fdr_impala_env_frames(uint64_t env_seed, int32_t n_act, int64_t env_id, int32_t t0, int32_t n,
                           const int32_t* actions, float* frames, float* reward, fdr_stream stream);
-
-/* Opt-in phase timing of fdr_impala_rollout (these four act on the default context; fdr_ctx_* above on one
- * context; not thread-safe): when enabled, HIP
- * events are recorded between the step-loop launches; fdr_impala_profile_read waits for the last
- * profiled rollout and returns HOST ms[3] = summed conv-stack / core (fc+LSTM+head) / entropy-replay
- * kernel time.  Used by bench.py for the live roofline figure. */
-int fdr_impala_profile(int32_t enable);
-int fdr_impala_profile_read(double* ms);
-/* Diagnostics: subsequent fdr_impala_rollout launches write s_memtime clocks of conv workgroup 0 at
- * its phase boundaries into the DEVICE buffer buf (u64[128]: stage / block / entry-band boundaries at
- * 0..63, diagnostics builds also 64..127; overwritten each step); NULL = off. */
-int fdr_impala_debug_clock(uint64_t* buf);
-/* Entropy replay of fdr_impala_rollout (process-wide, default on): 1 = the x W_ih^T half of the
- * replayed LSTM gates is one MFMA GEMM per lane over 64-step chunks (bit-identical gates; the replay
- * streams W_hh only), 0 = every replay step streams [W_ih | W_hh] (the step kernel's form). */
-int fdr_impala_set_replay_gemm(int32_t on);
 
 #ifdef __cplusplus
 }

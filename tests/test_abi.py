@@ -1,4 +1,5 @@
-"""CPU checks of the C-ABI boundary: libfdr.so loads and exports every symbol include/fdr.h declares."""
+"""CPU checks of the C-ABI boundary: libfdr.so loads and exports every symbol include/fdr.h (the drop-in boundary)
+and include/fdr_diag.h (diagnostics outside it) declare."""
 import ctypes
 import os
 import re
@@ -8,12 +9,26 @@ import pytest
 from conftest import REPO
 
 HEADER = os.path.join(REPO, "include", "fdr.h")
+DIAG = os.path.join(REPO, "include", "fdr_diag.h")
 
 
-def declared_functions():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(fdr_[a-z0-9_]+)\s*\(", src)))
+def declared_functions(headers=(HEADER, DIAG)):
+    out = set()
+    for h in headers:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        out |= set(re.findall(r"\b(fdr_[a-z0-9_]+)\s*\(", src))
+    return sorted(out)
+
+
+def test_boundary_header_carries_no_diagnostics():
+    """the A/B setters of the pruned kernel forms are gone, and the measurement hooks (phase
+    profile, debug clocks, replay switch) live in fdr_diag.h, outside the drop-in boundary."""
+    names = declared_functions((HEADER,))
+    for gone in ("fdr_ctx_set_core_mfma", "fdr_ctx_set_conv_h2"):
+        assert gone not in declared_functions()
+    for diag in ("fdr_impala_debug_clock", "fdr_ctx_impala_debug_clock", "fdr_impala_profile", "fdr_ctx_set_replay_gemm",
+                 "fdr_impala_set_replay_gemm"):
+        assert diag not in names and diag in declared_functions((DIAG,))
 
 
 def test_header_declares_the_boundary():
@@ -37,7 +52,7 @@ def test_version_and_workspace_queries():
     assert _lib.lib.fdr_fd_grad_workspace_bytes(2048, 6092) >= 6092 * 8
     assert _lib.lib.fdr_dsgd_workspace_bytes(6092) > 0
     # the MOMENTS output length is queryable and checked (fdr 0.3; it was 2P + 3 before)
-    assert _lib.version().startswith("fdr 0.4")   # 0.4: fdr_env_desc.done_threshold / done_dim
+    assert _lib.version().startswith("fdr 0.5")   # 0.5: impala bn refresh, atari strategies; 0.4: done_threshold
     assert _lib.lib.fdr_fd_grad_fused_out_len(_lib.FDR_WEIGHT_ZSCORE, 6092, 4096) == 6092
     assert _lib.lib.fdr_fd_grad_fused_out_len(_lib.FDR_WEIGHT_MOMENTS, 6092, 4096) == 2 * 6092 + 1 + 4096
     assert _lib.lib.fdr_fd_grad_fused_out_len(_lib.FDR_WEIGHT_MOMENTS, 6092, 0) == -1

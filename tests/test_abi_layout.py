@@ -23,7 +23,7 @@ CTYPES_OF = {"fdr_policy_desc": "PolicyDesc", "fdr_env_desc": "EnvDesc", "fdr_la
 
 
 def _header_text():
-    src = open(HEADER).read()
+    src = open(HEADER).read() + "\n" + open(os.path.join(os.path.dirname(HEADER), "fdr_diag.h")).read()
     src = re.sub(r"/\*.*?\*/", " ", src, flags=re.S)
     return "\n".join(l for l in src.splitlines() if not l.lstrip().startswith("#"))
 

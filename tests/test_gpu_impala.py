@@ -326,9 +326,10 @@ def test_fp16_multistep_drift_bound_vs_f32_oracle(engine, table):
 
 def test_fp16_pair_core_matches_per_lane_core(engine, table):
     """fdr_impala_desc.pairs (config 5's antithetic pairs): the core step computes W_l x = theta x + s_l (E x) on MFMA
-    from theta's and the pair's sigma-eps fragment images (default), or forms w = f16(theta) + s f16(sigma eps) per
-    element on the VALU (core_mfma off), instead of streaming each lane's f16(theta + s sigma eps).  Step 0 sees identical conv features in both forms: probabilities within the fp16
-    tolerance of the per-lane form and of the f32 path; norms identical; whole episodes finite."""
+    from theta's and the pairs' sigma-eps fragment images (core_kernel_hpm2) instead of streaming each lane's
+    f16(theta + s sigma eps).  Step 0 sees identical conv features in both forms: probabilities within the fp16
+    tolerance of the per-lane form and of the f32 path; norms identical; whole episodes finite; the replayed
+    entropies within the fp16 tolerance of f32."""
     A, E, T = 4, 4, 5
     theta = _theta(A)
     idx = np.repeat(np.array([77, 2_000_000, 3_000_000, 4_500_000], np.int64), 2)
@@ -336,58 +337,63 @@ def test_fp16_pair_core_matches_per_lane_core(engine, table):
     dev = "cuda"
     lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
                               torch.tensor(idx, device=dev), torch.tensor(sign, device=dev), 0.02)
-    valu = engine.Context()   # the VALU pair form (core_kernel_hp); the default context runs the MFMA form
-    valu.set_core_mfma(False)
     outs = {}
-    for name, fp16, pairs, ctx in (("lane", True, False, None), ("pair", True, True, None),
-                                   ("pair_valu", True, True, valu), ("f32", False, False, None)):
+    for name, fp16, pairs in (("lane", True, False), ("pair", True, True), ("f32", False, False)):
         outs[name] = engine.impala_rollout(engine.ImpalaSpec(A, E, T, env_seed=5, fp16=fp16, pairs=pairs), lanes,
-                                           len(idx), 11, record=True, ctx=ctx)
+                                           len(idx), 11, record=True)
     torch.cuda.synchronize()
-    for form in ("pair", "pair_valu"):
-        p_pair = outs[form].probs.cpu().numpy()[:, 0]
-        np.testing.assert_allclose(p_pair, outs["lane"].probs.cpu().numpy()[:, 0], rtol=F16_RTOL / 4)
-        np.testing.assert_allclose(p_pair, outs["f32"].probs.cpu().numpy()[:, 0], rtol=F16_RTOL)
-        np.testing.assert_array_equal(outs[form].norm2.cpu().numpy(), outs["lane"].norm2.cpu().numpy())
-        for t in (outs[form].reward, outs[form].entropy):
-            assert np.all(np.isfinite(t.cpu().numpy()))
-    # the entropy replay in both pair forms (MFMA: core_kernel_hpm<kReplay>; VALU: core_kernel_hpr)
-    np.testing.assert_allclose(outs["pair"].entropy.cpu().numpy(), outs["pair_valu"].entropy.cpu().numpy(),
-                               rtol=F16_RTOL)
+    p_pair = outs["pair"].probs.cpu().numpy()[:, 0]
+    np.testing.assert_allclose(p_pair, outs["lane"].probs.cpu().numpy()[:, 0], rtol=F16_RTOL / 4)
+    np.testing.assert_allclose(p_pair, outs["f32"].probs.cpu().numpy()[:, 0], rtol=F16_RTOL)
+    np.testing.assert_array_equal(outs["pair"].norm2.cpu().numpy(), outs["lane"].norm2.cpu().numpy())
+    for t in (outs["pair"].reward, outs["pair"].entropy):
+        assert np.all(np.isfinite(t.cpu().numpy()))
     np.testing.assert_allclose(outs["pair"].entropy.cpu().numpy(), outs["f32"].entropy.cpu().numpy(), rtol=F16_RTOL)
 
 
 @pytest.mark.parametrize("E,n_pairs", [(4, 4), (4, 3), (1, 6), (2, 2)])
-def test_fp16_two_pairs_per_workgroup_bit_identical(engine, table, E, n_pairs):
-    """core_mfma 2 (core_kernel_hpm2, the default: two pairs per 8-wave workgroup, theta's fragments read once for
-    both, three MFMAs per tile and k-step) against core_mfma 1 (core_kernel_hpm, one pair per workgroup): a masked
-    B column adds exact zeros, so whole recorded episodes with the entropy replay are BITWISE equal -- actions,
-    probabilities, returns, entropies, norms.  3 pairs (6 lanes, n_lanes % 4 == 2) take the one-pair kernel."""
-    A, T = 5, 70
+def test_fp16_pair_form_episodes_vs_f32_oracle(engine, table, E, n_pairs):
+    """VERDICT r5 item 4 (the HIP-vs-HIP bitwise tests re-pointed at the oracle): the fp16 pair form (core_kernel_hpm2:
+    two pairs per 8-wave workgroup, three MFMAs per tile and k-step; the replay as replay_chunk_hpm2 after
+    xproj_pair_kernel) over whole recorded episodes with the entropy replay, T = 70 = two replay chunks, against the f32
+    oracle along the kernel's own actions: probabilities and replayed entropies within the fp16 tolerance, returns
+    exact up to the jiggle, sampled actions the reference's outside the rounding margin.  3 pairs (6 lanes, n_lanes %
+    4 == 2) have no two-pair workgroup: they run the per-lane form, bitwise a pairs = False launch."""
+    A, T, seed = 5, 70, 11
     theta = _theta(A)
-    offs = np.array([77, 2_000_000, 3_000_000, 4_500_000, 1_111_111, 999], np.int64)[:n_pairs]
+    offs = np.array([77, 2_000_000, 3_000_000, 1_500_000, 1_111_111, 999], np.int64)[:n_pairs]  # < 2^22 - P
     idx = np.repeat(offs, 2)
     sign = np.tile(np.array([1, -1], np.int8), n_pairs)
+    L = len(idx)
     dev = "cuda"
     lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
                               torch.tensor(idx, device=dev), torch.tensor(sign, device=dev), 0.02)
-    spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=True, pairs=True)
-    outs = []
-    for mode in (1, 2):
-        ctx = engine.Context()
-        ctx.set_core_mfma(mode)
-        outs.append(engine.impala_rollout(spec, lanes, len(idx), 11, record=True, ctx=ctx))
+    out = engine.impala_rollout(engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=True, pairs=True), lanes, L,
+                                seed, record=True)
     torch.cuda.synchronize()
-    for f in ("actions", "probs", "reward", "entropy", "norm2"):
-        np.testing.assert_array_equal(getattr(outs[0], f).cpu().numpy(), getattr(outs[1], f).cpu().numpy(), err_msg=f)
-    assert np.all(np.isfinite(outs[1].entropy.cpu().numpy()))
+    if L % 4:
+        lane = engine.impala_rollout(engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=True), lanes, L, seed,
+                                     record=True)
+        torch.cuda.synchronize()
+        for f in ("actions", "probs", "reward", "entropy", "norm2"):
+            np.testing.assert_array_equal(getattr(out, f).cpu().numpy(), getattr(lane, f).cpu().numpy(), err_msg=f)
+    acts = out.actions.cpu().numpy().reshape(L, E, T)
+    nb = oi.num_bn()
+    ref = oi.follow_lanes(theta, table, idx, sign, 0.02, A, E, T, 5, np.zeros(nb, np.float32), np.ones(nb, np.float32),
+                          acts)
+    from oracle import rng as crng
+    jig = np.stack([crng.jiggle(seed, np.uint64(l) * np.uint64(E) + np.arange(E, dtype=np.uint64)) for l in range(L)])
+    _, _, amb = _check_vs_followed_oracle(out.probs.cpu().numpy().reshape(L, E, T, A), acts,
+                                          out.reward.cpu().numpy().reshape(L, E) - jig,
+                                          out.entropy.cpu().numpy().reshape(L, E), ref, seed, range(L), E, F16_RTOL)
+    assert amb <= 0.01 * L * E * T
+    np.testing.assert_array_equal(out.norm2.cpu().numpy()[0::2], out.norm2.cpu().numpy()[1::2])
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2])
-def test_fp16_pair_core_sign_zero_lanes(engine, table, mode):
+def test_fp16_pair_core_sign_zero_lanes(engine, table):
     """fdr_impala_desc.pairs allows signs +-1 or 0 in any combination (include/fdr.h): an unperturbed (sign-0) lane
-    of a pair sees theta alone.  The MFMA forms zero its S X column (E adds exact zeros), the VALU form multiplies E
-    by 0, so a sign-0 lane's recorded episode (with the entropy replay) is BITWISE the same whatever its pair's table
+    of a pair sees theta alone.  The MFMA pair form zeroes its S X column (E adds exact zeros), so a sign-0 lane's
+    recorded episode (with the entropy replay) is BITWISE the same whatever its pair's table
     offset, and a +-1 lane's the same whatever its partner's sign.  Step 0's probabilities agree with the per-lane
     form (f16(theta') per lane) within the fp16 tolerance, and the norms are the per-lane ones (0 for sign 0)."""
     A, T, E = 5, 40, 4
@@ -401,9 +407,7 @@ def test_fp16_pair_core_sign_zero_lanes(engine, table, mode):
         lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
                                   torch.tensor(idx, device=dev), torch.tensor(signs_, device=dev), 0.02)
         spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=True, pairs=pairs)
-        ctx = engine.Context()
-        ctx.set_core_mfma(mode)
-        o = engine.impala_rollout(spec, lanes, len(idx), 11, record=True, ctx=ctx)
+        o = engine.impala_rollout(spec, lanes, len(idx), 11, record=True)
         torch.cuda.synchronize()
         return {f: getattr(o, f).cpu().numpy() for f in ("actions", "probs", "reward", "entropy", "norm2")}
 
@@ -526,12 +530,10 @@ def _check_vs_followed_oracle(out_probs, out_acts, out_ret, out_ent, ref, seed, 
     return dp, de.max(), flips
 
 
-@pytest.mark.parametrize("core_mfma", [True, False])
-def test_fp16_pair_default_path_whole_episode_vs_f32_oracle(engine, table, core_mfma):
+def test_fp16_pair_default_path_whole_episode_vs_f32_oracle(engine, table):
     """the kernels config 5 actually runs -- Worker.evaluate(antithetic) sets pairs, and the
-    default context's fp16 pair core is core_kernel_hpm (MFMA step: theta x + s (E x) on f16 fragment images)
-    with the replay's input projection on xproj_pair_kernel and core_kernel_hpm<kReplay>; core_mfma=False runs
-    the VALU pair forms (core_kernel_hp / core_kernel_hpr).  2 antithetic pairs, A = 4, E = 4, T = 130 (the
+    fp16 pair core is core_kernel_hpm2 (MFMA step: theta x + s (E x) on f16 fragment images) with the replay's
+    input projection on xproj_pair_kernel and the chunked replay_chunk_hpm2.  2 antithetic pairs, A = 4, E = 4, T = 130 (the
     replay crosses two 64-step chunk boundaries), stochastic actions; the f32 oracle follows the kernel's own
     actions (policies/impala.py:136-186, worker/agent.py:20-71): per-step probabilities within 2e-2, replayed
     entropies within 2e-2, returns exact up to the jiggle, sampled actions consistent with the reference."""
@@ -542,12 +544,8 @@ def test_fp16_pair_default_path_whole_episode_vs_f32_oracle(engine, table, core_
     dev = "cuda"
     lanes = engine.lanes_desc(torch.tensor(theta, device=dev), 0, torch.tensor(table, device=dev),
                               torch.tensor(idx, device=dev), torch.tensor(sign, device=dev), 0.02)
-    ctx = None
-    if not core_mfma:
-        ctx = engine.Context()
-        ctx.set_core_mfma(False)
     spec = engine.ImpalaSpec(A, E, T, entropy=True, env_seed=5, fp16=True, pairs=True)
-    out = engine.impala_rollout(spec, lanes, L, seed, record=True, ctx=ctx)
+    out = engine.impala_rollout(spec, lanes, L, seed, record=True)
     torch.cuda.synchronize()
     acts = out.actions.cpu().numpy().reshape(L, E, T)
     nb = oi.num_bn()
@@ -558,79 +556,51 @@ def test_fp16_pair_default_path_whole_episode_vs_f32_oracle(engine, table, core_
     dp, de, amb = _check_vs_followed_oracle(out.probs.cpu().numpy().reshape(L, E, T, A), acts,
                                             out.reward.cpu().numpy().reshape(L, E) - jig,
                                             out.entropy.cpu().numpy().reshape(L, E), ref, seed, range(L), E, F16_RTOL)
-    print("fp16 pair core (%s): max |dp| %.3g, max rel d(ent) %.3g, %d / %d explained action flips"
-          % ("mfma" if core_mfma else "valu", dp, de, amb, L * E * T))
+    print("fp16 pair core: max |dp| %.3g, max rel d(ent) %.3g, %d / %d explained action flips" % (dp, de, amb, L * E * T))
     assert amb <= 0.01 * L * E * T
 
 
-def test_conv_h2_matches_conv_h(engine, table):
-    """(Modes 0 / 1 / 2 / 3 of fdr_ctx_set_conv_h2.)  VERDICT r2 item 4: conv_kernel_h2<256> (80 KiB LDS, two workgroups per CU; banded entry convs, single-buffered
-    residual blocks, 4 waves) computes every conv output with conv_kernel_h's fragments, K order and f32 epilogues,
-    so its outputs are BITWISE equal to conv_kernel_h's: forward features / probs / LSTM state (13 envs, ragged over
-    the 8 XCD slots), a recorded fp16 pair rollout with the entropy replay, and strategies.  The default
-    conv_kernel_h2<512> (8 waves, streamed 32-channel A fragments, tap 8 as a chained K = 32 MFMA) sums in another
-    order: its outputs equal conv_kernel_h's within rounding (2e-3 relative), recorded rollout included."""
+def test_fp16_conv_stack_forward_and_strategies_vs_oracle(engine, table):
+    """VERDICT r5 item 4 (the conv-mode bitwise test re-pointed at the oracle): the fp16 conv stack (conv_kernel_h2,
+    the only conv form) in the forward API -- 13 envs, ragged over the 8 XCD slots, non-trivial BN statistics, three
+    steps of carried LSTM state -- and in fdr_impala_strategies (8 perturbed lanes in the pair form, 5 probe frames),
+    against the f32 oracle: features, LSTM state and probabilities within the fp16 tolerance."""
     A = 4
     theta_np = _theta(A)
     theta = torch.tensor(theta_np, device="cuda")
     spec = engine.ImpalaSpec(A, fp16=True)
     g = torch.Generator().manual_seed(3)
     n = 13
-    frames = (torch.rand(n, 3, 64, 64, generator=g) * 255).floor().cuda()
-    reward = torch.randn(n, generator=g).cuda()
+    frames = (torch.rand(n, 3, 64, 64, generator=g) * 255).floor()
+    reward = torch.randn(n, generator=g)
     nb = oi.num_bn()
-    rm = torch.randn(nb, generator=g).mul(0.1).cuda()
-    rv = torch.rand(nb, generator=g).add(0.5).cuda()
-    idx = np.repeat(np.array([77, 2_000_000, 3_000_000], np.int64), 2)
-    sign = np.tile(np.array([1, -1], np.int8), 3)
+    rm = torch.randn(nb, generator=g).mul(0.1)
+    rv = torch.rand(nb, generator=g).add(0.5)
+    p = oi.unflatten(theta_np, A)
+    bn = oi.split_bn(rm.numpy(), rv.numpy())
+    h = torch.zeros(n, 256, device="cuda")
+    c = torch.zeros(n, 256, device="cuda")
+    hr, cr = torch.zeros(n, oi.HID), torch.zeros(n, oi.HID)
+    for t in range(3):
+        fr = frames.roll(t, 0)
+        probs, feat = engine.impala_forward(spec, theta, fr.cuda(), h, c, reward=reward.cuda(), bn_mean=rm.cuda(),
+                                            bn_var=rv.cuda(), feat=True)
+        torch.cuda.synchronize()
+        pr, hr, cr, fe, _ = oi.forward(p, bn, fr.numpy(), reward.numpy(), hr, cr)
+        for got, want in ((feat, fe), (h, hr), (c, cr)):
+            w = want.numpy()
+            assert np.abs(got.cpu().numpy() - w).max() <= F16_RTOL * max(1.0, np.abs(w).max())
+        np.testing.assert_allclose(probs.cpu().numpy(), pr.numpy(), atol=F16_RTOL)
+    idx = np.repeat(np.array([77, 2_000_000, 3_000_000, 999], np.int64), 2)
+    sign = np.tile(np.array([1, -1], np.int8), 4)
     lanes = engine.lanes_desc(theta, 0, torch.tensor(table, device="cuda"), torch.tensor(idx, device="cuda"),
                               torch.tensor(sign, device="cuda"), 0.02)
-    rspec = engine.ImpalaSpec(A, 4, 20, entropy=True, env_seed=5, fp16=True, pairs=True)
-    res = {}
-    ctx = engine.context()
-    import os
-    env = os.environ.get("FDR_CONV_H2", "2")   # the default context's setting
-    prior = {"0": 0, "1": 1, "3": 3}.get(env, 2)
-    try:
-        for on in (0, 1, 2, 3):
-            ctx.set_conv_h2(on)
-            h = torch.zeros(n, 256, device="cuda")
-            c = torch.zeros(n, 256, device="cuda")
-            fw = []
-            for t in range(3):
-                probs, feat = engine.impala_forward(spec, theta, frames.roll(t, 0), h, c, reward=reward, bn_mean=rm,
-                                                    bn_var=rv, feat=True)
-                fw += [probs.clone(), feat.clone(), h.clone(), c.clone()]
-            ro = engine.impala_rollout(rspec, lanes, len(idx), 11, record=True, bn_mean=rm, bn_var=rv)
-            st = engine.impala_strategies(spec, lanes, len(idx), frames[:5], reward=reward[:5], bn_mean=rm, bn_var=rv)
-            torch.cuda.synchronize()
-            res[on] = [x.cpu().numpy() for x in fw] + [getattr(ro, f).cpu().numpy() for f in
-                                                       ("actions", "probs", "reward", "entropy")] + [st.cpu().numpy()]
-    finally:
-        ctx.set_conv_h2(prior)
-    assert np.abs(res[1][1]).max() > 0 and np.all(np.isfinite(res[1][1]))
-    for a, b in zip(res[0], res[1]):
-        np.testing.assert_array_equal(a, b)
-    # mode 3 (r11, VERDICT r4 item 1): conv_kernel_h2<512> through the stage-3 entry + conv_s3_kernel (four envs per
-    # workgroup; 13 forward envs, 24 rollout envs and 30 strategy envs leave dead env slots) -- the same products, K
-    # order and epilogue arithmetic as mode 2: bitwise equal, recorded rollout and strategies included
-    for i, (a, b) in enumerate(zip(res[2], res[3])):
-        np.testing.assert_array_equal(a, b, err_msg=str(i))
-    # conv_kernel_h2<512> runs the tap-8 remainder as a chained K = 32 MFMA (FDR_R32): the same products, summed in
-    # another order -- forward probabilities / features / LSTM state and strategies within rounding of conv_kernel_h
-    # (the recorded rollout's sampled actions may then differ; its parity is the oracle tests' subject)
-    nfw = 12
-    for i, (a, b) in enumerate(zip(res[0][:nfw] + res[0][-1:], res[2][:nfw] + res[2][-1:])):
-        scale = max(1.0, float(np.abs(a).max()))
-        err = float(np.abs(a - b).max()) / scale
-        assert err < 2e-3, (i, err)
-    # the <512> recorded rollout (ADVICE r3): the same sampled actions (a flip needs u * sum p within rounding of a
-    # partition boundary), so its probabilities, returns and replayed entropies agree within rounding too
-    act0, act2 = res[0][nfw], res[2][nfw]
-    assert np.mean(act0 == act2) >= 0.99, np.mean(act0 == act2)
-    if np.array_equal(act0, act2):
-        for i in (nfw + 1, nfw + 2, nfw + 3):
-            np.testing.assert_allclose(res[2][i], res[0][i], rtol=2e-3, atol=2e-3, err_msg=str(i))
+    st = engine.impala_strategies(engine.ImpalaSpec(A, fp16=True, pairs=True), lanes, len(idx), frames[:5].cuda(),
+                                  reward=reward[:5].cuda(), bn_mean=rm.cuda(), bn_var=rv.cuda())
+    torch.cuda.synchronize()
+    ref = oi.lane_strategies(theta_np, table, idx, sign, 0.02, A, frames[:5].numpy(), reward[:5].numpy(), rm.numpy(),
+                             rv.numpy())
+    np.testing.assert_allclose(st.cpu().numpy(), ref, atol=F16_RTOL)
 
 
 @pytest.mark.parametrize("fp16,pairs", [(False, False), (False, True), (True, False), (True, True)])

@@ -38,7 +38,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lanes", type=int, default=1024)
     ap.add_argument("--envs", type=int, default=4)
-    ap.add_argument("--mode", type=int, default=1, help="1: conv_kernel_h2<256>, 2: conv_kernel_h2<512>, 3: <512> + conv_s3_kernel")
     args = ap.parse_args()
     A = 4
     P = engine.impala_num_params(A)
@@ -50,32 +49,16 @@ def main():
     lanes = engine.lanes_desc(theta, 0, table, idx, sign, 0.02)
     dbg = torch.zeros(128, dtype=torch.int64).cuda()
     ctx = engine.context()
-    ctx.set_conv_h2(args.mode)
     ctx.impala_debug_clock(dbg)
     spec = engine.ImpalaSpec(A, args.envs, 2, entropy=False, fp16=True)
     engine.impala_rollout(spec, lanes, args.lanes, 1)
     torch.cuda.synchronize()
     ctx.impala_debug_clock(None)
     c = dbg.cpu().numpy().astype(np.int64)
-    n = names(h3=args.mode in (2, 3))
-    if args.mode == 3:  # conv_s3_kernel's workgroup 0 (stamps 100 .. 110), printed separately
-        s3 = {101: "s3 prologue (loads, tables, zero, W11)", 102: "s3 T0 = relu(BN(X3))"}
-        for k in range(4):
-            s3[103 + 2 * k] = "s3 conv%d fragments + barrier" % k
-            s3[104 + 2 * k] = "s3 conv%d K loop + epilogue" % k
-        t3 = c[110] - c[100]
-        print("conv_s3_kernel workgroup 0: %d clocks total" % t3)
-        for k in range(101, 111):
-            print("%-40s %9d  %5.1f%%" % (s3[k], c[k] - c[k - 1], 100.0 * (c[k] - c[k - 1]) / max(t3, 1)))
-        if c[112]:  # FDR_S3_PROBE build: the prologue's load groups, each waited for
-            for k, what in ((112, "entry -> first wait"), (113, "W11 LDS DMA"), (114, "X3 loads"), (115, "tables"),
-                            (116, "zero images")):
-                print("  probe %-30s %9d" % (what, c[k] - c[k - 1 if k > 112 else 100]))
-        for k in list(range(100, 111)) + list(range(112, 117)):
-            c[k] = 0
+    n = names(h3=True)
     order = [0] + sorted(k for k in n if c[k] != 0)  # the 4-wave kernel has one stage-3 band
     tot = c[order[-1]] - c[0]
-    print("conv_kernel_h2 (mode %d) workgroup 0: %d clocks total" % (args.mode, tot))
+    print("conv_kernel_h2 workgroup 0: %d clocks total" % tot)
     groups = {}
     for a, b in zip(order[:-1], order[1:]):
         d = int(c[b] - c[a])
