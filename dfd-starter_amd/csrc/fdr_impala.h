@@ -95,6 +95,9 @@ struct StepArgs {
   // MFMA form (fp16 pairs): theta's image and the pairs' sigma-eps images [n_lanes / 2][kMImg]
   const _Float16* thm;
   const _Float16* epm;
+  // fp16 conv: the lanes' folded BN / bias tables [lane][3][kBnTab] (scale | shift | conv bias), built once per rollout
+  // by bn_table_kernel -- constant over the episode -- or NULL (each conv workgroup folds them itself)
+  const float* bntab;
 };
 
 // phase clock of the first conv workgroup (s_memtime), for the phase breakdown in DESIGN.md
@@ -218,6 +221,8 @@ __global__ void finish_kernel(int n_lanes, int envs, int T, int entropy, int jig
                               int64_t lane_offset, const double* n2_part, int nblk, double* ret,
                               double* ent, int32_t* steps, double* norm2);
 
+// the fp16 conv stack's folded BN / bias tables of n lanes (one workgroup per lane): tab [lane][3 * kBnTab]
+__global__ void bn_table_kernel(Layout L, StepArgs a, float* tab);
 // fp16 mode kernels (fdr_impala_h.hip)
 // the conv stack: one env per 8-wave workgroup (kHThreads), 80 KiB LDS, <= 128 VGPRs -- two workgroups per CU
 template <int NTH>
@@ -246,7 +251,7 @@ __global__ void mfma_image_kernel(Layout L, const _Float16* src, int64_t src_str
 constexpr int kHThreads = 512;
 
 struct Plan {  // workspace carve-up (byte offsets)
-  int64_t pack, hpack, feat, h, c, rprev, ci, gx, n2, zeros, thpack, epack, idxe, n2x, mimg, total;
+  int64_t pack, hpack, feat, h, c, rprev, ci, gx, n2, zeros, thpack, epack, idxe, n2x, mimg, bntab, total;
   int nblk;    // prep blocks per lane
 };
 // pairs: the fp16 pair form (theta half pack, one sigma-eps half pack per pair, a zero base, pair offsets)

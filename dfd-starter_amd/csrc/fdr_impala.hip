@@ -144,6 +144,7 @@ Plan plan(const Layout& L, int n_lanes, int envs, int T, bool entropy, bool fp16
   p.idxe = take(pr ? (int64_t)(n_lanes / 2) * 8 : 0);
   p.n2x = take(pr && !fp16 ? (int64_t)(n_lanes / 2 + 1) * p.nblk * 8 : 0);  // the f32 pack kernels' n2 partials
   p.mimg = take(pr && fp16 ? (int64_t)(n_lanes / 2 + 1) * kMImg * 2 : 0);  // theta's + the pairs' MFMA images
+  p.bntab = take(fp16 ? (int64_t)n_lanes * 3 * kBnTab * 4 : 0);       // the conv stack's folded BN / bias tables
   p.total = o;
   return p;
 }
@@ -1558,6 +1559,11 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
       a.ep_stride = L.pack;
     }
     a.sign = c.lanes.sign;
+  }
+  if (c.fp16) {  // the lanes' BN / bias tables, folded once per rollout (r12: conv launch -1.4 %, same box)
+    float* tab = reinterpret_cast<float*>(w + p.bntab);
+    hipLaunchKernelGGL(bn_table_kernel, dim3(c.n_lanes), dim3(256), 0, stream, L, a, tab);
+    a.bntab = tab;
   }
   const int64_t ne = (int64_t)c.n_lanes * c.envs;
   hipLaunchKernelGGL(init_kernel, dim3((unsigned)((ne * kHid + 255) / 256)), dim3(256), 0, stream, ne, a.h, a.c,

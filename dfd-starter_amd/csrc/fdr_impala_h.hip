@@ -894,88 +894,22 @@ __device__ __forceinline__ void res_blocks_h2(_Float16* T, _Float16* X, h8 (&af)
   do {                       \
   } while (0)
 #endif
-template <int NTH>
-__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))) void conv_kernel_h2(Layout L, StepArgs a) {
-  static_assert(NTH == kHThreads, "8 waves (zero_border_h's thread count; the h3 entries' band rows)");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[kH2LdsBytes];
-  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
-  const int lane = (slot / a.envs) * 8 + xcd, e = slot % a.envs;
-  if (lane >= a.n_lanes) return;
-  FDR_STAMP(a, 0);
-#ifdef FDR_WG_TIMELINE  // diagnostics build: every workgroup's start / end (s_memrealtime, 100 MHz) and HW_ID / XCC_ID
-  if (a.dbg && threadIdx.x == 0) {
-    a.dbg[256 + 4 * b] = wall_clock64();
-    a.dbg[256 + 4 * b + 2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
-    a.dbg[256 + 4 * b + 3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);
-  }
-#endif
-  // wave index in an SGPR: every wave-uniform tile / address term derived from it stays scalar (VGPR pressure)
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
-  const int64_t env = (int64_t)lane * a.envs + e;
-  const float* pk = a.pack + (int64_t)lane * a.pack_stride;
-  const _Float16* hp = a.hpack + (int64_t)lane * a.hpack_stride;
+// The conv stack after the BN / bias tables' inputs are in hand: frame band 0, the tables into LDS (store_tables), the
+// first barrier, the three stages.  Shared by both table sources of conv_kernel_h2.
+template <int NTH, class StoreTables>
+__device__ __forceinline__ void conv_body_h2(const Layout& L, const StepArgs& a, int lane, int e, int64_t env, int wave,
+                                             int ln, const _Float16* hp, unsigned char* smem, FrameBn fbn,
+                                             const h8 (&af3n)[2], WStageT<NTH>& st, StoreTables&& store_tables) {
   float* bsc = reinterpret_cast<float*>(smem);
   float* bsh = bsc + kBnTab;
   float* bcb = bsh + kBnTab;  // conv biases [15][32]
   _Float16* R = reinterpret_cast<_Float16*>(smem + 3 * kBnTab * 4);  // the tables double as row -1's guard
-
-  // BN / bias tables (conv_kernel_h's folding), two entries per thread: their inputs are loaded first, the first
-  // frame band (which folds BN2d(3) per thread from the same inputs) covers the latency, then the tables are
-  // written.  The weight block of the first residual conv is issued now and committed in the first pool phase.
-  constexpr int kTabIt = (kBnTab + NTH - 1) / NTH;
-  float rm[kTabIt], rv[kTabIt], bnw[kTabIt], bnb[kTabIt], cbv[kTabIt];
-  // Branch-free (r11): every load unconditional from an in-bounds address, the unused values selected away after.
-  // A conditional load ends its basic block with s_waitcnt vmcnt(0), and the layout offsets were read per lane from
-  // the kernel argument block -- together 4-5 serialised global round trips in this phase (r11 probe of the same
-  // table in conv_s3_kernel: 3.3-3.9 K clocks); the offsets are now scalar loads (the wave's two table rows).
-  {
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hi = (threadIdx.x >> 5) & 1;
-    const float* bmp = a.bn_mean ? a.bn_mean : pk;  // a valid address either way
-    const float* bvp = a.bn_var ? a.bn_var : pk;
-#pragma unroll
-    for (int k = 0; k < kTabIt; ++k) {
-      const int bi = threadIdx.x + k * NTH, bidx = bi >> 5, bch = bi & 31;
-      const int r0 = min((wv * 64 + k * NTH) >> 5, kConvs - 1), r1 = min(r0 + 1, kConvs - 1);  // wave-uniform rows
-      auto pick = [&](const int32_t* arr) { return hi ? arr[r1] : arr[r0]; };
-      const bool has_bn = bi < kBnTab && bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
-      const bool has_cb = bi < kBnTab && bch < (bidx < 5 ? 16 : 32);
-      const int so = pick(L.bn_stat) + bch;
-      const float m_ = bmp[so], v_ = bvp[so], w_ = pk[pick(L.bn_w) + bch], b_ = pk[pick(L.bn_b) + bch],
-                  c_ = pk[pick(L.conv_b) + bch];
-      rm[k] = has_bn && a.bn_mean ? m_ : 0.f;
-      rv[k] = has_bn && a.bn_var ? v_ : 1.f;
-      bnw[k] = has_bn ? w_ : 0.f;
-      bnb[k] = has_bn ? b_ : 0.f;
-      cbv[k] = has_cb ? c_ : 0.f;
-    }
-  }
-  h8 af3n[2];  // conv_band_s1's K order
-  s1_frag(hp + L.conv_h[0], af3n, ln);
-  WStageT<NTH> st;
-  st.template issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);
-  float fsc[3], fsh[3];  // BN2d(3) of the frame, per thread (table entries 0..2)
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const float m_ = (a.bn_mean ? a.bn_mean : pk)[L.bn_stat[0] + c], v_ = (a.bn_var ? a.bn_var : pk)[L.bn_stat[0] + c];
-    const float m = a.bn_mean ? m_ : 0.f, v = a.bn_var ? v_ : 1.f;
-    fsc[c] = pk[L.bn_w[0] + c] * (1.f / sqrtf(v + kBnEps));
-    fsh[c] = pk[L.bn_b[0] + c] - m * fsc[c];
-  }
-  const FrameBn fbn{fsc[0], fsc[1], fsc[2], fsh[0], fsh[1], fsh[2]};
+  (void)lane;
   auto FB3 = [&](int k) { return R + ((k & 1) ? kH3FB1 : kH3FB0); };
   frame_band_h2<NTH, kH3FR>(FB3(0), nullptr, 0, 0, a, env, e, fbn);
   if (threadIdx.x < 2)  // the frame buffers' pad pixels (conv_band_s1)
     *reinterpret_cast<h4*>(R + (threadIdx.x ? kH3FB1 : kH3FB0) + kH3FB) = h4{0, 0, 0, 0};
-#pragma unroll
-  for (int k = 0; k < kTabIt; ++k) {
-    const int bi = threadIdx.x + k * NTH, bidx = bi >> 5, bch = bi & 31;
-    if (bi >= kBnTab) break;
-    const bool has_bn = bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
-    const float sc = has_bn ? bnw[k] * (1.f / sqrtf(rv[k] + kBnEps)) : 0.f;
-    bsc[bi] = sc;
-    bsh[bi] = has_bn ? bnb[k] - rm[k] * sc : 0.f;
-    bcb[bi] = cbv[k];
-  }
+  store_tables();
   __syncthreads();
   FDR_STAMP(a, 1);
 
@@ -1089,12 +1023,134 @@ __global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))
     res_blocks_h2<NTH, 32, 8, 1, 0>(R + kH2T3, R, af, hp, L, 2, bsc, bsh, bcb, wave, ln, a.feat + env * kFeat, st,
                                R + kH2WBB, nullptr, a, 50);
   }
+}
+
+template <int NTH>
+__global__ __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(NTH / 128))) void conv_kernel_h2(Layout L, StepArgs a) {
+  static_assert(NTH == kHThreads, "8 waves (zero_border_h's thread count; the h3 entries' band rows)");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kH2LdsBytes];
+  const int b = blockIdx.x, xcd = b & 7, slot = b >> 3;
+  const int lane = (slot / a.envs) * 8 + xcd, e = slot % a.envs;
+  if (lane >= a.n_lanes) return;
+  FDR_STAMP(a, 0);
+#ifdef FDR_WG_TIMELINE  // diagnostics build: every workgroup's start / end (s_memrealtime, 100 MHz) and HW_ID / XCC_ID
+  if (a.dbg && threadIdx.x == 0) {
+    a.dbg[256 + 4 * b] = wall_clock64();
+    a.dbg[256 + 4 * b + 2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    a.dbg[256 + 4 * b + 3] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+  }
+#endif
+  // wave index in an SGPR: every wave-uniform tile / address term derived from it stays scalar (VGPR pressure)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), ln = threadIdx.x & 63;
+  const int64_t env = (int64_t)lane * a.envs + e;
+  const float* pk = a.pack + (int64_t)lane * a.pack_stride;
+  const _Float16* hp = a.hpack + (int64_t)lane * a.hpack_stride;
+  float* bsc = reinterpret_cast<float*>(smem);
+  float* bsh = bsc + kBnTab;
+  float* bcb = bsh + kBnTab;  // conv biases [15][32]
+
+  // BN / bias tables: with a.bntab (the rollout) the lane's tables were folded once per rollout by bn_table_kernel
+  // and are copied here (one 16-B load per thread, L2-resident: the lane's E envs read the same 5.6 KB); otherwise
+  // folded here, two entries per thread: their inputs are loaded first, the first frame band (which folds BN2d(3)
+  // per thread from the same inputs) covers the latency, then the tables are written.  The weight block of the
+  // first residual conv is issued now and committed in the first pool phase.
+  if (a.bntab) {
+    constexpr int kQ = 3 * kBnTab / 4;  // float4s of the three tables
+    static_assert(kQ <= NTH, "one float4 per thread");
+    const float4* src = reinterpret_cast<const float4*>(a.bntab + (int64_t)lane * 3 * kBnTab);
+    const float4 v = src[min((int)threadIdx.x, kQ - 1)];
+    const float f0 = a.bntab[(int64_t)lane * 3 * kBnTab + 0], f1 = a.bntab[(int64_t)lane * 3 * kBnTab + 1],
+                f2 = a.bntab[(int64_t)lane * 3 * kBnTab + 2];
+    const float g0 = a.bntab[(int64_t)lane * 3 * kBnTab + kBnTab], g1 = a.bntab[(int64_t)lane * 3 * kBnTab + kBnTab + 1],
+                g2 = a.bntab[(int64_t)lane * 3 * kBnTab + kBnTab + 2];
+    h8 af3n[2];
+    s1_frag(hp + L.conv_h[0], af3n, ln);
+    WStageT<NTH> st;
+    st.template issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);
+    conv_body_h2<NTH>(L, a, lane, e, env, wave, ln, hp, smem, FrameBn{f0, f1, f2, g0, g1, g2}, af3n, st, [&]() {
+      if ((int)threadIdx.x < kQ) reinterpret_cast<float4*>(bsc)[threadIdx.x] = v;
+    });
+    return;
+  }
+  constexpr int kTabIt = (kBnTab + NTH - 1) / NTH;
+  float rm[kTabIt], rv[kTabIt], bnw[kTabIt], bnb[kTabIt], cbv[kTabIt];
+  // Branch-free (r11): every load unconditional from an in-bounds address, the unused values selected away after.
+  // A conditional load ends its basic block with s_waitcnt vmcnt(0), and the layout offsets were read per lane from
+  // the kernel argument block -- together 4-5 serialised global round trips in this phase (r11 probe of the same
+  // table in conv_s3_kernel: 3.3-3.9 K clocks); the offsets are now scalar loads (the wave's two table rows).
+  {
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), hi = (threadIdx.x >> 5) & 1;
+    const float* bmp = a.bn_mean ? a.bn_mean : pk;  // a valid address either way
+    const float* bvp = a.bn_var ? a.bn_var : pk;
+#pragma unroll
+    for (int k = 0; k < kTabIt; ++k) {
+      const int bi = threadIdx.x + k * NTH, bidx = bi >> 5, bch = bi & 31;
+      const int r0 = min((wv * 64 + k * NTH) >> 5, kConvs - 1), r1 = min(r0 + 1, kConvs - 1);  // wave-uniform rows
+      auto pick = [&](const int32_t* arr) { return hi ? arr[r1] : arr[r0]; };
+      const bool has_bn = bi < kBnTab && bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
+      const bool has_cb = bi < kBnTab && bch < (bidx < 5 ? 16 : 32);
+      const int so = pick(L.bn_stat) + bch;
+      const float m_ = bmp[so], v_ = bvp[so], w_ = pk[pick(L.bn_w) + bch], b_ = pk[pick(L.bn_b) + bch],
+                  c_ = pk[pick(L.conv_b) + bch];
+      rm[k] = has_bn && a.bn_mean ? m_ : 0.f;
+      rv[k] = has_bn && a.bn_var ? v_ : 1.f;
+      bnw[k] = has_bn ? w_ : 0.f;
+      bnb[k] = has_bn ? b_ : 0.f;
+      cbv[k] = has_cb ? c_ : 0.f;
+    }
+  }
+  h8 af3n[2];  // conv_band_s1's K order
+  s1_frag(hp + L.conv_h[0], af3n, ln);
+  WStageT<NTH> st;
+  st.template issue<kBlockHalves<16, 1>>(hp + L.conv_h[1]);
+  float fsc[3], fsh[3];  // BN2d(3) of the frame, per thread (table entries 0..2)
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float m_ = (a.bn_mean ? a.bn_mean : pk)[L.bn_stat[0] + c], v_ = (a.bn_var ? a.bn_var : pk)[L.bn_stat[0] + c];
+    const float m = a.bn_mean ? m_ : 0.f, v = a.bn_var ? v_ : 1.f;
+    fsc[c] = pk[L.bn_w[0] + c] * (1.f / sqrtf(v + kBnEps));
+    fsh[c] = pk[L.bn_b[0] + c] - m * fsc[c];
+  }
+  const FrameBn fbn{fsc[0], fsc[1], fsc[2], fsh[0], fsh[1], fsh[2]};
+  conv_body_h2<NTH>(L, a, lane, e, env, wave, ln, hp, smem, fbn, af3n, st, [&]() {
+#pragma unroll
+    for (int k = 0; k < kTabIt; ++k) {
+      const int bi = threadIdx.x + k * NTH, bidx = bi >> 5, bch = bi & 31;
+      if (bi >= kBnTab) break;
+      const bool has_bn = bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
+      const float sc = has_bn ? bnw[k] * (1.f / sqrtf(rv[k] + kBnEps)) : 0.f;
+      bsc[bi] = sc;
+      bsh[bi] = has_bn ? bnb[k] - rm[k] * sc : 0.f;
+      bcb[bi] = cbv[k];
+    }
+  });
 #ifdef FDR_WG_TIMELINE
   __syncthreads();
   if (a.dbg && threadIdx.x == 0) a.dbg[256 + 4 * b + 1] = wall_clock64();
 #endif
 }
 template __global__ void conv_kernel_h2<kHThreads>(Layout, StepArgs);
+
+// The folded BN / bias tables of each lane (conv_kernel_h2's in-kernel folding, the same formulas): theta' and the
+// running statistics are constant over a rollout, so they are folded once here instead of by every conv workgroup
+// of every step.  tab [lane][scale kBnTab | shift kBnTab | conv bias kBnTab], row = conv index, 32 channels a row.
+__global__ __launch_bounds__(256) void bn_table_kernel(Layout L, StepArgs a, float* tab) {
+  const int lane = blockIdx.x;
+  const float* pk = a.pack + (int64_t)lane * a.pack_stride;
+  float* t = tab + (int64_t)lane * 3 * kBnTab;
+  for (int bi = threadIdx.x; bi < kBnTab; bi += blockDim.x) {
+    const int bidx = bi >> 5, bch = bi & 31;
+    const bool has_bn = bch < (bidx == 0 ? 3 : (bidx == 5 ? 16 : (bidx < 5 ? 16 : 32)));
+    const bool has_cb = bch < (bidx < 5 ? 16 : 32);
+    const float rm = has_bn && a.bn_mean ? a.bn_mean[L.bn_stat[bidx] + bch] : 0.f;
+    const float rv = has_bn && a.bn_var ? a.bn_var[L.bn_stat[bidx] + bch] : 1.f;
+    const float bnw = has_bn ? pk[L.bn_w[bidx] + bch] : 0.f, bnb = has_bn ? pk[L.bn_b[bidx] + bch] : 0.f;
+    const float sc = has_bn ? bnw * (1.f / sqrtf(rv + kBnEps)) : 0.f;
+    t[bi] = sc;
+    t[kBnTab + bi] = has_bn ? bnb - rm * sc : 0.f;
+    t[2 * kBnTab + bi] = has_cb ? pk[L.conv_b[bidx] + bch] : 0.f;
+  }
+}
 
 // ---- core (fc + LSTM + head) with f16 weights ------------------------------------------------------
 template <int E, int MODE>
