@@ -98,7 +98,11 @@ struct StepArgs {
   // fp16 conv: the lanes' folded BN / bias tables [lane][3][kBnTab] (scale | shift | conv bias), built once per rollout
   // by bn_table_kernel -- constant over the episode -- or NULL (each conv workgroup folds them itself)
   const float* bntab;
+  // fp16 MFMA pair rollout with the replay GEMM: the core inputs as f16 rows of kCiPitch halves (zero beyond
+  // kCoreIn) -- xproj_pair_kernel's B operand, rounded as it would round the f32 rows -- in place of ci, or NULL
+  _Float16* ci16;
 };
+constexpr int kCiPitch = (kCoreIn + 31) / 32 * 32;
 
 // phase clock of the first conv workgroup (s_memtime), for the phase breakdown in DESIGN.md
 #define FDR_STAMP(a, k)                                                      \
@@ -237,8 +241,9 @@ __global__ void core_kernel_pr(Layout L, StepArgs a);  // f32 pair form of the r
 // grid n_lanes / 4 (n_lanes % 4 == 0)
 template <int E, int MODE>
 __global__ void core_kernel_hpm2(Layout L, StepArgs a);
-// replay input projection of a chunk in the fp16 pair form on MFMA: grid xproj_grid(n_lanes) (XCD-aware, 1-D)
-template <int E>
+// replay input projection of a chunk in the fp16 pair form on MFMA: grid xproj_grid(n_lanes) (XCD-aware, 1-D);
+// H16: the core inputs from a.ci16 (the rollout), else from the f32 rows a.ci (lane strategies)
+template <int E, bool H16>
 __global__ void xproj_pair_kernel(Layout L, StepArgs a, int t0, int tc, float* gx);
 inline dim3 xproj_grid(int n_lanes) { return dim3((unsigned)(((n_lanes / 2 + 7) / 8) * 8 * (kGateNT / 4))); }
 // the entropy replay of one chunk (steps t0 .. t0 + tc - 1 on a.gx) in ONE launch: the W_hh step of the pair form

@@ -1429,7 +1429,7 @@ static int launch_steps(const Context& ctx, const Layout& L, StepArgs a, int ent
         bool pair_xproj = false;
         if constexpr (E <= 4) {
           if (h && a.epm) {  // fp16 pair form on MFMA: theta X + s (E X) from the gate images
-            hipLaunchKernelGGL((xproj_pair_kernel<E>), xproj_grid(a.n_lanes), dim3(256), 0, stream, L, a,
+            hipLaunchKernelGGL((xproj_pair_kernel<E, true>), xproj_grid(a.n_lanes), dim3(256), 0, stream, L, a,
                                t0, tc, gx);
             pair_xproj = true;
           }
@@ -1540,6 +1540,10 @@ int launch_rollout(const RolloutCall& c, void* ws, int64_t ws_bytes, hipStream_t
       a.th = th;
       a.ep = ep;
       a.ep_stride = L.hpack;
+      if (c.entropy && c.ctx->replay_gemm) {  // core inputs as f16 rows for xproj_pair_kernel<E, true> (the ci space)
+        a.ci16 = reinterpret_cast<_Float16*>(a.ci);
+        a.ci = nullptr;
+      }
       {  // MFMA-fragment images of theta's and the pairs' fc / LSTM weights
         _Float16* im = reinterpret_cast<_Float16*>(w + p.mimg);
         const unsigned nb = kFcKS + 4 * kGateKS;
@@ -1845,7 +1849,7 @@ int launch_strategies(const StrategiesCall& c, void* ws, int64_t ws_bytes, hipSt
     const dim3 grid(c.n_lanes, (tc + 63) / 64, kGates / 256);
     a.gx = nullptr;
     if (pair_form)
-      hipLaunchKernelGGL((xproj_pair_kernel<1>), xproj_grid(c.n_lanes), dim3(256), 0, stream, L, a, t0, tc,
+      hipLaunchKernelGGL((xproj_pair_kernel<1, false>), xproj_grid(c.n_lanes), dim3(256), 0, stream, L, a, t0, tc,
                          gx);
     else if (half)
       hipLaunchKernelGGL(lstm_xproj_kernel<true>, grid, dim3(256), 0, stream, L, a, t0, tc, gx);

@@ -1588,6 +1588,17 @@ __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_e
   }
   }  // !kRep
   __syncthreads();
+  if (a.ci16) {  // the gate rows' x part as f16 core inputs for the replay's x W_ih^T (zero beyond kCoreIn)
+    constexpr int kR8 = kCiPitch / 8;
+    _Float16* dst = a.ci16 + ((int64_t)a.t * a.n_lanes * E + e0) * kCiPitch;
+    for (int i = j; i < NE * kR8; i += 2 * kCoreThreads) {
+      const int e = i / kR8, k8 = 8 * (i - e * kR8);
+      h8 v = *reinterpret_cast<const h8*>(gh + e * GP + k8);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = k8 + q < kCoreIn ? v[q] : (_Float16)0.f;
+      *reinterpret_cast<h8*>(dst + e * kCiPitch + k8) = v;
+    }
+  }
   {  // gates
     f32x4 acc[2];
     const _Float16* grow = gh + benv * GP;
@@ -1832,7 +1843,7 @@ template __global__ void replay_chunk_hpm2<1, kStrategy>(Layout, StepArgs, int, 
 // core inputs (64 steps x 2E envs x 257 f32, 0.5 MB) is fetched from HBM once and re-read from that XCD's L2 by the
 // other 15 (with the pair as the fast grid index the 16 readers were ~n_pairs workgroups apart: 16 HBM reads).
 constexpr int kXprojGroups = kGateNT / 4;
-template <int E>
+template <int E, bool H16>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void xproj_pair_kernel(Layout L, StepArgs a, int t0,
                                                                                             int tc, float* __restrict__ gx) {
   constexpr int E2 = 2 * E, KS = (kCoreIn + 31) / 32;
@@ -1856,7 +1867,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void x
     const int row = rt * 16 + (l & 15);  // this lane's B column
     const bool ok = row < rows;
     const int rr = ok ? row : 0, t = rr / E2, env = rr - t * E2;
-    const float* xr = a.ci + ((int64_t)(t0 + t) * ne + e0 + env) * kCoreIn;
+    const float* xr = H16 ? nullptr : a.ci + ((int64_t)(t0 + t) * ne + e0 + env) * kCoreIn;
+    const _Float16* xr16 = H16 ? a.ci16 + ((int64_t)(t0 + t) * ne + e0 + env) * kCiPitch + 8 * (l >> 4) : nullptr;
     const unsigned smask = (env < E ? neg0 : neg1) ? 0x80008000u : 0u;
     const unsigned zmask = (env < E ? zero0 : zero1) ? 0u : ~0u;  // sign-0 lane: E X = 0
     f32x4 acc[4];
@@ -1865,11 +1877,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void x
 #pragma unroll 3
     for (int ks = 0; ks < KS; ++ks) {
       h8 x;
+      if constexpr (H16) {  // the rollout's f16 rows (zero beyond kCoreIn); a dead row reads row 0 and is dropped
+        const h8 v = *reinterpret_cast<const h8*>(xr16 + 32 * ks);
+        const unsigned okm = ok ? ~0u : 0u;
+        x = __builtin_bit_cast(h8, __builtin_bit_cast(u32x4, v) & u32x4{okm, okm, okm, okm});
+      } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int k = 32 * ks + 8 * (l >> 4) + i;
-        const float v = xr[k < kCoreIn ? k : 0];  // branch-free: the clamped load is discarded
-        x[i] = (_Float16)(ok && k < kCoreIn ? v : 0.f);
+        for (int i = 0; i < 8; ++i) {
+          const int k = 32 * ks + 8 * (l >> 4) + i;
+          const float v = xr[k < kCoreIn ? k : 0];  // branch-free: the clamped load is discarded
+          x[i] = (_Float16)(ok && k < kCoreIn ? v : 0.f);
+        }
       }
       u32x4 u = __builtin_bit_cast(u32x4, x);
       u = (u ^ u32x4{smask, smask, smask, smask}) & u32x4{zmask, zmask, zmask, zmask};
@@ -1887,9 +1905,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void x
     }
   }
 }
-template __global__ void xproj_pair_kernel<1>(Layout, StepArgs, int, int, float*);
-template __global__ void xproj_pair_kernel<2>(Layout, StepArgs, int, int, float*);
-template __global__ void xproj_pair_kernel<4>(Layout, StepArgs, int, int, float*);
+template __global__ void xproj_pair_kernel<1, false>(Layout, StepArgs, int, int, float*);
+template __global__ void xproj_pair_kernel<1, true>(Layout, StepArgs, int, int, float*);
+template __global__ void xproj_pair_kernel<2, true>(Layout, StepArgs, int, int, float*);
+template __global__ void xproj_pair_kernel<4, true>(Layout, StepArgs, int, int, float*);
 
 template __global__ void core_kernel_h<1, kRollout>(Layout, StepArgs);
 template __global__ void core_kernel_h<1, kReplay>(Layout, StepArgs);
