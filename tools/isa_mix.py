@@ -3,8 +3,8 @@
 
   python tools/isa_mix.py 'rollout_pair_kernelILi17ELi6ELb0ELi0E'   [--so path] [--dump]
 
-Finds the function whose mangled name contains the pattern, takes the largest region closed by a backward branch
-(the unrolled step loop) and counts its instructions by class: packed f32 FMA, other VALU, transcendental, DPP,
+Finds the function whose mangled name contains the pattern, takes the step loop (hot_loop: the smallest region closed
+by a backward branch that holds the most packed-FMA / MFMA / DPP-FMA work -- the unrolled step loop) and counts its instructions by class: packed f32 FMA, other VALU, transcendental, DPP,
 permlane, LDS, global, scalar, waits.  Per-step numbers: divide by the unroll (5 steps for 6 action dims).
 """
 import argparse
@@ -68,6 +68,20 @@ def classify(line):
     return "other"
 
 
+def hot_loop(insns, lines):
+    """The step loop: among regions closed by a backward branch, the one holding the most packed / MFMA / DPP compute,
+    the smallest such (regions that merely wrap out-of-line blocks -- the compiler places the prologue's conditional
+    loads after the function body and branches back -- hold the same compute plus unrelated code)."""
+    def work(a, b):
+        return sum(1 for x in insns[a:b + 1] if lines[x.addr].startswith(("v_pk_fma", "v_mfma", "v_fmac_f32_dpp")))
+    cands = []
+    for k, ins in enumerate(insns):
+        if ins.target is not None and ins.target <= ins.addr:
+            lo = next(i for i, x in enumerate(insns) if x.addr == ins.target)
+            cands.append((lo, k))
+    return max(cands, key=lambda r: (work(*r), -(r[1] - r[0])))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("pattern")
@@ -92,13 +106,7 @@ def main():
             mm = ih._INSN.match(line)
             if mm:
                 lines[int(mm.group(3), 16)] = line.split("//")[0].strip()
-    best = None
-    for k, ins in enumerate(insns):
-        if ins.target is not None and ins.target <= ins.addr:
-            lo = next(i for i, x in enumerate(insns) if x.addr == ins.target)
-            if best is None or k - lo > best[1] - best[0]:
-                best = (lo, k)
-    lo, hi = best
+    lo, hi = hot_loop(insns, lines)
     body = [lines[x.addr] for x in insns[lo:hi + 1]]
     cnt = collections.Counter(classify(b) for b in body)
     print("%s\nloop body: %d instructions (0x%x..0x%x)" % (name, len(body), insns[lo].addr, insns[hi].addr))

@@ -113,13 +113,8 @@ def main():
             mm = ih._INSN.match(line)
             if mm:
                 lines[int(mm.group(3), 16)] = line.split("//")[0].strip()
-    best = None
-    for k, ins in enumerate(insns):
-        if ins.target is not None and ins.target <= ins.addr:
-            lo = next(i for i, x in enumerate(insns) if x.addr == ins.target)
-            if best is None or k - lo > best[1] - best[0]:
-                best = (lo, k)
-    body = [lines[x.addr] for x in insns[best[0]:best[1] + 1]]
+    lo, hi = isa_mix.hot_loop(insns, lines)
+    body = [lines[x.addr] for x in insns[lo:hi + 1]]
     table = collections.Counter()
     slack = collections.Counter()
     rows = []
