@@ -25,6 +25,9 @@ int launch_env_frames(uint64_t env_seed, uint64_t env_id, int t0, int n, float* 
 int64_t strategies_workspace_bytes(int n_act, int n_lanes, int Z);
 int launch_strategies(int n_act, const LanesArgs& lanes, int n_lanes, int Z, const float* frames, const float* bn_mean,
                       const float* bn_var, float* probs, void* ws, int64_t ws_bytes, hipStream_t stream);
+int64_t vbn_workspace_bytes(int n);  // (fdr_impala_vbn.hip)
+int launch_vbn(const float* theta, int n, const float* frames, float momentum, float* bn_mean, float* bn_var, void* ws,
+               int64_t ws_bytes, hipStream_t stream);
 }  // namespace atari
 }  // namespace fdr
 
@@ -737,6 +740,20 @@ int fdr_atari_forward(fdr_ctx* ctx, const fdr_atari_desc* d, const float* theta,
   if (!theta || !frames || !probs || n < 0) return set_error(FDR_ERR_INVALID, "NULL pointer / bad n");
   return atari::launch_forward(d->n_act, theta, n, frames, d->bn_mean, d->bn_var, probs, feat, ws, ws_bytes,
                                (hipStream_t)stream);
+}
+
+int64_t fdr_atari_bn_refresh_workspace_bytes(int32_t n) { return atari::vbn_workspace_bytes(n); }
+
+int fdr_atari_bn_refresh(fdr_ctx* ctx, const fdr_atari_desc* d, const float* theta, int32_t n, const float* frames,
+                         float momentum, float* bn_mean, float* bn_var, void* ws, int64_t ws_bytes, fdr_stream stream) {
+  FDR_CTX(ctx, C);
+  if (!d) return set_error(FDR_ERR_INVALID, "atari desc is NULL");
+  const int64_t P = atari::num_params(d->n_act);
+  if (P < 0) return set_error(FDR_ERR_UNSUPPORTED, "n_act must be in 1..32");
+  if (d->n_params != P) return set_error(FDR_ERR_INVALID, "n_params does not match the AtariPolicy layout");
+  if (!theta || !frames || !bn_mean || !bn_var) return set_error(FDR_ERR_INVALID, "NULL pointer");
+  if (n < 2) return set_error(FDR_ERR_INVALID, "train-mode BatchNorm1d needs n >= 2 samples");
+  return atari::launch_vbn(theta, n, frames, momentum, bn_mean, bn_var, ws, ws_bytes, (hipStream_t)stream);
 }
 
 int64_t fdr_atari_strategies_workspace_bytes(const fdr_atari_desc* d, int32_t n_lanes, int32_t n_states) {

@@ -15,6 +15,10 @@
 //                    iff the first obs is done (impala.py:165-176); the end state is written back (:184)
 // then the head BatchNorm1d(256)'s statistics over the n hidden states.  Off the hot path (once per epoch); parity:
 // tests/test_gpu_impala_vbn.py against the reference's own compute_vbn (tests/golden/g14_impala_vbn.npz).
+//
+// AtariPolicy.compute_vbn (policies/policy.py:31-34 on atari.py:36-51) is the same statistics -> BN-fused layer chain
+// over its three BNs (atari::launch_vbn at the end of this file): conv 4->16 k8 s4, BN2d(16), ReLU, conv 16->32 k4 s2,
+// BN2d(32), ReLU, Linear 2592->256, BN1d(256) -- the head after it feeds no statistic.  Parity: G16.
 #include <cfloat>
 
 #include "fdr_impala.h"
@@ -419,4 +423,131 @@ int launch_vbn(const VbnCall& a, void* ws, int64_t ws_bytes, hipStream_t s) {
 }
 
 }  // namespace impala
+
+namespace atari {
+namespace {
+
+using impala::finalize_kernel;
+using impala::kFcRows;
+using impala::stats_kernel;
+using impala::transpose_kernel;
+
+constexpr int kA1 = 16, kA2 = 32, kO1 = 20, kO2 = 9, kAFeat = kA2 * kO2 * kO2, kAFc = 256;
+// theta offsets in the reference's parameters() order (atari.py:36-51): conv1 w [16][4][8][8], b; BN2d(16) w, b;
+// conv2 w [32][16][4][4], b; BN2d(32) w, b; fc w [256][2592], b; BN1d(256) w, b; head
+constexpr int64_t kC1w = 0, kC1b = kC1w + kA1 * 4 * 64, kBn1 = kC1b + kA1, kC2w = kBn1 + 2 * kA1,
+                  kC2b = kC2w + kA2 * kA1 * 16, kBn2 = kC2b + kA2, kFcw = kBn2 + 2 * kA2,
+                  kFcb = kFcw + (int64_t)kAFc * kAFeat, kBn3 = kFcb + kAFc;
+
+// Y[i][co][oy][ox] = b[co] + sum_{ci,ky,kx} W[co][ci][ky][kx] * act(X[i][ci][S oy + ky][S ox + kx])  (no padding);
+// act = relu(scale[ci] x + shift[ci]) (the previous layer's train-mode BN) when BNIN, else the raw input
+template <int CIN, int COUT, int K, int S, int HI, int HO, bool BNIN>
+__global__ __launch_bounds__(256) void sconv_kernel(const float* __restrict__ X, const float* __restrict__ scale,
+                                                    const float* __restrict__ shift, const float* __restrict__ W,
+                                                    const float* __restrict__ b, float* __restrict__ Y, int64_t total) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int ox = (int)(e % HO), oy = (int)((e / HO) % HO), co = (int)((e / (HO * HO)) % COUT);
+  const int64_t i = e / ((int64_t)HO * HO * COUT);
+  float acc = 0.f;
+  for (int ci = 0; ci < CIN; ++ci) {
+    const float* xp = X + ((i * CIN + ci) * HI + S * oy) * HI + S * ox;
+    const float* wp = W + ((int64_t)co * CIN + ci) * K * K;
+    const float sc = BNIN ? scale[ci] : 1.f, sh = BNIN ? shift[ci] : 0.f;
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) {
+        float v = xp[ky * HI + kx];
+        if (BNIN) v = fmaxf(fmaf(v, sc, sh), 0.f);
+        acc = fmaf(wp[ky * K + kx], v, acc);
+      }
+  }
+  Y[e] = acc + b[co];
+}
+
+// F[i][o] = fc_b[o] + sum_k fc_w[o][k] relu(BN2d(X2))[i][k]  (k = c * 81 + p: the C, H, W flatten of atari.py:47)
+__global__ __launch_bounds__(256) void afc_kernel(const float* __restrict__ X, int n, const float* __restrict__ scale,
+                                                  const float* __restrict__ shift, const float* __restrict__ WT,
+                                                  const float* __restrict__ b, float* __restrict__ F) {
+  __shared__ float xs[kFcRows][kAFeat];
+  const int i0 = blockIdx.x * kFcRows, tid = threadIdx.x;
+  for (int e = tid; e < kFcRows * kAFeat; e += 256) {
+    const int r = e / kAFeat, k = e % kAFeat, c = k / (kO2 * kO2);
+    xs[r][k] = i0 + r < n ? fmaxf(fmaf(X[(int64_t)(i0 + r) * kAFeat + k], scale[c], shift[c]), 0.f) : 0.f;
+  }
+  __syncthreads();
+  float acc[kFcRows];
+#pragma unroll
+  for (int r = 0; r < kFcRows; ++r) acc[r] = 0.f;
+  for (int k = 0; k < kAFeat; ++k) {
+    const float w = WT[(int64_t)k * kAFc + tid];
+#pragma unroll
+    for (int r = 0; r < kFcRows; ++r) acc[r] = fmaf(w, xs[r][k], acc[r]);
+  }
+  for (int r = 0; r < kFcRows && i0 + r < n; ++r) F[(int64_t)(i0 + r) * kAFc + tid] = acc[r] + b[tid];
+}
+
+struct AVbnPlan {
+  int64_t X1, X2, F, WT, part, scale, shift, total;
+};
+
+AVbnPlan avbn_plan(int n) {
+  AVbnPlan p{};
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) {
+    const int64_t at = off;
+    off += (bytes + 255) / 256 * 256;
+    return at;
+  };
+  p.X1 = take((int64_t)n * kA1 * kO1 * kO1 * 4);
+  p.X2 = take((int64_t)n * kAFeat * 4);
+  p.F = take((int64_t)n * kAFc * 4);
+  p.WT = take((int64_t)kAFeat * kAFc * 4);
+  p.part = take((int64_t)kAFc * impala::kStatBlocks * 2 * 8);
+  p.scale = take((int64_t)kAFc * 4);
+  p.shift = take((int64_t)kAFc * 4);
+  p.total = off;
+  return p;
+}
+
+}  // namespace
+
+int64_t vbn_workspace_bytes(int n) { return n < 0 ? -1 : avbn_plan(n).total; }
+
+int launch_vbn(const float* theta, int n, const float* frames, float momentum, float* bn_mean, float* bn_var, void* ws,
+               int64_t ws_bytes, hipStream_t s) {
+  const AVbnPlan pl = avbn_plan(n);
+  if (!ws || ws_bytes < pl.total) return set_error(FDR_ERR_WORKSPACE, "atari bn refresh workspace too small");
+  char* base = static_cast<char*>(ws);
+  float* X1 = reinterpret_cast<float*>(base + pl.X1);
+  float* X2 = reinterpret_cast<float*>(base + pl.X2);
+  float* F = reinterpret_cast<float*>(base + pl.F);
+  float* WT = reinterpret_cast<float*>(base + pl.WT);
+  double* part = reinterpret_cast<double*>(base + pl.part);
+  float* sc = reinterpret_cast<float*>(base + pl.scale);
+  float* sh = reinterpret_cast<float*>(base + pl.shift);
+  const float* th = theta;
+  const int nb = n < impala::kStatBlocks ? n : impala::kStatBlocks;
+  // statistics of a BN's input [n][C][HW] -> its running stats (at `at` in the flat [16 | 32 | 256]) + sc / sh
+  auto bn_stats = [&](const float* in, int C, int HW, int64_t w, int at) {
+    hipLaunchKernelGGL(stats_kernel, dim3(C, nb), dim3(256), 0, s, in, n, C, HW, 0, 1.f, part);
+    hipLaunchKernelGGL(finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, C, nb, (int64_t)n * HW, part, th + w,
+                       th + w + C, momentum, bn_mean + at, bn_var + at, sc, sh);
+  };
+  auto grid = [](int64_t total) { return dim3((unsigned)((total + 255) / 256)); };
+  const int64_t t1 = (int64_t)n * kA1 * kO1 * kO1, t2 = (int64_t)n * kAFeat;
+  hipLaunchKernelGGL((sconv_kernel<4, kA1, 8, 4, 84, kO1, false>), grid(t1), dim3(256), 0, s, frames, nullptr, nullptr,
+                     th + kC1w, th + kC1b, X1, t1);
+  bn_stats(X1, kA1, kO1 * kO1, kBn1, 0);
+  hipLaunchKernelGGL((sconv_kernel<kA1, kA2, 4, 2, kO1, kO2, true>), grid(t2), dim3(256), 0, s, X1, sc, sh, th + kC2w,
+                     th + kC2b, X2, t2);
+  bn_stats(X2, kA2, kO2 * kO2, kBn2, kA1);
+  hipLaunchKernelGGL(transpose_kernel, dim3(kAFc * kAFeat / 256), dim3(256), 0, s, th + kFcw, kAFc, kAFeat, WT);
+  hipLaunchKernelGGL(afc_kernel, dim3((n + kFcRows - 1) / kFcRows), dim3(256), 0, s, X2, n, sc, sh, WT, th + kFcb, F);
+  bn_stats(F, kAFc, 1, kBn3, kA1 + kA2);
+  return check_launch("atari bn refresh");
+}
+
+}  // namespace atari
 }  // namespace fdr

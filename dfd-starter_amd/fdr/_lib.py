@@ -33,7 +33,7 @@ EXPORTS = ("fdr_version", "fdr_last_error", "fdr_ctx_create", "fdr_ctx_destroy",
            "fdr_ctx_set_rollout_impl", "fdr_ctx_set_replay_gemm", "fdr_ctx_impala_profile",
            "fdr_ctx_impala_profile_read", "fdr_ctx_impala_debug_clock", "fdr_noise_draw_indices",
            "fdr_impala_bn_refresh_workspace_bytes", "fdr_impala_bn_refresh", "fdr_atari_strategies_workspace_bytes",
-           "fdr_atari_strategies")
+           "fdr_atari_strategies", "fdr_atari_bn_refresh_workspace_bytes", "fdr_atari_bn_refresh")
 
 
 class FDRError(RuntimeError):
@@ -115,6 +115,8 @@ def _load():
         "fdr_atari_strategies_workspace_bytes": (I64, [ctypes.POINTER(AtariDesc), I32, I32]),
         "fdr_atari_strategies": (ctypes.c_int, [P, ctypes.POINTER(AtariDesc), ctypes.POINTER(LanesDesc), I32, I32, P, P,
                                                 P, I64, P]),
+        "fdr_atari_bn_refresh_workspace_bytes": (I64, [I32]),
+        "fdr_atari_bn_refresh": (ctypes.c_int, [P, ctypes.POINTER(AtariDesc), P, I32, P, F32, P, P, P, I64, P]),
         "fdr_rollout_set_impl": (ctypes.c_int, [I32]),
         "fdr_ctx_set_rollout_impl": (ctypes.c_int, [P, I32]),
         "fdr_ctx_set_replay_gemm": (ctypes.c_int, [P, I32]),

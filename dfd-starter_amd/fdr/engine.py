@@ -698,6 +698,22 @@ def atari_forward(spec, theta, frames, bn_mean=None, bn_var=None, feat=False):
     return (probs, f) if feat else probs
 
 
+def atari_bn_refresh(spec, theta, frames, bn_mean, bn_var, momentum=0.1):
+    """AtariPolicy.compute_vbn on the device (policies/policy.py:31-34): a train-mode pass of the n frames
+    [n, 4, 84, 84] (0..255) updating the running stats bn_mean / bn_var [16 | 32 | 256] in place (fdr_atari_bn_refresh).
+    n >= 2 (torch's train-mode BatchNorm1d raises for one value per channel)."""
+    _check_dev(frames)
+    dev = frames.device
+    frames = frames.to(torch.float32).reshape(-1, 4 * 84 * 84).contiguous()
+    n = frames.shape[0]
+    if n < 2:
+        raise ValueError("Expected more than 1 value per channel when training (compute_vbn needs >= 2 obs)")
+    d = spec.desc(None, None)
+    ws = _workspace("atari_vbn", lib.fdr_atari_bn_refresh_workspace_bytes(n), dev)
+    check(lib.fdr_atari_bn_refresh(_c(dev), ctypes.byref(d), _p(theta), n, _p(frames), float(momentum), _p(bn_mean),
+                                   _p(bn_var), _p(ws), ws.numel(), _stream(dev)), "fdr_atari_bn_refresh")
+
+
 def atari_strategies(spec, lanes, n_lanes, frames, bn_mean=None, bn_var=None):
     """AtariPolicy.get_strategy of n_lanes parameter vectors (lanes descriptor) over the Z shared probe frames
     [Z, 4, 84, 84] (0..255) -> probs [n_lanes, Z, A] f32, batched (fdr_atari_strategies)."""

@@ -62,8 +62,18 @@ class AtariPolicy(Policy):
 
     @torch.no_grad()
     def compute_vbn(self, buffer):
-        """policy.py:31-34: one train-mode torch pass (device tensors) refreshes the BN statistics."""
-        self.train()
-        x = torch.as_tensor(np.asarray(buffer), dtype=torch.float32).reshape(-1, 4, 84, 84)
-        self.model(x.to(self.flat.device))
+        """policy.py:31-34 on the device (fdr_atari_bn_refresh): one train-mode pass of the buffer -- each BN
+        normalises with its batch statistics and folds them into its running stats; the policy stays in eval mode."""
+        x = torch.as_tensor(np.asarray(buffer) if not torch.is_tensor(buffer) else buffer, dtype=torch.float32)
+        x = x.reshape(-1, 4 * 84 * 84).to(self.flat.device)
+        bns = [m for m in self.model if isinstance(m, (nn.BatchNorm1d, nn.BatchNorm2d))]
+        bm, bv = self.bn_stats()
+        engine.atari_bn_refresh(self.spec, self.flat, x, bm, bv, momentum=bns[0].momentum)
+        off = 0
+        for m in bns:
+            k = m.num_features
+            m.running_mean.copy_(bm[off:off + k])
+            m.running_var.copy_(bv[off:off + k])
+            m.num_batches_tracked += 1
+            off += k
         self.eval()

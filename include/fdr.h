@@ -95,7 +95,7 @@ typedef struct fdr_lanes_desc {
  * the ctx's device (FDR_ERR_INVALID otherwise).  A ctx is not shared across threads without external locking; two
  * contexts -- on one device or on two -- are independent.  ctx = NULL selects the process-wide default context
  * (device-agnostic; FDR_ROLLOUT in the environment sets its initial rollout selection, and new contexts copy it). */
-const char* fdr_version(void); /* "fdr 0.5 gfx950" (0.5: fdr_impala_bn_refresh, fdr_atari_strategies; 0.4:
+const char* fdr_version(void); /* "fdr 0.5 gfx950" (0.5: fdr_impala_bn_refresh, fdr_atari_bn_refresh, fdr_atari_strategies; 0.4:
                                   fdr_env_desc.done_threshold / done_dim) */
 const char* fdr_last_error(void);
 typedef struct fdr_ctx fdr_ctx;
@@ -402,6 +402,17 @@ int fdr_atari_env_frames(uint64_t env_seed, int64_t env_id, int32_t t0, int32_t 
 int64_t fdr_atari_forward_workspace_bytes(int32_t n_act, int32_t n);
 int fdr_atari_forward(fdr_ctx* ctx, const fdr_atari_desc* desc, const float* theta, int32_t n, const float* frames,
                       float* probs, float* feat, void* workspace, int64_t workspace_bytes, fdr_stream stream);
+
+/* AtariPolicy.compute_vbn (policies/policy.py:31-34 on atari.py:36-51): one train-mode pass of the VBN buffer of
+ * n >= 2 frames [n, 4, 84, 84] f32 (raw 0..255).  Each of the three BatchNorms (2d(16), 2d(32), 1d(256))
+ * normalises with its batch statistics (biased variance, double accumulation) and updates its running stats in place
+ * in bn_mean / bn_var [16 | 32 | 256] (rm <- momentum * mean + (1 - momentum) * rm, rv with the unbiased variance);
+ * the head feeds no statistic.  Only n_act and n_params of desc are read.
+ * workspace: fdr_atari_bn_refresh_workspace_bytes(n) bytes (~2.9 MB + 37 KB per frame). */
+int64_t fdr_atari_bn_refresh_workspace_bytes(int32_t n);
+int fdr_atari_bn_refresh(fdr_ctx* ctx, const fdr_atari_desc* desc, const float* theta, int32_t n, const float* frames,
+                         float momentum, float* bn_mean, float* bn_var, void* workspace, int64_t workspace_bytes,
+                         fdr_stream stream);
 
 /* AtariPolicy.get_strategy (policies/atari.py:30-31) of every lane's theta'_l (lanes as for fdr_atari_rollout) over
  * Z shared probe frames [Z, 4, 84, 84] f32 (0..255): probs [n_lanes, Z, A] -- the lane novelty's strategies

@@ -2,7 +2,7 @@
 synthetic stacked-frame env.
 
 TEST INFRASTRUCTURE ONLY (see oracle/__init__.py); pinned by tests/golden/g11_atari.npz (the
-reference AtariPolicy: normc init fingerprint and eval-mode forwards).
+reference AtariPolicy: normc init fingerprint and eval-mode forwards) and g16_atari_vbn.npz (compute_vbn).
 
 Network, eval mode (atari.py:36-51), input [4, 84, 84] (no /255 scaling in the reference):
   conv 4->16 k8 s4 -> BN2d -> ReLU -> conv 16->32 k4 s2 -> BN2d -> ReLU -> flatten (C,H,W) 2592
@@ -87,6 +87,25 @@ def forward(p, bn, frames):
     f = features(p, bn, frames)
     h = F.relu(_bn(F.linear(f, p["fc.w"], p["fc.b"]), p, bn, "bn3"))
     return torch.softmax(F.linear(h, p["head.w"], p["head.b"]), dim=-1), f
+
+
+@torch.no_grad()
+def compute_vbn(p, rm, rv, frames, momentum=0.1):
+    """AtariPolicy.compute_vbn (policies/policy.py:31-34 on atari.py:36-51): one train-mode pass of the buffer -- every
+    BN normalises with its batch statistics (biased variance) and updates its running stats (unbiased variance,
+    momentum).  Returns the new (rm, rv) flat [16 | 32 | 256]; pinned by tests/golden/g16_atari_vbn.npz."""
+    rm = torch.as_tensor(np.array(rm, np.float32))
+    rv = torch.as_tensor(np.array(rv, np.float32))
+    bn = {"bn1": (rm[:16], rv[:16]), "bn2": (rm[16:48], rv[16:48]), "bn3": (rm[48:304], rv[48:304])}
+
+    def tbn(x, name):
+        return F.batch_norm(x, bn[name][0], bn[name][1], p[name + ".w"], p[name + ".b"], training=True,
+                            momentum=momentum, eps=BN_EPS)
+    x = torch.as_tensor(np.asarray(frames, np.float32)).reshape(-1, FRAME_C, FRAME_H, FRAME_W)
+    x = F.relu(tbn(F.conv2d(x, p["c1.w"], p["c1.b"], stride=4), "bn1"))
+    x = F.relu(tbn(F.conv2d(x, p["c2.w"], p["c2.b"], stride=2), "bn2"))
+    tbn(F.linear(x.reshape(x.shape[0], -1), p["fc.w"], p["fc.b"]), "bn3")
+    return rm.numpy(), rv.numpy()
 
 
 # synthetic stacked-frame env: the Impala frame env's hash (oracle/impala.py) over a 4 x 84 x 84 image

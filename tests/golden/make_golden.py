@@ -781,6 +781,44 @@ def g14_impala_vbn():
          momentum=np.array(0.1), **out)
 
 
+def g16_atari_vbn():
+    """AtariPolicy.compute_vbn (policy.py:31-34: train(); forward(buffer); eval()) over a VBN buffer of N = 12
+    stacked-frame obs, fed as a tensor (policy.py:27-28's tuple view is rejected by torch, as in G11): every
+    BatchNorm (2d(16), 2d(32), 1d(256)) normalises with its batch statistics and folds them into its running stats.
+    theta = 0.05 * RandomState(16).randn(P) (f32), running stats as G11's scales; records the running stats after
+    one call (a) and after a second call on the same buffer (a2)."""
+    from policies import AtariPolicy
+    A, N = 6, 12
+    torch.manual_seed(124)
+    pol = AtariPolicy((84, 84), A, seed=124)
+    P = pol.num_params
+    flat = (np.random.RandomState(16).randn(P) * 0.05).astype(np.float32)
+    pol.set_trainable_flat(flat)
+    rs = np.random.RandomState(116)
+    bns = [m for m in pol.model if isinstance(m, (torch.nn.BatchNorm1d, torch.nn.BatchNorm2d))]
+    nbn = sum(m.num_features for m in bns)
+    scale = np.concatenate([np.full(16, 3e1), np.full(32, 1e1), np.full(256, 1.0)]).astype(np.float32)
+    rm = (rs.randn(nbn) * scale).astype(np.float32)
+    rv = ((1.0 + rs.rand(nbn)) * scale * scale).astype(np.float32)
+    frames = rs.randint(0, 256, size=(N, 4, 84, 84)).astype(np.uint8)
+    off = 0
+    with torch.no_grad():
+        for m in bns:
+            n = m.num_features
+            m.running_mean.copy_(torch.as_tensor(rm[off:off + n]))
+            m.running_var.copy_(torch.as_tensor(rv[off:off + n]))
+            off += n
+    out = {}
+    with torch.no_grad():
+        for tag in ("a", "a2"):
+            pol.compute_vbn(torch.as_tensor(frames.astype(np.float32)))
+            assert not pol.training
+            out[tag + "_rm"] = torch.cat([m.running_mean for m in bns]).numpy().copy()
+            out[tag + "_rv"] = torch.cat([m.running_var for m in bns]).numpy().copy()
+    save("g16_atari_vbn.npz", A=np.array(A), P=np.array(P), N=np.array(N), param_seed=np.array(16),
+         param_scale=np.array(0.05), rm=rm, rv=rv, frames=frames, momentum=np.array(0.1), **out)
+
+
 def _patch_rng_noise_source():
     """SURVEY finding 3: RNGNoiseSource reads Generator.__getstate__(), which returns None on numpy >= 2; the
     harness patch reads / writes bit_generator.state instead -- otherwise the reference's code as it is
@@ -857,7 +895,7 @@ def g15_rng_noise_source():
     save("g15_rng_noise_source.npz", **out)
 
 
-GENERATORS = {"g15": g15_rng_noise_source, "g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
+GENERATORS = {"g16": g16_atari_vbn, "g15": g15_rng_noise_source, "g1": g1_noise, "g2": g2_perturb, "g3": g3_forward, "g4": g4_fd_step, "g5": g5_trap,
               "g6": g6_runner_trap, "g7": g7_worker_synthetic, "g13": g13_worker_terminating, "g8": g8_impala,
               "g9": g9_novelty, "g10": g10_welford, "g11": g11_atari, "g12": g12_history,
               "g12i": g12_impala, "g12iu": lambda: g12_impala(patched=False), "g14": g14_impala_vbn}

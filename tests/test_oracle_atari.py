@@ -35,3 +35,18 @@ def test_synthetic_stacked_frames():
     assert f.shape == (2, 4, 84, 84) and f.dtype == np.uint8
     assert not np.array_equal(f[0], f[1])
     assert np.array_equal(oa.frames(3, [1], 0)[0], f[1])
+
+
+def test_compute_vbn_matches_reference(golden):
+    """oracle.atari.compute_vbn == the reference's AtariPolicy.compute_vbn (G16): every BN's running stats after one
+    train-mode pass of the VBN buffer and after a second (chained) pass."""
+    g = golden("g16_atari_vbn.npz")
+    A, P = int(g["A"]), int(g["P"])
+    assert P == oa.num_params(A)
+    flat = (np.random.RandomState(int(g["param_seed"])).randn(P) * float(g["param_scale"])).astype(np.float32)
+    p = oa.unflatten(flat, A)
+    rm, rv = g["rm"], g["rv"]
+    for tag in ("a", "a2"):
+        rm, rv = oa.compute_vbn(p, rm, rv, g["frames"].astype(np.float32), float(g["momentum"]))
+        np.testing.assert_allclose(rm, g[tag + "_rm"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(rv, g[tag + "_rv"], rtol=1e-5, atol=1e-6)
