@@ -152,7 +152,13 @@ class Policy(nn.Module):
     def compute_vbn(self, buffer):
         """policies/policy.py:31-34: one train-mode pass refreshes the BN running statistics.
 
-        Not on the hot path: it runs the torch module (device tensors) once per epoch."""
+        DiscretePolicy, ImpalaPolicy and AtariPolicy override this with their device passes (fdr_bn_refresh,
+        fdr_impala_bn_refresh, fdr_atari_bn_refresh).  A policy without BatchNorm (MujocoPolicy) has no statistic to
+        refresh -- the reference's train-mode forward changes nothing -- so nothing runs.  Any other subclass gets the
+        torch module's train-mode pass (device tensors, once per epoch, off the hot path)."""
+        if not self._bn_layers:
+            self.eval()
+            return
         self.train()
         x = torch.as_tensor(np.asarray(buffer), dtype=torch.float32).reshape(-1, self.input_shape)
         self.model(x.to(self.flat.device))
