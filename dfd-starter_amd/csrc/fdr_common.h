@@ -67,32 +67,31 @@ __device__ __forceinline__ T wave_sum(T v) {
 }
 
 // theta'[p] = fl32(base[p] +/- fl32(sigma * eps[p]))  -- no contraction (bit-exact with numpy).
+// Branch-free: eps is always a readable address (the lane's base when it is not perturbed -- its value is then
+// discarded by the select), so every element's two loads are unconditional and the compiler batches them.  (r12: a
+// per-element `if (sgn != 0)` around the eps load put each load behind its own exec branch and wait -- ~200 serialised
+// HBM round trips per thread in the MLP rollouts' prologue.)
 struct ParamSrc {
   const float* base;
-  const float* eps;  // table + idx, or nullptr
+  const float* eps;  // table + idx, or base (unperturbed lane: loaded, not used)
   float sigma;
   int sgn;           // +1 / -1 / 0
   double n2;         // running sum of fl32(sigma*eps)^2 over the elements this thread loaded
 
   __device__ __forceinline__ float get(int64_t p) {
 #pragma clang fp contract(off)
-    float t = base[p];
-    if (sgn != 0) {
-      const float st = sigma * eps[p];
-      n2 += (double)st * (double)st;
-      t = sgn > 0 ? t + st : t - st;
-    }
-    return t;
+    const float t = base[p];
+    const float st = sigma * eps[p];
+    const double d = (double)st;
+    n2 += sgn != 0 ? d * d : 0.0;
+    return sgn > 0 ? t + st : (sgn < 0 ? t - st : t);
   }
   // same value, but not counted in n2 (an element several threads replicate)
   __device__ __forceinline__ float get_nocount(int64_t p) const {
 #pragma clang fp contract(off)
-    float t = base[p];
-    if (sgn != 0) {
-      const float st = sigma * eps[p];
-      t = sgn > 0 ? t + st : t - st;
-    }
-    return t;
+    const float t = base[p];
+    const float st = sigma * eps[p];
+    return sgn > 0 ? t + st : (sgn < 0 ? t - st : t);
   }
 };
 

@@ -53,7 +53,7 @@ struct LanesArgs {
     s.sigma = sigma;
     s.n2 = 0.0;
     s.sgn = 0;
-    s.eps = nullptr;
+    s.eps = s.base;  // unperturbed: a readable address whose value ParamSrc discards
     if (table != nullptr) {
       const int64_t off = idx[lane];
       const int sg = sign ? (int)sign[lane] : 1;

@@ -230,6 +230,11 @@ struct MlpLane {
       for (int k = 0; k < 8; ++k)
         w2[p * 8 + k] = f2{src.get(L::L2W + (int64_t)row0 * kHidden + 8 * c + k),
                            src.get(L::L2W + (int64_t)row1 * kHidden + 8 * c + k)};
+      // the group's weights and norm terms are final here (MlpPair::load: no deferred selects held in scratch)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) asm volatile("" : "+v"(w2[p * 8 + k]));
+      asm volatile("" : "+v"(src.n2));
+      __builtin_amdgcn_sched_barrier(0);
     }
     b2 = src.get(L::L2B + j);
     if (o < NOUT) {
@@ -595,8 +600,10 @@ __global__ __launch_bounds__(64 * kLanesPerBlock, WIDE ? 2 : 4) void rollout_ker
   const bool det = a.lanes.deterministic ? a.lanes.deterministic[lane] != 0 : false;
   Lane pl;
   pl.load(src, j, a.bn_mean, a.bn_var, wtile + wv * Lane::kTileF4);
-  {  // written now: a double live across the T-step loop would be spilled
-    const double n2 = wave_sum(src.n2);
+  {  // written now: a double live across the T-step loop would be spilled (and the asm keeps the compiler from
+     // sinking the norm past the loop with every element's sigma * eps in scratch)
+    double n2 = wave_sum(src.n2);
+    asm volatile("" : "+v"(n2));
     if (j == 0 && a.norm2) a.norm2[lane] = n2;
   }
 
@@ -983,6 +990,9 @@ struct MlpPair {
     }
     b1a = kBiasCol ? 0.f : kWS * src.get(L::L1B + ua);
     b1b = kBiasCol ? 0.f : kWS * src.get(L::L1B + ub);
+    // (load groups: each group's loads are issued together, the next group's after it -- hoisting every load of the
+    // prologue to its top spilled ~140 values to scratch)
+    __builtin_amdgcn_sched_barrier(0);
     // quad q = t / 4 owns units 8q .. 8q + 7; thread c = t % 4 of it takes inputs 16c .. 16c + 15 and pair p the
     // units (8q + (c ^ p), 8q + 4 + (c ^ p)): the quad's reduce-scatter (partners c ^ 2, c ^ 1) leaves pair 0
     const int q4 = t >> 2, c4 = t & 3;
@@ -995,6 +1005,12 @@ struct MlpPair {
         const float e1 = src.get(L::L2W + (int64_t)row1 * kHidden + 16 * c4 + k);
         w2[p * 16 + k] = f2{kWS * e0, kWS * e1};
       }
+      // the group's weights and its norm terms are final here (else the compiler defers the selects past the other
+      // groups' loads and keeps every sigma * eps in scratch meanwhile)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) asm volatile("" : "+v"(w2[p * 16 + k]));
+      asm volatile("" : "+v"(src.n2));
+      __builtin_amdgcn_sched_barrier(0);
     }
     const int u2a = 8 * q4 + c4, u2b = 8 * q4 + 4 + c4;  // this thread's layer-2 units
     b2a = kWS * src.get(L::L2B + u2a);
@@ -1399,6 +1415,9 @@ __global__ __launch_bounds__(64 * kPairWaves, 2) void rollout_pair_kernel(Rollou
     double n2 = src.n2;
 #pragma unroll
     for (int m = 16; m >= 1; m >>= 1) n2 += __shfl_xor(n2, m, kWave);
+    // formed here: otherwise the compiler sinks the norm (and its store) past the step loop and keeps every
+    // element's sigma * eps in scratch across it
+    asm volatile("" : "+v"(n2));
     if (t == 0 && active && a.norm2) a.norm2[lane] = n2;
   }
 
