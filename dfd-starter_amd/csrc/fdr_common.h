@@ -86,6 +86,16 @@ struct ParamSrc {
     n2 += sgn != 0 ? d * d : 0.0;
     return sgn > 0 ? t + st : (sgn < 0 ? t - st : t);
   }
+  // get(p) counted in n2 only when `use` (an element read unconditionally from a clamped index whose value the caller
+  // discards otherwise: no load behind a branch)
+  __device__ __forceinline__ float get_if(int64_t p, bool use) {
+#pragma clang fp contract(off)
+    const float t = base[p];
+    const float st = sigma * eps[p];
+    const double d = (double)st;
+    n2 += (use && sgn != 0) ? d * d : 0.0;
+    return sgn > 0 ? t + st : (sgn < 0 ? t - st : t);
+  }
   // same value, but not counted in n2 (an element several threads replicate)
   __device__ __forceinline__ float get_nocount(int64_t p) const {
 #pragma clang fp contract(off)

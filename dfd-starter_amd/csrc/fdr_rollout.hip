@@ -237,34 +237,53 @@ struct MlpLane {
       __builtin_amdgcn_sched_barrier(0);
     }
     b2 = src.get(L::L2B + j);
-    if (o < NOUT) {
+    // Branch-free from here (r12): a load behind a condition ends its block with a vmcnt(0) wait.  The head rows
+    // and the input BN are read from clamped indices by every lane, counted and kept only where they exist; the
+    // running stats from a valid address whether or not they were given.
+    {
+      const bool has_o = o < NOUT;
+      const int oc = has_o ? o : 0;
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
-        const int64_t base = L::L3W + (int64_t)o * kHidden + 16 * q + 4 * m;
-        const float e0 = src.get(base), e1 = src.get(base + 1), e2 = src.get(base + 2), e3 = src.get(base + 3);
-        my[(kW1Chunks + m) * kWave] = float4{e0, e1, e2, e3};
+        const int64_t base = L::L3W + (int64_t)oc * kHidden + 16 * q + 4 * m;
+        const float e0 = src.get_if(base, has_o), e1 = src.get_if(base + 1, has_o), e2 = src.get_if(base + 2, has_o),
+                    e3 = src.get_if(base + 3, has_o);
+        my[(kW1Chunks + m) * kWave] = has_o ? float4{e0, e1, e2, e3} : float4{0.f, 0.f, 0.f, 0.f};
       }
-      b3 = q == 0 ? src.get(L::L3B + o) : src.get_nocount(L::L3B + o);
-    } else {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) my[(kW1Chunks + m) * kWave] = float4{0.f, 0.f, 0.f, 0.f};
-      b3 = 0.f;
+      const float b3v = src.get_if(L::L3B + oc, has_o && q == 0);
+      b3 = has_o ? b3v : 0.f;
     }
     wave_lds_sync();
     a0 = c0 = a1 = c1 = a2 = c2 = 0.f;
     if constexpr (DISC) {
-      if (j < NIN) {
-        const float w = src.get(L::BN0W + j), b = src.get(L::BN0B + j);
-        bn_fold(w, b, bn_mean ? bn_mean[j] : 0.f, bn_var ? bn_var[j] : 1.f, a0, c0);
+      const float* bm = bn_mean ? bn_mean : src.base;  // a readable address either way
+      const float* bv = bn_var ? bn_var : src.base;
+      auto stat = [&](int k, float& rm, float& rv) {
+        const float m = bm[k], v = bv[k];
+        rm = bn_mean ? m : 0.f;
+        rv = bn_var ? v : 1.f;
+      };
+      {
+        const bool in = j < NIN;
+        const int jc = in ? j : 0;
+        const float w = src.get_if(L::BN0W + jc, in), b = src.get_if(L::BN0B + jc, in);
+        float rm, rv, a, c;
+        stat(jc, rm, rv);
+        bn_fold(w, b, rm, rv, a, c);
+        a0 = in ? a : 0.f;
+        c0 = in ? c : 0.f;
       }
       {
         const float w = src.get(L::BN1W + j), b = src.get(L::BN1B + j);
-        bn_fold(w, b, bn_mean ? bn_mean[NIN + j] : 0.f, bn_var ? bn_var[NIN + j] : 1.f, a1, c1);
+        float rm, rv;
+        stat(NIN + j, rm, rv);
+        bn_fold(w, b, rm, rv, a1, c1);
       }
       {
         const float w = src.get(L::BN2W + j), b = src.get(L::BN2B + j);
-        bn_fold(w, b, bn_mean ? bn_mean[NIN + kHidden + j] : 0.f,
-                bn_var ? bn_var[NIN + kHidden + j] : 1.f, a2, c2);
+        float rm, rv;
+        stat(NIN + kHidden + j, rm, rv);
+        bn_fold(w, b, rm, rv, a2, c2);
       }
     }
   }
@@ -1015,7 +1034,10 @@ struct MlpPair {
     const int u2a = 8 * q4 + c4, u2b = 8 * q4 + 4 + c4;  // this thread's layer-2 units
     b2a = kWS * src.get(L::L2B + u2a);
     b2b = kWS * src.get(L::L2B + u2b);
-    if (o < NOUT) {
+    // branch-free (MlpLane::load): clamped indices, counted and kept only where the element exists
+    {
+      const bool has_o = o < NOUT;
+      const int oc = has_o ? o : 0;
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
         float e[4];
@@ -1023,26 +1045,39 @@ struct MlpPair {
         for (int i = 0; i < 4; ++i) {
           const int w = 4 * m + i;
           // w < 16: value z.x of row-thread w; else z.y of row-thread w - 16
-          e[i] = src.get(L::L3W + (int64_t)o * kHidden + head_unit(rho, w & 15, w >> 4));
+          e[i] = src.get_if(L::L3W + (int64_t)oc * kHidden + head_unit(rho, w & 15, w >> 4), has_o);
         }
-        my[(2 * kW1Chunks + m) * kWave] = float4{kWS * e[0], kWS * e[1], kWS * e[2], kWS * e[3]};
+        my[(2 * kW1Chunks + m) * kWave] =
+            has_o ? float4{kWS * e[0], kWS * e[1], kWS * e[2], kWS * e[3]} : float4{0.f, 0.f, 0.f, 0.f};
       }
-      b3 = kWS * (rho == 0 ? src.get(L::L3B + o) : src.get_nocount(L::L3B + o));
-    } else {
-#pragma unroll
-      for (int m = 0; m < 8; ++m) my[(2 * kW1Chunks + m) * kWave] = float4{0.f, 0.f, 0.f, 0.f};
-      b3 = 0.f;
+      const float b3v = src.get_if(L::L3B + oc, has_o && rho == 0);
+      b3 = has_o ? kWS * b3v : 0.f;
     }
     wave_lds_sync();
     a0 = c0 = a1a = c1a = a1b = c1b = a2a = c2a = a2b = c2b = 0.f;
     if constexpr (DISC) {
-      if (t < NIN) {
-        const float w = src.get(L::BN0W + t), b = src.get(L::BN0B + t);
-        bn_fold(w, b, bn_mean ? bn_mean[t] : 0.f, bn_var ? bn_var[t] : 1.f, a0, c0);
+      const float* bm = bn_mean ? bn_mean : src.base;  // a readable address either way
+      const float* bv = bn_var ? bn_var : src.base;
+      auto stat = [&](int k, float& rm, float& rv) {
+        const float m = bm[k], v = bv[k];
+        rm = bn_mean ? m : 0.f;
+        rv = bn_var ? v : 1.f;
+      };
+      {
+        const bool in = t < NIN;
+        const int tc = in ? t : 0;
+        const float w = src.get_if(L::BN0W + tc, in), b = src.get_if(L::BN0B + tc, in);
+        float rm, rv, a, c;
+        stat(tc, rm, rv);
+        bn_fold(w, b, rm, rv, a, c);
+        a0 = in ? a : 0.f;
+        c0 = in ? c : 0.f;
       }
-      auto fold = [&](int64_t wofs, int64_t bofs, int stat, int u, float& av, float& cv) {
+      auto fold = [&](int64_t wofs, int64_t bofs, int st, int u, float& av, float& cv) {
         const float w = src.get(wofs + u), b = src.get(bofs + u);
-        bn_fold(w, b, bn_mean ? bn_mean[stat + u] : 0.f, bn_var ? bn_var[stat + u] : 1.f, av, cv);
+        float rm, rv;
+        stat(st + u, rm, rv);
+        bn_fold(w, b, rm, rv, av, cv);
       };
       fold(L::BN1W, L::BN1B, NIN, ua, a1a, c1a);
       fold(L::BN1W, L::BN1B, NIN, ub, a1b, c1b);
