@@ -104,11 +104,20 @@ struct StepArgs {
 };
 constexpr int kCiPitch = (kCoreIn + 31) / 32 * 32;
 
-// phase clock of the first conv workgroup (s_memtime), for the phase breakdown in DESIGN.md
+// phase clock of the first conv workgroup (s_memtime), for the phase breakdown in DESIGN.md -- a diagnostics build
+// only (make STAMPS=1 -> -DFDR_CONV_STAMPS; tools/impala_phases_h2.py).  In the product the stamps compile away: even
+// runtime-gated, each conditional store was a control-flow join at which the waitcnt pass drained every load in flight
+// (vmcnt(0), CDNA4 counts stores too), including the next conv's weight-block prefetch.
+#ifdef FDR_CONV_STAMPS
 #define FDR_STAMP(a, k)                                                      \
   do {                                                                       \
     if ((a).dbg && blockIdx.x == 0 && threadIdx.x == 0) (a).dbg[k] = clock64(); \
   } while (0)
+#else
+#define FDR_STAMP(a, k) \
+  do {                  \
+  } while (0)
+#endif
 
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
 constexpr float kBnEps = 1e-5f;

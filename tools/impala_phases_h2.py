@@ -1,6 +1,10 @@
 """Phase clocks of conv_kernel_h2 (fdr_impala_debug_clock: s_memtime of workgroup 0 at each barrier).
 
-    python tools/impala_phases_h2.py [--lanes 1024 --envs 4]
+    make -C dfd-starter_amd/csrc STAMPS=1 OUT=../fdr/libfdr_stamps.so OBJDIR=../../build/obj_stamps
+    FDR_LIB=$PWD/dfd-starter_amd/fdr/libfdr_stamps.so python tools/impala_phases_h2.py [--lanes 1024 --envs 4]
+
+(The stamps are compiled only into that diagnostics build: in the product even runtime-gated stamps drained the
+loads in flight at every phase boundary.)
 
 Workgroup 0 shares its CU with a second workgroup for the whole launch (2 per CU), so a phase's clocks
 include the issue slots the other workgroup takes."""
