@@ -1429,6 +1429,32 @@ __device__ __forceinline__ MfmaRing2<NQ, Frag> mfma_ring2(const _Float16* thm, c
   return MfmaRing2<NQ, Frag>{thm, ep0, ep1, f};
 }
 
+// The head logits of a workgroup's NE envs (policies/impala.py:122): logit[e][ai] = b[ai] + sum_k W[ai][k] hs[k][e],
+// split over the 512 threads -- P parts of 256 / P inputs each, the parts added in part order (P = 8 at A * NE <= 64).
+// (One wave walking the 256 dependent FMAs per logit left the other seven waiting at the next barrier.)
+template <int E, int NE>
+__device__ __forceinline__ void head_split(const float* pack, int64_t pack_stride, int l0, const Layout& L, int A,
+                                           const float* hs, float* part, float* logit) {
+  const int j = threadIdx.x, nl = A * NE;
+  const int parts = nl <= 64 ? 8 : (nl <= 128 ? 4 : (nl <= 256 ? 2 : 1));
+  const int kn = kHid / parts;
+  if (j < parts * nl) {
+    const int pi = j / nl, r = j - pi * nl, ai = r / NE, e = r - ai * NE;
+    const float* wh = pack + (int64_t)(l0 + e / E) * pack_stride + L.head_w + ai * kHid + pi * kn;
+    const float* hp = hs + (pi * kn) * NE + e;
+    float s = 0.f;
+    for (int k = 0; k < kn; ++k) s = fmaf(wh[k], hp[k * NE], s);
+    part[j] = s;
+  }
+  __syncthreads();
+  if (j < nl) {
+    const int ai = j / NE, e = j - ai * NE;
+    float s = part[j];
+    for (int pi = 1; pi < parts; ++pi) s += part[pi * nl + j];
+    logit[e * kMaxAct + ai] = s + pack[(int64_t)(l0 + e / E) * pack_stride + L.head_b + ai];
+  }
+}
+
 template <int E, int MODE>
 __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_eu(2))) void core_kernel_hpm2(
     Layout L, StepArgs a) {
@@ -1444,6 +1470,7 @@ __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_e
   __shared__ __attribute__((aligned(16))) _Float16 gh[NE * GP];
   __shared__ float hs[kHid * NE];
   __shared__ float logit[NE * kMaxAct];
+  __shared__ float hpart[2 * kCoreThreads];  // head_split's partial sums
   __shared__ float bsum[4 * kGates];               // b_ih + b_hh of the 4 lanes
   _Float16* xh = reinterpret_cast<_Float16*>(xg);
   float* gates = reinterpret_cast<float*>(xg);
@@ -1657,14 +1684,7 @@ __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_e
     }
   }
   __syncthreads();
-  if (j < A * NE) {
-    const int ai = j / NE, e = j - ai * NE;
-    const float* pk = pkl(e / E);
-    const float* wh = pk + L.head_w + ai * kHid;
-    float s = 0.f;
-    for (int k = 0; k < kHid; ++k) s = fmaf(wh[k], hs[k * NE + e], s);
-    logit[e * kMaxAct + ai] = s + pk[L.head_b + ai];
-  }
+  head_split<E, NE>(a.pack, a.pack_stride, l0, L, A, hs, hpart, logit);
   __syncthreads();
   if (j < NE) core_finish<E, MODE>(a, logit + (j / E) * E * kMaxAct, l0 + j / E, j % E);
 }
@@ -1691,6 +1711,7 @@ __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_e
   __shared__ __attribute__((aligned(16))) _Float16 gh[NE * GP];
   __shared__ float hs[kHid * NE];
   __shared__ float logit[NE * kMaxAct];
+  __shared__ float hpart[2 * kCoreThreads];  // head_split's partial sums
   __shared__ float bsum[4 * kGates];
   const int j = threadIdx.x, w = j >> 6, l = j & 63;
   const int u = j & (kHid - 1), hf = j >> 8;
@@ -1811,14 +1832,7 @@ __global__ __launch_bounds__(2 * kCoreThreads) __attribute__((amdgpu_waves_per_e
 #pragma unroll
       for (int e = 0; e < E; ++e) hs[u * NE + ep_ + h2i * E + e] = fmaf(hj[h2i * E + e], bsc[h2i], bsh[h2i]);
     __syncthreads();
-    if (j < A * NE) {
-      const int ai = j / NE, e = j - ai * NE;
-      const float* pk = pkl(e / E);
-      const float* wh = pk + L.head_w + ai * kHid;
-      float sacc = 0.f;
-      for (int k = 0; k < kHid; ++k) sacc = fmaf(wh[k], hs[k * NE + e], sacc);
-      logit[e * kMaxAct + ai] = sacc + pk[L.head_b + ai];
-    }
+    head_split<E, NE>(a.pack, a.pack_stride, l0, L, A, hs, hpart, logit);
     __syncthreads();
     if (j < NE) core_finish<E, MODE>(a, logit + (j / E) * E * kMaxAct, l0 + j / E, j % E, false, &ent, t);
   }
